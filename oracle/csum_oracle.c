@@ -1,0 +1,349 @@
+/*
+ * csum_oracle.c -- CPU restatement of the reference's checksum path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see csum_oracle.h).  Pinned against fixtures that
+ * the reference's own routines produced (tests/golden/, oracle/golden_gen.c).
+ *
+ * The scalar loops deliberately keep the reference's loop shape -- 16-bit
+ * loads into a 32-bit accumulator, one fold per call, 127-byte block chaining
+ * -- so that this file is also a faithful CPU baseline ("kind": "port").
+ */
+#define _GNU_SOURCE
+#include "csum_oracle.h"
+
+#include <pthread.h>
+#include <string.h>
+#include <time.h>
+
+/* Fold a 32-bit partial sum to 16 bits by end-around carry (tools.c:47-51). */
+static inline uint32_t fold32(uint32_t s)
+{
+    while (s >> 16)
+        s = (s & 0xFFFFu) + (s >> 16);
+    return s;
+}
+
+/* tools.c:24-54.  A byte at logical position (offset + i) is the high byte of
+ * its 16-bit word when that position is odd.  The reference walks the buffer
+ * as host (little-endian) u16 words; so does this. */
+uint16_t orc_checksum16(int offset, const void *buf, uint16_t len,
+                        uint32_t pre_sum, int complement)
+{
+    const uint8_t *p = (const uint8_t *)buf;
+    uint32_t acc = pre_sum;
+    uint32_t left = len;
+
+    if ((offset & 1) && left > 0) { /* tools.c:29-35 (len==0 is a no-op here) */
+        acc += (uint32_t)p[0] << 8;
+        p++;
+        left--;
+    }
+    while (left > 1) { /* tools.c:36-40 */
+        uint16_t w;
+        memcpy(&w, p, 2);
+        acc += w;
+        p += 2;
+        left -= 2;
+    }
+    if (left) /* tools.c:42-45: trailing byte is a low byte */
+        acc += p[0];
+
+    acc = fold32(acc);
+    return complement ? (uint16_t)~acc : (uint16_t)acc;
+}
+
+/* pktbuf.c:646-670.  `offset` counts bytes from the start of this call, the
+ * running sum is kept in a uint16_t (pktbuf.c:657) and folded per block. */
+uint16_t orc_pieces_checksum16(const orc_piece_t *pieces, int npieces, int len,
+                               int pre_sum, int complement)
+{
+    long avail = 0;
+    for (int i = 0; i < npieces; i++)
+        avail += pieces[i].size;
+    if (avail < len) /* pktbuf.c:650-655 */
+        return 0;
+
+    uint16_t sum = (uint16_t)pre_sum;
+    uint32_t offset = 0;
+    for (int i = 0; len > 0 && i < npieces; i++) {
+        int take = pieces[i].size < len ? pieces[i].size : len;
+        if (take <= 0)
+            continue;
+        sum = orc_checksum16((int)offset, pieces[i].data, (uint16_t)take, sum, 0);
+        len -= take;
+        offset += (uint32_t)take;
+    }
+    return complement ? (uint16_t)~sum : sum;
+}
+
+uint16_t orc_flat_checksum16(const uint8_t *buf, uint64_t len, int pre_sum,
+                             int complement)
+{
+    uint16_t sum = (uint16_t)pre_sum;
+    uint64_t offset = 0;
+    while (len > 0) {
+        uint32_t take = len > ORC_PKTBUF_BLK_SIZE ? ORC_PKTBUF_BLK_SIZE : (uint32_t)len;
+        sum = orc_checksum16((int)(offset & 1), buf + offset, (uint16_t)take, sum, 0);
+        len -= take;
+        offset += take;
+    }
+    return complement ? (uint16_t)~sum : sum;
+}
+
+/* tools.c:58-70: src, dst, {0, proto}, htons((uint16_t)len), in memory order,
+ * each through checksum16 with the running offset. */
+uint16_t orc_pseudo_sum(const uint8_t src[4], const uint8_t dst[4],
+                        uint8_t protocol, uint32_t len)
+{
+    uint8_t zp[2] = {0, protocol};
+    uint16_t l16 = (uint16_t)len;
+    uint8_t lbe[2] = {(uint8_t)(l16 >> 8), (uint8_t)(l16 & 0xFF)}; /* x_htons on LE */
+    uint32_t s = orc_checksum16(0, src, 4, 0, 0);
+    s = orc_checksum16(4, dst, 4, s, 0);
+    s = orc_checksum16(8, zp, 2, s, 0);
+    s = orc_checksum16(10, lbe, 2, s, 0);
+    return (uint16_t)s;
+}
+
+/* tools.c:56-75 (argument order dest, src as in the reference). */
+uint16_t orc_checksum_peso(const uint8_t *seg, uint32_t len,
+                           const uint8_t dest[4], const uint8_t src[4],
+                           uint8_t protocol)
+{
+    uint16_t pre = orc_pseudo_sum(src, dest, protocol, len);
+    return orc_flat_checksum16(seg, len, (int)pre, 1);
+}
+
+/* Flag bits, identical to TCSUM_PKT_* in include/tcsum.h. */
+#define F_BAD_VERSION 0x01u
+#define F_BAD_HDRLEN 0x02u
+#define F_BAD_TOTLEN 0x04u
+#define F_PROTO_OTHER 0x08u
+#define F_SHORT 0x10u
+
+void orc_ipv4_pair(const uint8_t *pkt, uint32_t frame_len, uint16_t *ip_out,
+                   uint16_t *l4_out, uint8_t *flags_out)
+{
+    uint8_t flags = 0;
+    if (frame_len < 20) {
+        *ip_out = 0;
+        *l4_out = 0;
+        *flags_out = F_SHORT;
+        return;
+    }
+    uint32_t version = pkt[0] >> 4;
+    uint32_t ihl4 = (uint32_t)(pkt[0] & 0x0F) * 4u;
+    uint32_t tl = ((uint32_t)pkt[2] << 8) | pkt[3];
+    uint8_t proto = pkt[9];
+
+    if (version != 4) /* ipv4.c:222 */
+        flags |= F_BAD_VERSION;
+    if (ihl4 < 20 || ihl4 > frame_len) /* ipv4.c:229 */
+        flags |= F_BAD_HDRLEN;
+    if (tl < 20 || tl > frame_len || tl < ihl4) /* ipv4.c:236 */
+        flags |= F_BAD_TOTLEN;
+
+    uint32_t hl = ihl4 < 20 ? 20 : ihl4;
+    if (hl > frame_len)
+        hl = frame_len;
+    uint32_t end = tl < hl ? hl : tl;
+    if (end > frame_len)
+        end = frame_len;
+
+    *ip_out = orc_checksum16(0, pkt, (uint16_t)hl, 0, 1); /* ipv4.c:243 */
+
+    const uint8_t *l4 = pkt + hl;
+    uint32_t l4len = end - hl;
+    if (proto == 6 || proto == 17) { /* tcp_in.c:80 / udp.c:410 */
+        *l4_out = orc_checksum_peso(l4, l4len, pkt + 16, pkt + 12, proto);
+    } else if (proto == 1) { /* icmpv4.c:36 */
+        *l4_out = orc_flat_checksum16(l4, l4len, 0, 1);
+    } else {
+        *l4_out = 0;
+        flags |= F_PROTO_OTHER;
+    }
+    *flags_out = flags;
+}
+
+/* ---------------------------------------------------------------- batches */
+
+typedef struct job {
+    int kind; /* 0 seg, 1 peso, 2 ipv4 */
+    const uint8_t *arena;
+    const void *descs;
+    uint32_t lo, hi;
+    void *out;
+    uint8_t *flags;
+    int complement;
+} job_t;
+
+static void run_range(const job_t *j)
+{
+    for (uint32_t i = j->lo; i < j->hi; i++) {
+        if (j->kind == 0) {
+            const orc_seg_t *d = (const orc_seg_t *)j->descs + i;
+            ((uint16_t *)j->out)[i] =
+                orc_flat_checksum16(j->arena + d->offset, d->len, (int)d->pre_sum,
+                                    j->complement);
+        } else if (j->kind == 1) {
+            const orc_peso_t *d = (const orc_peso_t *)j->descs + i;
+            ((uint16_t *)j->out)[i] = orc_checksum_peso(j->arena + d->offset, d->len,
+                                                        d->dst, d->src, d->protocol);
+        } else {
+            const orc_pkt_t *d = (const orc_pkt_t *)j->descs + i;
+            uint16_t ip, l4;
+            uint8_t fl;
+            orc_ipv4_pair(j->arena + d->offset, d->len, &ip, &l4, &fl);
+            ((uint32_t *)j->out)[i] = (uint32_t)ip | ((uint32_t)l4 << 16);
+            if (j->flags)
+                j->flags[i] = fl;
+        }
+    }
+}
+
+static void *job_thread(void *arg)
+{
+    run_range((const job_t *)arg);
+    return NULL;
+}
+
+static void run_batch(job_t base, uint32_t n, int nthreads)
+{
+    if (nthreads <= 1 || n < 2) {
+        base.lo = 0;
+        base.hi = n;
+        run_range(&base);
+        return;
+    }
+    if (nthreads > 256)
+        nthreads = 256;
+    pthread_t th[256];
+    job_t jobs[256];
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = base;
+        jobs[t].lo = (uint32_t)((uint64_t)n * t / nthreads);
+        jobs[t].hi = (uint32_t)((uint64_t)n * (t + 1) / nthreads);
+        pthread_create(&th[t], NULL, job_thread, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; t++)
+        pthread_join(th[t], NULL);
+}
+
+void orc_batch_segments(const uint8_t *arena, const orc_seg_t *segs, uint32_t n,
+                        uint16_t *out, int complement, int nthreads)
+{
+    job_t j = {0, arena, segs, 0, 0, out, NULL, complement};
+    run_batch(j, n, nthreads);
+}
+
+void orc_batch_peso(const uint8_t *arena, const orc_peso_t *segs, uint32_t n,
+                    uint16_t *out, int nthreads)
+{
+    job_t j = {1, arena, segs, 0, 0, out, NULL, 0};
+    run_batch(j, n, nthreads);
+}
+
+void orc_batch_ipv4(const uint8_t *arena, const orc_pkt_t *pkts, uint32_t n,
+                    uint32_t *out, uint8_t *flags, int nthreads)
+{
+    job_t j = {2, arena, pkts, 0, 0, out, flags, 0};
+    run_batch(j, n, nthreads);
+}
+
+/* ---------------------------------------------------------- synthetic data */
+
+uint64_t orc_splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+void orc_synth_fill(uint8_t *dst, uint64_t byte_offset, uint64_t nbytes,
+                    uint64_t seed)
+{
+    for (uint64_t i = 0; i < nbytes; i++) {
+        uint64_t pos = byte_offset + i;
+        uint64_t w = orc_splitmix64(seed + (pos >> 3));
+        dst[i] = (uint8_t)(w >> (8 * (pos & 7)));
+    }
+}
+
+/* ------------------------------------------------------------ CPU baseline */
+
+typedef struct tjob {
+    orc_peso_fn fn;
+    const uint8_t *arena;
+    const orc_peso_t *segs;
+    uint32_t lo, hi;
+    double min_seconds;
+    pthread_barrier_t *bar;
+    uint64_t bytes;
+    uint64_t csum;
+    double secs;
+} tjob_t;
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static void *time_thread(void *arg)
+{
+    tjob_t *j = (tjob_t *)arg;
+    pthread_barrier_wait(j->bar);
+    double t0 = now_s(), t1;
+    uint64_t bytes = 0, csum = 0;
+    do {
+        csum = 0;
+        for (uint32_t i = j->lo; i < j->hi; i++) {
+            const orc_peso_t *d = j->segs + i;
+            csum += j->fn(j->arena + d->offset, d->len, d->dst, d->src, d->protocol);
+            bytes += d->len;
+        }
+        t1 = now_s();
+    } while (t1 - t0 < j->min_seconds);
+    j->bytes = bytes;
+    j->csum = csum;
+    j->secs = t1 - t0;
+    return NULL;
+}
+
+double orc_time_peso(orc_peso_fn fn, const uint8_t *arena, const orc_peso_t *segs,
+                     uint32_t n, int nthreads, double min_seconds,
+                     uint64_t *checksum_of_checksums)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > 256)
+        nthreads = 256;
+    pthread_t th[256];
+    tjob_t jobs[256];
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = (tjob_t){fn, arena, segs,
+                           (uint32_t)((uint64_t)n * t / nthreads),
+                           (uint32_t)((uint64_t)n * (t + 1) / nthreads),
+                           min_seconds, &bar, 0, 0, 0.0};
+        pthread_create(&th[t], NULL, time_thread, &jobs[t]);
+    }
+    double rate = 0.0, max_secs = 0.0;
+    uint64_t total = 0, csum = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        total += jobs[t].bytes;
+        csum += jobs[t].csum;
+        if (jobs[t].secs > max_secs)
+            max_secs = jobs[t].secs;
+    }
+    pthread_barrier_destroy(&bar);
+    if (max_secs > 0)
+        rate = (double)total / max_secs;
+    if (checksum_of_checksums)
+        *checksum_of_checksums = csum;
+    return rate;
+}

@@ -1,0 +1,120 @@
+"""Pin the CPU oracle to the reference's own outputs (tests/golden/).
+
+Every expected value in the fixtures is what the reference's checksum16 /
+pktbuf_checksum16 / checksum_peso returned (net/src/tools.c:24-75,
+net/src/pktbuf.c:646-670), compiled from /root/reference by oracle/golden_gen.c.
+"""
+import numpy as np
+import pytest
+
+import golden_io as G
+
+
+def test_kats(oracle):
+    k = G.kat_inputs()
+    h, e = k["KAT-1"]
+    assert oracle.checksum16(0, h, 20, 0, 1) == e == 0x61B8
+    filled = bytearray(h)
+    filled[10:12] = e.to_bytes(2, "little")
+    assert oracle.checksum16(0, filled, 20, 0, 1) == 0
+    b, e = k["KAT-2"]
+    assert oracle.flat_checksum16(b, 0, 1) == e == 0x8EE9
+    assert oracle.checksum16(0, b, 999, 0, 1) == e
+    b, e = k["KAT-3"]
+    assert oracle.checksum_peso(b, bytes([192, 168, 74, 3]), bytes([192, 168, 74, 2]), 6) == e == 0x4AD0
+    b, e = k["KAT-4"]
+    assert oracle.checksum16(0, b, 4, 0, 1) == e == 0xFFFF
+    b, e = k["KAT-5"]
+    assert oracle.checksum16(0, b, 2, 0, 1) == e == 0x0000
+
+
+def test_flat_checksum16(oracle):
+    pool = G.pool()
+    cases = G.flat_cases()
+    assert cases.size == 6000
+    bad = []
+    for c in cases:
+        off, n = int(c["pool_off"]), int(c["len"])
+        got = oracle.checksum16(int(c["offset"]), pool[off: off + n], n, int(c["pre_sum"]),
+                                int(c["complement"]))
+        if got != int(c["expected"]):
+            bad.append((c, got))
+    assert not bad, bad[:5]
+
+
+def test_pktbuf_checksum16(oracle):
+    pool = G.pool()
+    cases, blocks = G.pktbuf_cases()
+    assert cases.size == 1500
+    for c in cases:
+        pieces = G.case_blocks(c, blocks, pool)
+        # drop the bytes before the cursor (pktbuf_seek), keeping block shapes
+        skip, rest = int(c["seek"]), []
+        for p in pieces:
+            if skip >= p.size:
+                skip -= p.size
+                continue
+            rest.append(p[skip:])
+            skip = 0
+        got = oracle.pieces_checksum16(rest, int(c["len"]), int(c["pre_sum"]), int(c["complement"]))
+        assert got == int(c["expected"]), c
+
+
+def test_checksum_peso(oracle):
+    pool = G.pool()
+    cases, _ = G.peso_cases()
+    assert cases.size == 1248
+    for c in cases:
+        off, n = int(c["pool_off"]), int(c["total"])
+        got = oracle.checksum_peso(pool[off: off + n], c["dst"], c["src"], int(c["proto"]))
+        assert got == int(c["expected"]), c
+
+
+def test_ipv4_pair(oracle):
+    cases, ipool = G.ipv4_cases()
+    assert cases.size == 500
+    for c in cases:
+        off, n = int(c["pool_off"]), int(c["frame_len"])
+        ip, l4, fl = oracle.ipv4_pair(ipool[off: off + max(n, 1)], n)
+        assert (ip, l4, fl) == (int(c["ip"]), int(c["l4"]), int(c["flags"])), c
+
+
+def test_batch_forms_agree_with_scalar(oracle):
+    """The threaded batch entry points are the scalar routines, per item."""
+    pool = G.pool()
+    cases, _ = G.peso_cases()
+    segs = np.zeros(cases.size, oracle.PESO_DTYPE)
+    segs["offset"] = cases["pool_off"]
+    segs["len"] = cases["total"]
+    segs["src"] = cases["src"]
+    segs["dst"] = cases["dst"]
+    segs["protocol"] = cases["proto"]
+    out = oracle.batch_peso(pool, segs, nthreads=4)
+    np.testing.assert_array_equal(out, cases["expected"].astype(np.uint16))
+
+    icases, ipool = G.ipv4_cases()
+    pk = np.zeros(icases.size, oracle.PKT_DTYPE)
+    pk["offset"] = icases["pool_off"]
+    pk["len"] = icases["frame_len"]
+    out, flags = oracle.batch_ipv4(ipool, pk, nthreads=3)
+    np.testing.assert_array_equal(out & 0xFFFF, icases["ip"])
+    np.testing.assert_array_equal(out >> 16, icases["l4"])
+    np.testing.assert_array_equal(flags, icases["flags"])
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 127, 128, 1500, 65535, 65536, 65537, 200000])
+def test_closed_form(oracle, n):
+    """S = pre + sum b[i]*256^(i&1); fold(S) = 0 if S == 0 else 1 + (S-1) % 0xFFFF."""
+    rng = np.random.default_rng(n)
+    b = rng.integers(0, 256, n, dtype=np.uint8)
+    pre = int(rng.integers(0, 0x10000))
+    s = pre + int(b[0::2].astype(np.uint64).sum()) + 256 * int(b[1::2].astype(np.uint64).sum())
+    f = 0 if s == 0 else 1 + (s - 1) % 0xFFFF
+    assert oracle.flat_checksum16(b, pre, 0) == f
+    assert oracle.flat_checksum16(b, pre, 1) == (~f) & 0xFFFF
+
+
+def test_synth_fill_is_splitmix(oracle):
+    a = oracle.synth_fill(0, 64, 7)
+    b = oracle.synth_fill(13, 40, 7)
+    np.testing.assert_array_equal(a[13:53], b)

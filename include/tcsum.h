@@ -1,0 +1,143 @@
+/*
+ * tcsum.h -- MI355X Internet-checksum engine: C ABI.
+ *
+ * This library replaces one leaf of the wj9806/tcp stack: the one's-complement
+ * 16-bit folding sum over IPv4 headers and TCP/UDP pseudo-header + payload.
+ *
+ *   Legacy, drop-in (same names and signatures as the reference): see
+ *   tcsum_legacy.h -- checksum16 / checksum_peso / pktbuf_checksum16.
+ *
+ *   Batched, device-resident (this header): packets sit contiguously in HBM
+ *   (an "arena") and are described by an offset/length array; one launch
+ *   checksums the whole batch with hand-written gfx950 kernels.
+ *
+ * Conventions
+ *   - All pointers marked [dev] are device (HBM) pointers; [host] are host.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream).
+ *     Batch calls are asynchronous on that stream; nothing is allocated or
+ *     freed inside them (they are safe to capture in a hipGraph).
+ *   - Results are the u16 exactly as the reference returns it: the value as it
+ *     sits in little-endian host memory, so storing it into the header field
+ *     yields network-order bytes (net/src/tools.c:24-54).
+ *   - Return codes are the reference's net_err_t values
+ *     (net/net/net_err.h:8-29): 0 = OK, negative = error.
+ */
+#ifndef TCSUM_H
+#define TCSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TCSUM_OK 0               /* NET_ERR_OK */
+#define TCSUM_ERR_SYS (-1)       /* NET_ERR_SYS: HIP runtime failure */
+#define TCSUM_ERR_MEM (-2)       /* NET_ERR_MEM: allocation failed */
+#define TCSUM_ERR_SIZE (-5)      /* NET_ERR_SIZE */
+#define TCSUM_ERR_PARAM (-7)     /* NET_ERR_PARAM: bad argument */
+#define TCSUM_ERR_NOT_SUPPORT (-11) /* NET_ERR_NOT_SUPPORT: no usable gfx950 device */
+
+/* ------------------------------------------------------------ descriptors */
+
+/* A byte range with a caller-supplied partial sum: one pktbuf_checksum16 call
+ * (net/src/pktbuf.c:646-670).  pre_sum is truncated to 16 bits exactly like
+ * `uint16_t sum = pre_sum` (pktbuf.c:657); byte parity counts from `offset`. */
+typedef struct tcsum_seg {
+    uint64_t offset; /* byte offset of the range in the arena (any alignment) */
+    uint32_t len;    /* bytes; may exceed 65535 (chained like the pktbuf walk) */
+    uint32_t pre_sum;
+} tcsum_seg_t;
+
+/* A TCP/UDP segment: one checksum_peso call (net/src/tools.c:56-75).  The
+ * pseudo-header (src, dst, {0,protocol}, htons((uint16_t)len)) is built
+ * in-kernel. */
+typedef struct tcsum_peso {
+    uint64_t offset;  /* L4 header start in the arena */
+    uint32_t len;     /* L4 header + payload bytes (buf->total_size) */
+    uint8_t src[4];   /* ipaddr_t.addr of the source, network order */
+    uint8_t dst[4];   /* ipaddr_t.addr of the destination */
+    uint8_t protocol; /* 6 (TCP) or 17 (UDP); any value is summed as given */
+    uint8_t rsv[3];
+} tcsum_peso_t;
+
+/* A captured IPv4 packet (header + L4) for tcsum_batch_ipv4. */
+typedef struct tcsum_pkt {
+    uint64_t offset; /* first byte of the IPv4 header in the arena */
+    uint32_t len;    /* captured frame length from the IPv4 header on */
+    uint32_t rsv;
+} tcsum_pkt_t;
+
+/* tcsum_batch_ipv4 flag bits: what is_pkt_ok (net/src/ipv4.c:220-239) would
+ * reject, plus protocols with no L4 checksum here. */
+#define TCSUM_PKT_BAD_VERSION 0x01u /* version != 4                   (ipv4.c:222) */
+#define TCSUM_PKT_BAD_HDRLEN 0x02u  /* ihl*4 < 20 or > len            (ipv4.c:229) */
+#define TCSUM_PKT_BAD_TOTLEN 0x04u  /* total_len < 20, > len, < ihl*4 (ipv4.c:236) */
+#define TCSUM_PKT_PROTO_OTHER 0x08u /* not TCP/UDP/ICMP: l4 result is 0 */
+#define TCSUM_PKT_SHORT 0x10u       /* len < 20: both results are 0 */
+
+/* ------------------------------------------------ device-resident batches */
+
+/* out[i] = pktbuf_checksum16 over segs[i] with complement (0/1).
+ * total_bytes_hint = sum of lens if known (selects the lane mapping), else 0. */
+int tcsum_batch_segments(const void *arena /*[dev]*/, const tcsum_seg_t *segs /*[dev]*/,
+                         uint32_t n, uint16_t *out /*[dev]*/, int complement,
+                         uint64_t total_bytes_hint, void *stream);
+
+/* out[i] = checksum_peso over segs[i]: the value tcp_out.c:20 / udp.c:321
+ * store, or 0 on rx for a segment whose stored checksum is right
+ * (tcp_in.c:80, udp.c:410). */
+int tcsum_batch_peso(const void *arena /*[dev]*/, const tcsum_peso_t *segs /*[dev]*/,
+                     uint32_t n, uint16_t *out /*[dev]*/, uint64_t total_bytes_hint,
+                     void *stream);
+
+/* Both checksums of each IPv4 packet, pseudo-header taken from the packet:
+ *   out[i] & 0xFFFF = checksum16(0, hdr, ihl*4, 0, 1)                (ipv4.c:243, 656)
+ *   out[i] >> 16    = checksum_peso(l4, dst, src, proto) for TCP/UDP (tcp_in.c:80, udp.c:410)
+ *                   = pktbuf_checksum16(l4, l4len, 0, 1) for ICMP    (icmpv4.c:36)
+ *                   = 0 otherwise
+ * with l4 = [ihl*4, total_len).  On a rejected packet the ranges are clamped
+ * to [20 .. len] and flags[i] says why; flags may be NULL. */
+int tcsum_batch_ipv4(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/,
+                     uint32_t n, uint32_t *out /*[dev]*/, uint8_t *flags /*[dev] or NULL*/,
+                     uint64_t total_bytes_hint, void *stream);
+
+/* --------------------------------------------------- host-resident batches */
+
+/* End to end: host arena -> hipMemcpyAsync H2D (chunked, pipelined over
+ * several streams) -> tcsum_batch_peso -> D2H of the results; returns after
+ * the results are in host_out.  host_arena should come from tcsum_host_alloc
+ * (pinned) for full PCIe rate.  Segments may be in any order. */
+int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_bytes,
+                          const tcsum_peso_t *segs /*[host]*/, uint32_t n,
+                          uint16_t *out /*[host]*/);
+
+/* ------------------------------------------------------------ platform */
+
+/* HIP device init for the stack's net_plat_init hook (plat/net_plat.c:7):
+ * selects `device`, creates the legacy-call stream and its pinned staging.
+ * Optional -- the first checksum call does it lazily on device 0 (or
+ * $TCSUM_DEVICE). */
+int tcsum_plat_init(int device);
+
+/* Pinned host memory (hipHostMalloc) for packet arenas: the "pinned host
+ * buffer pool" that plat/ gains.  Returns NULL on failure. */
+void *tcsum_host_alloc(size_t bytes);
+void tcsum_host_free(void *p);
+
+/* Number of usable gfx950 devices (0 when none); never aborts. */
+int tcsum_device_count(void);
+
+/* Kernel geometry the batch calls choose for a mean length: lanes per packet
+ * (G) and 16-byte loads in flight per lane (U).  Exposed for tests/tuning;
+ * TCSUM_G / TCSUM_U in the environment override the choice. */
+void tcsum_pick_geometry(uint64_t mean_len, int *lanes_per_packet, int *loads_per_lane);
+
+/* Library identification string. */
+const char *tcsum_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TCSUM_H */

@@ -1,0 +1,35 @@
+/*
+ * tcsum_synth.h -- on-device synthetic packet batches for tests and bench.py.
+ *
+ * Not part of the checksum path.  The byte stream is the one the CPU oracle
+ * reproduces (oracle/csum_oracle.c: orc_synth_fill): byte p of the stream is
+ * byte (p & 7) of splitmix64(seed + (p >> 3)), so host and device see the same
+ * packets without a transfer.
+ */
+#ifndef TCSUM_SYNTH_H
+#define TCSUM_SYNTH_H
+
+#include <stdint.h>
+
+#include "tcsum.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* arena[0 .. nbytes) := stream bytes [byte_base, byte_base + nbytes).
+ * arena must be 16-byte aligned and byte_base a multiple of 16. */
+int tcsum_synth_fill(void *arena /*[dev]*/, uint64_t nbytes, uint64_t byte_base,
+                     uint64_t seed, void *stream);
+
+/* Overwrite the first 20 bytes of every packet with an IPv4 header:
+ * version 4, IHL 5, total_len = pkts[i].len, TTL 64, protocol TCP or UDP
+ * (from the hash of seed and i), header checksum 0 (tx form), random src/dst.
+ * Packets shorter than 20 bytes are left alone. */
+int tcsum_synth_ipv4(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,
+                     uint64_t seed, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TCSUM_SYNTH_H */

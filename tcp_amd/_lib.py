@@ -1,0 +1,68 @@
+"""ctypes binding of libtcsum.so (the C ABI declared in include/*.h).
+
+The library is loaded from this package directory only; if it is missing the
+import of any compute entry point raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libtcsum.so")
+
+# Return codes (net_err_t values, net/net/net_err.h:8-29)
+OK = 0
+ERR_SYS = -1
+ERR_MEM = -2
+ERR_SIZE = -5
+ERR_PARAM = -7
+ERR_NOT_SUPPORT = -11
+
+# (name, restype, argtypes) for every symbol include/*.h declares
+_V, _U16, _U32, _U64, _I, _SZ = (ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64,
+                                  ctypes.c_int, ctypes.c_size_t)
+SIGNATURES = {
+    # tcsum.h
+    "tcsum_batch_segments": (_I, [_V, _V, _U32, _V, _I, _U64, _V]),
+    "tcsum_batch_peso": (_I, [_V, _V, _U32, _V, _U64, _V]),
+    "tcsum_batch_ipv4": (_I, [_V, _V, _U32, _V, _V, _U64, _V]),
+    "tcsum_host_batch_peso": (_I, [_I, _V, _U64, _V, _U32, _V]),
+    "tcsum_plat_init": (_I, [_I]),
+    "tcsum_host_alloc": (_V, [_SZ]),
+    "tcsum_host_free": (None, [_V]),
+    "tcsum_device_count": (_I, []),
+    "tcsum_pick_geometry": (None, [_U64, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "tcsum_version": (ctypes.c_char_p, []),
+    # tcsum_legacy.h
+    "checksum16": (_U16, [_I, _V, _U16, _U32, _I]),
+    "checksum_peso": (_U16, [_V, _V, _V, ctypes.c_uint8]),
+    "pktbuf_checksum16": (_U16, [_V, _I, _I, _I]),
+    # tcsum_synth.h
+    "tcsum_synth_fill": (_I, [_V, _U64, _U64, _U64, _V]),
+    "tcsum_synth_ipv4": (_I, [_V, _V, _U32, _U64, _V]),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """The loaded product library; raises if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                " (there is no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != OK:
+        raise RuntimeError(f"{what} failed with net_err_t {rc}")

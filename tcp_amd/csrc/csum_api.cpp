@@ -1,0 +1,506 @@
+// csum_api.cpp -- the C ABI of libtcsum.so (include/tcsum.h, tcsum_legacy.h,
+// tcsum_synth.h): argument checks, per-device context, pinned staging, and
+// the legacy drop-in entry points.  Every checksum is computed by the gfx950
+// kernels in csum_kernels.hip; nothing here sums bytes.
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <stddef.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+#include "csum_launch.h"
+#include "tcsum.h"
+#include "tcsum_legacy.h"
+#include "tcsum_synth.h"
+
+// The drop-in symbols are called with the reference's own structs: the
+// mirror types must have the reference's LP64 layout (net/net/list.h:9-34,
+// net/net/pktbuf.h:15-41, net/net/ipaddr.h:12-22).
+static_assert(sizeof(tcsum_node_t) == 16, "node_t");
+static_assert(sizeof(tcsum_list_t) == 24, "list_t");
+static_assert(offsetof(tcsum_pktblk_t, size) == 16 && offsetof(tcsum_pktblk_t, data) == 24,
+              "pktblk_t");
+static_assert(offsetof(tcsum_pktbuf_t, blk_list) == 8 && offsetof(tcsum_pktbuf_t, ref) == 32 &&
+                  offsetof(tcsum_pktbuf_t, pos) == 56 && offsetof(tcsum_pktbuf_t, curr_blk) == 64 &&
+                  offsetof(tcsum_pktbuf_t, blk_offset) == 72 && sizeof(tcsum_pktbuf_t) == 80,
+              "pktbuf_t");
+static_assert(offsetof(tcsum_ipaddr_t, addr) == 4 && sizeof(tcsum_ipaddr_t) == 8, "ipaddr_t");
+static_assert(sizeof(tcsum_seg_t) == 16 && sizeof(tcsum_peso_t) == 24 && sizeof(tcsum_pkt_t) == 16,
+              "descriptors");
+
+namespace {
+
+using tcsum::Geometry;
+
+constexpr int kMaxDev = 16;
+constexpr int kHostStreams = 3;
+
+struct Ctx {
+    std::mutex mu;
+    bool ready = false;
+    int device = -1;
+    hipStream_t stream = nullptr; // legacy (synchronous) calls
+    // pinned, fine-grained staging the kernel reads/writes directly
+    uint8_t *stage = nullptr;
+    size_t stage_cap = 0;
+    void *desc = nullptr;       // one tcsum_seg_t / tcsum_peso_t
+    uint16_t *result = nullptr; // one u16
+    uint8_t *d_stage = nullptr; // device-side addresses of the three above
+    void *d_desc = nullptr;
+    uint16_t *d_result = nullptr;
+    // host-resident batches
+    hipStream_t hs[kHostStreams] = {};
+    uint8_t *d_arena = nullptr;
+    size_t d_arena_cap = 0;
+    tcsum_peso_t *d_descs = nullptr;
+    size_t d_descs_cap = 0;
+    uint16_t *d_out = nullptr;
+    size_t d_out_cap = 0;
+};
+
+Ctx g_ctx[kMaxDev];
+std::mutex g_default_mu;
+int g_default_dev = -1;
+
+[[noreturn]] void die(const char *what, hipError_t e)
+{
+    fprintf(stderr, "tcsum: %s failed: %s -- no CPU fallback, aborting\n", what,
+            hipGetErrorString(e));
+    abort();
+}
+
+bool is_gfx950(int dev)
+{
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, dev) != hipSuccess)
+        return false;
+    return strncmp(p.gcnArchName, "gfx950", 6) == 0;
+}
+
+// Initialise ctx for `dev`; returns a net_err_t-style code.
+int ctx_init(Ctx &c, int dev)
+{
+    if (c.ready)
+        return TCSUM_OK;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || dev < 0 || dev >= count)
+        return TCSUM_ERR_NOT_SUPPORT;
+    if (!is_gfx950(dev))
+        return TCSUM_ERR_NOT_SUPPORT;
+    if (hipSetDevice(dev) != hipSuccess)
+        return TCSUM_ERR_SYS;
+    if (hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess)
+        return TCSUM_ERR_SYS;
+    for (auto &s : c.hs)
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+            return TCSUM_ERR_SYS;
+    if (hipHostMalloc(&c.desc, 64, hipHostMallocCoherent) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&c.result), 64, hipHostMallocCoherent) != hipSuccess)
+        return TCSUM_ERR_MEM;
+    if (hipHostGetDevicePointer(&c.d_desc, c.desc, 0) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void **>(&c.d_result), c.result, 0) != hipSuccess)
+        return TCSUM_ERR_SYS;
+    c.device = dev;
+    c.ready = true;
+    return TCSUM_OK;
+}
+
+int default_device()
+{
+    std::lock_guard<std::mutex> lk(g_default_mu);
+    if (g_default_dev < 0) {
+        const char *s = getenv("TCSUM_DEVICE");
+        g_default_dev = s ? atoi(s) : 0;
+    }
+    return g_default_dev;
+}
+
+// Legacy context: initialised or abort (the three drop-in symbols have no
+// error channel -- SURVEY §8(b)).
+Ctx &legacy_ctx()
+{
+    const int dev = default_device();
+    if (dev < 0 || dev >= kMaxDev)
+        die("TCSUM_DEVICE", hipErrorInvalidDevice);
+    Ctx &c = g_ctx[dev];
+    if (!c.ready) {
+        std::lock_guard<std::mutex> lk(c.mu);
+        const int rc = ctx_init(c, dev);
+        if (rc != TCSUM_OK)
+            die(rc == TCSUM_ERR_NOT_SUPPORT ? "finding a gfx950 device" : "device init",
+                rc == TCSUM_ERR_NOT_SUPPORT ? hipErrorNoDevice : hipErrorOutOfMemory);
+    }
+    const hipError_t e = hipSetDevice(c.device); // HIP's current device is per thread
+    if (e != hipSuccess)
+        die("hipSetDevice", e);
+    return c;
+}
+
+void ensure_stage(Ctx &c, size_t bytes)
+{
+    bytes += 32; // parity slot + 16-byte tail
+    if (bytes <= c.stage_cap)
+        return;
+    size_t cap = 1 << 16;
+    while (cap < bytes)
+        cap <<= 1;
+    if (c.stage)
+        hipHostFree(c.stage);
+    c.stage = nullptr;
+    c.stage_cap = 0;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&c.stage), cap, hipHostMallocCoherent);
+    if (e != hipSuccess)
+        die("hipHostMalloc(staging)", e);
+    e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c.d_stage), c.stage, 0);
+    if (e != hipSuccess)
+        die("hipHostGetDevicePointer(staging)", e);
+    c.stage_cap = cap;
+}
+
+void run_sync(Ctx &c, hipError_t launched)
+{
+    if (launched != hipSuccess)
+        die("kernel launch", launched);
+    hipError_t e = hipStreamSynchronize(c.stream);
+    if (e != hipSuccess)
+        die("hipStreamSynchronize", e);
+}
+
+// ---- pktbuf cursor, restated from net/src/pktbuf.c:153-170, 446-483 ----
+
+inline tcsum_pktblk_t *blk_next(tcsum_pktblk_t *b)
+{
+    tcsum_node_t *n = b->node.next;
+    return n ? reinterpret_cast<tcsum_pktblk_t *>(n) : nullptr; // node is the first member
+}
+
+inline int curr_blk_remain(const tcsum_pktbuf_t *buf) // pktbuf.c:162-170
+{
+    const tcsum_pktblk_t *b = buf->curr_blk;
+    return b ? (int)(b->data + b->size - buf->blk_offset) : 0;
+}
+
+inline void move_forward(tcsum_pktbuf_t *buf, int size) // pktbuf.c:463-483
+{
+    buf->pos += size;
+    buf->blk_offset += size;
+    tcsum_pktblk_t *cur = buf->curr_blk;
+    if (buf->blk_offset >= cur->data + cur->size) {
+        buf->curr_blk = blk_next(cur);
+        buf->blk_offset = buf->curr_blk ? buf->curr_blk->data : nullptr;
+    }
+}
+
+inline void reset_access(tcsum_pktbuf_t *buf) // pktbuf.c:446-458
+{
+    buf->pos = 0;
+    tcsum_node_t *first = buf->blk_list.first;
+    buf->curr_blk = first ? reinterpret_cast<tcsum_pktblk_t *>(first) : nullptr;
+    buf->blk_offset = buf->curr_blk ? buf->curr_blk->data : nullptr;
+}
+
+void check_ref(const tcsum_pktbuf_t *buf)
+{
+    if (buf->ref == 0) { // pktbuf.c:648 assert
+        fprintf(stderr, "tcsum: pktbuf ref == 0 (assert in pktbuf.c:648), aborting\n");
+        abort();
+    }
+}
+
+// Walk `len` bytes from the cursor the way pktbuf.c:659-668 does, copying
+// them into the staging buffer at `dst` and advancing the cursor.
+void gather(tcsum_pktbuf_t *buf, int len, uint8_t *dst)
+{
+    while (len > 0) {
+        const int blk = curr_blk_remain(buf);
+        const int take = blk > len ? len : blk;
+        if (!buf->curr_blk)
+            break; // inconsistent total_size; the reference would fault here
+        if (take > 0)
+            memcpy(dst, buf->blk_offset, (size_t)take);
+        dst += take;
+        move_forward(buf, take);
+        len -= take;
+    }
+}
+
+} // namespace
+
+// ===================================================================== ABI
+
+extern "C" {
+
+const char *tcsum_version(void) { return "tcsum 0.1 (gfx950, hand-written HIP)"; }
+
+int tcsum_device_count(void)
+{
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess)
+        return 0;
+    int ok = 0;
+    for (int d = 0; d < count; ++d)
+        ok += is_gfx950(d) ? 1 : 0;
+    return ok;
+}
+
+void tcsum_pick_geometry(uint64_t mean_len, int *lanes, int *loads)
+{
+    const Geometry g = tcsum::pick_geometry(mean_len);
+    if (lanes)
+        *lanes = g.lanes;
+    if (loads)
+        *loads = g.loads;
+}
+
+int tcsum_plat_init(int device)
+{
+    if (device < 0 || device >= kMaxDev)
+        return TCSUM_ERR_PARAM;
+    {
+        std::lock_guard<std::mutex> lk(g_default_mu);
+        g_default_dev = device;
+    }
+    Ctx &c = g_ctx[device];
+    std::lock_guard<std::mutex> lk(c.mu);
+    return ctx_init(c, device);
+}
+
+void *tcsum_host_alloc(size_t bytes)
+{
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
+        return nullptr;
+    return p;
+}
+
+void tcsum_host_free(void *p)
+{
+    if (p)
+        hipHostFree(p);
+}
+
+static uint64_t mean_of(uint64_t total, uint32_t n) { return total && n ? total / n : 1500; }
+
+int tcsum_batch_segments(const void *arena, const tcsum_seg_t *segs, uint32_t n, uint16_t *out,
+                         int complement, uint64_t total_bytes_hint, void *stream)
+{
+    if (n == 0)
+        return TCSUM_OK;
+    if (!arena || !segs || !out)
+        return TCSUM_ERR_PARAM;
+    const hipError_t e = tcsum::launch_segments(tcsum::MODE_SEG, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
+                                                arena, segs, n, out, complement ? 1u : 0u,
+                                                static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
+}
+
+int tcsum_batch_peso(const void *arena, const tcsum_peso_t *segs, uint32_t n, uint16_t *out,
+                     uint64_t total_bytes_hint, void *stream)
+{
+    if (n == 0)
+        return TCSUM_OK;
+    if (!arena || !segs || !out)
+        return TCSUM_ERR_PARAM;
+    const hipError_t e = tcsum::launch_segments(tcsum::MODE_PESO, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
+                                                arena, segs, n, out, 0u, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
+}
+
+int tcsum_batch_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
+                     uint8_t *flags, uint64_t total_bytes_hint, void *stream)
+{
+    if (n == 0)
+        return TCSUM_OK;
+    if (!arena || !pkts || !out)
+        return TCSUM_ERR_PARAM;
+    const hipError_t e = tcsum::launch_ipv4(tcsum::pick_geometry(mean_of(total_bytes_hint, n)), arena,
+                                            pkts, n, out, flags, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
+}
+
+int tcsum_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, uint64_t seed, void *stream)
+{
+    if (!arena || (reinterpret_cast<uintptr_t>(arena) & 15u) || (byte_base & 15u))
+        return TCSUM_ERR_PARAM;
+    return tcsum::launch_synth_fill(arena, nbytes, byte_base, seed, static_cast<hipStream_t>(stream)) ==
+                   hipSuccess
+               ? TCSUM_OK
+               : TCSUM_ERR_SYS;
+}
+
+int tcsum_synth_ipv4(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t seed, void *stream)
+{
+    if (n && (!arena || !pkts))
+        return TCSUM_ERR_PARAM;
+    return tcsum::launch_synth_ipv4(arena, pkts, n, seed, static_cast<hipStream_t>(stream)) == hipSuccess
+               ? TCSUM_OK
+               : TCSUM_ERR_SYS;
+}
+
+// ------------------------------------------------------------ host batches
+
+int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_bytes,
+                          const tcsum_peso_t *segs, uint32_t n, uint16_t *out)
+{
+    if (n == 0)
+        return TCSUM_OK;
+    if (!host_arena || !segs || !out || device < 0 || device >= kMaxDev)
+        return TCSUM_ERR_PARAM;
+    Ctx &c = g_ctx[device];
+    std::lock_guard<std::mutex> lk(c.mu);
+    int rc = ctx_init(c, device);
+    if (rc != TCSUM_OK)
+        return rc;
+    if (hipSetDevice(device) != hipSuccess)
+        return TCSUM_ERR_SYS;
+    for (uint32_t i = 0; i < n; ++i)
+        if (segs[i].offset + segs[i].len > arena_bytes)
+            return TCSUM_ERR_PARAM;
+
+    // device buffers (grow-only; the arena keeps a 16-byte tail so the last
+    // aligned chunk is in bounds)
+    const size_t need_arena = ((arena_bytes + 15) & ~size_t(15)) + 16;
+    if (need_arena > c.d_arena_cap) {
+        if (c.d_arena)
+            hipFree(c.d_arena);
+        c.d_arena_cap = 0;
+        if (hipMalloc(reinterpret_cast<void **>(&c.d_arena), need_arena) != hipSuccess)
+            return TCSUM_ERR_MEM;
+        c.d_arena_cap = need_arena;
+    }
+    if (n > c.d_descs_cap) {
+        if (c.d_descs)
+            hipFree(c.d_descs);
+        if (c.d_out)
+            hipFree(c.d_out);
+        c.d_descs_cap = c.d_out_cap = 0;
+        if (hipMalloc(reinterpret_cast<void **>(&c.d_descs), sizeof(tcsum_peso_t) * n) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&c.d_out), sizeof(uint16_t) * n) != hipSuccess)
+            return TCSUM_ERR_MEM;
+        c.d_descs_cap = c.d_out_cap = n;
+    }
+
+    // chunks of ~32 MiB of packet bytes, round-robin over the streams:
+    // H2D(bytes, descriptors) -> kernel -> D2H(results)
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        total += segs[i].len;
+    const uint64_t target = 32ull << 20;
+    uint32_t per = (uint32_t)(total ? ((uint64_t)n * target + total - 1) / total : n);
+    if (per == 0)
+        per = 1;
+    const uint8_t *h = static_cast<const uint8_t *>(host_arena);
+    int k = 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += per, ++k) {
+        const uint32_t i1 = i0 + per < n ? i0 + per : n;
+        uint64_t lo = UINT64_MAX, hi = 0, bytes = 0;
+        for (uint32_t i = i0; i < i1; ++i) {
+            if (segs[i].len == 0)
+                continue;
+            lo = segs[i].offset < lo ? segs[i].offset : lo;
+            const uint64_t end = segs[i].offset + segs[i].len;
+            hi = end > hi ? end : hi;
+            bytes += segs[i].len;
+        }
+        hipStream_t s = c.hs[k % kHostStreams];
+        if (hi > lo) {
+            lo &= ~uint64_t(15);
+            hi = (hi + 15) & ~uint64_t(15);
+            if (hi > arena_bytes)
+                hi = arena_bytes;
+            if (hipMemcpyAsync(c.d_arena + lo, h + lo, hi - lo, hipMemcpyHostToDevice, s) != hipSuccess)
+                return TCSUM_ERR_SYS;
+        }
+        if (hipMemcpyAsync(c.d_descs + i0, segs + i0, sizeof(tcsum_peso_t) * (i1 - i0),
+                           hipMemcpyHostToDevice, s) != hipSuccess)
+            return TCSUM_ERR_SYS;
+        const hipError_t e = tcsum::launch_segments(tcsum::MODE_PESO, tcsum::pick_geometry(mean_of(bytes, i1 - i0)),
+                                                    c.d_arena, c.d_descs + i0, i1 - i0, c.d_out + i0, 0u, s);
+        if (e != hipSuccess)
+            return TCSUM_ERR_SYS;
+        if (hipMemcpyAsync(out + i0, c.d_out + i0, sizeof(uint16_t) * (i1 - i0), hipMemcpyDeviceToHost, s) !=
+            hipSuccess)
+            return TCSUM_ERR_SYS;
+    }
+    for (auto &s : c.hs)
+        if (hipStreamSynchronize(s) != hipSuccess)
+            return TCSUM_ERR_SYS;
+    return TCSUM_OK;
+}
+
+// ================================================== drop-in legacy symbols
+
+// net/src/tools.c:24-54
+uint16_t checksum16(int offset, void *buf, uint16_t len, uint32_t pre_sum, int complement)
+{
+    Ctx &c = legacy_ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    ensure_stage(c, len);
+    // place the bytes so that address parity == logical parity: the kernel
+    // then has the exact u32 word sum for the reference's u32 wrap
+    const uint32_t par = (uint32_t)offset & 1u;
+    uint8_t *dst = c.stage + par;
+    if (len)
+        memcpy(dst, buf, len);
+    tcsum_seg_t *d = static_cast<tcsum_seg_t *>(c.desc);
+    d->offset = par;
+    d->len = len;
+    d->pre_sum = pre_sum;
+    const hipError_t e = tcsum::launch_segments(tcsum::MODE_EXACT, Geometry{64, 8, false}, c.d_stage, c.d_desc,
+                                                1, c.d_result, (complement ? 1u : 0u) | (par << 1), c.stream);
+    run_sync(c, e);
+    return *c.result;
+}
+
+// net/src/pktbuf.c:646-670
+uint16_t pktbuf_checksum16(tcsum_pktbuf_t *buf, int len, int pre_sum, int complement)
+{
+    check_ref(buf);
+    const int remain = buf->total_size - buf->pos; // total_blk_remain, pktbuf.c:153-156
+    if (remain < len)
+        return 0; // pktbuf.c:650-655
+    if (len < 0)
+        len = 0; // loop not entered: the kernel returns (uint16_t)pre_sum, complemented or not
+    Ctx &c = legacy_ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    ensure_stage(c, (size_t)len);
+    gather(buf, len, c.stage);
+    tcsum_seg_t *d = static_cast<tcsum_seg_t *>(c.desc);
+    d->offset = 0;
+    d->len = (uint32_t)len;
+    d->pre_sum = (uint32_t)pre_sum;
+    const hipError_t e = tcsum::launch_segments(tcsum::MODE_SEG, tcsum::pick_geometry((uint64_t)len), c.d_stage,
+                                                c.d_desc, 1, c.d_result, complement ? 1u : 0u, c.stream);
+    run_sync(c, e);
+    return *c.result;
+}
+
+// net/src/tools.c:56-75
+uint16_t checksum_peso(tcsum_pktbuf_t *buf, const tcsum_ipaddr_t *dest, const tcsum_ipaddr_t *src,
+                       uint8_t protocol)
+{
+    check_ref(buf);
+    reset_access(buf); // tools.c:72
+    const int total = buf->total_size;
+    Ctx &c = legacy_ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    ensure_stage(c, total > 0 ? (size_t)total : 0);
+    if (total > 0)
+        gather(buf, total, c.stage); // leaves the cursor at the end, like tools.c:73
+    tcsum_peso_t *d = static_cast<tcsum_peso_t *>(c.desc);
+    d->offset = 0;
+    d->len = total > 0 ? (uint32_t)total : 0;
+    memcpy(d->src, src->addr, 4);
+    memcpy(d->dst, dest->addr, 4);
+    d->protocol = protocol;
+    d->rsv[0] = d->rsv[1] = d->rsv[2] = 0;
+    const hipError_t e = tcsum::launch_segments(tcsum::MODE_PESO, tcsum::pick_geometry((uint64_t)d->len),
+                                                c.d_stage, c.d_desc, 1, c.d_result, 0u, c.stream);
+    run_sync(c, e);
+    return *c.result;
+}
+
+} // extern "C"

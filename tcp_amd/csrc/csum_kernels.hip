@@ -1,0 +1,569 @@
+// csum_kernels.hip -- gfx950 kernels for the Internet checksum (RFC 1071 sum as
+// the wj9806/tcp stack computes it: net/src/tools.c:24-75, pktbuf.c:646-670).
+//
+// Arithmetic.  The reference adds the range as little-endian u16 words into a
+// u32 and folds with end-around carry.  For a range of bytes b[0..n) whose
+// byte parity starts at 0 that is
+//     S = pre + sum_i b[i] * 256^(i & 1),   fold(S) = S == 0 ? 0 : 1 + (S-1) % 0xFFFF.
+// 65536 == 1 (mod 0xFFFF), so any regrouping of the words gives the same
+// fold, and folding never turns a non-zero sum into zero.  The kernels
+//   * read the range as 16-byte-aligned chunks (global_load_dwordx4; an
+//     aligned chunk never crosses a page, so touching a chunk's bytes outside
+//     the range is safe and they are masked to zero),
+//   * add each dword's two halves with one v_dot2_u32_u16 (d . {1,1} + acc),
+//   * keep a u32 per lane, folded once per pass (never exact-overflows),
+//   * reduce the G lanes that share a packet with DPP-free xor shuffles,
+//   * and let the packet's first lane fold, rotate and complement.
+// Address parity vs logical parity: the loads weight a byte by the parity of
+// its ADDRESS; when the range starts at an odd address every byte is in the
+// other half of its word, and the folded sum is the 8-bit rotation of the
+// logical one (x*256 mod 0xFFFF), so one rotate fixes it.
+//
+// Lane mapping.  G lanes (4..64) share one packet and each issues U 16-byte
+// loads per pass before adding anything, so a wave keeps 64*U*16 bytes in
+// flight (8 KiB at U=8).  64/G packets ride in one wave; 4 waves per 256-thread
+// workgroup; no LDS and no barriers -- the reduction stays inside a wave.
+#include "csum_launch.h"
+
+#include <stdlib.h>
+
+namespace tcsum {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// a.lo + a.hi + acc in one VALU op (v_dot2_u32_u16 with {1,1}).
+__device__ __forceinline__ uint32_t add_halves(uint32_t acc, uint32_t d)
+{
+    const u16x2 one = {1, 1};
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, d), one, acc, false);
+}
+
+__device__ __forceinline__ uint32_t chunk_sum(uint32_t acc, u32x4 v)
+{
+    acc = add_halves(acc, v.x);
+    acc = add_halves(acc, v.y);
+    acc = add_halves(acc, v.z);
+    return add_halves(acc, v.w);
+}
+
+// acc + d.lo * w.lo + d.hi * w.hi.  The operands are taken by value: clang
+// (ROCm 7.2) miscompiles __builtin_bit_cast applied directly to an
+// ext_vector element (v.y reads v.x), so never bit_cast `v.y` in place.
+__device__ __forceinline__ uint32_t dot_halves(uint32_t acc, uint32_t d, uint32_t w)
+{
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, d), __builtin_bit_cast(u16x2, w), acc, false);
+}
+
+// acc + w.lo * (sum of the chunk's low halves) + w.hi * (high halves), w in
+// {0x00010001, 0}: adds the chunk or nothing, without a branch.
+__device__ __forceinline__ uint32_t chunk_sum_w(uint32_t acc, u32x4 v, uint32_t w)
+{
+    acc = dot_halves(acc, v.x, w);
+    acc = dot_halves(acc, v.y, w);
+    acc = dot_halves(acc, v.z, w);
+    return dot_halves(acc, v.w, w);
+}
+
+// Keep only bytes [lo, hi) of a chunk (positions 0..16).
+__device__ __forceinline__ u32x4 mask_chunk(u32x4 v, int lo, int hi);
+
+// Bytes [a, b) of a dword (0 <= a, b <= 4); empty when b <= a.
+__device__ __forceinline__ uint32_t byte_mask(int a, int b)
+{
+    const uint64_t hi = (1ull << (8 * b)) - 1ull;
+    const uint64_t lo = (1ull << (8 * a)) - 1ull;
+    return (uint32_t)(hi & ~lo);
+}
+
+__device__ __forceinline__ int clamp4(int x) { return x < 0 ? 0 : (x > 4 ? 4 : x); }
+
+__device__ __forceinline__ u32x4 mask_chunk(u32x4 v, int lo, int hi)
+{
+    v.x &= byte_mask(clamp4(lo), clamp4(hi));
+    v.y &= byte_mask(clamp4(lo - 4), clamp4(hi - 4));
+    v.z &= byte_mask(clamp4(lo - 8), clamp4(hi - 8));
+    v.w &= byte_mask(clamp4(lo - 12), clamp4(hi - 12));
+    return v;
+}
+
+// Sum of the chunk's bytes [lo, hi) (positions 0..16 inside the chunk).
+__device__ __forceinline__ uint32_t chunk_sum_masked(uint32_t acc, u32x4 v, int lo, int hi)
+{
+    acc = add_halves(acc, v.x & byte_mask(clamp4(lo), clamp4(hi)));
+    acc = add_halves(acc, v.y & byte_mask(clamp4(lo - 4), clamp4(hi - 4)));
+    acc = add_halves(acc, v.z & byte_mask(clamp4(lo - 8), clamp4(hi - 8)));
+    return add_halves(acc, v.w & byte_mask(clamp4(lo - 12), clamp4(hi - 12)));
+}
+
+// One end-around step: keeps x == 0 iff input == 0, x mod 0xFFFF, x <= 0x1FFFE.
+__device__ __forceinline__ uint32_t fold_step(uint32_t x) { return (x & 0xFFFFu) + (x >> 16); }
+
+// tools.c:47-51 closed form.
+__device__ __forceinline__ uint32_t fold16(uint32_t x)
+{
+    x = fold_step(x);
+    x = fold_step(x);
+    return fold_step(x);
+}
+
+__device__ __forceinline__ uint32_t rot8(uint32_t x) { return ((x & 0xFFu) << 8) | (x >> 8); }
+
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
+
+template <bool NT>
+__device__ __forceinline__ u32x4 load16(const u32x4 *p)
+{
+    if constexpr (NT)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t group_sum(uint32_t x)
+{
+#pragma unroll
+    for (int m = G / 2; m >= 1; m >>= 1)
+        x += __shfl_xor(x, m, 64);
+    return x;
+}
+
+// ---------------------------------------------------------------- segments
+//
+// One descriptor per range.  MODE_SEG: pktbuf_checksum16 (u16 pre_sum);
+// MODE_EXACT: checksum16 (u32 pre_sum, u32 wrap, len <= 65535);
+// MODE_PESO: checksum_peso with the pseudo-header built here (tools.c:58-70).
+template <int G, int U, int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_segments(const uint8_t *__restrict__ arena,
+                                                  const void *__restrict__ descs, uint32_t n,
+                                                  uint16_t *__restrict__ out, uint32_t aux)
+{
+    static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G");
+    const uint32_t gl = threadIdx.x & (G - 1);
+    const uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / G;
+    const bool live = seg < n;
+
+    uint64_t off = 0;
+    uint32_t len = 0, pre = 0, src = 0, dst = 0, proto = 0;
+    if (live) {
+        if constexpr (MODE == MODE_PESO) {
+            const tcsum_peso_t *d = static_cast<const tcsum_peso_t *>(descs) + seg;
+            off = d->offset;
+            len = d->len;
+            src = *reinterpret_cast<const uint32_t *>(d->src);
+            dst = *reinterpret_cast<const uint32_t *>(d->dst);
+            proto = d->protocol;
+        } else {
+            const tcsum_seg_t *d = static_cast<const tcsum_seg_t *>(descs) + seg;
+            off = d->offset;
+            len = d->len;
+            pre = d->pre_sum;
+        }
+    }
+
+    // Keep the pointer derived from the kernel argument so loads stay
+    // global_load (not flat_load, which would also count in lgkmcnt).
+    const uint8_t *p = arena + off;
+    const uintptr_t start = reinterpret_cast<uintptr_t>(p);
+    const uint32_t s0 = (uint32_t)(start & 15u);
+    const u32x4 *base = reinterpret_cast<const u32x4 *>(p - s0);
+    const uint64_t e = (uint64_t)len + s0; // range end, in bytes from base
+    const uint32_t nch = len ? (uint32_t)((e + 15) >> 4) : 0u;
+
+    uint32_t acc = 0;
+    for (uint32_t b0 = 0; b0 < nch; b0 += G * U) {
+        // Unconditional loads: a lane past the end re-reads the range's last
+        // chunk (same lines as a live lane -> merged) and adds it with weight 0.
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t idx = b0 + u * G + gl;
+            v[u] = load16<NT>(base + (idx < nch ? idx : nch - 1));
+        }
+        uint32_t part = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t idx = b0 + u * G + gl;
+            const bool valid = idx < nch;
+            const uint64_t c = 16ull * idx;
+            if (valid && (idx == 0 || c + 16 > e)) { // first / last chunk: rare
+                const int lo = idx == 0 ? (int)s0 : 0;
+                const int hi = (int)(e - c < 16 ? e - c : 16);
+                v[u] = mask_chunk(v[u], lo, hi);
+            }
+            part = chunk_sum_w(part, v[u], valid ? 0x00010001u : 0u);
+        }
+        acc = MODE == MODE_EXACT ? acc + part : fold_step(acc + part);
+    }
+    acc = group_sum<G>(acc);
+
+    if (live && gl == 0) {
+        uint32_t r;
+        if constexpr (MODE == MODE_EXACT) {
+            // tools.c:27-53: u32 accumulator from pre_sum; acc is the exact
+            // word sum (< 2^31 for len <= 65535).  The host stages the bytes
+            // so address parity == logical parity (aux bit 1).
+            uint32_t s;
+            if (((start ^ (aux >> 1)) & 1u) == 0) {
+                s = pre + acc;
+            } else { // not reached from the C ABI; mod-0xFFFF result
+                uint32_t f = rot8(fold16(acc));
+                s = fold_step(f + fold16(pre));
+            }
+            s = fold16(s);
+            r = (aux & 1u) ? (~s & 0xFFFFu) : s;
+        } else {
+            uint32_t f = fold16(acc);
+            if (start & 1u)
+                f = rot8(f);
+            if constexpr (MODE == MODE_SEG) {
+                uint32_t t = fold_step(f + (pre & 0xFFFFu)); // pktbuf.c:657
+                r = (aux & 1u) ? (~t & 0xFFFFu) : t;
+            } else {
+                // tools.c:58-70: src, dst, {0, proto}, htons((uint16_t)len)
+                uint32_t p = add_halves(0u, src);
+                p = add_halves(p, dst);
+                p += proto << 8;
+                p += bswap16(len & 0xFFFFu);
+                uint32_t t = fold_step(f + fold16(p));
+                r = ~t & 0xFFFFu; // pktbuf_checksum16(..., 1), tools.c:73
+            }
+        }
+        out[seg] = (uint16_t)r;
+    }
+}
+
+// ---------------------------------------------------------------- IPv4
+//
+// Header and L4 checksum of a captured IPv4 packet in one pass over its bytes
+// (ipv4.c:243 / tcp_in.c:80 / udp.c:410 / icmpv4.c:36).  The 20 fixed header
+// bytes are read as two or three aligned chunks and realigned with
+// v_alignbyte; the data pass accumulates [0, hl) and [hl, end) separately.
+__device__ __forceinline__ void pick6(uint32_t q, const uint32_t w[12], uint32_t x[6])
+{
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        x[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
+}
+
+template <int G, int U, bool NT>
+__global__ __launch_bounds__(256) void k_ipv4(const uint8_t *__restrict__ arena,
+                                              const tcsum_pkt_t *__restrict__ pkts, uint32_t n,
+                                              uint32_t *__restrict__ out,
+                                              uint8_t *__restrict__ flags_out)
+{
+    const uint32_t gl = threadIdx.x & (G - 1);
+    const uint32_t pk = (blockIdx.x * 256u + threadIdx.x) / G;
+    const bool live = pk < n;
+
+    uint64_t off = 0;
+    uint32_t frame = 0;
+    if (live) {
+        off = pkts[pk].offset;
+        frame = pkts[pk].len;
+    }
+    const bool big_enough = frame >= 20;
+    const uint8_t *pp = arena + off;
+    const uintptr_t start = reinterpret_cast<uintptr_t>(pp);
+    const uint32_t s0 = (uint32_t)(start & 15u);
+    const u32x4 *base = reinterpret_cast<const u32x4 *>(pp - s0);
+
+    // fixed header: bytes [s0, s0 + 20) of base[0..2]
+    u32x4 h0 = u32x4(0u), h1 = u32x4(0u), h2 = u32x4(0u);
+    if (big_enough) {
+        h0 = load16<false>(base);
+        h1 = load16<false>(base + 1);
+        if (s0 > 12)
+            h2 = load16<false>(base + 2);
+    }
+
+    const uint64_t e_frame = big_enough ? (uint64_t)frame + s0 : 0;
+    const uint32_t nch = (uint32_t)((e_frame + 15) >> 4);
+
+    // Issue the first pass of data loads before the header is consumed, so the
+    // header's latency overlaps them (vmcnt counts in issue order).
+    u32x4 v[U];
+    if (nch) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t idx = u * G + gl;
+            v[u] = load16<NT>(base + (idx < nch ? idx : nch - 1));
+        }
+    }
+
+    uint32_t hd[5];
+    {
+        const uint32_t w[12] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w, h2.x, h2.y, h2.z, h2.w};
+        uint32_t x[6];
+        pick6(s0 >> 2, w, x);
+        const uint32_t r = s0 & 3u;
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            hd[k] = __builtin_amdgcn_alignbyte(x[k + 1], x[k], r);
+    }
+    const uint32_t b0h = hd[0] & 0xFFu;
+    const uint32_t version = b0h >> 4;
+    const uint32_t ihl4 = (b0h & 0xFu) << 2;
+    const uint32_t tl = (((hd[0] >> 16) & 0xFFu) << 8) | (hd[0] >> 24);
+    const uint32_t proto = (hd[2] >> 8) & 0xFFu;
+    uint32_t fl = 0;
+    if (version != 4)
+        fl |= TCSUM_PKT_BAD_VERSION;
+    if (ihl4 < 20 || ihl4 > frame)
+        fl |= TCSUM_PKT_BAD_HDRLEN;
+    if (tl < 20 || tl > frame || tl < ihl4)
+        fl |= TCSUM_PKT_BAD_TOTLEN;
+    uint32_t hl = ihl4 < 20 ? 20u : ihl4;
+    hl = hl > frame ? frame : hl;
+    uint32_t end = tl < hl ? hl : tl;
+    end = end > frame ? frame : end;
+    // range bounds in bytes from base
+    const int64_t h_end = (int64_t)hl + s0;
+    const int64_t l_end = (int64_t)end + s0;
+
+    uint32_t acc_h = 0, acc_l = 0;
+    for (uint32_t b0 = 0; b0 < nch;) {
+        uint32_t ph = 0, pl = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t idx = b0 + u * G + gl;
+            const bool valid = idx < nch;
+            const int64_t c = 16ll * idx;
+            const bool inner = valid && c >= h_end && c + 16 <= l_end;
+            if (valid && !inner) { // header chunks and the last chunk: rare
+                // header bytes [s0, h_end), L4 bytes [h_end, l_end), chunk-relative
+                const int64_t hlo = (int64_t)s0 - c, hhi = h_end - c;
+                const int64_t llo = h_end - c, lhi = l_end - c;
+                const int a0 = (int)(hlo < 0 ? 0 : (hlo > 16 ? 16 : hlo));
+                const int a1 = (int)(hhi < 0 ? 0 : (hhi > 16 ? 16 : hhi));
+                const int c0 = (int)(llo < 0 ? 0 : (llo > 16 ? 16 : llo));
+                const int c1 = (int)(lhi < 0 ? 0 : (lhi > 16 ? 16 : lhi));
+                ph = chunk_sum_masked(ph, v[u], a0, a1);
+                pl = chunk_sum_masked(pl, v[u], c0, c1);
+            }
+            pl = chunk_sum_w(pl, v[u], inner ? 0x00010001u : 0u);
+        }
+        acc_h += ph; // header <= 60 bytes: no overflow
+        acc_l = fold_step(acc_l + pl);
+        b0 += G * U;
+        if (b0 >= nch)
+            break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t idx = b0 + u * G + gl;
+            v[u] = load16<NT>(base + (idx < nch ? idx : nch - 1));
+        }
+    }
+    acc_h = group_sum<G>(acc_h);
+    acc_l = group_sum<G>(acc_l);
+
+    if (live && gl == 0) {
+        uint32_t ip = 0, l4 = 0;
+        if (!big_enough) {
+            fl = TCSUM_PKT_SHORT;
+        } else {
+            const bool odd = start & 1u;
+            uint32_t fh = fold16(acc_h);
+            uint32_t fl4 = fold16(acc_l);
+            if (odd) {
+                fh = rot8(fh);
+                fl4 = rot8(fl4);
+            }
+            ip = ~fh & 0xFFFFu;
+            if (proto == 6 || proto == 17) {
+                uint32_t p = add_halves(0u, hd[3]); // src, packet bytes 12..15
+                p = add_halves(p, hd[4]);           // dst, packet bytes 16..19
+                p += proto << 8;
+                p += bswap16((end - hl) & 0xFFFFu);
+                l4 = ~fold_step(fl4 + fold16(p)) & 0xFFFFu;
+            } else if (proto == 1) {
+                l4 = ~fl4 & 0xFFFFu;
+            } else {
+                fl |= TCSUM_PKT_PROTO_OTHER;
+            }
+        }
+        out[pk] = ip | (l4 << 16);
+        if (flags_out)
+            flags_out[pk] = (uint8_t)fl;
+    }
+}
+
+// ---------------------------------------------------------------- synthetic
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_synth_fill(uint8_t *__restrict__ arena, uint64_t nbytes,
+                                                    uint64_t word_base, uint64_t seed)
+{
+    const uint64_t units = (nbytes + 15) / 16;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < units; i += (uint64_t)gridDim.x * 256ull) {
+        const uint64_t w0 = splitmix64(seed + word_base + 2 * i);
+        const uint64_t w1 = splitmix64(seed + word_base + 2 * i + 1);
+        if (16 * i + 16 <= nbytes) {
+            uint64_t *p = reinterpret_cast<uint64_t *>(arena + 16 * i);
+            p[0] = w0;
+            p[1] = w1;
+        } else {
+            for (uint64_t b = 16 * i; b < nbytes; ++b)
+                arena[b] = (uint8_t)((b - 16 * i < 8 ? w0 : w1) >> (8 * (b & 7)));
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_synth_ipv4(uint8_t *__restrict__ arena,
+                                                    const tcsum_pkt_t *__restrict__ pkts,
+                                                    uint32_t n, uint64_t seed)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t len = pkts[i].len;
+    if (len < 20)
+        return;
+    uint8_t *p = arena + pkts[i].offset;
+    const uint64_t h = splitmix64(seed ^ (0x1000000ull + i));
+    const uint64_t a = splitmix64(h);
+    const uint32_t tl = len > 0xFFFFu ? 0xFFFFu : len;
+    p[0] = 0x45;
+    p[1] = 0;
+    p[2] = (uint8_t)(tl >> 8);
+    p[3] = (uint8_t)tl;
+    p[4] = (uint8_t)(h >> 8);
+    p[5] = (uint8_t)h;
+    p[6] = 0x40;
+    p[7] = 0;
+    p[8] = 64;
+    p[9] = (h >> 20) & 1u ? 17 : 6;
+    p[10] = 0;
+    p[11] = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        p[12 + k] = (uint8_t)(a >> (8 * k));
+}
+
+// ---------------------------------------------------------------- dispatch
+
+Geometry pick_geometry(uint64_t mean_len)
+{
+    Geometry g{16, 8, true};
+    const uint64_t chunks = mean_len / 16 + 1;
+    // enough lanes that one pass of U=8 loads covers a typical packet,
+    // capped at one packet per wave
+    int lanes = 4;
+    while (lanes < 64 && (uint64_t)lanes * 8 < chunks)
+        lanes *= 2;
+    g.lanes = lanes;
+    g.loads = 8;
+    if (const char *s = getenv("TCSUM_G"))
+        g.lanes = atoi(s);
+    if (const char *s = getenv("TCSUM_U"))
+        g.loads = atoi(s);
+    if (const char *s = getenv("TCSUM_NT"))
+        g.nt = atoi(s) != 0;
+    return g;
+}
+
+template <int MODE, bool NT>
+static hipError_t seg_u(int G, int U, dim3 grid, const void *arena, const void *descs, uint32_t n,
+                        uint16_t *out, uint32_t aux, hipStream_t s)
+{
+#define TCSUM_SEG(GG, UU)                                                                            \
+    if (G == GG && U == UU) {                                                                      \
+        hipLaunchKernelGGL((k_segments<GG, UU, MODE, NT>), grid, dim3(256), 0, s,                   \
+                           static_cast<const uint8_t *>(arena), descs, n, out, aux);               \
+        return hipGetLastError();                                                                  \
+    }
+#define TCSUM_SEG_U(GG) TCSUM_SEG(GG, 4) TCSUM_SEG(GG, 8) TCSUM_SEG(GG, 16)
+    TCSUM_SEG_U(4)
+    TCSUM_SEG_U(8)
+    TCSUM_SEG_U(16)
+    TCSUM_SEG_U(32)
+    TCSUM_SEG_U(64)
+#undef TCSUM_SEG_U
+#undef TCSUM_SEG
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void *descs, uint32_t n,
+                           uint16_t *out, uint32_t aux, hipStream_t stream)
+{
+    if (n == 0)
+        return hipSuccess;
+    const uint64_t per_block = 256u / (uint32_t)g.lanes;
+    const dim3 grid((uint32_t)((n + per_block - 1) / per_block));
+    if (mode == MODE_EXACT) {
+        hipLaunchKernelGGL((k_segments<64, 8, MODE_EXACT, false>), dim3((n + 3) / 4), dim3(256), 0,
+                           stream, static_cast<const uint8_t *>(arena), descs, n, out, aux);
+        return hipGetLastError();
+    }
+    if (mode == MODE_SEG)
+        return g.nt ? seg_u<MODE_SEG, true>(g.lanes, g.loads, grid, arena, descs, n, out, aux, stream)
+                    : seg_u<MODE_SEG, false>(g.lanes, g.loads, grid, arena, descs, n, out, aux, stream);
+    return g.nt ? seg_u<MODE_PESO, true>(g.lanes, g.loads, grid, arena, descs, n, out, aux, stream)
+                : seg_u<MODE_PESO, false>(g.lanes, g.loads, grid, arena, descs, n, out, aux, stream);
+}
+
+template <bool NT>
+static hipError_t ipv4_u(int G, int U, dim3 grid, const void *arena, const tcsum_pkt_t *pkts,
+                         uint32_t n, uint32_t *out, uint8_t *flags, hipStream_t s)
+{
+#define TCSUM_IP(GG, UU)                                                                             \
+    if (G == GG && U == UU) {                                                                      \
+        hipLaunchKernelGGL((k_ipv4<GG, UU, NT>), grid, dim3(256), 0, s,                             \
+                           static_cast<const uint8_t *>(arena), pkts, n, out, flags);              \
+        return hipGetLastError();                                                                  \
+    }
+#define TCSUM_IP_U(GG) TCSUM_IP(GG, 4) TCSUM_IP(GG, 8) TCSUM_IP(GG, 16)
+    TCSUM_IP_U(16)
+    TCSUM_IP_U(32)
+    TCSUM_IP_U(64)
+#undef TCSUM_IP_U
+#undef TCSUM_IP
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_ipv4(Geometry g, const void *arena, const tcsum_pkt_t *pkts, uint32_t n,
+                       uint32_t *out, uint8_t *flags, hipStream_t stream)
+{
+    if (n == 0)
+        return hipSuccess;
+    if (g.lanes < 16)
+        g.lanes = 16;
+    const uint64_t per_block = 256u / (uint32_t)g.lanes;
+    const dim3 grid((uint32_t)((n + per_block - 1) / per_block));
+    return g.nt ? ipv4_u<true>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, stream)
+                : ipv4_u<false>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, stream);
+}
+
+hipError_t launch_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, uint64_t seed,
+                             hipStream_t stream)
+{
+    if (nbytes == 0)
+        return hipSuccess;
+    const uint64_t units = (nbytes + 15) / 16;
+    uint64_t blocks = (units + 255) / 256;
+    if (blocks > 65536)
+        blocks = 65536;
+    hipLaunchKernelGGL(k_synth_fill, dim3((uint32_t)blocks), dim3(256), 0, stream,
+                       static_cast<uint8_t *>(arena), nbytes, byte_base / 8, seed);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_ipv4(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t seed,
+                             hipStream_t stream)
+{
+    if (n == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_synth_ipv4, dim3((n + 255) / 256), dim3(256), 0, stream,
+                       static_cast<uint8_t *>(arena), pkts, n, seed);
+    return hipGetLastError();
+}
+
+} // namespace tcsum

@@ -1,0 +1,40 @@
+// csum_launch.h -- internal interface between the C ABI (csum_api.cpp) and the
+// gfx950 kernels (csum_kernels.hip).  Not installed; not part of include/.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tcsum.h"
+
+namespace tcsum {
+
+// What a segment kernel computes per range (see csum_kernels.hip).
+enum Mode : int {
+    MODE_SEG = 0,   // pktbuf_checksum16: u16 pre_sum, optional complement
+    MODE_EXACT = 1, // checksum16: u32 pre_sum with the reference's u32 wrap
+    MODE_PESO = 2,  // checksum_peso: pseudo-header built in-kernel
+};
+
+struct Geometry {
+    int lanes; // G: lanes that share one packet (4..64, power of two)
+    int loads; // U: 16-byte loads in flight per lane per pass
+    bool nt;   // nontemporal (stream-once) loads
+};
+
+Geometry pick_geometry(uint64_t mean_len);
+
+// aux: MODE_SEG -> complement; MODE_EXACT -> complement | (offset parity << 1).
+hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void *descs,
+                           uint32_t n, uint16_t *out, uint32_t aux, hipStream_t stream);
+
+hipError_t launch_ipv4(Geometry g, const void *arena, const tcsum_pkt_t *pkts, uint32_t n,
+                       uint32_t *out, uint8_t *flags, hipStream_t stream);
+
+hipError_t launch_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, uint64_t seed,
+                             hipStream_t stream);
+
+hipError_t launch_synth_ipv4(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t seed,
+                             hipStream_t stream);
+
+} // namespace tcsum

@@ -1,0 +1,143 @@
+"""Python face of the engine: the reference's checksum interface, plus batches.
+
+Same names, argument meanings and results as the reference:
+
+    checksum16(offset, buf, len, pre_sum, complement)   net/src/tools.c:24-54
+    checksum_peso(buf, dest, src, protocol)              net/src/tools.c:56-75
+    pktbuf_checksum16(buf, len, pre_sum, complement)     net/src/pktbuf.c:646-670
+
+each a thin call into libtcsum.so, where the sum runs on the GPU.  The batch
+forms take device (torch CUDA) tensors: a uint8 arena and a descriptor array
+laid out as include/tcsum.h's structs (SEG_DTYPE / PESO_DTYPE / PKT_DTYPE).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .pktbuf import IpAddr, PktBuf
+
+SEG_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("pre_sum", "<u4")])
+PESO_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("src", "u1", 4),
+                       ("dst", "u1", 4), ("protocol", "u1"), ("rsv", "u1", 3)])
+PKT_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("rsv", "<u4")])
+
+PKT_BAD_VERSION, PKT_BAD_HDRLEN, PKT_BAD_TOTLEN, PKT_PROTO_OTHER, PKT_SHORT = 1, 2, 4, 8, 16
+
+
+# ------------------------------------------------------------- drop-in trio
+
+def checksum16(offset: int, buf, length: int, pre_sum: int, complement: int) -> int:
+    """tools.c:24-54 on a host buffer (bytes-like or numpy)."""
+    if isinstance(buf, np.ndarray):
+        a = np.ascontiguousarray(buf.reshape(-1).view(np.uint8))
+        ptr = a.ctypes.data if a.size else None
+        assert length <= a.size
+        return _lib.lib().checksum16(offset, ptr, length, pre_sum & 0xFFFFFFFF, complement)
+    b = bytes(buf)
+    assert length <= len(b)
+    cbuf = ctypes.create_string_buffer(b, max(1, len(b)))
+    return _lib.lib().checksum16(offset, ctypes.addressof(cbuf), length, pre_sum & 0xFFFFFFFF, complement)
+
+
+def pktbuf_checksum16(buf: PktBuf, length: int, pre_sum: int, complement: int) -> int:
+    """pktbuf.c:646-670: from the cursor; advances it by `length`."""
+    return _lib.lib().pktbuf_checksum16(buf.ptr, length, pre_sum, complement)
+
+
+def checksum_peso(buf: PktBuf, dest: IpAddr, src: IpAddr, protocol: int) -> int:
+    """tools.c:56-75: resets the cursor, leaves it at the end."""
+    return _lib.lib().checksum_peso(buf.ptr, ctypes.addressof(dest), ctypes.addressof(src), protocol)
+
+
+# ------------------------------------------------------------------ batches
+
+def _torch():
+    import torch
+    return torch
+
+
+def descs_to_device(descs: np.ndarray, device="cuda"):
+    """Copy a structured descriptor array to the device as raw bytes."""
+    torch = _torch()
+    raw = np.ascontiguousarray(descs).view(np.uint8)
+    return torch.from_numpy(raw.copy()).to(device)
+
+
+def _stream_ptr(stream) -> int | None:
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def batch_segments(arena, segs, n: int, complement: int, total_bytes: int = 0, out=None, stream=None):
+    """out[i] = pktbuf_checksum16 over each tcsum_seg_t (device tensors)."""
+    torch = _torch()
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint16, device=arena.device)
+    rc = _lib.lib().tcsum_batch_segments(arena.data_ptr(), segs.data_ptr(), n, out.data_ptr(),
+                                         complement, total_bytes, _stream_ptr(stream))
+    _lib.check(rc, "tcsum_batch_segments")
+    return out
+
+
+def batch_peso(arena, segs, n: int, total_bytes: int = 0, out=None, stream=None):
+    """out[i] = checksum_peso over each tcsum_peso_t (device tensors)."""
+    torch = _torch()
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint16, device=arena.device)
+    rc = _lib.lib().tcsum_batch_peso(arena.data_ptr(), segs.data_ptr(), n, out.data_ptr(), total_bytes,
+                                     _stream_ptr(stream))
+    _lib.check(rc, "tcsum_batch_peso")
+    return out
+
+
+def batch_ipv4(arena, pkts, n: int, total_bytes: int = 0, out=None, flags=None, want_flags=True, stream=None):
+    """(out, flags): out[i] = ip | l4 << 16 for each tcsum_pkt_t (device tensors)."""
+    torch = _torch()
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint32, device=arena.device)
+    if flags is None and want_flags:
+        flags = torch.empty(n, dtype=torch.uint8, device=arena.device)
+    rc = _lib.lib().tcsum_batch_ipv4(arena.data_ptr(), pkts.data_ptr(), n, out.data_ptr(),
+                                     flags.data_ptr() if flags is not None else None, total_bytes,
+                                     _stream_ptr(stream))
+    _lib.check(rc, "tcsum_batch_ipv4")
+    return out, flags
+
+
+def host_batch_peso(host_arena: np.ndarray, segs: np.ndarray, device: int = 0) -> np.ndarray:
+    """End-to-end: host arena -> H2D -> kernel -> D2H (tcsum_host_batch_peso)."""
+    assert segs.dtype == PESO_DTYPE
+    out = np.zeros(segs.size, np.uint16)
+    rc = _lib.lib().tcsum_host_batch_peso(device, host_arena.ctypes.data, host_arena.nbytes,
+                                          np.ascontiguousarray(segs).ctypes.data, segs.size, out.ctypes.data)
+    _lib.check(rc, "tcsum_host_batch_peso")
+    return out
+
+
+def synth_fill(arena, nbytes: int | None = None, byte_base: int = 0, seed: int = 20240807, stream=None):
+    n = arena.numel() if nbytes is None else nbytes
+    _lib.check(_lib.lib().tcsum_synth_fill(arena.data_ptr(), n, byte_base, seed, _stream_ptr(stream)),
+               "tcsum_synth_fill")
+
+
+def synth_ipv4(arena, pkts, n: int, seed: int = 20240807, stream=None):
+    _lib.check(_lib.lib().tcsum_synth_ipv4(arena.data_ptr(), pkts.data_ptr(), n, seed, _stream_ptr(stream)),
+               "tcsum_synth_ipv4")
+
+
+def pick_geometry(mean_len: int):
+    g, u = ctypes.c_int(), ctypes.c_int()
+    _lib.lib().tcsum_pick_geometry(mean_len, ctypes.byref(g), ctypes.byref(u))
+    return g.value, u.value
+
+
+def device_count() -> int:
+    return _lib.lib().tcsum_device_count()
+
+
+def plat_init(device: int = 0) -> None:
+    _lib.check(_lib.lib().tcsum_plat_init(device), "tcsum_plat_init")

@@ -1,0 +1,113 @@
+"""CPU-side checks of the C ABI: the library builds, loads, and exports exactly
+what include/*.h declares.  No compute call is made here (no GPU)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADERS = ["tcsum.h", "tcsum_legacy.h", "tcsum_synth.h"]
+
+
+@pytest.fixture(scope="module")
+def libpath():
+    from tcp_amd import build
+    return build.build()
+
+
+def declared_functions():
+    names = set()
+    for h in HEADERS:
+        text = open(os.path.join(ROOT, "include", h)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        text = re.sub(r"//[^\n]*", "", text)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b(\w+)\s*\([^;{]*\)\s*;", text, flags=re.M):
+            if not m.group(0).lstrip().startswith(("typedef", "#")):
+                names.add(m.group(1))
+    return names
+
+
+def test_headers_declare_the_drop_in_trio():
+    names = declared_functions()
+    assert {"checksum16", "checksum_peso", "pktbuf_checksum16"} <= names
+    assert {"tcsum_batch_segments", "tcsum_batch_peso", "tcsum_batch_ipv4", "tcsum_host_batch_peso",
+            "tcsum_plat_init", "tcsum_host_alloc", "tcsum_host_free", "tcsum_synth_fill",
+            "tcsum_synth_ipv4"} <= names
+
+
+def test_every_declared_symbol_is_exported(libpath):
+    out = subprocess.run(["nm", "-D", "--defined-only", libpath], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = declared_functions() - exported
+    assert not missing, missing
+
+
+def test_binding_table_matches_headers(libpath):
+    from tcp_amd import _lib
+    assert set(_lib.SIGNATURES) == declared_functions()
+    L = _lib.lib()  # loads libamdhip64 too; no device is touched
+    for name in _lib.SIGNATURES:
+        assert getattr(L, name)
+
+
+def test_descriptor_layouts():
+    from tcp_amd import PESO_DTYPE, PKT_DTYPE, SEG_DTYPE
+    from oracle import pyoracle
+    assert SEG_DTYPE.itemsize == 16 and PESO_DTYPE.itemsize == 24 and PKT_DTYPE.itemsize == 16
+    assert SEG_DTYPE == pyoracle.SEG_DTYPE and PESO_DTYPE == pyoracle.PESO_DTYPE
+    assert PKT_DTYPE == pyoracle.PKT_DTYPE
+    assert PESO_DTYPE.fields["protocol"][1] == 20
+
+
+def test_pktbuf_mirror_layout():
+    """tcsum_legacy.h restates net/net/pktbuf.h:15-41 (LP64)."""
+    from tcp_amd.pktbuf import IpAddr, List, Node, PktBlk, PktBufStruct
+    assert ctypes.sizeof(Node) == 16 and ctypes.sizeof(List) == 24
+    assert PktBlk.size.offset == 16 and PktBlk.data.offset == 24 and PktBlk.payload.offset == 32
+    assert PktBufStruct.blk_list.offset == 8 and PktBufStruct.ref.offset == 32
+    assert PktBufStruct.pos.offset == 56 and PktBufStruct.curr_blk.offset == 64
+    assert PktBufStruct.blk_offset.offset == 72 and ctypes.sizeof(PktBufStruct) == 80
+    assert ctypes.sizeof(IpAddr) == 8
+
+
+def test_pktbuf_cursor_walk_on_host():
+    """The Python chain builder places the cursor the way pktbuf_seek does."""
+    from tcp_amd import PktBuf
+    b = PktBuf([b"abc", b"", b"defgh", b"i" * 200])
+    assert b.s.total_size == 208
+    assert b.cursor() == (0, 0, 0)
+    b.seek(3)
+    assert b.cursor() == (3, 1, 0)  # move_forward steps one block at a boundary
+    b.seek(9)
+    assert b.cursor() == (9, 3, 1)
+    b.seek(2)
+    assert b.cursor() == (2, 0, 2)
+
+
+def test_geometry_choice(libpath):
+    from tcp_amd import pick_geometry
+    assert pick_geometry(1500) == (16, 8)
+    assert pick_geometry(65536) == (64, 8)
+    g, u = pick_geometry(64)
+    assert g == 4
+
+
+def test_device_count_without_gpu(libpath):
+    from tcp_amd import device_count
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    assert device_count() == 0
+
+
+def test_product_never_imports_oracle():
+    """The shipped path must not route through the checker."""
+    for dirpath, _, files in os.walk(os.path.join(ROOT, "tcp_amd")):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h")):
+                text = open(os.path.join(dirpath, f)).read()
+                assert not re.search(r"(from|import)\s+oracle|pyoracle|liboracle|libtcpref|orc_\w+\(", text), f

@@ -1,0 +1,336 @@
+"""Parity of the HIP path with the reference, on an MI355X.
+
+Every call goes through libtcsum.so's C ABI.  Expected values come from
+  * tests/golden/ -- outputs of the reference's own checksum16 /
+    pktbuf_checksum16 / checksum_peso (net/src/tools.c:24-75,
+    net/src/pktbuf.c:646-670) on recorded inputs, and
+  * the CPU oracle (oracle/, pinned to those fixtures) on seeded inputs.
+The bar is bit-exact: these are 16-bit integer results.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import golden_io as G
+
+pytestmark = pytest.mark.gpu
+
+GEOMS_SEG = [(g, u) for g in (4, 8, 16, 32, 64) for u in (4, 8, 16)]
+GEOMS_IP = [(g, u) for g in (16, 32, 64) for u in (4, 8, 16)]
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "gpu tests need an MI355X"
+    return t
+
+
+@pytest.fixture(scope="module")
+def tc(torch):
+    from tcp_amd import build
+    build.build()
+    import tcp_amd
+    tcp_amd.plat_init(0)
+    return tcp_amd
+
+
+@pytest.fixture
+def geometry(monkeypatch):
+    def set_geometry(g, u, nt=1):
+        monkeypatch.setenv("TCSUM_G", str(g))
+        monkeypatch.setenv("TCSUM_U", str(u))
+        monkeypatch.setenv("TCSUM_NT", str(nt))
+    return set_geometry
+
+
+def to_dev(torch, a: np.ndarray, pad: int = 64):
+    t = torch.zeros(a.nbytes + pad, dtype=torch.uint8)
+    t[: a.nbytes] = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1))
+    return t.cuda()
+
+
+def test_native_library_is_loaded(tc):
+    assert tc.checksum16(0, b"\xff\xff", 2, 0, 1) == 0
+    maps = open("/proc/self/maps").read()
+    assert "libtcsum.so" in maps
+
+
+# ------------------------------------------------------------ drop-in trio
+
+def test_kats(tc):
+    k = G.kat_inputs()
+    h, e = k["KAT-1"]
+    assert tc.checksum16(0, h, 20, 0, 1) == e == 0x61B8
+    filled = bytearray(h)
+    filled[10:12] = e.to_bytes(2, "little")
+    assert tc.checksum16(0, bytes(filled), 20, 0, 1) == 0
+    b, e = k["KAT-2"]
+    assert tc.checksum16(0, b, 999, 0, 1) == e
+    buf = tc.PktBuf([b[i: i + 127] for i in range(0, 999, 127)])
+    assert tc.pktbuf_checksum16(buf, 999, 0, 1) == e == 0x8EE9
+    b, e = k["KAT-3"]
+    buf = tc.PktBuf([b[i: i + 127] for i in range(0, 999, 127)])
+    got = tc.checksum_peso(buf, tc.IpAddr.v4([192, 168, 74, 3]), tc.IpAddr.v4([192, 168, 74, 2]), 6)
+    assert got == e == 0x4AD0
+    assert tc.checksum16(0, bytes(4), 4, 0, 1) == 0xFFFF
+    assert tc.checksum16(0, b"\xff\xff", 2, 0, 1) == 0
+
+
+def test_checksum16_golden(tc):
+    pool = G.pool()
+    bad = []
+    for c in G.flat_cases():
+        off, n = int(c["pool_off"]), int(c["len"])
+        got = tc.checksum16(int(c["offset"]), pool[off: off + n], n, int(c["pre_sum"]), int(c["complement"]))
+        if got != int(c["expected"]):
+            bad.append((dict(zip(c.dtype.names, c.tolist())), got))
+    assert not bad, bad[:5]
+
+
+def test_pktbuf_checksum16_golden(tc):
+    """Result AND cursor side effect (pktbuf.c:665) match the reference."""
+    pool = G.pool()
+    cases, blocks = G.pktbuf_cases()
+    for c in cases:
+        buf = tc.PktBuf([p.tobytes() for p in G.case_blocks(c, blocks, pool)])
+        if int(c["seek"]):
+            buf.seek(int(c["seek"]))
+        got = tc.pktbuf_checksum16(buf, int(c["len"]), int(c["pre_sum"]), int(c["complement"]))
+        assert got == int(c["expected"]), c
+        pos, blk, boff = buf.cursor()
+        exp_blk = None if int(c["final_blk"]) == G.NO_BLOCK else int(c["final_blk"])
+        assert (pos, blk) == (int(c["final_pos"]), exp_blk), c
+        if blk is not None:
+            assert boff == int(c["final_blk_off"]), c
+
+
+def test_checksum_peso_golden(tc):
+    pool = G.pool()
+    cases, blocks = G.peso_cases()
+    for c in cases:
+        buf = tc.PktBuf([p.tobytes() for p in G.case_blocks(c, blocks, pool)])
+        buf.seek(min(3, int(c["total"]) - 1))  # checksum_peso resets the cursor itself
+        got = tc.checksum_peso(buf, tc.IpAddr.v4(c["dst"].tobytes()), tc.IpAddr.v4(c["src"].tobytes()),
+                               int(c["proto"]))
+        assert got == int(c["expected"]), c
+        pos, blk, _ = buf.cursor()
+        assert pos == int(c["final_pos"]) == int(c["total"]) and blk is None
+
+
+# ------------------------------------------------------------ batches
+
+def peso_descs(tc, cases):
+    d = np.zeros(cases.size, tc.PESO_DTYPE)
+    d["offset"] = cases["pool_off"]
+    d["len"] = cases["total"]
+    d["src"] = cases["src"]
+    d["dst"] = cases["dst"]
+    d["protocol"] = cases["proto"]
+    return d
+
+
+@pytest.mark.parametrize("g,u", GEOMS_SEG)
+def test_batch_peso_golden(tc, torch, geometry, g, u):
+    geometry(g, u, nt=(g + u) % 2)
+    pool = G.pool()
+    cases, _ = G.peso_cases()
+    arena = to_dev(torch, pool)
+    d = peso_descs(tc, cases)
+    out = tc.batch_peso(arena, tc.descs_to_device(d), d.size, int(d["len"].sum()))
+    np.testing.assert_array_equal(out.cpu().numpy(), cases["expected"].astype(np.uint16))
+
+
+def test_batch_segments_golden(tc, torch):
+    """pktbuf_checksum16 cases (from the cursor) and even-offset checksum16 cases
+    with 16-bit pre_sum, where the two routines agree, as one batch each."""
+    pool = G.pool()
+    cases, _ = G.pktbuf_cases()
+    keep = cases[(cases["len"] > 0) & (cases["len"] <= cases["total"] - cases["seek"])]
+    flat = G.flat_cases()
+    fkeep = flat[(flat["offset"] % 2 == 0) & (flat["pre_sum"] <= 0xFFFF)]
+    arena = to_dev(torch, pool)
+    for comp in (0, 1):
+        k = keep[keep["complement"] == comp]
+        f = fkeep[fkeep["complement"] == comp]
+        s = np.zeros(k.size + f.size, tc.SEG_DTYPE)
+        s["offset"][: k.size] = k["pool_off"].astype(np.uint64) + k["seek"]
+        s["len"][: k.size] = k["len"]
+        s["pre_sum"][: k.size] = k["pre_sum"].view(np.uint32)
+        s["offset"][k.size:] = f["pool_off"]
+        s["len"][k.size:] = f["len"]
+        s["pre_sum"][k.size:] = f["pre_sum"]
+        exp = np.concatenate([k["expected"], f["expected"]]).astype(np.uint16)
+        out = tc.batch_segments(arena, tc.descs_to_device(s), s.size, comp, int(s["len"].sum()))
+        np.testing.assert_array_equal(out.cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("g,u", GEOMS_IP)
+@pytest.mark.parametrize("nt", [0, 1])
+def test_batch_ipv4_golden(tc, torch, geometry, g, u, nt):
+    geometry(g, u, nt)
+    cases, ipool = G.ipv4_cases()
+    arena = to_dev(torch, ipool)
+    pk = np.zeros(cases.size, tc.PKT_DTYPE)
+    pk["offset"] = cases["pool_off"]
+    pk["len"] = cases["frame_len"]
+    out, flags = tc.batch_ipv4(arena, tc.descs_to_device(pk), pk.size, int(pk["len"].sum()))
+    out = out.cpu().numpy()
+    np.testing.assert_array_equal(out & 0xFFFF, cases["ip"])
+    np.testing.assert_array_equal(out >> 16, cases["l4"])
+    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+
+
+def test_ipv4_odd_arena_base(tc, torch):
+    """Same packets one byte further into the arena: address parity flips."""
+    cases, ipool = G.ipv4_cases()
+    arena = to_dev(torch, np.concatenate([np.zeros(1, np.uint8), ipool]))
+    pk = np.zeros(cases.size, tc.PKT_DTYPE)
+    pk["offset"] = cases["pool_off"].astype(np.uint64) + 1
+    pk["len"] = cases["frame_len"]
+    out, flags = tc.batch_ipv4(arena, tc.descs_to_device(pk), pk.size)
+    out = out.cpu().numpy()
+    np.testing.assert_array_equal(out & 0xFFFF, cases["ip"])
+    np.testing.assert_array_equal(out >> 16, cases["l4"])
+    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+
+
+# ------------------------------------------------- seeded batches vs oracle
+
+def run_config(tc, torch, config, n):
+    from tcp_amd import workload
+    b = workload.make_batch(config, rank=1, n=n)
+    arena, descs = workload.materialize(b)
+    if b.kind == "peso":
+        out = tc.batch_peso(arena, descs, b.n, b.total_bytes)
+    else:
+        out, flags = tc.batch_ipv4(arena, descs, b.n, b.total_bytes)
+    torch.cuda.synchronize()
+    return b, arena, out
+
+
+@pytest.mark.parametrize("config,n", [("mtu", 50000), ("tso", 600), ("mixed", 20000), ("mixed_aligned", 20000)])
+def test_config_vs_oracle(tc, torch, oracle, config, n):
+    b, arena, out = run_config(tc, torch, config, n)
+    host = arena.cpu().numpy()
+    # the device generator is the oracle's stream
+    np.testing.assert_array_equal(host[:4096], oracle.synth_fill(b.byte_base, 4096, b.seed)[:4096]
+                                  if b.kind == "peso" else host[:4096])
+    if b.kind == "peso":
+        exp = oracle.batch_peso(host, b.descs, nthreads=8)
+        np.testing.assert_array_equal(out.cpu().numpy(), exp)
+    else:
+        exp, fl = oracle.batch_ipv4(host, b.descs, nthreads=8)
+        np.testing.assert_array_equal(out.cpu().numpy(), exp)
+        assert (fl == 0).all()  # synthetic headers are well formed
+
+
+@pytest.mark.parametrize("g,u", GEOMS_SEG)
+def test_geometries_vs_oracle(tc, torch, oracle, geometry, g, u):
+    geometry(g, u, nt=u % 2)
+    b, arena, out = run_config(tc, torch, "mtu", 4096)
+    exp = oracle.batch_peso(arena.cpu().numpy(), b.descs, nthreads=8)
+    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+
+
+def test_edge_segments(tc, torch, oracle):
+    """Empty, 1-byte, odd starts, all-zero, all-0xFF, sums folding to 0xFFFF,
+    a segment ending on the allocation's last byte, and a 32 MiB segment."""
+    rng = np.random.default_rng(7)
+    size = (32 << 20) + 8192
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    host[1000:3000] = 0
+    host[4000:6000] = 0xFF
+    # 0xFF00 + 0x00FF = 0xFFFF: folds to 0xFFFF, complement 0
+    host[7000:7004] = [0x00, 0xFF, 0xFF, 0x00]
+    segs = [(0, 0), (5, 0), (9, 1), (10, 1), (11, 2), (12, 3), (1000, 2000), (1001, 1998), (4000, 2000),
+            (4001, 1999), (7000, 4), (7001, 3), (13, 65535), (17, 65536), (19, 65537), (8191, 1),
+            (size - 1, 1), (size - 17, 17), (size - 100, 100), (8192, 32 << 20)]
+    segs += [(int(o), int(n)) for o, n in zip(rng.integers(0, size - 70000, 300), rng.integers(0, 70000, 300))]
+    s = np.zeros(len(segs), tc.SEG_DTYPE)
+    s["offset"] = [o for o, _ in segs]
+    s["len"] = [n for _, n in segs]
+    s["pre_sum"] = rng.integers(0, 1 << 32, len(segs), dtype=np.uint64).astype(np.uint32)
+    s["pre_sum"][:12] = 0
+    arena = torch.from_numpy(host).cuda()  # no padding: the last chunk ends the allocation
+    for comp in (0, 1):
+        out = tc.batch_segments(arena, tc.descs_to_device(s), s.size, comp).cpu().numpy()
+        exp = oracle.batch_segments(host, s, comp, nthreads=8)
+        np.testing.assert_array_equal(out, exp)
+    assert exp[10] == 0  # the 0xFFFF-folding range, complemented
+    # peso form of the same ranges
+    p = np.zeros(len(segs), tc.PESO_DTYPE)
+    p["offset"], p["len"] = s["offset"], s["len"]
+    p["src"] = rng.integers(0, 256, (len(segs), 4))
+    p["dst"] = rng.integers(0, 256, (len(segs), 4))
+    p["protocol"] = rng.choice([6, 17], len(segs))
+    out = tc.batch_peso(arena, tc.descs_to_device(p), p.size).cpu().numpy()
+    np.testing.assert_array_equal(out, oracle.batch_peso(host, p, nthreads=8))
+
+
+def test_host_batch_end_to_end(tc, oracle):
+    """Pinned host arena -> H2D -> kernel -> D2H matches the device-resident path."""
+    from tcp_amd import workload
+    b = workload.make_batch("mtu", n=30000)
+    host = oracle.synth_fill(b.byte_base, b.alloc_bytes, b.seed)
+    rng = np.random.default_rng(3)
+    d = b.descs[rng.permutation(b.n)]  # any order
+    out = tc.host_batch_peso(host, d)
+    np.testing.assert_array_equal(out, oracle.batch_peso(host, d, nthreads=8))
+
+
+# --------------------------------------------------- full BASELINE sizes
+
+def test_full_mtu_batch_exact(tc, torch, oracle):
+    """configs[1] at full size (1M x 1500 B): every result checked."""
+    b, arena, out = run_config(tc, torch, "mtu", None)
+    exp = oracle.batch_peso(arena.cpu().numpy(), b.descs, nthreads=16)
+    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+
+
+def test_full_mixed_batch_exact(tc, torch, oracle):
+    """configs[3] at full size (1M packets, ~4.4 GiB): every result checked."""
+    b, arena, out = run_config(tc, torch, "mixed", None)
+    exp, fl = oracle.batch_ipv4(arena.cpu().numpy(), b.descs, nthreads=16)
+    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+
+
+def test_full_tso_batch_properties(tc, torch, oracle):
+    """configs[2] at full size (256K x 64 KiB = 16 GiB): a sampled exact check,
+    run-to-run determinism, geometry invariance, and the RFC 1624 incremental
+    update on every segment (changing one 16-bit word m -> m' turns checksum
+    HC into ~(~HC + ~m + m'))."""
+    from tcp_amd import workload
+    b = workload.make_batch("tso")
+    arena, descs = workload.materialize(b)
+    out1 = tc.batch_peso(arena, descs, b.n, b.total_bytes)
+    out2 = tc.batch_peso(arena, descs, b.n, b.total_bytes)
+    torch.cuda.synchronize()
+    hc = out1.cpu().numpy()
+    np.testing.assert_array_equal(hc, out2.cpu().numpy())
+    os.environ["TCSUM_G"], os.environ["TCSUM_U"] = "32", "16"
+    try:
+        out3 = tc.batch_peso(arena, descs, b.n, b.total_bytes)
+    finally:
+        del os.environ["TCSUM_G"], os.environ["TCSUM_U"]
+    np.testing.assert_array_equal(hc, out3.cpu().numpy())
+    # sampled exact parity
+    rng = np.random.default_rng(11)
+    idx = np.sort(rng.choice(b.n, 512, replace=False))
+    for i in idx:
+        o, L = int(b.descs["offset"][i]), int(b.descs["len"][i])
+        seg = arena[o: o + L].cpu().numpy()
+        assert hc[i] == oracle.checksum_peso(seg, b.descs["dst"][i], b.descs["src"][i], 6)
+    # incremental update: rewrite the word at offset 100 of every segment
+    words = arena[: b.n * 65536].view(b.n, 65536)
+    old = words[:, 100:102].cpu().numpy().copy().view("<u2").reshape(-1).astype(np.uint32)
+    new_bytes = torch.from_numpy(rng.integers(0, 256, (b.n, 2), dtype=np.uint8)).cuda()
+    words[:, 100:102] = new_bytes
+    new = new_bytes.cpu().numpy().copy().view("<u2").reshape(-1).astype(np.uint32)
+    out4 = tc.batch_peso(arena, descs, b.n, b.total_bytes).cpu().numpy().astype(np.uint32)
+    s = (~hc.astype(np.uint32) & 0xFFFF) + (~old & 0xFFFF) + new
+    s = (s & 0xFFFF) + (s >> 16)
+    s = (s & 0xFFFF) + (s >> 16)
+    np.testing.assert_array_equal(out4, ~s & 0xFFFF)

@@ -94,7 +94,19 @@ def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None):
         dist.barrier()
     torch.cuda.synchronize()
     ms = t0.elapsed_time(t1)  # events on the launch stream: pure kernel time of K launches
-    return dict(batch=batch, arena=arena, descs=descs, out=out, ms=ms, wall_s=wall)
+    # the achievable side: a plain streaming read of the same bytes, same loads
+    sink = torch.zeros(1, dtype=torch.uint32, device=arena.device)
+    for _ in range(2):
+        tc.probe_read(arena, batch.arena_bytes, sink)
+    p0 = torch.cuda.Event(enable_timing=True)
+    p1 = torch.cuda.Event(enable_timing=True)
+    p0.record(stream)
+    for _ in range(steps):
+        tc.probe_read(arena, batch.arena_bytes, sink)
+    p1.record(stream)
+    torch.cuda.synchronize()
+    probe_gbs = batch.arena_bytes / (p0.elapsed_time(p1) / steps * 1e-3) / 1e9
+    return dict(batch=batch, arena=arena, descs=descs, out=out, ms=ms, wall_s=wall, probe_gbs=probe_gbs)
 
 
 def result_entry(r, steps):
@@ -109,7 +121,9 @@ def result_entry(r, steps):
         "gib_s": b.total_bytes / (ms_step * 1e-3) / GIB,
         "ms_per_step": ms_step,
         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(ach / HBM_PEAK_GBS, 4)},
+                     "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "achievable_read": round(r["probe_gbs"], 1),
+                     "frac_of_achievable": round(ach / r["probe_gbs"], 4)},
     }
 
 
@@ -213,9 +227,8 @@ def e2e(torch, tc, r):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from tcp_amd import dist as D
+    rank, local, world = D.env()
     n_gpus = max(world, 1)
 
     traffic, pmc_note = None, "skipped"
@@ -229,21 +242,14 @@ def main():
     from tcp_amd import workload
 
     torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dist = D.init("nccl", local)  # barrier + max-time only; no data-path collective
 
     if args.pmc_child:
         time_config(torch, tc, workload, args.config, 0, args.steps, args.warmup)
         return
 
     head = time_config(torch, tc, workload, args.config, rank, args.steps, args.warmup, dist)
-    ms = head["ms"]
-    if dist is not None:
-        t = torch.tensor([ms], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms = float(t.item())
+    ms = D.max_over_ranks(dist, head["ms"], device="cuda")
     b = head["batch"]
     ms_step = ms / args.steps
     value = n_gpus * b.total_bytes * args.steps / (ms * 1e-3) / GIB
@@ -299,7 +305,7 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
-        dist.barrier()
+        D.barrier(dist)
         dist.destroy_process_group()
 
 

@@ -1,5 +1,6 @@
 /*
- * tcsum_synth.h -- on-device synthetic packet batches for tests and bench.py.
+ * tcsum_synth.h -- on-device synthetic packet batches and a read probe, for
+ * tests and bench.py.
  *
  * Not part of the checksum path.  The byte stream is the one the CPU oracle
  * reproduces (oracle/csum_oracle.c: orc_synth_fill): byte p of the stream is
@@ -28,6 +29,11 @@ int tcsum_synth_fill(void *arena /*[dev]*/, uint64_t nbytes, uint64_t byte_base,
  * Packets shorter than 20 bytes are left alone. */
 int tcsum_synth_ipv4(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,
                      uint64_t seed, void *stream);
+
+/* Stream-read nbytes (rounded down to 16) with the checksum kernels' load
+ * shape and nothing else: the measured "achievable" HBM read rate for the
+ * roofline.  sink: one device u32 (written only on a 2^-32 fluke). */
+int tcsum_probe_read(const void *p /*[dev]*/, uint64_t nbytes, uint32_t *sink /*[dev]*/, void *stream);
 
 #ifdef __cplusplus
 }

@@ -41,6 +41,7 @@ SIGNATURES = {
     # tcsum_synth.h
     "tcsum_synth_fill": (_I, [_V, _U64, _U64, _U64, _V]),
     "tcsum_synth_ipv4": (_I, [_V, _V, _U32, _U64, _V]),
+    "tcsum_probe_read": (_I, [_V, _U64, _V, _V]),
 }
 
 _lib = None

@@ -148,7 +148,7 @@ void ensure_stage(Ctx &c, size_t bytes)
     while (cap < bytes)
         cap <<= 1;
     if (c.stage)
-        hipHostFree(c.stage);
+        (void)hipHostFree(c.stage);
     c.stage = nullptr;
     c.stage_cap = 0;
     hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&c.stage), cap, hipHostMallocCoherent);
@@ -279,7 +279,7 @@ void *tcsum_host_alloc(size_t bytes)
 void tcsum_host_free(void *p)
 {
     if (p)
-        hipHostFree(p);
+        (void)hipHostFree(p);
 }
 
 static uint64_t mean_of(uint64_t total, uint32_t n) { return total && n ? total / n : 1500; }
@@ -340,6 +340,15 @@ int tcsum_synth_ipv4(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t 
                : TCSUM_ERR_SYS;
 }
 
+int tcsum_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, void *stream)
+{
+    if (!p || !sink || (reinterpret_cast<uintptr_t>(p) & 15u))
+        return TCSUM_ERR_PARAM;
+    return tcsum::launch_probe_read(p, nbytes, sink, static_cast<hipStream_t>(stream)) == hipSuccess
+               ? TCSUM_OK
+               : TCSUM_ERR_SYS;
+}
+
 // ------------------------------------------------------------ host batches
 
 int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_bytes,
@@ -365,7 +374,7 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     const size_t need_arena = ((arena_bytes + 15) & ~size_t(15)) + 16;
     if (need_arena > c.d_arena_cap) {
         if (c.d_arena)
-            hipFree(c.d_arena);
+            (void)hipFree(c.d_arena);
         c.d_arena_cap = 0;
         if (hipMalloc(reinterpret_cast<void **>(&c.d_arena), need_arena) != hipSuccess)
             return TCSUM_ERR_MEM;
@@ -373,9 +382,9 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     }
     if (n > c.d_descs_cap) {
         if (c.d_descs)
-            hipFree(c.d_descs);
+            (void)hipFree(c.d_descs);
         if (c.d_out)
-            hipFree(c.d_out);
+            (void)hipFree(c.d_out);
         c.d_descs_cap = c.d_out_cap = 0;
         if (hipMalloc(reinterpret_cast<void **>(&c.d_descs), sizeof(tcsum_peso_t) * n) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&c.d_out), sizeof(uint16_t) * n) != hipSuccess)

@@ -448,19 +448,70 @@ __global__ __launch_bounds__(256) void k_synth_ipv4(uint8_t *__restrict__ arena,
         p[12 + k] = (uint8_t)(a >> (8 * k));
 }
 
+// ---------------------------------------------------------------- read probe
+//
+// The "achievable" side of the roofline: a plain streaming read of the same
+// bytes with the same load shape (nontemporal dwordx4, one contiguous
+// 64*U-chunk tile per wave), XOR-folded so the loads stay live; a store only
+// happens if the fold hits a magic value.
+template <int U>
+__global__ __launch_bounds__(256) void k_probe_read(const u32x4 *__restrict__ p, uint64_t nchunks,
+                                                    uint32_t *__restrict__ sink)
+{
+    const uint64_t wave = (blockIdx.x * 256ull + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t base = wave * 64ull * U;
+    uint32_t acc = 0;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t idx = base + u * 64ull + lane;
+        v[u] = idx < nchunks ? load16<true>(p + idx) : u32x4(0u);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    if (acc == 0x9E3779B9u)
+        sink[0] = acc;
+}
+
+hipError_t launch_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, hipStream_t stream)
+{
+    const uint64_t nchunks = nbytes / 16;
+    if (nchunks == 0)
+        return hipSuccess;
+    const uint64_t per_block = 4ull * 64 * 8;
+    hipLaunchKernelGGL(k_probe_read<8>, dim3((uint32_t)((nchunks + per_block - 1) / per_block)), dim3(256),
+                       0, stream, static_cast<const u32x4 *>(p), nchunks, sink);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- dispatch
 
+// Measured on MI355X (scripts/tune.py, profiles/r01_tune.txt): fewer loads
+// per lane and more lanes per packet win until one pass covers a typical
+// packet; only TSO-size ranges want deep per-lane queues.  Nontemporal loads
+// win everywhere (the bytes are read once).
 Geometry pick_geometry(uint64_t mean_len)
 {
-    Geometry g{16, 8, true};
+    Geometry g{32, 4, true};
     const uint64_t chunks = mean_len / 16 + 1;
-    // enough lanes that one pass of U=8 loads covers a typical packet,
-    // capped at one packet per wave
-    int lanes = 4;
-    while (lanes < 64 && (uint64_t)lanes * 8 < chunks)
-        lanes *= 2;
-    g.lanes = lanes;
-    g.loads = 8;
+    if (chunks >= 2048) {        // >= 32 KiB: 1 packet per wave, 16 KiB in flight
+        g.lanes = 64;
+        g.loads = 16;
+    } else if (chunks >= 48) {   // ~750 B .. 32 KiB (MTU, mixed 64-9000 B)
+        g.lanes = 32;
+        g.loads = 4;
+    } else if (chunks >= 24) {
+        g.lanes = 16;
+        g.loads = 4;
+    } else if (chunks >= 12) {
+        g.lanes = 8;
+        g.loads = 4;
+    } else {
+        g.lanes = 4;
+        g.loads = 4;
+    }
     if (const char *s = getenv("TCSUM_G"))
         g.lanes = atoi(s);
     if (const char *s = getenv("TCSUM_U"))

@@ -129,6 +129,17 @@ def synth_ipv4(arena, pkts, n: int, seed: int = 20240807, stream=None):
                "tcsum_synth_ipv4")
 
 
+def probe_read(buf, nbytes: int | None = None, sink=None, stream=None):
+    """Plain streaming read of `buf` (the roofline's achievable side)."""
+    torch = _torch()
+    if sink is None:
+        sink = torch.zeros(1, dtype=torch.uint32, device=buf.device)
+    n = buf.numel() * buf.element_size() if nbytes is None else nbytes
+    _lib.check(_lib.lib().tcsum_probe_read(buf.data_ptr(), n, sink.data_ptr(), _stream_ptr(stream)),
+               "tcsum_probe_read")
+    return sink
+
+
 def pick_geometry(mean_len: int):
     g, u = ctypes.c_int(), ctypes.c_int()
     _lib.lib().tcsum_pick_geometry(mean_len, ctypes.byref(g), ctypes.byref(u))

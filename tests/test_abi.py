@@ -90,8 +90,9 @@ def test_pktbuf_cursor_walk_on_host():
 
 def test_geometry_choice(libpath):
     from tcp_amd import pick_geometry
-    assert pick_geometry(1500) == (16, 8)
-    assert pick_geometry(65536) == (64, 8)
+    assert pick_geometry(1500) == (32, 4)
+    assert pick_geometry(4500) == (32, 4)
+    assert pick_geometry(65536) == (64, 16)
     g, u = pick_geometry(64)
     assert g == 4
 

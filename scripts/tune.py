@@ -12,20 +12,20 @@ import tcp_amd as tc  # noqa: E402
 from tcp_amd import workload  # noqa: E402
 
 configs = sys.argv[1].split(",") if len(sys.argv) > 1 else ["mtu", "tso", "mixed"]
-rounds = 5
+rounds = 3
 for cfg in configs:
     b = workload.make_batch(cfg)
     arena, descs = workload.materialize(b)
     ref = None
     if b.kind == "peso":
-        geoms = list(itertools.product((8, 16, 32, 64), (4, 8, 16), (0, 1)))
+        geoms = list(itertools.product((8, 16, 32, 64), (1, 2, 3, 4, 6, 8, 16), (0, 1)))
     else:
-        geoms = list(itertools.product((16, 32, 64), (4, 8, 16), (0, 1)))
+        geoms = list(itertools.product((16, 32, 64), (2, 4, 8, 16), (0,)))
     times = {g: [] for g in geoms}
     out = torch.empty(b.n, dtype=torch.uint16 if b.kind == "peso" else torch.uint32, device="cuda")
     for r in range(rounds):
         for g in geoms:
-            os.environ["TCSUM_G"], os.environ["TCSUM_U"], os.environ["TCSUM_NT"] = map(str, g)
+            os.environ["TCSUM_G"], os.environ["TCSUM_U"], os.environ["TCSUM_P"] = map(str, g)
             def run():
                 if b.kind == "peso":
                     tc.batch_peso(arena, descs, b.n, b.total_bytes, out=out)
@@ -47,6 +47,6 @@ for cfg in configs:
     rows = sorted((np.median(t), g) for g, t in times.items())
     print(f"== {cfg}: n={b.n} bytes={b.total_bytes}")
     for ms, g in rows:
-        print(f"  G={g[0]:2d} U={g[1]:2d} NT={g[2]}  {ms*1e3:8.1f} us  {alg/ms/1e6:7.1f} GB/s  {alg/ms/1e6/8000:.3f}")
+        print(f"  G={g[0]:2d} U={g[1]:2d} P={g[2]}  {ms*1e3:8.1f} us  {alg/ms/1e6:7.1f} GB/s  {alg/ms/1e6/8000:.3f}")
     del arena, descs
     torch.cuda.empty_cache()

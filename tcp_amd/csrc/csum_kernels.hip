@@ -134,7 +134,137 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t x)
 // One descriptor per range.  MODE_SEG: pktbuf_checksum16 (u16 pre_sum);
 // MODE_EXACT: checksum16 (u32 pre_sum, u32 wrap, len <= 65535);
 // MODE_PESO: checksum_peso with the pseudo-header built here (tools.c:58-70).
-template <int G, int U, int MODE, bool NT>
+
+struct SegDesc {
+    uint64_t off;
+    uint32_t len, pre, src, dst, proto;
+};
+
+template <int MODE>
+__device__ __forceinline__ SegDesc load_desc(const void *__restrict__ descs, uint32_t seg, bool live)
+{
+    SegDesc d{0, 0, 0, 0, 0, 0};
+    if (live) {
+        if constexpr (MODE == MODE_PESO) {
+            const tcsum_peso_t *x = static_cast<const tcsum_peso_t *>(descs) + seg;
+            d.off = x->offset;
+            d.len = x->len;
+            d.src = *reinterpret_cast<const uint32_t *>(x->src);
+            d.dst = *reinterpret_cast<const uint32_t *>(x->dst);
+            d.proto = x->protocol;
+        } else {
+            const tcsum_seg_t *x = static_cast<const tcsum_seg_t *>(descs) + seg;
+            d.off = x->offset;
+            d.len = x->len;
+            d.pre = x->pre_sum;
+        }
+    }
+    return d;
+}
+
+// This lane's share of the word sum of arena[off, off+len), G lanes per range.
+// Lane 0 takes the first chunk and lane 1 the last, masked, before the loop;
+// the interior chunks [1, nch-1) are whole, so the unrolled loop has no
+// divergent branch: lanes past the end re-read the last interior chunk (same
+// lines as a live lane, merged) and add it with weight 0.  `issued` runs right
+// after the first loads are in flight (the persistent kernel prefetches its
+// next descriptor there, so it overlaps this range's latency).
+// A valid, 16-byte aligned chunk of zeros in the code object: lanes with no
+// bytes to read load from here, so every load is unconditional (no branch
+// around a load -> the compiler can count vmcnt exactly instead of vmcnt(0)).
+__device__ u32x4 g_zero_chunk = {0u, 0u, 0u, 0u};
+
+template <int G, int U, bool EXACT, class Issued>
+__device__ __forceinline__ uint32_t sum_range(const uint8_t *__restrict__ arena, uint64_t off, uint32_t len,
+                                              uint32_t gl, Issued &&issued)
+{
+    const uint8_t *p = arena + off; // derived from the kernel argument: global_load, not flat_load
+    const uint32_t s0 = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
+    const u32x4 *base = reinterpret_cast<const u32x4 *>(p - s0);
+    const uint64_t e = (uint64_t)len + s0; // range end in bytes from base
+    const uint32_t nch = len ? (uint32_t)((e + 15) >> 4) : 0u;
+    const uint32_t ni = nch > 2 ? nch - 2 : 0u;
+    const uint32_t eidx = gl == 0 ? 0u : (nch ? nch - 1u : 0u);
+    const bool has_edge = gl < 2 && nch > 0 && (gl == 0 || nch >= 2);
+    const u32x4 *ebase = nch ? base : &g_zero_chunk;
+    const u32x4 *ibase = ni ? base + 1 : &g_zero_chunk;
+    const uint32_t ilast = ni ? ni - 1u : 0u;
+
+    const u32x4 ev = load16<true>(ebase + (nch ? eidx : 0u));
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t j = u * G + gl;
+        v[u] = load16<true>(ibase + (j < ni ? j : ilast));
+    }
+    issued();
+
+    uint32_t acc;
+    {
+        const uint64_t c = 16ull * eidx;
+        const int lo = has_edge && eidx == 0 ? (int)s0 : 0;
+        const int hi = has_edge ? (int)(e - c < 16 ? e - c : 16) : 0;
+        acc = chunk_sum_masked(0u, ev, lo, hi);
+    }
+    for (uint32_t b0 = 0; b0 < ni;) {
+        uint32_t part = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = b0 + u * G + gl;
+            part = chunk_sum_w(part, v[u], j < ni ? 0x00010001u : 0u);
+        }
+        acc = EXACT ? acc + part : fold_step(acc + part);
+        b0 += G * U;
+        if (b0 >= ni)
+            break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = b0 + u * G + gl;
+            v[u] = load16<true>(ibase + (j < ni ? j : ilast));
+        }
+    }
+    return acc;
+}
+
+// The packet's first lane turns the group's sum into the reference's u16.
+template <int MODE>
+__device__ __forceinline__ uint16_t finalize(uint32_t acc, uintptr_t start, const SegDesc &d, uint32_t aux)
+{
+    uint32_t r;
+    if constexpr (MODE == MODE_EXACT) {
+        // tools.c:27-53: u32 accumulator from pre_sum; acc is the exact word
+        // sum (< 2^31 for len <= 65535).  The host stages the bytes so that
+        // address parity == logical parity (aux bit 1).
+        uint32_t s;
+        if (((start ^ (aux >> 1)) & 1u) == 0) {
+            s = d.pre + acc;
+        } else { // not reached from the C ABI; mod-0xFFFF result
+            const uint32_t f = rot8(fold16(acc));
+            s = fold_step(f + fold16(d.pre));
+        }
+        s = fold16(s);
+        r = (aux & 1u) ? (~s & 0xFFFFu) : s;
+    } else {
+        uint32_t f = fold16(acc);
+        if (start & 1u)
+            f = rot8(f);
+        if constexpr (MODE == MODE_SEG) {
+            const uint32_t t = fold_step(f + (d.pre & 0xFFFFu)); // pktbuf.c:657
+            r = (aux & 1u) ? (~t & 0xFFFFu) : t;
+        } else {
+            // tools.c:58-70: src, dst, {0, proto}, htons((uint16_t)len)
+            uint32_t q = add_halves(0u, d.src);
+            q = add_halves(q, d.dst);
+            q += d.proto << 8;
+            q += bswap16(d.len & 0xFFFFu);
+            r = ~fold_step(f + fold16(q)) & 0xFFFFu; // pktbuf_checksum16(..., 1), tools.c:73
+        }
+    }
+    return (uint16_t)r;
+}
+
+// One wave-slice of packets per wave, one launch-wide pass.
+template <int G, int U, int MODE>
 __global__ __launch_bounds__(256) void k_segments(const uint8_t *__restrict__ arena,
                                                   const void *__restrict__ descs, uint32_t n,
                                                   uint16_t *__restrict__ out, uint32_t aux)
@@ -143,94 +273,37 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t *__restrict__ ar
     const uint32_t gl = threadIdx.x & (G - 1);
     const uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / G;
     const bool live = seg < n;
-
-    uint64_t off = 0;
-    uint32_t len = 0, pre = 0, src = 0, dst = 0, proto = 0;
-    if (live) {
-        if constexpr (MODE == MODE_PESO) {
-            const tcsum_peso_t *d = static_cast<const tcsum_peso_t *>(descs) + seg;
-            off = d->offset;
-            len = d->len;
-            src = *reinterpret_cast<const uint32_t *>(d->src);
-            dst = *reinterpret_cast<const uint32_t *>(d->dst);
-            proto = d->protocol;
-        } else {
-            const tcsum_seg_t *d = static_cast<const tcsum_seg_t *>(descs) + seg;
-            off = d->offset;
-            len = d->len;
-            pre = d->pre_sum;
-        }
-    }
-
-    // Keep the pointer derived from the kernel argument so loads stay
-    // global_load (not flat_load, which would also count in lgkmcnt).
-    const uint8_t *p = arena + off;
-    const uintptr_t start = reinterpret_cast<uintptr_t>(p);
-    const uint32_t s0 = (uint32_t)(start & 15u);
-    const u32x4 *base = reinterpret_cast<const u32x4 *>(p - s0);
-    const uint64_t e = (uint64_t)len + s0; // range end, in bytes from base
-    const uint32_t nch = len ? (uint32_t)((e + 15) >> 4) : 0u;
-
-    uint32_t acc = 0;
-    for (uint32_t b0 = 0; b0 < nch; b0 += G * U) {
-        // Unconditional loads: a lane past the end re-reads the range's last
-        // chunk (same lines as a live lane -> merged) and adds it with weight 0.
-        u32x4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t idx = b0 + u * G + gl;
-            v[u] = load16<NT>(base + (idx < nch ? idx : nch - 1));
-        }
-        uint32_t part = 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t idx = b0 + u * G + gl;
-            const bool valid = idx < nch;
-            const uint64_t c = 16ull * idx;
-            if (valid && (idx == 0 || c + 16 > e)) { // first / last chunk: rare
-                const int lo = idx == 0 ? (int)s0 : 0;
-                const int hi = (int)(e - c < 16 ? e - c : 16);
-                v[u] = mask_chunk(v[u], lo, hi);
-            }
-            part = chunk_sum_w(part, v[u], valid ? 0x00010001u : 0u);
-        }
-        acc = MODE == MODE_EXACT ? acc + part : fold_step(acc + part);
-    }
+    const SegDesc d = load_desc<MODE>(descs, seg, live);
+    uint32_t acc = sum_range<G, U, MODE == MODE_EXACT>(arena, d.off, d.len, gl, [] {});
     acc = group_sum<G>(acc);
+    if (live && gl == 0)
+        out[seg] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + d.off), d, aux);
+}
 
-    if (live && gl == 0) {
-        uint32_t r;
-        if constexpr (MODE == MODE_EXACT) {
-            // tools.c:27-53: u32 accumulator from pre_sum; acc is the exact
-            // word sum (< 2^31 for len <= 65535).  The host stages the bytes
-            // so address parity == logical parity (aux bit 1).
-            uint32_t s;
-            if (((start ^ (aux >> 1)) & 1u) == 0) {
-                s = pre + acc;
-            } else { // not reached from the C ABI; mod-0xFFFF result
-                uint32_t f = rot8(fold16(acc));
-                s = fold_step(f + fold16(pre));
-            }
-            s = fold16(s);
-            r = (aux & 1u) ? (~s & 0xFFFFu) : s;
-        } else {
-            uint32_t f = fold16(acc);
-            if (start & 1u)
-                f = rot8(f);
-            if constexpr (MODE == MODE_SEG) {
-                uint32_t t = fold_step(f + (pre & 0xFFFFu)); // pktbuf.c:657
-                r = (aux & 1u) ? (~t & 0xFFFFu) : t;
-            } else {
-                // tools.c:58-70: src, dst, {0, proto}, htons((uint16_t)len)
-                uint32_t p = add_halves(0u, src);
-                p = add_halves(p, dst);
-                p += proto << 8;
-                p += bswap16(len & 0xFFFFu);
-                uint32_t t = fold_step(f + fold16(p));
-                r = ~t & 0xFFFFu; // pktbuf_checksum16(..., 1), tools.c:73
-            }
-        }
-        out[seg] = (uint16_t)r;
+// Persistent form: a resident grid walks the batch; each wave prefetches its
+// next descriptor while the current packets' bytes are in flight, so the
+// descriptor -> data dependence costs one latency per wave, not per packet.
+template <int G, int U, int MODE>
+__global__ __launch_bounds__(256) void k_segments_p(const uint8_t *__restrict__ arena,
+                                                    const void *__restrict__ descs, uint32_t n,
+                                                    uint16_t *__restrict__ out, uint32_t aux)
+{
+    constexpr uint32_t PER_WAVE = 64 / G;
+    const uint32_t gl = threadIdx.x & (G - 1);
+    const uint32_t wave = (blockIdx.x * 256u + threadIdx.x) >> 6;
+    const uint32_t step = gridDim.x * 4u * PER_WAVE;
+    uint32_t seg = wave * PER_WAVE + ((threadIdx.x & 63u) / G);
+    SegDesc d = load_desc<MODE>(descs, seg, seg < n);
+    for (uint32_t first = wave * PER_WAVE; first < n; first += step) { // wave-uniform
+        const uint32_t nseg = seg + step;
+        SegDesc nd{0, 0, 0, 0, 0, 0};
+        uint32_t acc = sum_range<G, U, MODE == MODE_EXACT>(arena, d.off, d.len, gl,
+                                                           [&] { nd = load_desc<MODE>(descs, nseg, nseg < n); });
+        acc = group_sum<G>(acc);
+        if (seg < n && gl == 0)
+            out[seg] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + d.off), d, aux);
+        seg = nseg;
+        d = nd;
     }
 }
 
@@ -247,7 +320,7 @@ __device__ __forceinline__ void pick6(uint32_t q, const uint32_t w[12], uint32_t
         x[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
 }
 
-template <int G, int U, bool NT>
+template <int G, int U>
 __global__ __launch_bounds__(256) void k_ipv4(const uint8_t *__restrict__ arena,
                                               const tcsum_pkt_t *__restrict__ pkts, uint32_t n,
                                               uint32_t *__restrict__ out,
@@ -288,7 +361,7 @@ __global__ __launch_bounds__(256) void k_ipv4(const uint8_t *__restrict__ arena,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t idx = u * G + gl;
-            v[u] = load16<NT>(base + (idx < nch ? idx : nch - 1));
+            v[u] = load16<true>(base + (idx < nch ? idx : nch - 1));
         }
     }
 
@@ -352,7 +425,7 @@ __global__ __launch_bounds__(256) void k_ipv4(const uint8_t *__restrict__ arena,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t idx = b0 + u * G + gl;
-            v[u] = load16<NT>(base + (idx < nch ? idx : nch - 1));
+            v[u] = load16<true>(base + (idx < nch ? idx : nch - 1));
         }
     }
     acc_h = group_sum<G>(acc_h);
@@ -488,18 +561,30 @@ hipError_t launch_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, hip
 
 // ---------------------------------------------------------------- dispatch
 
-// Measured on MI355X (scripts/tune.py, profiles/r01_tune.txt): fewer loads
-// per lane and more lanes per packet win until one pass covers a typical
-// packet; only TSO-size ranges want deep per-lane queues.  Nontemporal loads
-// win everywhere (the bytes are read once).
+static int resident_blocks()
+{
+    static int blocks = 0;
+    if (blocks == 0) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess)
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        blocks = cus * 8; // 8 x 256-thread workgroups = 32 waves per CU
+    }
+    return blocks;
+}
+
+// Measured on MI355X (scripts/tune.py, profiles/r01/): enough lanes per packet
+// that a pass or two covers a typical packet, few loads per lane; only
+// TSO-size ranges want deep per-lane queues.  Loads are nontemporal (the
+// bytes are read once).
 Geometry pick_geometry(uint64_t mean_len)
 {
-    Geometry g{32, 4, true};
+    Geometry g{32, 4, false};
     const uint64_t chunks = mean_len / 16 + 1;
-    if (chunks >= 2048) {        // >= 32 KiB: 1 packet per wave, 16 KiB in flight
+    if (chunks >= 2048) { // >= 32 KiB: one packet per wave, 16 KiB in flight
         g.lanes = 64;
         g.loads = 16;
-    } else if (chunks >= 48) {   // ~750 B .. 32 KiB (MTU, mixed 64-9000 B)
+    } else if (chunks >= 48) { // ~750 B .. 32 KiB (MTU, mixed 64-9000 B)
         g.lanes = 32;
         g.loads = 4;
     } else if (chunks >= 24) {
@@ -516,22 +601,32 @@ Geometry pick_geometry(uint64_t mean_len)
         g.lanes = atoi(s);
     if (const char *s = getenv("TCSUM_U"))
         g.loads = atoi(s);
-    if (const char *s = getenv("TCSUM_NT"))
-        g.nt = atoi(s) != 0;
+    if (const char *s = getenv("TCSUM_P"))
+        g.persist = atoi(s) != 0;
     return g;
 }
 
-template <int MODE, bool NT>
-static hipError_t seg_u(int G, int U, dim3 grid, const void *arena, const void *descs, uint32_t n,
+template <int MODE>
+static hipError_t seg_u(int G, int U, bool persist, uint32_t n, const void *arena, const void *descs,
                         uint16_t *out, uint32_t aux, hipStream_t s)
 {
 #define TCSUM_SEG(GG, UU)                                                                            \
     if (G == GG && U == UU) {                                                                      \
-        hipLaunchKernelGGL((k_segments<GG, UU, MODE, NT>), grid, dim3(256), 0, s,                   \
-                           static_cast<const uint8_t *>(arena), descs, n, out, aux);               \
+        const uint32_t per_block = 256u / GG;                                                      \
+        uint32_t blocks = (n + per_block - 1) / per_block;                                         \
+        if (persist) {                                                                             \
+            blocks = blocks < (uint32_t)resident_blocks() ? blocks : (uint32_t)resident_blocks();  \
+            hipLaunchKernelGGL((k_segments_p<GG, UU, MODE>), dim3(blocks), dim3(256), 0, s,        \
+                               static_cast<const uint8_t *>(arena), descs, n, out, aux);           \
+        } else {                                                                                   \
+            hipLaunchKernelGGL((k_segments<GG, UU, MODE>), dim3(blocks), dim3(256), 0, s,          \
+                               static_cast<const uint8_t *>(arena), descs, n, out, aux);           \
+        }                                                                                          \
         return hipGetLastError();                                                                  \
     }
-#define TCSUM_SEG_U(GG) TCSUM_SEG(GG, 4) TCSUM_SEG(GG, 8) TCSUM_SEG(GG, 16)
+#define TCSUM_SEG_U(GG)                                                                              \
+    TCSUM_SEG(GG, 1) TCSUM_SEG(GG, 2) TCSUM_SEG(GG, 3) TCSUM_SEG(GG, 4) TCSUM_SEG(GG, 6)             \
+        TCSUM_SEG(GG, 8) TCSUM_SEG(GG, 16)
     TCSUM_SEG_U(4)
     TCSUM_SEG_U(8)
     TCSUM_SEG_U(16)
@@ -547,31 +642,26 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
 {
     if (n == 0)
         return hipSuccess;
-    const uint64_t per_block = 256u / (uint32_t)g.lanes;
-    const dim3 grid((uint32_t)((n + per_block - 1) / per_block));
     if (mode == MODE_EXACT) {
-        hipLaunchKernelGGL((k_segments<64, 8, MODE_EXACT, false>), dim3((n + 3) / 4), dim3(256), 0,
-                           stream, static_cast<const uint8_t *>(arena), descs, n, out, aux);
+        hipLaunchKernelGGL((k_segments<64, 8, MODE_EXACT>), dim3((n + 3) / 4), dim3(256), 0, stream,
+                           static_cast<const uint8_t *>(arena), descs, n, out, aux);
         return hipGetLastError();
     }
     if (mode == MODE_SEG)
-        return g.nt ? seg_u<MODE_SEG, true>(g.lanes, g.loads, grid, arena, descs, n, out, aux, stream)
-                    : seg_u<MODE_SEG, false>(g.lanes, g.loads, grid, arena, descs, n, out, aux, stream);
-    return g.nt ? seg_u<MODE_PESO, true>(g.lanes, g.loads, grid, arena, descs, n, out, aux, stream)
-                : seg_u<MODE_PESO, false>(g.lanes, g.loads, grid, arena, descs, n, out, aux, stream);
+        return seg_u<MODE_SEG>(g.lanes, g.loads, g.persist, n, arena, descs, out, aux, stream);
+    return seg_u<MODE_PESO>(g.lanes, g.loads, g.persist, n, arena, descs, out, aux, stream);
 }
 
-template <bool NT>
 static hipError_t ipv4_u(int G, int U, dim3 grid, const void *arena, const tcsum_pkt_t *pkts,
                          uint32_t n, uint32_t *out, uint8_t *flags, hipStream_t s)
 {
 #define TCSUM_IP(GG, UU)                                                                             \
     if (G == GG && U == UU) {                                                                      \
-        hipLaunchKernelGGL((k_ipv4<GG, UU, NT>), grid, dim3(256), 0, s,                             \
+        hipLaunchKernelGGL((k_ipv4<GG, UU>), grid, dim3(256), 0, s,                             \
                            static_cast<const uint8_t *>(arena), pkts, n, out, flags);              \
         return hipGetLastError();                                                                  \
     }
-#define TCSUM_IP_U(GG) TCSUM_IP(GG, 4) TCSUM_IP(GG, 8) TCSUM_IP(GG, 16)
+#define TCSUM_IP_U(GG) TCSUM_IP(GG, 2) TCSUM_IP(GG, 4) TCSUM_IP(GG, 8) TCSUM_IP(GG, 16)
     TCSUM_IP_U(16)
     TCSUM_IP_U(32)
     TCSUM_IP_U(64)
@@ -589,8 +679,7 @@ hipError_t launch_ipv4(Geometry g, const void *arena, const tcsum_pkt_t *pkts, u
         g.lanes = 16;
     const uint64_t per_block = 256u / (uint32_t)g.lanes;
     const dim3 grid((uint32_t)((n + per_block - 1) / per_block));
-    return g.nt ? ipv4_u<true>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, stream)
-                : ipv4_u<false>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, stream);
+    return ipv4_u(g.lanes, g.loads, grid, arena, pkts, n, out, flags, stream);
 }
 
 hipError_t launch_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, uint64_t seed,

@@ -19,7 +19,7 @@ enum Mode : int {
 struct Geometry {
     int lanes; // G: lanes that share one packet (4..64, power of two)
     int loads; // U: 16-byte loads in flight per lane per pass
-    bool nt;   // nontemporal (stream-once) loads
+    bool persist; // resident grid with descriptor prefetch (k_segments_p)
 };
 
 Geometry pick_geometry(uint64_t mean_len);

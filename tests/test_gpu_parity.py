@@ -17,8 +17,8 @@ import golden_io as G
 
 pytestmark = pytest.mark.gpu
 
-GEOMS_SEG = [(g, u) for g in (4, 8, 16, 32, 64) for u in (4, 8, 16)]
-GEOMS_IP = [(g, u) for g in (16, 32, 64) for u in (4, 8, 16)]
+GEOMS_SEG = [(g, u, p) for g in (4, 8, 16, 32, 64) for u in (1, 3, 4, 16) for p in (0, 1)]
+GEOMS_IP = [(g, u) for g in (16, 32, 64) for u in (2, 4, 8, 16)]
 
 
 @pytest.fixture(scope="module")
@@ -39,10 +39,10 @@ def tc(torch):
 
 @pytest.fixture
 def geometry(monkeypatch):
-    def set_geometry(g, u, nt=1):
+    def set_geometry(g, u, persist=0):
         monkeypatch.setenv("TCSUM_G", str(g))
         monkeypatch.setenv("TCSUM_U", str(u))
-        monkeypatch.setenv("TCSUM_NT", str(nt))
+        monkeypatch.setenv("TCSUM_P", str(persist))
     return set_geometry
 
 
@@ -132,9 +132,9 @@ def peso_descs(tc, cases):
     return d
 
 
-@pytest.mark.parametrize("g,u", GEOMS_SEG)
-def test_batch_peso_golden(tc, torch, geometry, g, u):
-    geometry(g, u, nt=(g + u) % 2)
+@pytest.mark.parametrize("g,u,p", GEOMS_SEG)
+def test_batch_peso_golden(tc, torch, geometry, g, u, p):
+    geometry(g, u, p)
     pool = G.pool()
     cases, _ = G.peso_cases()
     arena = to_dev(torch, pool)
@@ -143,9 +143,11 @@ def test_batch_peso_golden(tc, torch, geometry, g, u):
     np.testing.assert_array_equal(out.cpu().numpy(), cases["expected"].astype(np.uint16))
 
 
-def test_batch_segments_golden(tc, torch):
+@pytest.mark.parametrize("p", [0, 1])
+def test_batch_segments_golden(tc, torch, geometry, p):
     """pktbuf_checksum16 cases (from the cursor) and even-offset checksum16 cases
     with 16-bit pre_sum, where the two routines agree, as one batch each."""
+    geometry(32, 3, p)
     pool = G.pool()
     cases, _ = G.pktbuf_cases()
     keep = cases[(cases["len"] > 0) & (cases["len"] <= cases["total"] - cases["seek"])]
@@ -168,9 +170,8 @@ def test_batch_segments_golden(tc, torch):
 
 
 @pytest.mark.parametrize("g,u", GEOMS_IP)
-@pytest.mark.parametrize("nt", [0, 1])
-def test_batch_ipv4_golden(tc, torch, geometry, g, u, nt):
-    geometry(g, u, nt)
+def test_batch_ipv4_golden(tc, torch, geometry, g, u):
+    geometry(g, u)
     cases, ipool = G.ipv4_cases()
     arena = to_dev(torch, ipool)
     pk = np.zeros(cases.size, tc.PKT_DTYPE)
@@ -227,9 +228,9 @@ def test_config_vs_oracle(tc, torch, oracle, config, n):
         assert (fl == 0).all()  # synthetic headers are well formed
 
 
-@pytest.mark.parametrize("g,u", GEOMS_SEG)
-def test_geometries_vs_oracle(tc, torch, oracle, geometry, g, u):
-    geometry(g, u, nt=u % 2)
+@pytest.mark.parametrize("g,u,p", GEOMS_SEG)
+def test_geometries_vs_oracle(tc, torch, oracle, geometry, g, u, p):
+    geometry(g, u, p)
     b, arena, out = run_config(tc, torch, "mtu", 4096)
     exp = oracle.batch_peso(arena.cpu().numpy(), b.descs, nthreads=8)
     np.testing.assert_array_equal(out.cpu().numpy(), exp)
@@ -310,11 +311,11 @@ def test_full_tso_batch_properties(tc, torch, oracle):
     torch.cuda.synchronize()
     hc = out1.cpu().numpy()
     np.testing.assert_array_equal(hc, out2.cpu().numpy())
-    os.environ["TCSUM_G"], os.environ["TCSUM_U"] = "32", "16"
+    os.environ["TCSUM_G"], os.environ["TCSUM_U"], os.environ["TCSUM_P"] = "32", "3", "1"
     try:
         out3 = tc.batch_peso(arena, descs, b.n, b.total_bytes)
     finally:
-        del os.environ["TCSUM_G"], os.environ["TCSUM_U"]
+        del os.environ["TCSUM_G"], os.environ["TCSUM_U"], os.environ["TCSUM_P"]
     np.testing.assert_array_equal(hc, out3.cpu().numpy())
     # sampled exact parity
     rng = np.random.default_rng(11)

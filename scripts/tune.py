@@ -18,7 +18,7 @@ for cfg in configs:
     arena, descs = workload.materialize(b)
     ref = None
     if b.kind == "peso":
-        geoms = list(itertools.product((8, 16, 32, 64), (1, 2, 3, 4, 6, 8, 16), (0, 1)))
+        geoms = list(itertools.product((16, 32, 64), (1, 2, 3, 4, 6, 8, 16), (0, 1, 2)))
     else:
         geoms = list(itertools.product((16, 32, 64), (2, 4, 8, 16), (0,)))
     times = {g: [] for g in geoms}
@@ -43,10 +43,28 @@ for cfg in configs:
                 ref = out.clone()
             elif r == 0:
                 assert torch.equal(ref, out), g
+    # achievable: plain streaming read of the same bytes, by loads per lane
+    probe = {}
+    for pu in (1, 2, 4, 8, 16):
+        os.environ["TCSUM_PROBE_U"] = str(pu)
+        ts = []
+        for _ in range(rounds):
+            tc.probe_read(arena, b.arena_bytes)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                tc.probe_read(arena, b.arena_bytes)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / 10)
+        probe[pu] = np.median(ts)
+    del os.environ["TCSUM_PROBE_U"]
     alg = b.total_bytes + b.n * (26 if b.kind == "peso" else 20)
     rows = sorted((np.median(t), g) for g, t in times.items())
     print(f"== {cfg}: n={b.n} bytes={b.total_bytes}")
-    for ms, g in rows:
+    for pu, ms in probe.items():
+        print(f"  probe U={pu:2d}  {ms*1e3:8.1f} us  {b.arena_bytes/ms/1e6:7.1f} GB/s")
+    for ms, g in rows[:25]:
         print(f"  G={g[0]:2d} U={g[1]:2d} P={g[2]}  {ms*1e3:8.1f} us  {alg/ms/1e6:7.1f} GB/s  {alg/ms/1e6/8000:.3f}")
     del arena, descs
     torch.cuda.empty_cache()

@@ -140,90 +140,115 @@ struct SegDesc {
     uint32_t len, pre, src, dst, proto;
 };
 
+// Unconditional: a dead lane (seg >= n) reads descriptor 0 and gets len 0, so
+// no load sits behind a branch.
 template <int MODE>
 __device__ __forceinline__ SegDesc load_desc(const void *__restrict__ descs, uint32_t seg, bool live)
 {
-    SegDesc d{0, 0, 0, 0, 0, 0};
-    if (live) {
-        if constexpr (MODE == MODE_PESO) {
-            const tcsum_peso_t *x = static_cast<const tcsum_peso_t *>(descs) + seg;
-            d.off = x->offset;
-            d.len = x->len;
-            d.src = *reinterpret_cast<const uint32_t *>(x->src);
-            d.dst = *reinterpret_cast<const uint32_t *>(x->dst);
-            d.proto = x->protocol;
-        } else {
-            const tcsum_seg_t *x = static_cast<const tcsum_seg_t *>(descs) + seg;
-            d.off = x->offset;
-            d.len = x->len;
-            d.pre = x->pre_sum;
-        }
+    SegDesc d;
+    const uint32_t i = live ? seg : 0u;
+    if constexpr (MODE == MODE_PESO) {
+        const tcsum_peso_t *x = static_cast<const tcsum_peso_t *>(descs) + i;
+        d.off = x->offset;
+        d.len = x->len;
+        d.src = *reinterpret_cast<const uint32_t *>(x->src);
+        d.dst = *reinterpret_cast<const uint32_t *>(x->dst);
+        d.proto = x->protocol;
+        d.pre = 0;
+    } else {
+        const tcsum_seg_t *x = static_cast<const tcsum_seg_t *>(descs) + i;
+        d.off = x->offset;
+        d.len = x->len;
+        d.pre = x->pre_sum;
+        d.src = d.dst = d.proto = 0;
     }
+    d.len = live ? d.len : 0u;
     return d;
 }
 
-// This lane's share of the word sum of arena[off, off+len), G lanes per range.
-// Lane 0 takes the first chunk and lane 1 the last, masked, before the loop;
-// the interior chunks [1, nch-1) are whole, so the unrolled loop has no
-// divergent branch: lanes past the end re-read the last interior chunk (same
-// lines as a live lane, merged) and add it with weight 0.  `issued` runs right
-// after the first loads are in flight (the persistent kernel prefetches its
-// next descriptor there, so it overlaps this range's latency).
 // A valid, 16-byte aligned chunk of zeros in the code object: lanes with no
 // bytes to read load from here, so every load is unconditional (no branch
 // around a load -> the compiler can count vmcnt exactly instead of vmcnt(0)).
 __device__ u32x4 g_zero_chunk = {0u, 0u, 0u, 0u};
 
-template <int G, int U, bool EXACT, class Issued>
-__device__ __forceinline__ uint32_t sum_range(const uint8_t *__restrict__ arena, uint64_t off, uint32_t len,
-                                              uint32_t gl, Issued &&issued)
+// One range's loads in flight for this lane (G lanes per range).  Lane 0
+// takes the first chunk and lane 1 the last, masked; the interior chunks
+// [1, nch-1) are whole, so the unrolled loop has no divergent branch: lanes
+// past the end re-read the last interior chunk (same lines as a live lane,
+// merged) and add it with weight 0.
+template <int U>
+struct Frame {
+    const u32x4 *ibase;
+    uint64_t e; // range end in bytes from the first chunk
+    uint32_t s0, ni, ilast, eidx;
+    bool has_edge;
+    u32x4 ev;
+    u32x4 v[U];
+};
+
+template <int G, int U>
+__device__ __forceinline__ void frame_issue(Frame<U> &f, const uint8_t *__restrict__ arena, uint64_t off,
+                                            uint32_t len, uint32_t gl)
 {
     const uint8_t *p = arena + off; // derived from the kernel argument: global_load, not flat_load
-    const uint32_t s0 = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
-    const u32x4 *base = reinterpret_cast<const u32x4 *>(p - s0);
-    const uint64_t e = (uint64_t)len + s0; // range end in bytes from base
-    const uint32_t nch = len ? (uint32_t)((e + 15) >> 4) : 0u;
-    const uint32_t ni = nch > 2 ? nch - 2 : 0u;
-    const uint32_t eidx = gl == 0 ? 0u : (nch ? nch - 1u : 0u);
-    const bool has_edge = gl < 2 && nch > 0 && (gl == 0 || nch >= 2);
+    f.s0 = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
+    const u32x4 *base = reinterpret_cast<const u32x4 *>(p - f.s0);
+    f.e = (uint64_t)len + f.s0;
+    const uint32_t nch = len ? (uint32_t)((f.e + 15) >> 4) : 0u;
+    f.ni = nch > 2 ? nch - 2 : 0u;
+    f.eidx = gl == 0 ? 0u : (nch ? nch - 1u : 0u);
+    f.has_edge = gl < 2 && nch > 0 && (gl == 0 || nch >= 2);
     const u32x4 *ebase = nch ? base : &g_zero_chunk;
-    const u32x4 *ibase = ni ? base + 1 : &g_zero_chunk;
-    const uint32_t ilast = ni ? ni - 1u : 0u;
-
-    const u32x4 ev = load16<true>(ebase + (nch ? eidx : 0u));
-    u32x4 v[U];
+    f.ibase = f.ni ? base + 1 : &g_zero_chunk;
+    f.ilast = f.ni ? f.ni - 1u : 0u;
+    f.ev = load16<true>(ebase + (nch ? f.eidx : 0u));
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t j = u * G + gl;
-        v[u] = load16<true>(ibase + (j < ni ? j : ilast));
+        f.v[u] = load16<true>(f.ibase + (j < f.ni ? j : f.ilast));
     }
-    issued();
+}
 
+template <int G, int U, bool EXACT>
+__device__ __forceinline__ uint32_t frame_consume(Frame<U> &f, uint32_t gl)
+{
     uint32_t acc;
     {
-        const uint64_t c = 16ull * eidx;
-        const int lo = has_edge && eidx == 0 ? (int)s0 : 0;
-        const int hi = has_edge ? (int)(e - c < 16 ? e - c : 16) : 0;
-        acc = chunk_sum_masked(0u, ev, lo, hi);
+        const uint64_t c = 16ull * f.eidx;
+        const int lo = f.has_edge && f.eidx == 0 ? (int)f.s0 : 0;
+        const int hi = f.has_edge ? (int)(f.e - c < 16 ? f.e - c : 16) : 0;
+        acc = chunk_sum_masked(0u, f.ev, lo, hi);
     }
-    for (uint32_t b0 = 0; b0 < ni;) {
+    for (uint32_t b0 = 0; b0 < f.ni;) {
         uint32_t part = 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t j = b0 + u * G + gl;
-            part = chunk_sum_w(part, v[u], j < ni ? 0x00010001u : 0u);
+            part = chunk_sum_w(part, f.v[u], j < f.ni ? 0x00010001u : 0u);
         }
         acc = EXACT ? acc + part : fold_step(acc + part);
         b0 += G * U;
-        if (b0 >= ni)
+        if (b0 >= f.ni)
             break;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t j = b0 + u * G + gl;
-            v[u] = load16<true>(ibase + (j < ni ? j : ilast));
+            f.v[u] = load16<true>(f.ibase + (j < f.ni ? j : f.ilast));
         }
     }
     return acc;
+}
+
+// This lane's share of the word sum of arena[off, off+len).  `issued` runs
+// right after the first loads are in flight.
+template <int G, int U, bool EXACT, class Issued>
+__device__ __forceinline__ uint32_t sum_range(const uint8_t *__restrict__ arena, uint64_t off, uint32_t len,
+                                              uint32_t gl, Issued &&issued)
+{
+    Frame<U> f;
+    frame_issue<G, U>(f, arena, off, len, gl);
+    issued();
+    return frame_consume<G, U, EXACT>(f, gl);
 }
 
 // The packet's first lane turns the group's sum into the reference's u16.
@@ -304,6 +329,61 @@ __global__ __launch_bounds__(256) void k_segments_p(const uint8_t *__restrict__ 
             out[seg] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + d.off), d, aux);
         seg = nseg;
         d = nd;
+    }
+}
+
+// Pipelined persistent form: each wave keeps TWO ranges' loads in flight.
+// Descriptors run two ranges ahead and are issued before the data loads that
+// need the previous one, so with in-order vmcnt every wait is a counted one:
+//   order: d[i+2], L[i+1], (wait L[i]) sum, store
+// and the bytes of range i+1 stream while range i is summed.  The loop is
+// unrolled by two with two named frames: copying a frame whose loads are in
+// flight would force a wait on them (a v_mov of a pending register).
+template <int G, int U, int MODE>
+__device__ __forceinline__ void finish_range(Frame<U> &f, const SegDesc &d, uint32_t seg, uint32_t n,
+                                             uint32_t gl, const uint8_t *__restrict__ arena,
+                                             uint16_t *__restrict__ out, uint32_t aux)
+{
+    uint32_t acc = frame_consume<G, U, MODE == MODE_EXACT>(f, gl);
+    acc = group_sum<G>(acc);
+    if (seg < n && gl == 0)
+        out[seg] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + d.off), d, aux);
+}
+
+template <int G, int U, int MODE>
+__global__ __launch_bounds__(256) void k_segments_pp(const uint8_t *__restrict__ arena,
+                                                     const void *__restrict__ descs, uint32_t n,
+                                                     uint16_t *__restrict__ out, uint32_t aux)
+{
+    constexpr uint32_t PER_WAVE = 64 / G;
+    const uint32_t gl = threadIdx.x & (G - 1);
+    const uint32_t wave = (blockIdx.x * 256u + threadIdx.x) >> 6;
+    const uint32_t step = gridDim.x * 4u * PER_WAVE;
+    uint32_t seg = wave * PER_WAVE + ((threadIdx.x & 63u) / G);
+    uint32_t first = wave * PER_WAVE; // wave-uniform loop control
+    Frame<U> fa, fb;
+    SegDesc d0 = load_desc<MODE>(descs, seg, seg < n);
+    SegDesc d1 = load_desc<MODE>(descs, seg + step, seg + step < n);
+    frame_issue<G, U>(fa, arena, d0.off, d0.len, gl);
+    while (first < n) {
+        // fa in flight for d0, d1 loading
+        const SegDesc d2 = load_desc<MODE>(descs, seg + 2 * step, seg + 2 * step < n);
+        frame_issue<G, U>(fb, arena, d1.off, d1.len, gl);
+        finish_range<G, U, MODE>(fa, d0, seg, n, gl, arena, out, aux);
+        seg += step;
+        first += step;
+        if (first >= n)
+            break;
+        // fb in flight for d1, d2 loading
+        const SegDesc d3 = load_desc<MODE>(descs, seg + 2 * step, seg + 2 * step < n);
+        frame_issue<G, U>(fa, arena, d2.off, d2.len, gl);
+        finish_range<G, U, MODE>(fb, d1, seg, n, gl, arena, out, aux);
+        seg += step;
+        first += step;
+        // back to: fa in flight for d0 := d2, d1 := d3 loading (descriptor
+        // copies wait only for themselves: they were issued before fa's loads)
+        d0 = d2;
+        d1 = d3;
     }
 }
 
@@ -553,9 +633,19 @@ hipError_t launch_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, hip
     const uint64_t nchunks = nbytes / 16;
     if (nchunks == 0)
         return hipSuccess;
-    const uint64_t per_block = 4ull * 64 * 8;
-    hipLaunchKernelGGL(k_probe_read<8>, dim3((uint32_t)((nchunks + per_block - 1) / per_block)), dim3(256),
-                       0, stream, static_cast<const u32x4 *>(p), nchunks, sink);
+    int U = 8;
+    if (const char *s = getenv("TCSUM_PROBE_U"))
+        U = atoi(s);
+    const uint64_t per_block = 4ull * 64 * (uint64_t)U;
+    const dim3 grid((uint32_t)((nchunks + per_block - 1) / per_block));
+    const u32x4 *q = static_cast<const u32x4 *>(p);
+    switch (U) {
+    case 1: hipLaunchKernelGGL(k_probe_read<1>, grid, dim3(256), 0, stream, q, nchunks, sink); break;
+    case 2: hipLaunchKernelGGL(k_probe_read<2>, grid, dim3(256), 0, stream, q, nchunks, sink); break;
+    case 4: hipLaunchKernelGGL(k_probe_read<4>, grid, dim3(256), 0, stream, q, nchunks, sink); break;
+    case 16: hipLaunchKernelGGL(k_probe_read<16>, grid, dim3(256), 0, stream, q, nchunks, sink); break;
+    default: hipLaunchKernelGGL(k_probe_read<8>, grid, dim3(256), 0, stream, q, nchunks, sink); break;
+    }
     return hipGetLastError();
 }
 
@@ -579,7 +669,7 @@ static int resident_blocks()
 // bytes are read once).
 Geometry pick_geometry(uint64_t mean_len)
 {
-    Geometry g{32, 4, false};
+    Geometry g{32, 4, 0};
     const uint64_t chunks = mean_len / 16 + 1;
     if (chunks >= 2048) { // >= 32 KiB: one packet per wave, 16 KiB in flight
         g.lanes = 64;
@@ -602,12 +692,12 @@ Geometry pick_geometry(uint64_t mean_len)
     if (const char *s = getenv("TCSUM_U"))
         g.loads = atoi(s);
     if (const char *s = getenv("TCSUM_P"))
-        g.persist = atoi(s) != 0;
+        g.persist = atoi(s);
     return g;
 }
 
 template <int MODE>
-static hipError_t seg_u(int G, int U, bool persist, uint32_t n, const void *arena, const void *descs,
+static hipError_t seg_u(int G, int U, int persist, uint32_t n, const void *arena, const void *descs,
                         uint16_t *out, uint32_t aux, hipStream_t s)
 {
 #define TCSUM_SEG(GG, UU)                                                                            \
@@ -616,8 +706,12 @@ static hipError_t seg_u(int G, int U, bool persist, uint32_t n, const void *aren
         uint32_t blocks = (n + per_block - 1) / per_block;                                         \
         if (persist) {                                                                             \
             blocks = blocks < (uint32_t)resident_blocks() ? blocks : (uint32_t)resident_blocks();  \
-            hipLaunchKernelGGL((k_segments_p<GG, UU, MODE>), dim3(blocks), dim3(256), 0, s,        \
-                               static_cast<const uint8_t *>(arena), descs, n, out, aux);           \
+            if (persist == 2)                                                                      \
+                hipLaunchKernelGGL((k_segments_pp<GG, UU, MODE>), dim3(blocks), dim3(256), 0, s,   \
+                                   static_cast<const uint8_t *>(arena), descs, n, out, aux);       \
+            else                                                                                   \
+                hipLaunchKernelGGL((k_segments_p<GG, UU, MODE>), dim3(blocks), dim3(256), 0, s,    \
+                                   static_cast<const uint8_t *>(arena), descs, n, out, aux);       \
         } else {                                                                                   \
             hipLaunchKernelGGL((k_segments<GG, UU, MODE>), dim3(blocks), dim3(256), 0, s,          \
                                static_cast<const uint8_t *>(arena), descs, n, out, aux);           \

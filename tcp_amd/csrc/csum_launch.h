@@ -19,7 +19,8 @@ enum Mode : int {
 struct Geometry {
     int lanes; // G: lanes that share one packet (4..64, power of two)
     int loads; // U: 16-byte loads in flight per lane per pass
-    bool persist; // resident grid with descriptor prefetch (k_segments_p)
+    int persist; // 0: one pass per wave; 1: resident grid + descriptor prefetch;
+                 // 2: resident grid, two ranges in flight per wave (k_segments_pp)
 };
 
 Geometry pick_geometry(uint64_t mean_len);

@@ -17,7 +17,7 @@ import golden_io as G
 
 pytestmark = pytest.mark.gpu
 
-GEOMS_SEG = [(g, u, p) for g in (4, 8, 16, 32, 64) for u in (1, 3, 4, 16) for p in (0, 1)]
+GEOMS_SEG = [(g, u, p) for g in (4, 8, 16, 32, 64) for u in (1, 3, 4, 16) for p in (0, 1, 2)]
 GEOMS_IP = [(g, u) for g in (16, 32, 64) for u in (2, 4, 8, 16)]
 
 
@@ -143,7 +143,7 @@ def test_batch_peso_golden(tc, torch, geometry, g, u, p):
     np.testing.assert_array_equal(out.cpu().numpy(), cases["expected"].astype(np.uint16))
 
 
-@pytest.mark.parametrize("p", [0, 1])
+@pytest.mark.parametrize("p", [0, 1, 2])
 def test_batch_segments_golden(tc, torch, geometry, p):
     """pktbuf_checksum16 cases (from the cursor) and even-offset checksum16 cases
     with 16-bit pre_sum, where the two routines agree, as one batch each."""

@@ -663,29 +663,36 @@ static int resident_blocks()
     return blocks;
 }
 
-// Measured on MI355X (scripts/tune.py, profiles/r01/): enough lanes per packet
-// that a pass or two covers a typical packet, few loads per lane; only
-// TSO-size ranges want deep per-lane queues.  Loads are nontemporal (the
-// bytes are read once).
+// Measured on MI355X (scripts/tune.py; profiles/r01/tune.txt, tune2.txt, one
+// process, interleaved rounds).  Interior chunks per range c (edges excluded):
+//   c <= ~136 (<= ~2 KiB, e.g. MTU): 16 lanes, U = ceil(c/16) loads -> one
+//       pass with almost no idle slots (1500 B: G=16, U=6, 91% of the read
+//       probe on the same bytes);
+//   ~2 KiB .. 32 KiB (mixed 64-9000 B, mean 4.5 KiB): 32 lanes x 4 loads,
+//       several passes (96% of the probe);
+//   >= 32 KiB (TSO): one range per wave, 16 loads per lane (97% of the probe).
+// The resident-grid variants (persist 1, 2) measured slower on all three.
 Geometry pick_geometry(uint64_t mean_len)
 {
     Geometry g{32, 4, 0};
     const uint64_t chunks = mean_len / 16 + 1;
-    if (chunks >= 2048) { // >= 32 KiB: one packet per wave, 16 KiB in flight
+    const uint64_t interior = chunks > 2 ? chunks - 2 : 0;
+    if (chunks >= 2048) {
         g.lanes = 64;
         g.loads = 16;
-    } else if (chunks >= 48) { // ~750 B .. 32 KiB (MTU, mixed 64-9000 B)
+    } else if (interior > 128) {
         g.lanes = 32;
         g.loads = 4;
-    } else if (chunks >= 24) {
+    } else if (interior > 32) {
         g.lanes = 16;
-        g.loads = 4;
-    } else if (chunks >= 12) {
+        const uint64_t u = (interior + 15) / 16; // 3..8
+        g.loads = u <= 3 ? 3 : u <= 4 ? 4 : u <= 6 ? 6 : 8;
+    } else if (interior > 8) {
         g.lanes = 8;
         g.loads = 4;
     } else {
         g.lanes = 4;
-        g.loads = 4;
+        g.loads = interior > 4 ? 2 : 1;
     }
     if (const char *s = getenv("TCSUM_G"))
         g.lanes = atoi(s);
@@ -755,7 +762,9 @@ static hipError_t ipv4_u(int G, int U, dim3 grid, const void *arena, const tcsum
                            static_cast<const uint8_t *>(arena), pkts, n, out, flags);              \
         return hipGetLastError();                                                                  \
     }
-#define TCSUM_IP_U(GG) TCSUM_IP(GG, 2) TCSUM_IP(GG, 4) TCSUM_IP(GG, 8) TCSUM_IP(GG, 16)
+#define TCSUM_IP_U(GG)                                                                               \
+    TCSUM_IP(GG, 1) TCSUM_IP(GG, 2) TCSUM_IP(GG, 3) TCSUM_IP(GG, 4) TCSUM_IP(GG, 6) TCSUM_IP(GG, 8)  \
+        TCSUM_IP(GG, 16)
     TCSUM_IP_U(16)
     TCSUM_IP_U(32)
     TCSUM_IP_U(64)

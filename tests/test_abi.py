@@ -90,11 +90,13 @@ def test_pktbuf_cursor_walk_on_host():
 
 def test_geometry_choice(libpath):
     from tcp_amd import pick_geometry
-    assert pick_geometry(1500) == (32, 4)
+    assert pick_geometry(1500) == (16, 6)
     assert pick_geometry(4500) == (32, 4)
     assert pick_geometry(65536) == (64, 16)
-    g, u = pick_geometry(64)
-    assert g == 4
+    assert pick_geometry(64) == (4, 1)
+    for n in range(0, 70000, 37):  # every choice is an instantiated kernel
+        g, u = pick_geometry(n)
+        assert g in (4, 8, 16, 32, 64) and u in (1, 2, 3, 4, 6, 8, 16)
 
 
 def test_device_count_without_gpu(libpath):

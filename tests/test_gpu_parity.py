@@ -18,7 +18,7 @@ import golden_io as G
 pytestmark = pytest.mark.gpu
 
 GEOMS_SEG = [(g, u, p) for g in (4, 8, 16, 32, 64) for u in (1, 3, 4, 16) for p in (0, 1, 2)]
-GEOMS_IP = [(g, u) for g in (16, 32, 64) for u in (2, 4, 8, 16)]
+GEOMS_IP = [(g, u) for g in (16, 32, 64) for u in (1, 2, 3, 4, 6, 8, 16)]
 
 
 @pytest.fixture(scope="module")
@@ -182,6 +182,31 @@ def test_batch_ipv4_golden(tc, torch, geometry, g, u):
     np.testing.assert_array_equal(out & 0xFFFF, cases["ip"])
     np.testing.assert_array_equal(out >> 16, cases["l4"])
     np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+
+
+@pytest.mark.parametrize("mean", [0, 64, 300, 1500, 9000, 70000])
+def test_batch_ipv4_every_picked_geometry(tc, torch, mean):
+    """The length hint only changes the lane mapping, never the result."""
+    cases, ipool = G.ipv4_cases()
+    arena = to_dev(torch, ipool)
+    pk = np.zeros(cases.size, tc.PKT_DTYPE)
+    pk["offset"] = cases["pool_off"]
+    pk["len"] = cases["frame_len"]
+    out, flags = tc.batch_ipv4(arena, tc.descs_to_device(pk), pk.size, mean * pk.size)
+    out = out.cpu().numpy()
+    np.testing.assert_array_equal(out & 0xFFFF, cases["ip"])
+    np.testing.assert_array_equal(out >> 16, cases["l4"])
+    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+
+
+@pytest.mark.parametrize("mean", [0, 20, 64, 300, 1500, 9000, 70000])
+def test_batch_peso_every_picked_geometry(tc, torch, mean):
+    pool = G.pool()
+    cases, _ = G.peso_cases()
+    arena = to_dev(torch, pool)
+    d = peso_descs(tc, cases)
+    out = tc.batch_peso(arena, tc.descs_to_device(d), d.size, mean * d.size)
+    np.testing.assert_array_equal(out.cpu().numpy(), cases["expected"].astype(np.uint16))
 
 
 def test_ipv4_odd_arena_base(tc, torch):

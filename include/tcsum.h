@@ -37,6 +37,7 @@ extern "C" {
 #define TCSUM_ERR_MEM (-2)       /* NET_ERR_MEM: allocation failed */
 #define TCSUM_ERR_SIZE (-5)      /* NET_ERR_SIZE */
 #define TCSUM_ERR_PARAM (-7)     /* NET_ERR_PARAM: bad argument */
+#define TCSUM_ERR_BROKEN (-13)   /* NET_ERR_BROKEN: checksum mismatch (rx verdicts) */
 #define TCSUM_ERR_NOT_SUPPORT (-11) /* NET_ERR_NOT_SUPPORT: no usable gfx950 device */
 
 /* ------------------------------------------------------------ descriptors */
@@ -76,6 +77,9 @@ typedef struct tcsum_pkt {
 #define TCSUM_PKT_BAD_TOTLEN 0x04u  /* total_len < 20, > len, < ihl*4 (ipv4.c:236) */
 #define TCSUM_PKT_PROTO_OTHER 0x08u /* not TCP/UDP/ICMP: l4 result is 0 */
 #define TCSUM_PKT_SHORT 0x10u       /* len < 20: both results are 0 */
+#define TCSUM_PKT_FRAGMENT 0x20u    /* MF or fragment offset: the L4 checksum spans the
+                                       datagram, so tx fill / rx verify leave it (ipv4.c:506) */
+#define TCSUM_PKT_L4_SHORT 0x40u    /* L4 shorter than its header (TCP 20, UDP 8, ICMP 4 B) */
 
 /* ------------------------------------------------ device-resident batches */
 
@@ -102,6 +106,33 @@ int tcsum_batch_peso(const void *arena /*[dev]*/, const tcsum_peso_t *segs /*[de
 int tcsum_batch_ipv4(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/,
                      uint32_t n, uint32_t *out /*[dev]*/, uint8_t *flags /*[dev] or NULL*/,
                      uint64_t total_bytes_hint, void *stream);
+
+/* Batched tx fill, in place in the arena: for every
+ * well-formed packet the checksum fields are read as zero and the values the
+ * stack's tx path stores are written into them:
+ *   IPv4 header checksum (bytes 10-11)      ipv4.c:643,656 (fragments too)
+ *   TCP checksum (L4 + 16)                  tcp_out.c:19-20
+ *   UDP checksum (L4 + 6; 0 is stored as 0) udp.c:320-321
+ *   ICMP checksum (L4 + 2)                  icmpv4.c:45-58
+ * L4 fields are left alone for fragments and short L4s; nothing is written
+ * for SHORT / BAD_* packets.  out (ip | l4 << 16) and flags may be NULL. */
+int tcsum_batch_ipv4_tx_fill(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,
+                             uint32_t *out /*[dev] or NULL*/, uint8_t *flags /*[dev] or NULL*/,
+                             uint64_t total_bytes_hint, void *stream);
+
+/* Batched rx verify: verdict[i] = the net_err_t the
+ * reference's receive path returns from its size and checksum gates, in its
+ * order: frame < 20 -> SIZE; version != 4 -> NOT_SUPPORT; IHL/total length ->
+ * SIZE (ipv4.c:222-239); stored header checksum != 0 and wrong -> BROKEN
+ * (ipv4.c:241-249); fragments -> OK (L4 is checked after reassembly);
+ * L4 shorter than its header -> SIZE; stored TCP/UDP checksum != 0 and wrong
+ * -> BROKEN (tcp_in.c:77-85, udp.c:407-415); ICMP -> OK unless total <= 21
+ * (its checksum test cannot fail in the reference, icmpv4.c:31-43,71-77);
+ * otherwise OK.  Socket lookup and routing are not modelled.  out and flags
+ * may be NULL. */
+int tcsum_batch_ipv4_rx_verify(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/,
+                               uint32_t n, int8_t *verdict /*[dev]*/, uint32_t *out /*[dev] or NULL*/,
+                               uint8_t *flags /*[dev] or NULL*/, uint64_t total_bytes_hint, void *stream);
 
 /* --------------------------------------------------- host-resident batches */
 

@@ -120,6 +120,30 @@ uint16_t orc_checksum_peso(const uint8_t *seg, uint32_t len,
 #define F_BAD_TOTLEN 0x04u
 #define F_PROTO_OTHER 0x08u
 #define F_SHORT 0x10u
+#define F_FRAGMENT 0x20u
+#define F_L4_SHORT 0x40u
+
+/* net_err_t values (net/net/net_err.h) */
+#define E_SIZE (-5)
+#define E_NOT_SUPPORT (-11)
+#define E_BROKEN (-13)
+
+/* L4 checksum field offset and minimum header, by protocol. */
+static int l4_field(uint8_t proto, uint32_t *field, uint32_t *min_len)
+{
+    switch (proto) {
+    case 6: *field = 16; *min_len = 20; return 1;  /* tcp_hdr_t.checksum, tcp.h:71 */
+    case 17: *field = 6; *min_len = 8; return 1;   /* udp_hdr_t.checksum, udp.h:24 */
+    case 1: *field = 2; *min_len = 4; return 1;    /* icmpv4_hdr_t.checksum, icmpv4.h:28 */
+    default: return 0;
+    }
+}
+
+static int is_fragment(const uint8_t *pkt)
+{
+    /* frag_all after ntohs: offset = low 13 bits, more = bit 13 (ipv4.h:42-56) */
+    return (pkt[6] & 0x20) || (((pkt[6] & 0x1F) << 8) | pkt[7]);
+}
 
 void orc_ipv4_pair(const uint8_t *pkt, uint32_t frame_len, uint16_t *ip_out,
                    uint16_t *l4_out, uint8_t *flags_out)
@@ -142,6 +166,8 @@ void orc_ipv4_pair(const uint8_t *pkt, uint32_t frame_len, uint16_t *ip_out,
         flags |= F_BAD_HDRLEN;
     if (tl < 20 || tl > frame_len || tl < ihl4) /* ipv4.c:236 */
         flags |= F_BAD_TOTLEN;
+    if (is_fragment(pkt))
+        flags |= F_FRAGMENT;
 
     uint32_t hl = ihl4 < 20 ? 20 : ihl4;
     if (hl > frame_len)
@@ -154,6 +180,9 @@ void orc_ipv4_pair(const uint8_t *pkt, uint32_t frame_len, uint16_t *ip_out,
 
     const uint8_t *l4 = pkt + hl;
     uint32_t l4len = end - hl;
+    uint32_t fld, minl;
+    if (l4_field(proto, &fld, &minl) && l4len < minl)
+        flags |= F_L4_SHORT;
     if (proto == 6 || proto == 17) { /* tcp_in.c:80 / udp.c:410 */
         *l4_out = orc_checksum_peso(l4, l4len, pkt + 16, pkt + 12, proto);
     } else if (proto == 1) { /* icmpv4.c:36 */
@@ -163,6 +192,69 @@ void orc_ipv4_pair(const uint8_t *pkt, uint32_t frame_len, uint16_t *ip_out,
         flags |= F_PROTO_OTHER;
     }
     *flags_out = flags;
+}
+
+uint8_t orc_ipv4_tx_fill(uint8_t *pkt, uint32_t frame_len)
+{
+    uint16_t ip, l4;
+    uint8_t flags;
+    orc_ipv4_pair(pkt, frame_len, &ip, &l4, &flags); /* for the flags */
+    if (flags & (F_SHORT | F_BAD_VERSION | F_BAD_HDRLEN | F_BAD_TOTLEN))
+        return flags;
+    uint32_t hl = (uint32_t)(pkt[0] & 0x0F) * 4u;
+    uint32_t tl = ((uint32_t)pkt[2] << 8) | pkt[3];
+    uint8_t proto = pkt[9];
+    uint32_t fld, minl;
+    /* L4 first, as the stack does (send_out/udp_out run before ipv4_out) */
+    if (!(flags & (F_FRAGMENT | F_L4_SHORT)) && l4_field(proto, &fld, &minl)) {
+        uint8_t *l4p = pkt + hl;
+        uint32_t l4len = tl - hl;
+        l4p[fld] = l4p[fld + 1] = 0; /* tcp_out.c:19, udp.c:320, icmpv4.c:58 */
+        uint16_t v = proto == 1 ? orc_flat_checksum16(l4p, l4len, 0, 1)
+                                : orc_checksum_peso(l4p, l4len, pkt + 16, pkt + 12, proto);
+        memcpy(l4p + fld, &v, 2); /* stored in host order, like the struct field */
+    }
+    pkt[10] = pkt[11] = 0; /* ipv4.c:643 */
+    uint16_t h = orc_checksum16(0, pkt, (uint16_t)hl, 0, 1);
+    memcpy(pkt + 10, &h, 2); /* ipv4.c:656 */
+    return flags;
+}
+
+int8_t orc_ipv4_rx_verify(const uint8_t *pkt, uint32_t frame_len, uint8_t *flags_out)
+{
+    uint16_t ip, l4;
+    uint8_t flags;
+    orc_ipv4_pair(pkt, frame_len, &ip, &l4, &flags);
+    *flags_out = flags;
+    if (frame_len < 20) /* pktbuf_set_cont(buf, 20), ipv4.c:475 */
+        return E_SIZE;
+    uint32_t ihl4 = (uint32_t)(pkt[0] & 0x0F) * 4u;
+    uint32_t tl = ((uint32_t)pkt[2] << 8) | pkt[3];
+    if ((pkt[0] >> 4) != 4) /* ipv4.c:222 */
+        return E_NOT_SUPPORT;
+    if (ihl4 < 20) /* ipv4.c:229 */
+        return E_SIZE;
+    if (tl < 20 || frame_len < tl) /* ipv4.c:236 */
+        return E_SIZE;
+    if (ihl4 > tl) /* the reference would sum past the header (UB); defined here */
+        return E_SIZE;
+    if ((pkt[10] | pkt[11]) && ip != 0) /* ipv4.c:241-249 */
+        return E_BROKEN;
+    if (flags & F_FRAGMENT) /* ipv4.c:506: reassembly first; L4 is checked per datagram */
+        return 0;
+    uint8_t proto = pkt[9];
+    uint32_t fld, minl;
+    if (!l4_field(proto, &fld, &minl))
+        return 0; /* raw_in: no checksum */
+    uint32_t l4len = tl - ihl4;
+    if (l4len < minl) /* pktbuf_set_cont: tcp_in.c:69, udp.c:386, icmpv4.c:68 */
+        return E_SIZE;
+    if (proto == 1)
+        return tl <= 21 ? E_SIZE : 0; /* icmpv4.c:31; the checksum test cannot fail (A10) */
+    const uint8_t *f = pkt + ihl4 + fld;
+    if ((f[0] | f[1]) && l4 != 0) /* tcp_in.c:77-85, udp.c:407-415 */
+        return E_BROKEN;
+    return 0;
 }
 
 /* ---------------------------------------------------------------- batches */
@@ -189,12 +281,23 @@ static void run_range(const job_t *j)
             const orc_peso_t *d = (const orc_peso_t *)j->descs + i;
             ((uint16_t *)j->out)[i] = orc_checksum_peso(j->arena + d->offset, d->len,
                                                         d->dst, d->src, d->protocol);
-        } else {
+        } else if (j->kind == 2) {
             const orc_pkt_t *d = (const orc_pkt_t *)j->descs + i;
             uint16_t ip, l4;
             uint8_t fl;
             orc_ipv4_pair(j->arena + d->offset, d->len, &ip, &l4, &fl);
             ((uint32_t *)j->out)[i] = (uint32_t)ip | ((uint32_t)l4 << 16);
+            if (j->flags)
+                j->flags[i] = fl;
+        } else if (j->kind == 3) {
+            const orc_pkt_t *d = (const orc_pkt_t *)j->descs + i;
+            uint8_t fl = orc_ipv4_tx_fill((uint8_t *)j->arena + d->offset, d->len);
+            if (j->flags)
+                j->flags[i] = fl;
+        } else {
+            const orc_pkt_t *d = (const orc_pkt_t *)j->descs + i;
+            uint8_t fl;
+            ((int8_t *)j->out)[i] = orc_ipv4_rx_verify(j->arena + d->offset, d->len, &fl);
             if (j->flags)
                 j->flags[i] = fl;
         }
@@ -247,6 +350,20 @@ void orc_batch_ipv4(const uint8_t *arena, const orc_pkt_t *pkts, uint32_t n,
                     uint32_t *out, uint8_t *flags, int nthreads)
 {
     job_t j = {2, arena, pkts, 0, 0, out, flags, 0};
+    run_batch(j, n, nthreads);
+}
+
+void orc_batch_ipv4_tx_fill(uint8_t *arena, const orc_pkt_t *pkts, uint32_t n,
+                            uint8_t *flags, int nthreads)
+{
+    job_t j = {3, arena, pkts, 0, 0, NULL, flags, 0};
+    run_batch(j, n, nthreads);
+}
+
+void orc_batch_ipv4_rx_verify(const uint8_t *arena, const orc_pkt_t *pkts, uint32_t n,
+                              int8_t *verdict, uint8_t *flags, int nthreads)
+{
+    job_t j = {4, arena, pkts, 0, 0, verdict, flags, 0};
     run_batch(j, n, nthreads);
 }
 

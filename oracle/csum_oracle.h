@@ -96,6 +96,22 @@ typedef struct orc_pkt {
 void orc_ipv4_pair(const uint8_t *pkt, uint32_t frame_len, uint16_t *ip_out,
                    uint16_t *l4_out, uint8_t *flags_out);
 
+/* Batched tx fill of one packet, in place: zero the
+ * checksum fields and store the values the stack's tx path stores:
+ *   IPv4 header  ipv4.c:643,656  (every packet, fragments included)
+ *   TCP          tcp_out.c:19-20 (non-fragments, L4 >= 20 B)
+ *   UDP          udp.c:320-321   (non-fragments, L4 >= 8 B; 0 stays 0)
+ *   ICMP         icmpv4.c:45-52  (non-fragments, L4 >= 4 B)
+ * Nothing is written for a packet with SHORT/BAD_* flags.  Returns flags. */
+uint8_t orc_ipv4_tx_fill(uint8_t *pkt, uint32_t frame_len);
+
+/* Batched rx verify of one packet: the net_err_t the
+ * reference's receive path returns from its size and checksum gates, in its
+ * order -- ipv4_in/is_pkt_ok (ipv4.c:475-249), then for non-fragments
+ * tcp_in (tcp_in.c:69-85), udp_in (udp.c:386-415, socket lookup not modelled),
+ * icmpv4_in (icmpv4.c:29-43,71-77: its checksum test never fails, A10). */
+int8_t orc_ipv4_rx_verify(const uint8_t *pkt, uint32_t frame_len, uint8_t *flags_out);
+
 /* Batch forms over an arena; nthreads <= 1 runs on the calling thread. */
 void orc_batch_segments(const uint8_t *arena, const orc_seg_t *segs, uint32_t n,
                         uint16_t *out, int complement, int nthreads);
@@ -103,6 +119,10 @@ void orc_batch_peso(const uint8_t *arena, const orc_peso_t *segs, uint32_t n,
                     uint16_t *out, int nthreads);
 void orc_batch_ipv4(const uint8_t *arena, const orc_pkt_t *pkts, uint32_t n,
                     uint32_t *out, uint8_t *flags, int nthreads);
+void orc_batch_ipv4_tx_fill(uint8_t *arena, const orc_pkt_t *pkts, uint32_t n,
+                            uint8_t *flags, int nthreads);
+void orc_batch_ipv4_rx_verify(const uint8_t *arena, const orc_pkt_t *pkts, uint32_t n,
+                              int8_t *verdict, uint8_t *flags, int nthreads);
 
 /* Synthetic data shared with the device generator (tcsum_synth_fill):
  * 64-bit word w of the stream is splitmix64(seed + w), stored little-endian. */

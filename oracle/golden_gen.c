@@ -362,78 +362,174 @@ static void peso_cases(int n, int nbig)
 }
 
 /* ------------------------------------------------------------ IPv4 packets */
+/* The per-packet definitions of tcsum_batch_ipv4 / _tx_fill / _rx_verify
+ * (include/tcsum.h), with every checksum value taken from the reference's own
+ * checksum16 / checksum_peso / pktbuf_checksum16, and the call-site control
+ * flow of ipv4.c:475-515 / is_pkt_ok ipv4.c:220-250, tcp_out.c:19-20,
+ * udp.c:320-321, icmpv4.c:45-58, tcp_in.c:69-85, udp.c:386-415,
+ * icmpv4.c:29-43,71-77 restated. */
 
 #define IPV4_POOL_CAP (12u << 20)
 static uint8_t ipool[IPV4_POOL_CAP];
+
+#define F_BAD_VERSION 0x01u
+#define F_BAD_HDRLEN 0x02u
+#define F_BAD_TOTLEN 0x04u
+#define F_PROTO_OTHER 0x08u
+#define F_SHORT 0x10u
+#define F_FRAGMENT 0x20u
+#define F_L4_SHORT 0x40u
+
+static int l4_field(uint8_t proto, uint32_t *field, uint32_t *min_len)
+{
+    switch (proto) {
+    case 6: *field = 16; *min_len = 20; return 1; /* tcp.h:71  (sizeof tcp_hdr_t = 20) */
+    case 17: *field = 6; *min_len = 8; return 1;  /* udp.h:24  (sizeof udp_hdr_t = 8) */
+    case 1: *field = 2; *min_len = 4; return 1;   /* icmpv4.h:28 (sizeof icmpv4_hdr_t = 4) */
+    default: return 0;
+    }
+}
+
+static void ref_pair(const uint8_t *p, uint32_t frame, uint32_t *ip, uint32_t *l4, uint32_t *flags)
+{
+    *ip = *l4 = *flags = 0;
+    if (frame < 20) {
+        *flags = F_SHORT;
+        return;
+    }
+    uint32_t ver = p[0] >> 4, ihl4 = (uint32_t)(p[0] & 15) * 4;
+    uint32_t tl = ((uint32_t)p[2] << 8) | p[3];
+    if (ver != 4)
+        *flags |= F_BAD_VERSION;
+    if (ihl4 < 20 || ihl4 > frame)
+        *flags |= F_BAD_HDRLEN;
+    if (tl < 20 || tl > frame || tl < ihl4)
+        *flags |= F_BAD_TOTLEN;
+    if ((p[6] & 0x20) || (((p[6] & 0x1F) << 8) | p[7]))
+        *flags |= F_FRAGMENT;
+    uint32_t hl = ihl4 < 20 ? 20 : ihl4;
+    if (hl > frame)
+        hl = frame;
+    uint32_t end = tl < hl ? hl : tl;
+    if (end > frame)
+        end = frame;
+    *ip = checksum16(0, (void *)p, (uint16_t)hl, 0, 1);
+    uint8_t proto = p[9];
+    uint32_t fld, minl;
+    if (l4_field(proto, &fld, &minl) && end - hl < minl)
+        *flags |= F_L4_SHORT;
+    if (proto == 6 || proto == 17)
+        *l4 = ref_peso_flat(p + hl, (int)(end - hl), p + 16, p + 12, proto);
+    else if (proto == 1)
+        *l4 = ref_pktbuf_flat(p + hl, (int)(end - hl), 0, 1);
+    else
+        *flags |= F_PROTO_OTHER;
+}
+
+static uint32_t ref_tx_fill(uint8_t *p, uint32_t frame)
+{
+    uint32_t ip, l4, flags;
+    ref_pair(p, frame, &ip, &l4, &flags);
+    if (flags & (F_SHORT | F_BAD_VERSION | F_BAD_HDRLEN | F_BAD_TOTLEN))
+        return flags;
+    uint32_t hl = (uint32_t)(p[0] & 15) * 4, tl = ((uint32_t)p[2] << 8) | p[3];
+    uint8_t proto = p[9];
+    uint32_t fld, minl;
+    if (!(flags & (F_FRAGMENT | F_L4_SHORT)) && l4_field(proto, &fld, &minl)) {
+        uint8_t *l4p = p + hl;
+        l4p[fld] = l4p[fld + 1] = 0;
+        uint16_t v = proto == 1 ? ref_pktbuf_flat(l4p, (int)(tl - hl), 0, 1)
+                                : ref_peso_flat(l4p, (int)(tl - hl), p + 16, p + 12, proto);
+        memcpy(l4p + fld, &v, 2);
+    }
+    p[10] = p[11] = 0;
+    uint16_t h = checksum16(0, p, (uint16_t)hl, 0, 1);
+    memcpy(p + 10, &h, 2);
+    return flags;
+}
+
+static int32_t ref_rx_verify(const uint8_t *p, uint32_t frame, uint32_t *flags)
+{
+    uint32_t ip, l4;
+    ref_pair(p, frame, &ip, &l4, flags);
+    if (frame < 20)
+        return NET_ERR_SIZE;
+    uint32_t ihl4 = (uint32_t)(p[0] & 15) * 4, tl = ((uint32_t)p[2] << 8) | p[3];
+    if ((p[0] >> 4) != 4)
+        return NET_ERR_NOT_SUPPORT;
+    if (ihl4 < 20 || tl < 20 || frame < tl || ihl4 > tl)
+        return NET_ERR_SIZE;
+    if ((p[10] | p[11]) && ip != 0)
+        return NET_ERR_BROKEN;
+    if (*flags & F_FRAGMENT)
+        return NET_ERR_OK;
+    uint8_t proto = p[9];
+    uint32_t fld, minl;
+    if (!l4_field(proto, &fld, &minl))
+        return NET_ERR_OK;
+    if (tl - ihl4 < minl)
+        return NET_ERR_SIZE;
+    if (proto == 1)
+        return tl <= 21 ? NET_ERR_SIZE : NET_ERR_OK;
+    const uint8_t *f = p + ihl4 + fld;
+    if ((f[0] | f[1]) && l4 != 0)
+        return NET_ERR_BROKEN;
+    return NET_ERR_OK;
+}
+
+/* A random packet: mostly well formed, with the odd broken field. */
+static uint32_t make_packet(uint8_t *p, uint32_t max_frame)
+{
+    uint32_t fr = rnd_below(100);
+    uint32_t frame = fr < 2 ? rnd_below(20) : fr < 12 ? 20 + rnd_below(100)
+                                                      : 64 + rnd_below(max_frame - 64 + 1);
+    for (uint32_t k = 0; k < frame; k++)
+        p[k] = (uint8_t)rnd();
+    if (frame < 20)
+        return frame;
+    uint32_t ihl = rnd_below(100) < 80 ? 5 : 5 + rnd_below(11);
+    if (ihl * 4 > frame)
+        ihl = 5;
+    uint32_t vr = rnd_below(100);
+    uint32_t ver = vr < 96 ? 4 : vr < 98 ? 6 : rnd_below(16);
+    if (rnd_below(100) < 2)
+        ihl = rnd_below(5);
+    p[0] = (uint8_t)((ver << 4) | ihl);
+    uint32_t tr = rnd_below(100), tl;
+    if (tr < 85)
+        tl = frame;
+    else if (tr < 93)
+        tl = ihl * 4 + rnd_below(frame - ihl * 4 + 1);
+    else
+        tl = rnd_below(0x10000);
+    p[2] = (uint8_t)(tl >> 8);
+    p[3] = (uint8_t)tl;
+    uint32_t fg = rnd_below(100); /* fragments: MF and/or offset */
+    p[6] = fg < 85 ? 0x40 : (uint8_t)rnd(); /* DF, or random flag/offset bits */
+    p[7] = fg < 85 ? 0 : (uint8_t)rnd();
+    uint32_t pr = rnd_below(100);
+    p[9] = pr < 42 ? 6 : pr < 84 ? 17 : pr < 92 ? 1 : (uint8_t)rnd();
+    p[10] = p[11] = 0;
+    return frame;
+}
 
 static void ipv4_cases(int n)
 {
     FILE *f = open_out("ipv4_cases.bin");
     uint32_t at = 0;
     for (int i = 0; i < n; i++) {
-        uint32_t fr = rnd_below(100);
-        uint32_t frame = fr < 2 ? rnd_below(20) : fr < 10 ? 20 + rnd_below(100)
-                                                          : 64 + rnd_below(9000 - 64 + 1);
-        if (at + frame + 64 > IPV4_POOL_CAP)
-            break;
         uint8_t *p = ipool + at;
-        for (uint32_t k = 0; k < frame; k++)
-            p[k] = (uint8_t)rnd();
-        if (frame >= 20) {
-            uint32_t ihl = rnd_below(100) < 80 ? 5 : 5 + rnd_below(11);
-            if (ihl * 4 > frame)
-                ihl = 5;
-            uint32_t vr = rnd_below(100);
-            uint32_t ver = vr < 96 ? 4 : vr < 98 ? 6 : rnd_below(16);
-            if (rnd_below(100) < 2)
-                ihl = rnd_below(5); /* < 20 bytes: is_pkt_ok rejects */
-            p[0] = (uint8_t)((ver << 4) | ihl);
-            uint32_t tr = rnd_below(100), tl;
-            if (tr < 85)
-                tl = frame;
-            else if (tr < 93)
-                tl = ihl * 4 + rnd_below(frame - ihl * 4 + 1);
-            else
-                tl = rnd_below(0x10000);
-            p[2] = (uint8_t)(tl >> 8);
-            p[3] = (uint8_t)tl;
-            uint32_t pr = rnd_below(100);
-            p[9] = pr < 42 ? 6 : pr < 84 ? 17 : pr < 92 ? 1 : (uint8_t)rnd();
-            uint32_t hl = ihl * 4 < 20 ? 20 : ihl * 4;
-            p[10] = p[11] = 0;
-            if (rnd_below(2)) { /* rx-style: header checksum already filled */
-                uint16_t c = checksum16(0, p, (uint16_t)hl, 0, 1);
-                memcpy(p + 10, &c, 2);
-            }
+        if (at + 9000 + 64 > IPV4_POOL_CAP)
+            break;
+        uint32_t frame = make_packet(p, 9000);
+        if (frame >= 20 && rnd_below(2)) { /* rx-style: header checksum already filled */
+            uint32_t hl = (uint32_t)(p[0] & 15) * 4;
+            hl = hl < 20 ? 20 : hl;
+            uint16_t c = checksum16(0, p, (uint16_t)hl, 0, 1);
+            memcpy(p + 10, &c, 2);
         }
-        /* expected values: composed from the reference's own routines */
-        uint32_t ip = 0, l4 = 0, flags = 0;
-        if (frame < 20) {
-            flags = 0x10;
-        } else {
-            uint32_t ver = p[0] >> 4, ihl4 = (uint32_t)(p[0] & 15) * 4;
-            uint32_t tl = ((uint32_t)p[2] << 8) | p[3];
-            if (ver != 4)
-                flags |= 0x01;
-            if (ihl4 < 20 || ihl4 > frame)
-                flags |= 0x02;
-            if (tl < 20 || tl > frame || tl < ihl4)
-                flags |= 0x04;
-            uint32_t hl = ihl4 < 20 ? 20 : ihl4;
-            if (hl > frame)
-                hl = frame;
-            uint32_t end = tl < hl ? hl : tl;
-            if (end > frame)
-                end = frame;
-            ip = checksum16(0, p, (uint16_t)hl, 0, 1);
-            uint8_t proto = p[9];
-            if (proto == 6 || proto == 17)
-                l4 = ref_peso_flat(p + hl, (int)(end - hl), p + 16, p + 12, proto);
-            else if (proto == 1)
-                l4 = ref_pktbuf_flat(p + hl, (int)(end - hl), 0, 1);
-            else
-                flags |= 0x08;
-        }
+        uint32_t ip, l4, flags;
+        ref_pair(p, frame, &ip, &l4, &flags);
         put_u32(f, at);
         put_u32(f, frame);
         put_u32(f, ip);
@@ -443,6 +539,88 @@ static void ipv4_cases(int n)
     }
     fclose(f);
     FILE *fp = open_out("ipv4_pool.bin");
+    fwrite(ipool, 1, at + 64, fp);
+    fclose(fp);
+}
+
+/* tx: packets as the stack hands them over (fields arbitrary -- the fill zeroes
+ * them); expected = the whole pool after the reference's fill. */
+static void ipv4_tx_cases(int n)
+{
+    uint32_t *offs = (uint32_t *)malloc(sizeof(uint32_t) * 2 * (size_t)n);
+    uint32_t at = 0;
+    for (int i = 0; i < n; i++) {
+        uint8_t *p = ipool + at;
+        uint32_t frame = make_packet(p, 3000);
+        if (frame >= 20 && rnd_below(3) == 0) { /* stale values in the fields */
+            p[10] = (uint8_t)rnd();
+            p[11] = (uint8_t)rnd();
+        }
+        offs[2 * i] = at;
+        offs[2 * i + 1] = frame;
+        at += frame + (rnd_below(4) == 0 ? rnd_below(16) : 0);
+    }
+    const uint32_t total = at + 64;
+    FILE *fin = open_out("ipv4_tx_in.bin");
+    fwrite(ipool, 1, total, fin);
+    fclose(fin);
+    FILE *f = open_out("ipv4_tx_cases.bin");
+    for (int i = 0; i < n; i++) {
+        uint32_t flags = ref_tx_fill(ipool + offs[2 * i], offs[2 * i + 1]);
+        put_u32(f, offs[2 * i]);
+        put_u32(f, offs[2 * i + 1]);
+        put_u32(f, flags);
+    }
+    fclose(f);
+    FILE *fo = open_out("ipv4_tx_out.bin");
+    fwrite(ipool, 1, total, fo);
+    fclose(fo);
+    free(offs);
+}
+
+/* rx: well-formed packets filled by the reference's tx path, then damaged in
+ * the ways a receiver meets: payload or header bit flips, zeroed (skipped)
+ * checksums, fragments, short L4, ICMP with a wrong checksum (still accepted,
+ * A10). */
+static void ipv4_rx_cases(int n)
+{
+    FILE *f = open_out("ipv4_rx_cases.bin");
+    uint32_t at = 0;
+    for (int i = 0; i < n; i++) {
+        uint8_t *p = ipool + at;
+        uint32_t frame = make_packet(p, 3000);
+        if (frame >= 20)
+            ref_tx_fill(p, frame);
+        uint32_t d = rnd_below(100);
+        if (frame >= 24) {
+            uint32_t hl = (uint32_t)(p[0] & 15) * 4;
+            hl = hl < 20 ? 20 : hl;
+            uint32_t tl = ((uint32_t)p[2] << 8) | p[3];
+            if (d < 15 && tl > hl && tl <= frame) /* payload bit flip */
+                p[hl + rnd_below(tl - hl)] ^= (uint8_t)(1u << rnd_below(8));
+            else if (d < 25) /* header bit flip (not the version/IHL nibble) */
+                p[1 + rnd_below(19)] ^= (uint8_t)(1u << rnd_below(8));
+            else if (d < 35 && tl >= hl + 18 && tl <= frame) { /* zeroed L4 checksum + flip */
+                uint32_t fld, minl;
+                if (l4_field(p[9], &fld, &minl) && hl + fld + 2 <= tl) {
+                    p[hl + fld] = p[hl + fld + 1] = 0;
+                    p[hl + rnd_below(tl - hl)] ^= 0x10;
+                }
+            } else if (d < 40) { /* zeroed IP checksum + header flip */
+                p[10] = p[11] = 0;
+                p[12 + rnd_below(8)] ^= 0x01;
+            }
+        }
+        uint32_t flags;
+        int32_t v = ref_rx_verify(p, frame, &flags);
+        put_u32(f, at);
+        put_u32(f, frame);
+        put_u32(f, (uint32_t)v);
+        put_u32(f, flags);
+        at += frame + (rnd_below(4) == 0 ? rnd_below(16) : 0);
+    }
+    fclose(f);
+    FILE *fp = open_out("ipv4_rx_pool.bin");
     fwrite(ipool, 1, at + 64, fp);
     fclose(fp);
 }
@@ -458,6 +636,8 @@ int main(int argc, char **argv)
     pktbuf_cases(1500);
     peso_cases(1200, 48);
     ipv4_cases(500);
+    ipv4_tx_cases(400);
+    ipv4_rx_cases(600);
     printf("golden vectors written to %s\n", outdir);
     return 0;
 }

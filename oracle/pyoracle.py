@@ -66,6 +66,14 @@ def lib() -> ctypes.CDLL:
         L.orc_batch_ipv4.argtypes = [u8p, u8p, ctypes.c_uint32, u8p, u8p, ctypes.c_int]
         for f in ("orc_batch_segments", "orc_batch_peso", "orc_batch_ipv4"):
             getattr(L, f).restype = None
+        L.orc_ipv4_tx_fill.argtypes = [u8p, ctypes.c_uint32]
+        L.orc_ipv4_tx_fill.restype = ctypes.c_uint8
+        L.orc_ipv4_rx_verify.argtypes = [u8p, ctypes.c_uint32, u8p]
+        L.orc_ipv4_rx_verify.restype = ctypes.c_int8
+        L.orc_batch_ipv4_tx_fill.argtypes = [u8p, u8p, ctypes.c_uint32, u8p, ctypes.c_int]
+        L.orc_batch_ipv4_tx_fill.restype = None
+        L.orc_batch_ipv4_rx_verify.argtypes = [u8p, u8p, ctypes.c_uint32, u8p, u8p, ctypes.c_int]
+        L.orc_batch_ipv4_rx_verify.restype = None
         L.orc_synth_fill.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
         L.orc_synth_fill.restype = None
         L.orc_time_peso.argtypes = [ctypes.c_void_p, u8p, u8p, ctypes.c_uint32, ctypes.c_int,
@@ -154,6 +162,23 @@ def batch_ipv4(arena: np.ndarray, pkts: np.ndarray, nthreads: int = 8):
     flags = np.zeros(pkts.size, np.uint8)
     lib().orc_batch_ipv4(_ptr(arena), _ptr(pkts), pkts.size, _ptr(out), _ptr(flags), nthreads)
     return out, flags
+
+
+def batch_ipv4_tx_fill(arena: np.ndarray, pkts: np.ndarray, nthreads: int = 8) -> np.ndarray:
+    """Fill the checksum fields in place (arena is modified); returns flags."""
+    assert pkts.dtype == PKT_DTYPE and arena.flags["C_CONTIGUOUS"]
+    flags = np.zeros(pkts.size, np.uint8)
+    lib().orc_batch_ipv4_tx_fill(_ptr(arena), _ptr(pkts), pkts.size, _ptr(flags), nthreads)
+    return flags
+
+
+def batch_ipv4_rx_verify(arena: np.ndarray, pkts: np.ndarray, nthreads: int = 8):
+    """(verdict int8 net_err_t, flags) per packet."""
+    assert pkts.dtype == PKT_DTYPE
+    verdict = np.zeros(pkts.size, np.int8)
+    flags = np.zeros(pkts.size, np.uint8)
+    lib().orc_batch_ipv4_rx_verify(_ptr(arena), _ptr(pkts), pkts.size, _ptr(verdict), _ptr(flags), nthreads)
+    return verdict, flags
 
 
 def synth_fill(byte_offset: int, nbytes: int, seed: int) -> np.ndarray:

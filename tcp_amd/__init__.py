@@ -3,7 +3,8 @@
 The product is tcp_amd/libtcsum.so (C ABI: include/tcsum.h,
 include/tcsum_legacy.h); this package is its Python face.
 """
-from .csum import (PESO_DTYPE, PKT_DTYPE, SEG_DTYPE, batch_ipv4, batch_peso, batch_segments,
+from .csum import (PESO_DTYPE, PKT_DTYPE, SEG_DTYPE, batch_ipv4, batch_ipv4_rx_verify, batch_ipv4_tx_fill,
+                   batch_peso, batch_segments,
                    checksum16, checksum_peso, descs_to_device, device_count, host_batch_peso,
                    pick_geometry, pktbuf_checksum16, plat_init, probe_read, synth_fill, synth_ipv4)
 from .pktbuf import IpAddr, PktBuf
@@ -11,6 +12,7 @@ from . import workload
 
 __all__ = [
     "checksum16", "checksum_peso", "pktbuf_checksum16", "batch_segments", "batch_peso", "batch_ipv4",
+    "batch_ipv4_tx_fill", "batch_ipv4_rx_verify",
     "host_batch_peso", "synth_fill", "synth_ipv4", "descs_to_device", "device_count", "pick_geometry",
     "plat_init", "probe_read", "PktBuf", "IpAddr", "SEG_DTYPE", "PESO_DTYPE", "PKT_DTYPE", "workload",
 ]

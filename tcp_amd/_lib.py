@@ -18,6 +18,7 @@ ERR_MEM = -2
 ERR_SIZE = -5
 ERR_PARAM = -7
 ERR_NOT_SUPPORT = -11
+ERR_BROKEN = -13
 
 # (name, restype, argtypes) for every symbol include/*.h declares
 _V, _U16, _U32, _U64, _I, _SZ = (ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64,
@@ -27,6 +28,8 @@ SIGNATURES = {
     "tcsum_batch_segments": (_I, [_V, _V, _U32, _V, _I, _U64, _V]),
     "tcsum_batch_peso": (_I, [_V, _V, _U32, _V, _U64, _V]),
     "tcsum_batch_ipv4": (_I, [_V, _V, _U32, _V, _V, _U64, _V]),
+    "tcsum_batch_ipv4_tx_fill": (_I, [_V, _V, _U32, _V, _V, _U64, _V]),
+    "tcsum_batch_ipv4_rx_verify": (_I, [_V, _V, _U32, _V, _V, _V, _U64, _V]),
     "tcsum_host_batch_peso": (_I, [_I, _V, _U64, _V, _U32, _V]),
     "tcsum_plat_init": (_I, [_I]),
     "tcsum_host_alloc": (_V, [_SZ]),

@@ -316,8 +316,36 @@ int tcsum_batch_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uin
         return TCSUM_OK;
     if (!arena || !pkts || !out)
         return TCSUM_ERR_PARAM;
-    const hipError_t e = tcsum::launch_ipv4(tcsum::pick_geometry(mean_of(total_bytes_hint, n)), arena,
-                                            pkts, n, out, flags, static_cast<hipStream_t>(stream));
+    const hipError_t e = tcsum::launch_ipv4(0, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
+                                            const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts,
+                                            n, out, flags, nullptr, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
+}
+
+int tcsum_batch_ipv4_tx_fill(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out, uint8_t *flags,
+                             uint64_t total_bytes_hint, void *stream)
+{
+    if (n == 0)
+        return TCSUM_OK;
+    if (!arena || !pkts)
+        return TCSUM_ERR_PARAM;
+    const hipError_t e = tcsum::launch_ipv4(1, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
+                                            static_cast<uint8_t *>(arena), pkts, n, out, flags, nullptr,
+                                            static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
+}
+
+int tcsum_batch_ipv4_rx_verify(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, int8_t *verdict,
+                               uint32_t *out, uint8_t *flags, uint64_t total_bytes_hint, void *stream)
+{
+    if (n == 0)
+        return TCSUM_OK;
+    if (!arena || !pkts || !verdict)
+        return TCSUM_ERR_PARAM;
+    // the kernel never writes the arena in this mode
+    const hipError_t e = tcsum::launch_ipv4(2, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
+                                            const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts,
+                                            n, out, flags, verdict, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
 }
 

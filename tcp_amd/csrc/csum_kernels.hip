@@ -389,10 +389,21 @@ __global__ __launch_bounds__(256) void k_segments_pp(const uint8_t *__restrict__
 
 // ---------------------------------------------------------------- IPv4
 //
-// Header and L4 checksum of a captured IPv4 packet in one pass over its bytes
-// (ipv4.c:243 / tcp_in.c:80 / udp.c:410 / icmpv4.c:36).  The 20 fixed header
-// bytes are read as two or three aligned chunks and realigned with
-// v_alignbyte; the data pass accumulates [0, hl) and [hl, end) separately.
+// Both checksums of a captured IPv4 packet in one pass over its bytes, in one
+// of three modes:
+//   IP_SUMS  header + L4 values (ipv4.c:243 / tcp_in.c:80 / udp.c:410 /
+//            icmpv4.c:36) and is_pkt_ok flags;
+//   IP_TX    the stack's tx fill, in place: checksum fields read as zero,
+//            values stored into them (ipv4.c:643,656, tcp_out.c:19-20,
+//            udp.c:320-321, icmpv4.c:45-58);
+//   IP_RX    the stack's rx gates: net_err_t verdict per packet
+//            (ipv4.c:475-515, is_pkt_ok ipv4.c:220-250, tcp_in.c:69-85,
+//            udp.c:386-415, icmpv4.c:29-43,71-77).
+// The 20 fixed header bytes come from two or three aligned chunks realigned
+// with v_alignbyte; the data pass splits every chunk between the header range
+// [0,hl), the L4 range [hl,end) and the 2-byte checksum fields.
+enum IpMode : int { IP_SUMS = 0, IP_TX = 1, IP_RX = 2 };
+
 __device__ __forceinline__ void pick6(uint32_t q, const uint32_t w[12], uint32_t x[6])
 {
 #pragma unroll
@@ -400,49 +411,62 @@ __device__ __forceinline__ void pick6(uint32_t q, const uint32_t w[12], uint32_t
         x[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
 }
 
-template <int G, int U>
-__global__ __launch_bounds__(256) void k_ipv4(const uint8_t *__restrict__ arena,
-                                              const tcsum_pkt_t *__restrict__ pkts, uint32_t n,
-                                              uint32_t *__restrict__ out,
-                                              uint8_t *__restrict__ flags_out)
+// Sum of the chunk's bytes that fall in [r0, r1) (offsets from the chunk base c).
+__device__ __forceinline__ uint32_t region_sum(u32x4 v, int64_t c, int64_t r0, int64_t r1)
+{
+    const int64_t lo = r0 - c, hi = r1 - c;
+    const int a = (int)(lo < 0 ? 0 : (lo > 16 ? 16 : lo));
+    const int b = (int)(hi < 0 ? 0 : (hi > 16 ? 16 : hi));
+    return chunk_sum_masked(0u, v, a, b);
+}
+
+// L4 checksum field offset and minimum header length by protocol
+// (tcp.h:71, udp.h:24, icmpv4.h:28); 0 when the protocol has none here.
+__device__ __forceinline__ uint32_t l4_field(uint32_t proto, uint32_t &min_len)
+{
+    min_len = proto == 6 ? 20u : proto == 17 ? 8u : proto == 1 ? 4u : 0u;
+    return proto == 6 ? 16u : proto == 17 ? 6u : proto == 1 ? 2u : 0u;
+}
+
+template <int G, int U, int IPM>
+__global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
+                                              uint32_t n, uint32_t *__restrict__ out,
+                                              uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out)
 {
     const uint32_t gl = threadIdx.x & (G - 1);
     const uint32_t pk = (blockIdx.x * 256u + threadIdx.x) / G;
     const bool live = pk < n;
 
-    uint64_t off = 0;
-    uint32_t frame = 0;
-    if (live) {
-        off = pkts[pk].offset;
-        frame = pkts[pk].len;
-    }
+    // unconditional loads throughout (dead lanes read descriptor 0 / the zero chunk)
+    const tcsum_pkt_t *dp = pkts + (live ? pk : 0u);
+    const uint64_t off = dp->offset;
+    const uint32_t frame = live ? dp->len : 0u;
     const bool big_enough = frame >= 20;
-    const uint8_t *pp = arena + off;
+    uint8_t *pp = arena + off;
     const uintptr_t start = reinterpret_cast<uintptr_t>(pp);
     const uint32_t s0 = (uint32_t)(start & 15u);
     const u32x4 *base = reinterpret_cast<const u32x4 *>(pp - s0);
 
     // fixed header: bytes [s0, s0 + 20) of base[0..2]
-    u32x4 h0 = u32x4(0u), h1 = u32x4(0u), h2 = u32x4(0u);
-    if (big_enough) {
-        h0 = load16<false>(base);
-        h1 = load16<false>(base + 1);
-        if (s0 > 12)
-            h2 = load16<false>(base + 2);
-    }
+    const u32x4 *hb = big_enough ? base : &g_zero_chunk;
+    const uint32_t h1i = big_enough ? 1u : 0u;
+    const uint32_t h2i = big_enough ? (s0 > 12 ? 2u : 1u) : 0u;
+    const u32x4 h0 = load16<false>(hb);
+    const u32x4 h1 = load16<false>(hb + h1i);
+    const u32x4 h2v = load16<false>(hb + h2i);
+    const u32x4 h2 = s0 > 12 ? h2v : u32x4(0u);
 
-    const uint64_t e_frame = big_enough ? (uint64_t)frame + s0 : 0;
-    const uint32_t nch = (uint32_t)((e_frame + 15) >> 4);
+    const uint32_t nch = big_enough ? (uint32_t)(((uint64_t)frame + s0 + 15) >> 4) : 0u;
+    const u32x4 *dbase = nch ? base : &g_zero_chunk;
+    const uint32_t dlast = nch ? nch - 1u : 0u;
 
-    // Issue the first pass of data loads before the header is consumed, so the
-    // header's latency overlaps them (vmcnt counts in issue order).
+    // first pass of data loads before the header is consumed: its latency
+    // overlaps them (vmcnt counts in issue order)
     u32x4 v[U];
-    if (nch) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t idx = u * G + gl;
-            v[u] = load16<true>(base + (idx < nch ? idx : nch - 1));
-        }
+    for (int u = 0; u < U; ++u) {
+        const uint32_t idx = u * G + gl;
+        v[u] = load16<true>(dbase + (idx < nch ? idx : dlast));
     }
 
     uint32_t hd[5];
@@ -459,7 +483,10 @@ __global__ __launch_bounds__(256) void k_ipv4(const uint8_t *__restrict__ arena,
     const uint32_t version = b0h >> 4;
     const uint32_t ihl4 = (b0h & 0xFu) << 2;
     const uint32_t tl = (((hd[0] >> 16) & 0xFFu) << 8) | (hd[0] >> 24);
+    const uint32_t b6 = (hd[1] >> 16) & 0xFFu, b7 = hd[1] >> 24;
+    const bool frag = (b6 & 0x20u) || (((b6 & 0x1Fu) << 8) | b7);
     const uint32_t proto = (hd[2] >> 8) & 0xFFu;
+    const uint32_t stored_ip = hd[2] >> 16;
     uint32_t fl = 0;
     if (version != 4)
         fl |= TCSUM_PKT_BAD_VERSION;
@@ -467,15 +494,30 @@ __global__ __launch_bounds__(256) void k_ipv4(const uint8_t *__restrict__ arena,
         fl |= TCSUM_PKT_BAD_HDRLEN;
     if (tl < 20 || tl > frame || tl < ihl4)
         fl |= TCSUM_PKT_BAD_TOTLEN;
+    if (frag)
+        fl |= TCSUM_PKT_FRAGMENT;
     uint32_t hl = ihl4 < 20 ? 20u : ihl4;
     hl = hl > frame ? frame : hl;
     uint32_t end = tl < hl ? hl : tl;
     end = end > frame ? frame : end;
-    // range bounds in bytes from base
+    uint32_t min_l4;
+    const uint32_t fld = l4_field(proto, min_l4);
+    if (fld && end - hl < min_l4)
+        fl |= TCSUM_PKT_L4_SHORT;
+    const bool bad = !big_enough ||
+                     (fl & (TCSUM_PKT_BAD_VERSION | TCSUM_PKT_BAD_HDRLEN | TCSUM_PKT_BAD_TOTLEN));
+    // the L4 checksum field this mode treats specially (tx: zero + store;
+    // rx: is it zero?) -- none for fragments, short L4, or ICMP on rx
+    const bool field_on = IPM != IP_SUMS && !bad && !frag && fld && !(fl & TCSUM_PKT_L4_SHORT) &&
+                          !(IPM == IP_RX && proto == 1);
+
+    // byte ranges, from base
     const int64_t h_end = (int64_t)hl + s0;
     const int64_t l_end = (int64_t)end + s0;
+    const int64_t f0 = field_on ? (int64_t)(hl + fld) + s0 : -64;
+    const int64_t i0 = (int64_t)s0 + 10; // IPv4 header checksum field
 
-    uint32_t acc_h = 0, acc_l = 0;
+    uint32_t acc_h = 0, acc_l = 0, acc_f = 0;
     for (uint32_t b0 = 0; b0 < nch;) {
         uint32_t ph = 0, pl = 0;
 #pragma unroll
@@ -483,17 +525,21 @@ __global__ __launch_bounds__(256) void k_ipv4(const uint8_t *__restrict__ arena,
             const uint32_t idx = b0 + u * G + gl;
             const bool valid = idx < nch;
             const int64_t c = 16ll * idx;
-            const bool inner = valid && c >= h_end && c + 16 <= l_end;
-            if (valid && !inner) { // header chunks and the last chunk: rare
-                // header bytes [s0, h_end), L4 bytes [h_end, l_end), chunk-relative
-                const int64_t hlo = (int64_t)s0 - c, hhi = h_end - c;
-                const int64_t llo = h_end - c, lhi = l_end - c;
-                const int a0 = (int)(hlo < 0 ? 0 : (hlo > 16 ? 16 : hlo));
-                const int a1 = (int)(hhi < 0 ? 0 : (hhi > 16 ? 16 : hhi));
-                const int c0 = (int)(llo < 0 ? 0 : (llo > 16 ? 16 : llo));
-                const int c1 = (int)(lhi < 0 ? 0 : (lhi > 16 ? 16 : lhi));
-                ph = chunk_sum_masked(ph, v[u], a0, a1);
-                pl = chunk_sum_masked(pl, v[u], c0, c1);
+            const bool inner = valid && c >= h_end && c + 16 <= l_end && (f0 + 2 <= c || f0 >= c + 16);
+            if (valid && !inner) { // header chunks, the field chunk(s), the last chunk: rare
+                uint32_t th = region_sum(v[u], c, (int64_t)s0, h_end);
+                uint32_t tl4 = region_sum(v[u], c, h_end, l_end);
+                if (field_on) {
+                    const uint32_t tf = region_sum(v[u], c, f0, f0 + 2);
+                    if (IPM == IP_TX)
+                        tl4 -= tf; // tcp_out.c:19 / udp.c:320 / icmpv4.c:58 zero it first
+                    else
+                        acc_f += tf;
+                }
+                if (IPM == IP_TX)
+                    th -= region_sum(v[u], c, i0, i0 + 2); // ipv4.c:643
+                ph += th;
+                pl += tl4;
             }
             pl = chunk_sum_w(pl, v[u], inner ? 0x00010001u : 0u);
         }
@@ -505,11 +551,13 @@ __global__ __launch_bounds__(256) void k_ipv4(const uint8_t *__restrict__ arena,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t idx = b0 + u * G + gl;
-            v[u] = load16<true>(base + (idx < nch ? idx : nch - 1));
+            v[u] = load16<true>(dbase + (idx < nch ? idx : dlast));
         }
     }
     acc_h = group_sum<G>(acc_h);
     acc_l = group_sum<G>(acc_l);
+    if (IPM == IP_RX)
+        acc_f = group_sum<G>(acc_f);
 
     if (live && gl == 0) {
         uint32_t ip = 0, l4 = 0;
@@ -518,25 +566,58 @@ __global__ __launch_bounds__(256) void k_ipv4(const uint8_t *__restrict__ arena,
         } else {
             const bool odd = start & 1u;
             uint32_t fh = fold16(acc_h);
-            uint32_t fl4 = fold16(acc_l);
+            uint32_t f4 = fold16(acc_l);
             if (odd) {
                 fh = rot8(fh);
-                fl4 = rot8(fl4);
+                f4 = rot8(f4);
             }
             ip = ~fh & 0xFFFFu;
             if (proto == 6 || proto == 17) {
-                uint32_t p = add_halves(0u, hd[3]); // src, packet bytes 12..15
-                p = add_halves(p, hd[4]);           // dst, packet bytes 16..19
-                p += proto << 8;
-                p += bswap16((end - hl) & 0xFFFFu);
-                l4 = ~fold_step(fl4 + fold16(p)) & 0xFFFFu;
+                uint32_t q = add_halves(0u, hd[3]); // src, packet bytes 12..15
+                q = add_halves(q, hd[4]);           // dst, packet bytes 16..19
+                q += proto << 8;
+                q += bswap16((end - hl) & 0xFFFFu);
+                l4 = ~fold_step(f4 + fold16(q)) & 0xFFFFu;
             } else if (proto == 1) {
-                l4 = ~fl4 & 0xFFFFu;
+                l4 = ~f4 & 0xFFFFu;
             } else {
                 fl |= TCSUM_PKT_PROTO_OTHER;
             }
         }
-        out[pk] = ip | (l4 << 16);
+        if constexpr (IPM == IP_TX) {
+            if (!bad) { // stored in host order, like the struct fields
+                pp[10] = (uint8_t)ip;
+                pp[11] = (uint8_t)(ip >> 8);
+                if (field_on) {
+                    pp[hl + fld] = (uint8_t)l4;
+                    pp[hl + fld + 1] = (uint8_t)(l4 >> 8);
+                }
+            }
+        }
+        if constexpr (IPM == IP_RX) {
+            int v8;
+            if (!big_enough)
+                v8 = TCSUM_ERR_SIZE; // pktbuf_set_cont(buf, 20), ipv4.c:475
+            else if (version != 4)
+                v8 = TCSUM_ERR_NOT_SUPPORT; // ipv4.c:222
+            else if (ihl4 < 20 || tl < 20 || frame < tl || ihl4 > tl)
+                v8 = TCSUM_ERR_SIZE; // ipv4.c:229-239 (ihl4 > tl: defined here, UB there)
+            else if (stored_ip != 0 && ip != 0)
+                v8 = TCSUM_ERR_BROKEN; // ipv4.c:241-249
+            else if (frag || !fld)
+                v8 = TCSUM_OK; // reassembly first (ipv4.c:506) / raw_in: no checksum
+            else if (tl - ihl4 < min_l4)
+                v8 = TCSUM_ERR_SIZE; // pktbuf_set_cont: tcp_in.c:69, udp.c:386, icmpv4.c:68
+            else if (proto == 1)
+                v8 = tl <= 21 ? TCSUM_ERR_SIZE : TCSUM_OK; // icmpv4.c:31; its sum test never fails (A10)
+            else if (acc_f != 0 && l4 != 0)
+                v8 = TCSUM_ERR_BROKEN; // tcp_in.c:77-85, udp.c:407-415
+            else
+                v8 = TCSUM_OK;
+            verdict_out[pk] = (int8_t)v8;
+        }
+        if (out)
+            out[pk] = ip | (l4 << 16);
         if (flags_out)
             flags_out[pk] = (uint8_t)fl;
     }
@@ -753,13 +834,14 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
     return seg_u<MODE_PESO>(g.lanes, g.loads, g.persist, n, arena, descs, out, aux, stream);
 }
 
-static hipError_t ipv4_u(int G, int U, dim3 grid, const void *arena, const tcsum_pkt_t *pkts,
-                         uint32_t n, uint32_t *out, uint8_t *flags, hipStream_t s)
+template <int IPM>
+static hipError_t ipv4_u(int G, int U, dim3 grid, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
+                         uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t s)
 {
 #define TCSUM_IP(GG, UU)                                                                             \
     if (G == GG && U == UU) {                                                                      \
-        hipLaunchKernelGGL((k_ipv4<GG, UU>), grid, dim3(256), 0, s,                             \
-                           static_cast<const uint8_t *>(arena), pkts, n, out, flags);              \
+        hipLaunchKernelGGL((k_ipv4<GG, UU, IPM>), grid, dim3(256), 0, s, arena, pkts, n, out, flags, \
+                           verdict);                                                               \
         return hipGetLastError();                                                                  \
     }
 #define TCSUM_IP_U(GG)                                                                               \
@@ -773,8 +855,8 @@ static hipError_t ipv4_u(int G, int U, dim3 grid, const void *arena, const tcsum
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_ipv4(Geometry g, const void *arena, const tcsum_pkt_t *pkts, uint32_t n,
-                       uint32_t *out, uint8_t *flags, hipStream_t stream)
+hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
+                       uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream)
 {
     if (n == 0)
         return hipSuccess;
@@ -782,7 +864,14 @@ hipError_t launch_ipv4(Geometry g, const void *arena, const tcsum_pkt_t *pkts, u
         g.lanes = 16;
     const uint64_t per_block = 256u / (uint32_t)g.lanes;
     const dim3 grid((uint32_t)((n + per_block - 1) / per_block));
-    return ipv4_u(g.lanes, g.loads, grid, arena, pkts, n, out, flags, stream);
+    switch (ip_mode) {
+    case IP_TX:
+        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, stream);
+    case IP_RX:
+        return ipv4_u<IP_RX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, stream);
+    default:
+        return ipv4_u<IP_SUMS>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, stream);
+    }
 }
 
 hipError_t launch_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, uint64_t seed,

@@ -29,8 +29,9 @@ Geometry pick_geometry(uint64_t mean_len);
 hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void *descs,
                            uint32_t n, uint16_t *out, uint32_t aux, hipStream_t stream);
 
-hipError_t launch_ipv4(Geometry g, const void *arena, const tcsum_pkt_t *pkts, uint32_t n,
-                       uint32_t *out, uint8_t *flags, hipStream_t stream);
+// ip_mode: 0 sums, 1 tx fill (writes into arena), 2 rx verify (verdict required)
+hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
+                       uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream);
 
 hipError_t launch_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, uint64_t seed,
                              hipStream_t stream);

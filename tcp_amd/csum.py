@@ -25,6 +25,7 @@ PESO_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("src", "u1", 4),
 PKT_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("rsv", "<u4")])
 
 PKT_BAD_VERSION, PKT_BAD_HDRLEN, PKT_BAD_TOTLEN, PKT_PROTO_OTHER, PKT_SHORT = 1, 2, 4, 8, 16
+PKT_FRAGMENT, PKT_L4_SHORT = 32, 64
 
 
 # ------------------------------------------------------------- drop-in trio
@@ -106,6 +107,36 @@ def batch_ipv4(arena, pkts, n: int, total_bytes: int = 0, out=None, flags=None, 
                                      _stream_ptr(stream))
     _lib.check(rc, "tcsum_batch_ipv4")
     return out, flags
+
+
+def batch_ipv4_tx_fill(arena, pkts, n: int, total_bytes: int = 0, out=None, flags=None, want_flags=True,
+                       stream=None):
+    """Write the IPv4 / TCP / UDP / ICMP checksums into the packets in place."""
+    torch = _torch()
+    if flags is None and want_flags:
+        flags = torch.empty(n, dtype=torch.uint8, device=arena.device)
+    rc = _lib.lib().tcsum_batch_ipv4_tx_fill(arena.data_ptr(), pkts.data_ptr(), n,
+                                             out.data_ptr() if out is not None else None,
+                                             flags.data_ptr() if flags is not None else None, total_bytes,
+                                             _stream_ptr(stream))
+    _lib.check(rc, "tcsum_batch_ipv4_tx_fill")
+    return flags
+
+
+def batch_ipv4_rx_verify(arena, pkts, n: int, total_bytes: int = 0, verdict=None, out=None, flags=None,
+                         want_flags=True, stream=None):
+    """(verdict int8 net_err_t, flags) per packet, as the stack's rx gates decide."""
+    torch = _torch()
+    if verdict is None:
+        verdict = torch.empty(n, dtype=torch.int8, device=arena.device)
+    if flags is None and want_flags:
+        flags = torch.empty(n, dtype=torch.uint8, device=arena.device)
+    rc = _lib.lib().tcsum_batch_ipv4_rx_verify(arena.data_ptr(), pkts.data_ptr(), n, verdict.data_ptr(),
+                                               out.data_ptr() if out is not None else None,
+                                               flags.data_ptr() if flags is not None else None, total_bytes,
+                                               _stream_ptr(stream))
+    _lib.check(rc, "tcsum_batch_ipv4_rx_verify")
+    return verdict, flags
 
 
 def host_batch_peso(host_arena: np.ndarray, segs: np.ndarray, device: int = 0) -> np.ndarray:

@@ -27,6 +27,9 @@ PESO = np.dtype([("pool_off", "<u4"), ("total", "<u4"), ("blk_first", "<u4"), ("
 IPV4 = np.dtype([("pool_off", "<u4"), ("frame_len", "<u4"), ("ip", "<u4"), ("l4", "<u4"),
                  ("flags", "<u4")])
 
+IPV4_TX = np.dtype([("pool_off", "<u4"), ("frame_len", "<u4"), ("flags", "<u4")])
+IPV4_RX = np.dtype([("pool_off", "<u4"), ("frame_len", "<u4"), ("verdict", "<i4"), ("flags", "<u4")])
+
 NO_BLOCK = 0xFFFFFFFF
 
 
@@ -52,6 +55,22 @@ def peso_cases():
 
 def ipv4_cases():
     return _load("ipv4_cases.bin", IPV4), _load("ipv4_pool.bin")
+
+
+def ipv4_tx_cases():
+    """(cases, pool before the fill, pool after the reference's fill)."""
+    return _load("ipv4_tx_cases.bin", IPV4_TX), _load("ipv4_tx_in.bin"), _load("ipv4_tx_out.bin")
+
+
+def ipv4_rx_cases():
+    return _load("ipv4_rx_cases.bin", IPV4_RX), _load("ipv4_rx_pool.bin")
+
+
+def pkt_descs(cases, dtype):
+    d = np.zeros(cases.size, dtype)
+    d["offset"] = cases["pool_off"]
+    d["len"] = cases["frame_len"]
+    return d
 
 
 def kats() -> dict:

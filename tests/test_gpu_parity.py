@@ -223,6 +223,57 @@ def test_ipv4_odd_arena_base(tc, torch):
     np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
 
 
+@pytest.mark.parametrize("g,u", [(16, 1), (16, 4), (32, 3), (32, 4), (64, 2), (64, 16)])
+def test_batch_ipv4_tx_fill_golden(tc, torch, geometry, g, u):
+    """In-place fill == the reference's tx path on the same packets, byte for byte."""
+    geometry(g, u)
+    cases, pin, pout = G.ipv4_tx_cases()
+    arena = to_dev(torch, pin)
+    d = tc.descs_to_device(G.pkt_descs(cases, tc.PKT_DTYPE))
+    flags = tc.batch_ipv4_tx_fill(arena, d, cases.size, int(cases["frame_len"].sum()))
+    np.testing.assert_array_equal(arena.cpu().numpy()[: pout.size], pout)
+    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+    flags = tc.batch_ipv4_tx_fill(arena, d, cases.size)  # idempotent: fields read as zero
+    np.testing.assert_array_equal(arena.cpu().numpy()[: pout.size], pout)
+
+
+@pytest.mark.parametrize("g,u", [(16, 1), (16, 4), (32, 3), (32, 4), (64, 2), (64, 16)])
+def test_batch_ipv4_rx_verify_golden(tc, torch, oracle, geometry, g, u):
+    geometry(g, u)
+    cases, pool = G.ipv4_rx_cases()
+    arena = to_dev(torch, pool)
+    pk = G.pkt_descs(cases, tc.PKT_DTYPE)
+    out = torch.empty(cases.size, dtype=torch.uint32, device="cuda")
+    verdict, flags = tc.batch_ipv4_rx_verify(arena, tc.descs_to_device(pk), cases.size, out=out)
+    np.testing.assert_array_equal(verdict.cpu().numpy(), cases["verdict"])
+    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+    exp, _ = oracle.batch_ipv4(pool, pk)
+    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+
+
+def test_tx_then_rx_full_mixed(tc, torch, oracle):
+    """configs[3] at full size: fill on the GPU, verify on the GPU (all OK),
+    corrupt 2,000 packets, verify again; the oracle agrees on every packet."""
+    from tcp_amd import workload
+    b = workload.make_batch("mixed")
+    arena, descs = workload.materialize(b)
+    tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes)
+    verdict, _ = tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes)
+    assert (verdict.cpu().numpy() == 0).all()
+    rng = np.random.default_rng(5)
+    bad = rng.choice(b.n, 2000, replace=False)
+    pos = (b.descs["offset"][bad] + 20 + (rng.integers(0, 1 << 30, bad.size) % (b.descs["len"][bad] - 20))).astype(np.int64)
+    idx = torch.from_numpy(pos).cuda()
+    arena[idx] ^= 0x04
+    verdict, flags = tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes)
+    v = verdict.cpu().numpy()
+    assert (v[bad] == -13).mean() > 0.99 and (np.delete(v, bad) == 0).all()
+    host = arena.cpu().numpy()
+    ev, ef = oracle.batch_ipv4_rx_verify(host, b.descs, nthreads=16)
+    np.testing.assert_array_equal(v, ev)
+    np.testing.assert_array_equal(flags.cpu().numpy(), ef)
+
+
 # ------------------------------------------------- seeded batches vs oracle
 
 def run_config(tc, torch, config, n):

@@ -79,6 +79,27 @@ def test_ipv4_pair(oracle):
         assert (ip, l4, fl) == (int(c["ip"]), int(c["l4"]), int(c["flags"])), c
 
 
+def test_ipv4_tx_fill(oracle):
+    cases, pin, pout = G.ipv4_tx_cases()
+    assert cases.size == 400
+    arena = pin.copy()
+    flags = oracle.batch_ipv4_tx_fill(arena, G.pkt_descs(cases, oracle.PKT_DTYPE), nthreads=4)
+    np.testing.assert_array_equal(flags, cases["flags"])
+    np.testing.assert_array_equal(arena, pout)
+    assert (pin != pout).any()
+
+
+def test_ipv4_rx_verify(oracle):
+    cases, pool = G.ipv4_rx_cases()
+    assert cases.size == 600
+    verdict, flags = oracle.batch_ipv4_rx_verify(pool, G.pkt_descs(cases, oracle.PKT_DTYPE), nthreads=4)
+    np.testing.assert_array_equal(verdict, cases["verdict"])
+    np.testing.assert_array_equal(flags, cases["flags"])
+    # the fixture exercises every gate
+    for v in (0, -5, -11, -13):
+        assert (cases["verdict"] == v).sum() >= 5, v
+
+
 def test_batch_forms_agree_with_scalar(oracle):
     """The threaded batch entry points are the scalar routines, per item."""
     pool = G.pool()

@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="mtu", help="headline workload (mtu|tso|mixed|mixed_aligned)")
-    ap.add_argument("--secondary", default="tso,mixed", help="extra configs measured at N=1")
+    ap.add_argument("--secondary", default="tso,mixed,mixed_tx,mixed_rx",
+                    help="extra configs measured at N=1")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -57,14 +58,22 @@ def parse():
 def algorithmic_bytes(batch) -> int:
     """Bytes one launch must move: every packet byte once, its descriptor, its result.
 
-    peso: 24-B descriptor + 2-B result; ipv4: 16-B descriptor + 4-B result."""
-    per = 24 + 2 if batch.kind == "peso" else 16 + 4
+    peso: 24-B descriptor + 2-B result; ipv4 sums: 16-B descriptor + 4-B result;
+    tx fill: 16 B + 4 B written into the packet; rx verify: 16 B + 1-B verdict."""
+    if batch.kind == "peso":
+        per = 24 + 2
+    else:
+        per = {"sums": 16 + 4, "tx": 16 + 4, "rx": 16 + 1}[batch.op]
     return batch.total_bytes + per * batch.n
 
 
 def launch(tc, batch, arena, descs, out):
     if batch.kind == "peso":
         tc.batch_peso(arena, descs, batch.n, batch.total_bytes, out=out)
+    elif batch.op == "tx":
+        tc.batch_ipv4_tx_fill(arena, descs, batch.n, batch.total_bytes, want_flags=False)
+    elif batch.op == "rx":
+        tc.batch_ipv4_rx_verify(arena, descs, batch.n, batch.total_bytes, verdict=out, want_flags=False)
     else:
         tc.batch_ipv4(arena, descs, batch.n, batch.total_bytes, out=out, want_flags=False)
 
@@ -72,7 +81,7 @@ def launch(tc, batch, arena, descs, out):
 def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None):
     batch = workload.make_batch(config, rank=rank)
     arena, descs = workload.materialize(batch)
-    dt = torch.uint16 if batch.kind == "peso" else torch.uint32
+    dt = torch.uint16 if batch.kind == "peso" else torch.int8 if batch.op == "rx" else torch.uint32
     out = torch.empty(batch.n, dtype=dt, device=arena.device)
     for _ in range(warmup):
         launch(tc, batch, arena, descs, out)
@@ -154,7 +163,7 @@ def pmc_traffic(config: str):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
                     name = row.get("Kernel_Name", "")
-                    if "k_segments" in name or "k_ipv4" in name:
+                    if "k_segments" in name or "k_ipv4" in name:  # the checksum kernels only
                         if row.get("Counter_Name", counter) == counter:
                             per.append(float(row["Counter_Value"]))
         shutil.rmtree(d, ignore_errors=True)

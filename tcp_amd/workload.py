@@ -28,12 +28,17 @@ CONFIGS = {
     "tso": dict(n=1 << 18, len=65536, kind="peso"),
     "mixed": dict(n=1 << 20, lo=64, hi=9000, kind="ipv4", aligned=False),
     "mixed_aligned": dict(n=1 << 20, lo=64, hi=9000, kind="ipv4", aligned=True),
+    # the same packets through the tx fill / rx verify entry points
+    "mixed_tx": dict(n=1 << 20, lo=64, hi=9000, kind="ipv4", aligned=False, op="tx"),
+    "mixed_rx": dict(n=1 << 20, lo=64, hi=9000, kind="ipv4", aligned=False, op="rx"),
 }
 CONFIG_NAMES = {
     "mtu": "1M x 1500 B TCP segments (MTU), device-resident",
     "tso": "256K x 64 KiB TCP segments (TSO-size), device-resident",
     "mixed": "1M mixed IPv4 TCP/UDP packets, uniform 64-9000 B, packed (unaligned)",
     "mixed_aligned": "1M mixed IPv4 TCP/UDP packets, uniform 64-9000 B, 16-B aligned starts",
+    "mixed_tx": "1M mixed IPv4 packets: batched tx fill (checksums written in place)",
+    "mixed_rx": "1M mixed IPv4 packets: batched rx verify (net_err_t verdict per packet)",
 }
 
 
@@ -56,6 +61,7 @@ class Batch:
     total_bytes: int     # sum of packet lengths (the metric's byte count)
     byte_base: int       # where this rank's arena starts in the global stream
     seed: int = SEED
+    op: str = "sums"     # ipv4 only: "sums", "tx" (fill in place) or "rx" (verify)
 
     @property
     def alloc_bytes(self) -> int:
@@ -90,19 +96,21 @@ def make_batch(config: str, rank: int = 0, n: int | None = None, seed: int = SEE
         arena = int(offs[-1] + stride[-1]) if n else 0
         total = int(lens.sum())
     byte_base = rank * (((arena + 15) // 16) * 16)
-    return Batch(config, spec["kind"], n, d, arena, total, byte_base, seed)
+    return Batch(config, spec["kind"], n, d, arena, total, byte_base, seed, spec.get("op", "sums"))
 
 
 def materialize(batch: Batch, device="cuda", stream=None):
     """(arena, descs) on the device: bytes generated in HBM, descriptors copied."""
     import torch
 
-    from .csum import descs_to_device, synth_fill, synth_ipv4
+    from .csum import batch_ipv4_tx_fill, descs_to_device, synth_fill, synth_ipv4
     arena = torch.empty(batch.alloc_bytes, dtype=torch.uint8, device=device)
     synth_fill(arena, batch.alloc_bytes, batch.byte_base, batch.seed, stream=stream)
     descs = descs_to_device(batch.descs, device)
     if batch.kind == "ipv4":
         synth_ipv4(arena, descs, batch.n, batch.seed, stream=stream)
+        if batch.op == "rx":  # receive what a sender filled in
+            batch_ipv4_tx_fill(arena, descs, batch.n, batch.total_bytes, want_flags=False, stream=stream)
     return arena, descs
 
 

@@ -36,10 +36,12 @@ def build(force: bool = False) -> None:
 
 
 def build_ref() -> bool:
-    """Compile oracle/_ref from the reference sources; False when absent."""
+    """Compile oracle/_ref from the reference sources (golden generator, the
+    reference CPU baseline, and the drop-in link test against libtcsum.so);
+    False when /root/reference is absent (the GPU box uses the prebuilt files)."""
     if not os.path.isdir("/root/reference/net/src"):
         return False
-    subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
+    subprocess.run(["make", "-s", "-C", HERE, "ref", "dropin"], check=True)
     return True
 
 

@@ -120,6 +120,20 @@ def test_checksum_peso_golden(tc):
         assert pos == int(c["final_pos"]) == int(c["total"]) and blk is None
 
 
+def test_reference_stack_objects_link_against_libtcsum(tc):
+    """oracle/_ref/dropin_stack: the reference's own pktbuf.o/tools.o (checksum
+    definitions localized, as INTEGRATION.md patches them out) linked with
+    libtcsum.so, replaying every pktbuf/peso golden case through the reference's
+    own chain and cursor code."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(G.GOLDEN), "..", "oracle", "_ref", "dropin_stack")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref not built (needs /root/reference at build time)")
+    r = subprocess.run([exe, G.GOLDEN], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "2749/2749" in r.stdout
+
+
 # ------------------------------------------------------------ batches
 
 def peso_descs(tc, cases):

@@ -386,6 +386,9 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         return TCSUM_OK;
     if (!host_arena || !segs || !out || device < 0 || device >= kMaxDev)
         return TCSUM_ERR_PARAM;
+    for (uint32_t i = 0; i < n; ++i)
+        if (segs[i].offset > arena_bytes || segs[i].len > arena_bytes - segs[i].offset)
+            return TCSUM_ERR_PARAM;
     Ctx &c = g_ctx[device];
     std::lock_guard<std::mutex> lk(c.mu);
     int rc = ctx_init(c, device);
@@ -393,9 +396,6 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         return rc;
     if (hipSetDevice(device) != hipSuccess)
         return TCSUM_ERR_SYS;
-    for (uint32_t i = 0; i < n; ++i)
-        if (segs[i].offset + segs[i].len > arena_bytes)
-            return TCSUM_ERR_PARAM;
 
     // device buffers (grow-only; the arena keeps a 16-byte tail so the last
     // aligned chunk is in bounds)

@@ -732,14 +732,22 @@ hipError_t launch_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, hip
 
 // ---------------------------------------------------------------- dispatch
 
-static int resident_blocks()
+// Workgroups of `kernel` that fit on the device at once (occupancy API x CUs),
+// cached per kernel: a persistent grid larger than this runs a tail of
+// non-resident blocks after the rest.
+template <class K>
+static uint32_t resident_blocks(K kernel)
 {
-    static int blocks = 0;
+    static uint32_t blocks = 0;
     if (blocks == 0) {
-        int dev = 0, cus = 256;
+        int dev = 0, cus = 256, per_cu = 0;
         if (hipGetDevice(&dev) == hipSuccess)
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        blocks = cus * 8; // 8 x 256-thread workgroups = 32 waves per CU
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        if (per_cu > 8)
+            per_cu = 8;
+        blocks = (uint32_t)(cus * per_cu);
     }
     return blocks;
 }
@@ -792,14 +800,16 @@ static hipError_t seg_u(int G, int U, int persist, uint32_t n, const void *arena
     if (G == GG && U == UU) {                                                                      \
         const uint32_t per_block = 256u / GG;                                                      \
         uint32_t blocks = (n + per_block - 1) / per_block;                                         \
-        if (persist) {                                                                             \
-            blocks = blocks < (uint32_t)resident_blocks() ? blocks : (uint32_t)resident_blocks();  \
-            if (persist == 2)                                                                      \
-                hipLaunchKernelGGL((k_segments_pp<GG, UU, MODE>), dim3(blocks), dim3(256), 0, s,   \
-                                   static_cast<const uint8_t *>(arena), descs, n, out, aux);       \
-            else                                                                                   \
-                hipLaunchKernelGGL((k_segments_p<GG, UU, MODE>), dim3(blocks), dim3(256), 0, s,    \
-                                   static_cast<const uint8_t *>(arena), descs, n, out, aux);       \
+        if (persist == 2) {                                                                        \
+            const uint32_t rb = resident_blocks(k_segments_pp<GG, UU, MODE>);                     \
+            hipLaunchKernelGGL((k_segments_pp<GG, UU, MODE>), dim3(blocks < rb ? blocks : rb),     \
+                               dim3(256), 0, s, static_cast<const uint8_t *>(arena), descs, n, out, \
+                               aux);                                                               \
+        } else if (persist == 1) {                                                                 \
+            const uint32_t rb = resident_blocks(k_segments_p<GG, UU, MODE>);                      \
+            hipLaunchKernelGGL((k_segments_p<GG, UU, MODE>), dim3(blocks < rb ? blocks : rb),      \
+                               dim3(256), 0, s, static_cast<const uint8_t *>(arena), descs, n, out, \
+                               aux);                                                               \
         } else {                                                                                   \
             hipLaunchKernelGGL((k_segments<GG, UU, MODE>), dim3(blocks), dim3(256), 0, s,          \
                                static_cast<const uint8_t *>(arena), descs, n, out, aux);           \

@@ -114,3 +114,47 @@ def test_product_never_imports_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h")):
                 text = open(os.path.join(dirpath, f)).read()
                 assert not re.search(r"(from|import)\s+oracle|pyoracle|liboracle|libtcpref|orc_\w+\(", text), f
+
+
+def test_batch_argument_errors_without_device(libpath):
+    """Bad arguments come back as NET_ERR_PARAM before any device is touched."""
+    from tcp_amd import _lib
+    L = _lib.lib()
+    assert L.tcsum_batch_peso(None, None, 4, None, 0, None) == _lib.ERR_PARAM
+    assert L.tcsum_batch_segments(None, None, 4, None, 1, 0, None) == _lib.ERR_PARAM
+    assert L.tcsum_batch_ipv4(None, None, 4, None, None, 0, None) == _lib.ERR_PARAM
+    assert L.tcsum_batch_ipv4_tx_fill(None, None, 4, None, None, 0, None) == _lib.ERR_PARAM
+    assert L.tcsum_batch_ipv4_rx_verify(None, None, 4, None, None, None, 0, None) == _lib.ERR_PARAM
+    assert L.tcsum_batch_peso(None, None, 0, None, 0, None) == _lib.OK  # empty batch
+    assert L.tcsum_synth_fill(ctypes.c_void_p(8), 16, 0, 1, None) == _lib.ERR_PARAM  # misaligned
+    from tcp_amd import PESO_DTYPE
+    seg = np.zeros(1, PESO_DTYPE)
+    seg["offset"], seg["len"] = 10, 100
+    host = np.zeros(64, np.uint8)
+    out = np.zeros(1, np.uint16)
+    rc = L.tcsum_host_batch_peso(0, host.ctypes.data, host.nbytes, seg.ctypes.data, 1, out.ctypes.data)
+    assert rc == _lib.ERR_PARAM  # segment past the arena
+    assert L.tcsum_plat_init(99) == _lib.ERR_PARAM
+
+
+def test_no_cpu_fallback(libpath):
+    """Without a gfx950 device the drop-in symbols fail loudly (message + abort),
+    and the batch/host entry points return NET_ERR_NOT_SUPPORT."""
+    import sys
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    code = ("import sys; sys.path.insert(0, %r); import tcp_amd; "
+            "print(tcp_amd.checksum16(0, b'\\xff\\xff', 2, 0, 1))" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "no CPU fallback" in r.stderr
+    from tcp_amd import _lib, PESO_DTYPE
+    L = _lib.lib()
+    seg = np.zeros(1, PESO_DTYPE)
+    seg["len"] = 10
+    host = np.zeros(64, np.uint8)
+    out = np.zeros(1, np.uint16)
+    rc = L.tcsum_host_batch_peso(0, host.ctypes.data, host.nbytes, seg.ctypes.data, 1, out.ctypes.data)
+    assert rc == _lib.ERR_NOT_SUPPORT
+    assert L.tcsum_plat_init(0) == _lib.ERR_NOT_SUPPORT

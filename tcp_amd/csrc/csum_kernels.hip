@@ -411,12 +411,13 @@ __device__ __forceinline__ void pick6(uint32_t q, const uint32_t w[12], uint32_t
         x[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
 }
 
-// Sum of the chunk's bytes that fall in [r0, r1) (offsets from the chunk base c).
-__device__ __forceinline__ uint32_t region_sum(u32x4 v, int64_t c, int64_t r0, int64_t r1)
+// Sum of the chunk's bytes that fall in [r0, r1) (offsets from the chunk base c;
+// all positions are bytes from the packet's first chunk, < 2^17).
+__device__ __forceinline__ uint32_t region_sum(u32x4 v, int c, int r0, int r1)
 {
-    const int64_t lo = r0 - c, hi = r1 - c;
-    const int a = (int)(lo < 0 ? 0 : (lo > 16 ? 16 : lo));
-    const int b = (int)(hi < 0 ? 0 : (hi > 16 ? 16 : hi));
+    const int lo = r0 - c, hi = r1 - c;
+    const int a = lo < 0 ? 0 : (lo > 16 ? 16 : lo);
+    const int b = hi < 0 ? 0 : (hi > 16 ? 16 : hi);
     return chunk_sum_masked(0u, v, a, b);
 }
 
@@ -456,7 +457,10 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const
     const u32x4 h2v = load16<false>(hb + h2i);
     const u32x4 h2 = s0 > 12 ? h2v : u32x4(0u);
 
-    const uint32_t nch = big_enough ? (uint32_t)(((uint64_t)frame + s0 + 15) >> 4) : 0u;
+    // IPv4 bytes past 65,535 (the largest total_len) never count: bound the
+    // loads there, so every position below fits comfortably in 32 bits
+    const uint32_t frame_ld = frame < 65600u ? frame : 65600u;
+    const uint32_t nch = big_enough ? (frame_ld + s0 + 15) >> 4 : 0u;
     const u32x4 *dbase = nch ? base : &g_zero_chunk;
     const uint32_t dlast = nch ? nch - 1u : 0u;
 
@@ -511,11 +515,12 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const
     const bool field_on = IPM != IP_SUMS && !bad && !frag && fld && !(fl & TCSUM_PKT_L4_SHORT) &&
                           !(IPM == IP_RX && proto == 1);
 
-    // byte ranges, from base
-    const int64_t h_end = (int64_t)hl + s0;
-    const int64_t l_end = (int64_t)end + s0;
-    const int64_t f0 = field_on ? (int64_t)(hl + fld) + s0 : -64;
-    const int64_t i0 = (int64_t)s0 + 10; // IPv4 header checksum field
+    // byte ranges, from base (end <= tl <= 65535 whenever it matters; clamp so
+    // a huge bogus frame cannot overflow)
+    const int h_end = (int)(hl < 65600u ? hl : 65600u) + (int)s0;
+    const int l_end = (int)(end < 65600u ? end : 65600u) + (int)s0;
+    const int f0 = field_on ? (int)(hl + fld) + (int)s0 : -64;
+    const int i0 = (int)s0 + 10; // IPv4 header checksum field
 
     uint32_t acc_h = 0, acc_l = 0, acc_f = 0;
     for (uint32_t b0 = 0; b0 < nch;) {
@@ -524,10 +529,10 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const
         for (int u = 0; u < U; ++u) {
             const uint32_t idx = b0 + u * G + gl;
             const bool valid = idx < nch;
-            const int64_t c = 16ll * idx;
+            const int c = (int)(16u * idx);
             const bool inner = valid && c >= h_end && c + 16 <= l_end && (f0 + 2 <= c || f0 >= c + 16);
             if (valid && !inner) { // header chunks, the field chunk(s), the last chunk: rare
-                uint32_t th = region_sum(v[u], c, (int64_t)s0, h_end);
+                uint32_t th = region_sum(v[u], c, (int)s0, h_end);
                 uint32_t tl4 = region_sum(v[u], c, h_end, l_end);
                 if (field_on) {
                     const uint32_t tf = region_sum(v[u], c, f0, f0 + 2);

@@ -421,25 +421,6 @@ __device__ __forceinline__ uint32_t region_sum(u32x4 v, int c, int r0, int r1)
     return chunk_sum_masked(0u, v, a, b);
 }
 
-// Is chunk c (bytes [16c, 16c+16) from base) entirely inside the packet's
-// bytes [s0, l_end)?  Only such chunks may be rewritten whole.
-__device__ __forceinline__ bool chunk_inside(int c, uint32_t s0, int l_end)
-{
-    return c >= 0 && 16 * c >= (int)s0 && 16 * c + 16 <= l_end;
-}
-
-// Replace byte `pos` (0..15; anything else is ignored) of a chunk.
-__device__ __forceinline__ u32x4 put_byte(u32x4 w, int pos, uint32_t b)
-{
-    const uint32_t sh = 8u * (uint32_t)(pos & 3);
-    const uint32_t m = ~(0xFFu << sh), x = (b & 0xFFu) << sh;
-    w.x = pos >= 0 && pos < 4 ? (w.x & m) | x : w.x;
-    w.y = pos >= 4 && pos < 8 ? (w.y & m) | x : w.y;
-    w.z = pos >= 8 && pos < 12 ? (w.z & m) | x : w.z;
-    w.w = pos >= 12 && pos < 16 ? (w.w & m) | x : w.w;
-    return w;
-}
-
 // L4 checksum field offset and minimum header length by protocol
 // (tcp.h:71, udp.h:24, icmpv4.h:28); 0 when the protocol has none here.
 __device__ __forceinline__ uint32_t l4_field(uint32_t proto, uint32_t &min_len)
@@ -451,8 +432,7 @@ __device__ __forceinline__ uint32_t l4_field(uint32_t proto, uint32_t &min_len)
 template <int G, int U, int IPM>
 __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                               uint32_t n, uint32_t *__restrict__ out,
-                                              uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
-                                              uint32_t diag)
+                                              uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out)
 {
     const uint32_t gl = threadIdx.x & (G - 1);
     const uint32_t pk = (blockIdx.x * 256u + threadIdx.x) / G;
@@ -492,10 +472,6 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const
         const uint32_t idx = u * G + gl;
         v[u] = load16<true>(dbase + (idx < nch ? idx : dlast));
     }
-
-    // tx: lanes 0..5 hold chunks 0..5 (every checksum field lives there) in the
-    // first pass; keep them to write the filled fields back as whole chunks
-    const u32x4 keep = IPM == IP_TX ? v[0] : u32x4(0u);
 
     uint32_t hd[5];
     {
@@ -588,7 +564,6 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const
     if (IPM == IP_RX)
         acc_f = group_sum<G>(acc_f);
 
-    uint32_t fill_vals = 0;
     if (live && gl == 0) {
         uint32_t ip = 0, l4 = 0;
         if (!big_enough) {
@@ -615,18 +590,12 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const
             }
         }
         if constexpr (IPM == IP_TX) {
-            // field bytes whose chunk is shared with a neighbouring packet:
-            // single-byte stores (the rest go out as whole chunks below)
-            if (!bad && !(diag & 1u)) { // stored in host order, like the struct fields
-                if (!chunk_inside(i0 >> 4, s0, l_end))
-                    pp[10] = (uint8_t)ip;
-                if (!chunk_inside((i0 + 1) >> 4, s0, l_end))
-                    pp[11] = (uint8_t)(ip >> 8);
+            if (!bad) { // stored in host order, like the struct fields
+                pp[10] = (uint8_t)ip;
+                pp[11] = (uint8_t)(ip >> 8);
                 if (field_on) {
-                    if (!chunk_inside(f0 >> 4, s0, l_end))
-                        pp[hl + fld] = (uint8_t)l4;
-                    if (!chunk_inside((f0 + 1) >> 4, s0, l_end))
-                        pp[hl + fld + 1] = (uint8_t)(l4 >> 8);
+                    pp[hl + fld] = (uint8_t)l4;
+                    pp[hl + fld + 1] = (uint8_t)(l4 >> 8);
                 }
             }
         }
@@ -656,27 +625,6 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const
             out[pk] = ip | (l4 << 16);
         if (flags_out)
             flags_out[pk] = (uint8_t)fl;
-        if constexpr (IPM == IP_TX)
-            fill_vals = ip | (l4 << 16);
-    }
-    if constexpr (IPM == IP_TX) {
-        // whole-chunk write-back: one 16-byte store per field chunk that lies
-        // entirely inside this packet (a narrow store costs about as much per
-        // instruction as a 16-byte one -- MI355X_MICROARCH.md store table)
-        const uint32_t vals = __shfl(fill_vals, (threadIdx.x & 63u) & ~(uint32_t)(G - 1), 64);
-        const int cb = (int)(16u * gl);
-        const bool touch_ip = i0 < cb + 16 && i0 + 2 > cb;
-        const bool touch_l4 = field_on && f0 < cb + 16 && f0 + 2 > cb;
-        if (live && !bad && !(diag & 1u) && gl < 6 && (touch_ip || touch_l4) && chunk_inside(gl, s0, l_end)) {
-            u32x4 w = keep;
-            w = put_byte(w, i0 - cb, vals & 0xFFu);
-            w = put_byte(w, i0 + 1 - cb, (vals >> 8) & 0xFFu);
-            if (field_on) {
-                w = put_byte(w, f0 - cb, (vals >> 16) & 0xFFu);
-                w = put_byte(w, f0 + 1 - cb, vals >> 24);
-            }
-            *reinterpret_cast<u32x4 *>(pp - s0 + cb) = w; // from the kernel argument: global_store
-        }
     }
 }
 
@@ -903,12 +851,12 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
 
 template <int IPM>
 static hipError_t ipv4_u(int G, int U, dim3 grid, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
-                         uint32_t *out, uint8_t *flags, int8_t *verdict, uint32_t diag, hipStream_t s)
+                         uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t s)
 {
 #define TCSUM_IP(GG, UU)                                                                             \
     if (G == GG && U == UU) {                                                                      \
         hipLaunchKernelGGL((k_ipv4<GG, UU, IPM>), grid, dim3(256), 0, s, arena, pkts, n, out, flags, \
-                           verdict, diag);                                                         \
+                           verdict);                                                               \
         return hipGetLastError();                                                                  \
     }
 #define TCSUM_IP_U(GG)                                                                               \
@@ -931,15 +879,13 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
         g.lanes = 16;
     const uint64_t per_block = 256u / (uint32_t)g.lanes;
     const dim3 grid((uint32_t)((n + per_block - 1) / per_block));
-    // TCSUM_DIAG=1: tx fill computes but does not store (measurement only)
-    const uint32_t diag = getenv("TCSUM_DIAG") ? (uint32_t)atoi(getenv("TCSUM_DIAG")) : 0u;
     switch (ip_mode) {
     case IP_TX:
-        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, stream);
+        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, stream);
     case IP_RX:
-        return ipv4_u<IP_RX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, stream);
+        return ipv4_u<IP_RX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, stream);
     default:
-        return ipv4_u<IP_SUMS>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, stream);
+        return ipv4_u<IP_SUMS>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, stream);
     }
 }
 

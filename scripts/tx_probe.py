@@ -1,0 +1,45 @@
+"""Where does tx fill time go?  Interleaved rounds in one process: ipv4 sums,
+tx fill with stores, tx fill without stores (TCSUM_DIAG=1), rx verify."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import tcp_amd as tc  # noqa: E402
+from tcp_amd import workload  # noqa: E402
+
+b = workload.make_batch("mixed")
+arena, descs = workload.materialize(b)
+out = torch.empty(b.n, dtype=torch.uint32, device="cuda")
+verdict = torch.empty(b.n, dtype=torch.int8, device="cuda")
+
+
+def sums():
+    tc.batch_ipv4(arena, descs, b.n, b.total_bytes, out=out, want_flags=False)
+
+
+def tx():
+    tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
+
+
+def rx():
+    tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes, verdict=verdict, want_flags=False)
+
+
+variants = {"sums": (sums, "0"), "tx": (tx, "0"), "tx_nostore": (tx, "1"), "rx": (rx, "0")}
+times = {k: [] for k in variants}
+for r in range(5):
+    for k, (fn, diag) in variants.items():
+        os.environ["TCSUM_DIAG"] = diag
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        times[k].append(e0.elapsed_time(e1) / 10)
+for k, t in times.items():
+    print(f"{k:12s} {np.median(t)*1e3:8.1f} us")

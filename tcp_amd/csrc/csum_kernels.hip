@@ -432,7 +432,8 @@ __device__ __forceinline__ uint32_t l4_field(uint32_t proto, uint32_t &min_len)
 template <int G, int U, int IPM>
 __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                               uint32_t n, uint32_t *__restrict__ out,
-                                              uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out)
+                                              uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
+                                              uint32_t diag)
 {
     const uint32_t gl = threadIdx.x & (G - 1);
     const uint32_t pk = (blockIdx.x * 256u + threadIdx.x) / G;
@@ -590,7 +591,7 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const
             }
         }
         if constexpr (IPM == IP_TX) {
-            if (!bad) { // stored in host order, like the struct fields
+            if (!bad && !(diag & 1u)) { // stored in host order, like the struct fields
                 pp[10] = (uint8_t)ip;
                 pp[11] = (uint8_t)(ip >> 8);
                 if (field_on) {
@@ -851,12 +852,12 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
 
 template <int IPM>
 static hipError_t ipv4_u(int G, int U, dim3 grid, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
-                         uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t s)
+                         uint32_t *out, uint8_t *flags, int8_t *verdict, uint32_t diag, hipStream_t s)
 {
 #define TCSUM_IP(GG, UU)                                                                             \
     if (G == GG && U == UU) {                                                                      \
         hipLaunchKernelGGL((k_ipv4<GG, UU, IPM>), grid, dim3(256), 0, s, arena, pkts, n, out, flags, \
-                           verdict);                                                               \
+                           verdict, diag);                                                         \
         return hipGetLastError();                                                                  \
     }
 #define TCSUM_IP_U(GG)                                                                               \
@@ -879,13 +880,16 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
         g.lanes = 16;
     const uint64_t per_block = 256u / (uint32_t)g.lanes;
     const dim3 grid((uint32_t)((n + per_block - 1) / per_block));
+    // TCSUM_DIAG=1: tx fill computes but does not store (measurement only,
+    // scripts/tx_probe.py)
+    const uint32_t diag = getenv("TCSUM_DIAG") ? (uint32_t)atoi(getenv("TCSUM_DIAG")) : 0u;
     switch (ip_mode) {
     case IP_TX:
-        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, stream);
+        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, stream);
     case IP_RX:
-        return ipv4_u<IP_RX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, stream);
+        return ipv4_u<IP_RX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, stream);
     default:
-        return ipv4_u<IP_SUMS>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, stream);
+        return ipv4_u<IP_SUMS>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, stream);
     }
 }
 

@@ -120,6 +120,17 @@ __device__ __forceinline__ u32x4 load16(const u32x4 *p)
         return *p;
 }
 
+// Keep every load issued so far above this point: the optimizer may neither
+// sink them into a later loop (IR level: memory clobber) nor reorder their
+// consumers before them (machine scheduler barrier).  Without it hipcc moved
+// the first pass of data loads behind an s_waitcnt vmcnt(0) on the header /
+// edge loads -- one extra full memory latency per wave.
+__device__ __forceinline__ void issue_fence()
+{
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 template <int G>
 __device__ __forceinline__ uint32_t group_sum(uint32_t x)
 {
@@ -148,18 +159,21 @@ __device__ __forceinline__ SegDesc load_desc(const void *__restrict__ descs, uin
     SegDesc d;
     const uint32_t i = live ? seg : 0u;
     if constexpr (MODE == MODE_PESO) {
-        const tcsum_peso_t *x = static_cast<const tcsum_peso_t *>(descs) + i;
-        d.off = x->offset;
-        d.len = x->len;
-        d.src = *reinterpret_cast<const uint32_t *>(x->src);
-        d.dst = *reinterpret_cast<const uint32_t *>(x->dst);
-        d.proto = x->protocol;
+        // 24 B = 16 + 8: two loads (the array is 8-byte aligned)
+        const uint8_t *x = static_cast<const uint8_t *>(descs) + 24ull * i;
+        const u32x4 a = *reinterpret_cast<const u32x4 *>(x);
+        const uint2 b = *reinterpret_cast<const uint2 *>(x + 16);
+        d.off = (uint64_t)a.x | ((uint64_t)a.y << 32);
+        d.len = a.z;
+        d.src = a.w;
+        d.dst = b.x;
+        d.proto = b.y & 0xFFu;
         d.pre = 0;
     } else {
-        const tcsum_seg_t *x = static_cast<const tcsum_seg_t *>(descs) + i;
-        d.off = x->offset;
-        d.len = x->len;
-        d.pre = x->pre_sum;
+        const u32x4 a = *(reinterpret_cast<const u32x4 *>(descs) + i);
+        d.off = (uint64_t)a.x | ((uint64_t)a.y << 32);
+        d.len = a.z;
+        d.pre = a.w;
         d.src = d.dst = d.proto = 0;
     }
     d.len = live ? d.len : 0u;
@@ -248,6 +262,7 @@ __device__ __forceinline__ uint32_t sum_range(const uint8_t *__restrict__ arena,
     Frame<U> f;
     frame_issue<G, U>(f, arena, off, len, gl);
     issued();
+    issue_fence();
     return frame_consume<G, U, EXACT>(f, gl);
 }
 
@@ -369,6 +384,7 @@ __global__ __launch_bounds__(256) void k_segments_pp(const uint8_t *__restrict__
         // fa in flight for d0, d1 loading
         const SegDesc d2 = load_desc<MODE>(descs, seg + 2 * step, seg + 2 * step < n);
         frame_issue<G, U>(fb, arena, d1.off, d1.len, gl);
+        issue_fence();
         finish_range<G, U, MODE>(fa, d0, seg, n, gl, arena, out, aux);
         seg += step;
         first += step;
@@ -377,6 +393,7 @@ __global__ __launch_bounds__(256) void k_segments_pp(const uint8_t *__restrict__
         // fb in flight for d1, d2 loading
         const SegDesc d3 = load_desc<MODE>(descs, seg + 2 * step, seg + 2 * step < n);
         frame_issue<G, U>(fa, arena, d2.off, d2.len, gl);
+        issue_fence();
         finish_range<G, U, MODE>(fb, d1, seg, n, gl, arena, out, aux);
         seg += step;
         first += step;
@@ -404,11 +421,16 @@ __global__ __launch_bounds__(256) void k_segments_pp(const uint8_t *__restrict__
 // [0,hl), the L4 range [hl,end) and the 2-byte checksum fields.
 enum IpMode : int { IP_SUMS = 0, IP_TX = 1, IP_RX = 2 };
 
+// x[k] = w[q + k] for k < 6, q in 0..3: two stages of selects, no branches.
 __device__ __forceinline__ void pick6(uint32_t q, const uint32_t w[12], uint32_t x[6])
 {
+    uint32_t y[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        y[i] = (q & 1u) ? w[i + 1] : w[i];
 #pragma unroll
     for (int k = 0; k < 6; ++k)
-        x[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
+        x[k] = (q & 2u) ? y[k + 2] : y[k];
 }
 
 // Sum of the chunk's bytes that fall in [r0, r1) (offsets from the chunk base c;
@@ -440,9 +462,9 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const
     const bool live = pk < n;
 
     // unconditional loads throughout (dead lanes read descriptor 0 / the zero chunk)
-    const tcsum_pkt_t *dp = pkts + (live ? pk : 0u);
-    const uint64_t off = dp->offset;
-    const uint32_t frame = live ? dp->len : 0u;
+    const u32x4 dv = *reinterpret_cast<const u32x4 *>(pkts + (live ? pk : 0u));
+    const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+    const uint32_t frame = live ? dv.z : 0u;
     const bool big_enough = frame >= 20;
     uint8_t *pp = arena + off;
     const uintptr_t start = reinterpret_cast<uintptr_t>(pp);
@@ -473,6 +495,7 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const
         const uint32_t idx = u * G + gl;
         v[u] = load16<true>(dbase + (idx < nch ? idx : dlast));
     }
+    issue_fence();
 
     uint32_t hd[5];
     {

@@ -781,14 +781,14 @@ static uint32_t resident_blocks(K kernel)
     return blocks;
 }
 
-// Measured on MI355X (scripts/tune.py; profiles/r01/tune.txt, tune2.txt, one
-// process, interleaved rounds).  Interior chunks per range c (edges excluded):
+// Measured on MI355X (scripts/tune.py; profiles/r01/tune*.txt, one process,
+// interleaved rounds).  Interior chunks per range c (edges excluded):
 //   c <= ~136 (<= ~2 KiB, e.g. MTU): 16 lanes, U = ceil(c/16) loads -> one
-//       pass with almost no idle slots (1500 B: G=16, U=6, 91% of the read
+//       pass with almost no idle slots (1500 B: G=16, U=6, 95% of the read
 //       probe on the same bytes);
 //   ~2 KiB .. 32 KiB (mixed 64-9000 B, mean 4.5 KiB): 32 lanes x 4 loads,
-//       several passes (96% of the probe);
-//   >= 32 KiB (TSO): one range per wave, 16 loads per lane (97% of the probe).
+//       several passes (93-96% of the probe);
+//   >= 32 KiB (TSO): one range per wave, 16 loads per lane (98-100%).
 // The resident-grid variants (persist 1, 2) measured slower on all three.
 Geometry pick_geometry(uint64_t mean_len)
 {

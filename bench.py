@@ -250,15 +250,19 @@ def main():
     import tcp_amd as tc
     from tcp_amd import workload
 
-    torch.cuda.set_device(local)
-    dist = D.init("nccl", local)  # barrier + max-time only; no data-path collective
+    # one process per GPU; TCSUM_DIST_BACKEND=gloo rehearses N ranks on fewer
+    # GPUs (ranks share devices round-robin; RCCL refuses two ranks per GPU)
+    backend = os.environ.get("TCSUM_DIST_BACKEND", "nccl")
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    dist = D.init(backend, dev)  # barrier + max-time only; no data-path collective
 
     if args.pmc_child:
         time_config(torch, tc, workload, args.config, 0, args.steps, args.warmup)
         return
 
     head = time_config(torch, tc, workload, args.config, rank, args.steps, args.warmup, dist)
-    ms = D.max_over_ranks(dist, head["ms"], device="cuda")
+    ms = D.max_over_ranks(dist, head["ms"], device="cuda" if backend == "nccl" else "cpu")
     b = head["batch"]
     ms_step = ms / args.steps
     value = n_gpus * b.total_bytes * args.steps / (ms * 1e-3) / GIB

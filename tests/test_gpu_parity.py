@@ -134,6 +134,18 @@ def test_reference_stack_objects_link_against_libtcsum(tc):
     assert "2749/2749" in r.stdout
 
 
+def test_c_host_batch_demo(tc):
+    """tests/c/batch_demo.c: a plain C host (HIP C API + libtcsum.so) runs the
+    batch and end-to-end paths; the CPU oracle checks every result."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(G.GOLDEN), "c", "build", "batch_demo")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(os.path.dirname(exe))], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 mismatches" in r.stdout
+
+
 # ------------------------------------------------------------ batches
 
 def peso_descs(tc, cases):

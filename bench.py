@@ -234,6 +234,29 @@ def e2e(torch, tc, r):
         L.tcsum_host_free(p)
 
 
+def legacy_latency(tc):
+    """Per-call wall time of the synchronous drop-in symbols, the way the
+    stack calls them per packet: checksum16 on a 20-B IPv4 header (ipv4.c:243)
+    and checksum_peso on a 1500-B segment in 127-B blocks (tcp_out.c:20)."""
+    import numpy as np
+    hdr = bytes.fromhex("450000730000400040110000c0a80001c0a800c7")
+    seg = np.random.default_rng(1).integers(0, 256, 1500, dtype=np.uint8).tobytes()
+    buf = tc.PktBuf([seg[i: i + 127] for i in range(0, 1500, 127)])
+    d, s_ = tc.IpAddr.v4([192, 168, 74, 3]), tc.IpAddr.v4([192, 168, 74, 2])
+    res = {}
+    for name, fn in (("checksum16_20B_us", lambda: tc.checksum16(0, hdr, 20, 0, 1)),
+                     ("checksum_peso_1500B_us", lambda: tc.checksum_peso(buf, d, s_, 6))):
+        for _ in range(20):
+            fn()
+        t0 = time.perf_counter()
+        reps = 2000
+        for _ in range(reps):
+            fn()
+        res[name] = round((time.perf_counter() - t0) / reps * 1e6, 2)
+    res["note"] = "one launch + one sync per call: use the batch API for throughput"
+    return res
+
+
 def main():
     args = parse()
     from tcp_amd import dist as D
@@ -305,6 +328,10 @@ def main():
                 line["e2e"] = e2e(torch, tc, head)
             except Exception as e:
                 line["e2e"] = {"error": repr(e)}
+            try:
+                line["legacy_sync_call"] = legacy_latency(tc)
+            except Exception as e:
+                line["legacy_sync_call"] = {"error": repr(e)}
         del head
         torch.cuda.empty_cache()
         extra = {}

@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="mtu", help="headline workload (mtu|tso|mixed|mixed_aligned)")
-    ap.add_argument("--secondary", default="tso,mixed,mixed_tx,mixed_rx",
+    ap.add_argument("--secondary", default="tso,mixed,mixed_aligned,mixed_tx,mixed_rx",
                     help="extra configs measured at N=1")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")

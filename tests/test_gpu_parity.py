@@ -373,6 +373,70 @@ def test_edge_segments(tc, torch, oracle):
     np.testing.assert_array_equal(out, oracle.batch_peso(host, p, nthreads=8))
 
 
+def test_unsorted_overlapping_duplicate_descriptors(tc, torch, oracle):
+    """Descriptors are independent reads: any order, overlaps, duplicates."""
+    rng = np.random.default_rng(21)
+    host = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    n = 30000
+    p = np.zeros(n, tc.PESO_DTYPE)
+    p["len"] = rng.integers(0, 4000, n)
+    p["offset"] = rng.integers(0, host.size - 4000, n)
+    p[n // 2:] = p[: n - n // 2]  # duplicates
+    p["src"] = rng.integers(0, 256, (n, 4))
+    p["dst"] = rng.integers(0, 256, (n, 4))
+    p["protocol"] = rng.choice([6, 17, 1, 99], n)
+    arena = torch.from_numpy(host).cuda()
+    for mean in (0, 64, 1500, 70000):
+        out = tc.batch_peso(arena, tc.descs_to_device(p), n, mean * n).cpu().numpy()
+        np.testing.assert_array_equal(out, oracle.batch_peso(host, p, nthreads=8))
+
+
+def test_hip_graph_capture_and_replay(tc, torch, oracle):
+    """Batch calls allocate nothing and only enqueue: capturable in a hipGraph."""
+    from tcp_amd import workload
+    b = workload.make_batch("mtu", n=20000)
+    arena, descs = workload.materialize(b)
+    out = torch.empty(b.n, dtype=torch.uint16, device="cuda")
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        tc.batch_peso(arena, descs, b.n, b.total_bytes, out=out)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    exp = oracle.batch_peso(arena.cpu().numpy(), b.descs, nthreads=8)
+    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+    arena[: b.n * 1500].view(b.n, 1500)[:, 40] ^= 1  # new bytes, same graph
+    g.replay()
+    torch.cuda.synchronize()
+    exp2 = oracle.batch_peso(arena.cpu().numpy(), b.descs, nthreads=8)
+    np.testing.assert_array_equal(out.cpu().numpy(), exp2)
+    assert (exp2 != exp).mean() > 0.99
+
+
+def test_concurrent_streams(tc, torch, oracle):
+    """Independent batches on independent streams do not interfere."""
+    from tcp_amd import workload
+    bs = [workload.make_batch(c, rank=r, n=n) for c, r, n in (("mtu", 0, 30000), ("mixed", 1, 8000), ("tso", 2, 64))]
+    mats = [workload.materialize(b) for b in bs]
+    streams = [torch.cuda.Stream() for _ in bs]
+    torch.cuda.synchronize()
+    outs = []
+    for rep in range(3):
+        outs = []
+        for b, (arena, descs), st in zip(bs, mats, streams):
+            if b.kind == "peso":
+                outs.append(tc.batch_peso(arena, descs, b.n, b.total_bytes, stream=st))
+            else:
+                outs.append(tc.batch_ipv4(arena, descs, b.n, b.total_bytes, stream=st)[0])
+    torch.cuda.synchronize()
+    for b, (arena, _), o in zip(bs, mats, outs):
+        host = arena.cpu().numpy()
+        exp = oracle.batch_peso(host, b.descs) if b.kind == "peso" else oracle.batch_ipv4(host, b.descs)[0]
+        np.testing.assert_array_equal(o.cpu().numpy(), exp)
+
+
 def test_host_batch_end_to_end(tc, oracle):
     """Pinned host arena -> H2D -> kernel -> D2H matches the device-resident path."""
     from tcp_amd import workload

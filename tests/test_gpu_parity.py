@@ -416,20 +416,21 @@ def test_hip_graph_capture_and_replay(tc, torch, oracle):
 
 
 def test_concurrent_streams(tc, torch, oracle):
-    """Independent batches on independent streams do not interfere."""
+    """Independent batches on independent streams do not interfere.  Outputs
+    are allocated once up front: a tensor freed on one stream and reused by
+    the caching allocator while another stream still writes it would race."""
     from tcp_amd import workload
     bs = [workload.make_batch(c, rank=r, n=n) for c, r, n in (("mtu", 0, 30000), ("mixed", 1, 8000), ("tso", 2, 64))]
     mats = [workload.materialize(b) for b in bs]
+    outs = [torch.zeros(b.n, dtype=torch.uint16 if b.kind == "peso" else torch.uint32, device="cuda") for b in bs]
     streams = [torch.cuda.Stream() for _ in bs]
     torch.cuda.synchronize()
-    outs = []
-    for rep in range(3):
-        outs = []
-        for b, (arena, descs), st in zip(bs, mats, streams):
+    for _ in range(3):
+        for b, (arena, descs), o, st in zip(bs, mats, outs, streams):
             if b.kind == "peso":
-                outs.append(tc.batch_peso(arena, descs, b.n, b.total_bytes, stream=st))
+                tc.batch_peso(arena, descs, b.n, b.total_bytes, out=o, stream=st)
             else:
-                outs.append(tc.batch_ipv4(arena, descs, b.n, b.total_bytes, stream=st)[0])
+                tc.batch_ipv4(arena, descs, b.n, b.total_bytes, out=o, want_flags=False, stream=st)
     torch.cuda.synchronize()
     for b, (arena, _), o in zip(bs, mats, outs):
         host = arena.cpu().numpy()

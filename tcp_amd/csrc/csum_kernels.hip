@@ -131,12 +131,32 @@ __device__ __forceinline__ void issue_fence()
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// x + (x of another lane selected by a DPP control), all lanes active.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_add(uint32_t x)
+{
+    return x + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+
+// Sum over the G lanes that share a packet, in every lane of the group.
+// Inside a 16-lane DPP row the butterfly is four DPP adds (quad_perm xor1,
+// xor2; row_ror 4, 8: no LDS unit, no waits); only the cross-row steps
+// (G = 8's xor 4, G >= 32) go through ds_bpermute.
 template <int G>
 __device__ __forceinline__ uint32_t group_sum(uint32_t x)
 {
-#pragma unroll
-    for (int m = G / 2; m >= 1; m >>= 1)
-        x += __shfl_xor(x, m, 64);
+    x = dpp_add<0xB1>(x); // quad_perm [1,0,3,2]: lane ^ 1
+    x = dpp_add<0x4E>(x); // quad_perm [2,3,0,1]: lane ^ 2
+    if constexpr (G == 8)
+        x += __shfl_xor(x, 4, 64);
+    if constexpr (G >= 16) {
+        x = dpp_add<0x124>(x); // row_ror:4 -- quad sums of lanes i, i-4
+        x = dpp_add<0x128>(x); // row_ror:8 -- + lanes i-8, i-12: the row sum
+    }
+    if constexpr (G >= 32)
+        x += __shfl_xor(x, 16, 64);
+    if constexpr (G >= 64)
+        x += __shfl_xor(x, 32, 64);
     return x;
 }
 

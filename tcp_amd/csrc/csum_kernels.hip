@@ -331,7 +331,7 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t *__restrict__ ar
 {
     static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G");
     const uint32_t gl = threadIdx.x & (G - 1);
-    const uint32_t seg = (blockIdx.x * 256u + threadIdx.x) / G;
+    const uint32_t seg = blockIdx.x * (256u / G) + threadIdx.x / G; // no 32-bit wrap for any n
     const bool live = seg < n;
     const SegDesc d = load_desc<MODE>(descs, seg, live);
     uint32_t acc = sum_range<G, U, MODE == MODE_EXACT>(arena, d.off, d.len, gl, [] {});
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(256) void k_segments_p(const uint8_t *__restrict__ 
 {
     constexpr uint32_t PER_WAVE = 64 / G;
     const uint32_t gl = threadIdx.x & (G - 1);
-    const uint32_t wave = (blockIdx.x * 256u + threadIdx.x) >> 6;
+    const uint32_t wave = blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint32_t step = gridDim.x * 4u * PER_WAVE;
     uint32_t seg = wave * PER_WAVE + ((threadIdx.x & 63u) / G);
     SegDesc d = load_desc<MODE>(descs, seg, seg < n);
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(256) void k_segments_pp(const uint8_t *__restrict__
 {
     constexpr uint32_t PER_WAVE = 64 / G;
     const uint32_t gl = threadIdx.x & (G - 1);
-    const uint32_t wave = (blockIdx.x * 256u + threadIdx.x) >> 6;
+    const uint32_t wave = blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint32_t step = gridDim.x * 4u * PER_WAVE;
     uint32_t seg = wave * PER_WAVE + ((threadIdx.x & 63u) / G);
     uint32_t first = wave * PER_WAVE; // wave-uniform loop control
@@ -478,7 +478,7 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const
                                               uint32_t diag)
 {
     const uint32_t gl = threadIdx.x & (G - 1);
-    const uint32_t pk = (blockIdx.x * 256u + threadIdx.x) / G;
+    const uint32_t pk = blockIdx.x * (256u / G) + threadIdx.x / G; // no 32-bit wrap for any n
     const bool live = pk < n;
 
     // unconditional loads throughout (dead lanes read descriptor 0 / the zero chunk)
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(256) void k_synth_ipv4(uint8_t *__restrict__ arena,
                                                     const tcsum_pkt_t *__restrict__ pkts,
                                                     uint32_t n, uint64_t seed)
 {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
     if (i >= n)
         return;
     const uint32_t len = pkts[i].len;

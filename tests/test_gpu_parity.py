@@ -438,6 +438,24 @@ def test_concurrent_streams(tc, torch, oracle):
         np.testing.assert_array_equal(o.cpu().numpy(), exp)
 
 
+def test_huge_batch_index_math(tc, torch, oracle, geometry):
+    """> 2^24 workgroups (67M one-packet-per-wave ranges): packet indices
+    must not wrap in 32-bit block*256 arithmetic."""
+    geometry(64, 1)
+    rng = np.random.default_rng(17)
+    host = rng.integers(0, 256, 1 << 16, dtype=np.uint8)
+    n = (1 << 26) + 1000
+    s = np.zeros(n, tc.SEG_DTYPE)
+    s["offset"] = rng.integers(0, (1 << 16) - 40, n)
+    s["len"] = rng.integers(0, 33, n)
+    s["pre_sum"] = rng.integers(0, 1 << 16, n)
+    arena = torch.from_numpy(host).cuda()
+    d = tc.descs_to_device(s)
+    out = tc.batch_segments(arena, d, n, 1)
+    exp = oracle.batch_segments(host, s, 1, nthreads=16)
+    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+
+
 def test_host_batch_end_to_end(tc, oracle):
     """Pinned host arena -> H2D -> kernel -> D2H matches the device-resident path."""
     from tcp_amd import workload

@@ -878,11 +878,31 @@ static hipError_t seg_u(int G, int U, int persist, uint32_t n, const void *arena
     return hipErrorInvalidValue;
 }
 
+// The AQL dispatch packet counts work-items in 32 bits: one launch may carry
+// at most 2^24 - 1 workgroups of 256 threads.  Larger batches are split into
+// several launches over consecutive descriptor ranges.
+static constexpr uint64_t kMaxBlocks = (1u << 24) - 1;
+
 hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void *descs, uint32_t n,
                            uint16_t *out, uint32_t aux, hipStream_t stream)
 {
     if (n == 0)
         return hipSuccess;
+    {
+        const uint32_t lanes = mode == MODE_EXACT ? 64u : (uint32_t)g.lanes;
+        const uint64_t per_launch = kMaxBlocks * (256u / (lanes ? lanes : 64u));
+        if (n > per_launch) {
+            const size_t dsz = mode == MODE_PESO ? sizeof(tcsum_peso_t) : sizeof(tcsum_seg_t);
+            for (uint64_t i0 = 0; i0 < n; i0 += per_launch) {
+                const uint32_t m = (uint32_t)(n - i0 < per_launch ? n - i0 : per_launch);
+                const hipError_t e = launch_segments(mode, g, arena, static_cast<const uint8_t *>(descs) + i0 * dsz,
+                                                     m, out + i0, aux, stream);
+                if (e != hipSuccess)
+                    return e;
+            }
+            return hipSuccess;
+        }
+    }
     if (mode == MODE_EXACT) {
         hipLaunchKernelGGL((k_segments<64, 8, MODE_EXACT>), dim3((n + 3) / 4), dim3(256), 0, stream,
                            static_cast<const uint8_t *>(arena), descs, n, out, aux);
@@ -921,6 +941,17 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
         return hipSuccess;
     if (g.lanes < 16)
         g.lanes = 16;
+    const uint64_t per_launch = kMaxBlocks * (256u / (uint32_t)g.lanes);
+    if (n > per_launch) { // see kMaxBlocks
+        for (uint64_t i0 = 0; i0 < n; i0 += per_launch) {
+            const uint32_t m = (uint32_t)(n - i0 < per_launch ? n - i0 : per_launch);
+            const hipError_t e = launch_ipv4(ip_mode, g, arena, pkts + i0, m, out ? out + i0 : nullptr,
+                                             flags ? flags + i0 : nullptr, verdict ? verdict + i0 : nullptr, stream);
+            if (e != hipSuccess)
+                return e;
+        }
+        return hipSuccess;
+    }
     const uint64_t per_block = 256u / (uint32_t)g.lanes;
     const dim3 grid((uint32_t)((n + per_block - 1) / per_block));
     // TCSUM_DIAG=1: tx fill computes but does not store (measurement only,

@@ -144,6 +144,28 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
                           const tcsum_peso_t *segs /*[host]*/, uint32_t n,
                           uint16_t *out /*[host]*/);
 
+/* Host-queue IPv4 batches: the frames of a netif
+ * in_q / out_q (net/src/netif.c:339-349, exmsg.c:89-112) as they sit in host
+ * memory.  Same semantics as the device-resident calls above; every pointer
+ * is [host] and the calls return when the results are in place.
+ *   - host_arena from tcsum_host_alloc (or any pinned memory) is read -- and
+ *     by tx fill written -- IN PLACE by the kernel over PCIe: no staging copy,
+ *     the "DMA-able pktbuf storage" of plat/ (pktbuf.c:13).
+ *   - a pageable host_arena is copied into pinned staging first (and, for tx
+ *     fill, copied back afterwards).
+ *   - every [offset, offset+len) must lie inside [0, arena_bytes) ->
+ *     otherwise TCSUM_ERR_PARAM and nothing is touched.
+ * out / flags may be NULL except out for tcsum_host_batch_ipv4. */
+int tcsum_host_batch_ipv4(int device, const void *host_arena, uint64_t arena_bytes,
+                          const tcsum_pkt_t *pkts /*[host]*/, uint32_t n, uint32_t *out /*[host]*/,
+                          uint8_t *flags /*[host] or NULL*/);
+int tcsum_host_batch_ipv4_tx_fill(int device, void *host_arena, uint64_t arena_bytes,
+                                  const tcsum_pkt_t *pkts /*[host]*/, uint32_t n,
+                                  uint32_t *out /*[host] or NULL*/, uint8_t *flags /*[host] or NULL*/);
+int tcsum_host_batch_ipv4_rx_verify(int device, const void *host_arena, uint64_t arena_bytes,
+                                    const tcsum_pkt_t *pkts /*[host]*/, uint32_t n, int8_t *verdict /*[host]*/,
+                                    uint32_t *out /*[host] or NULL*/, uint8_t *flags /*[host] or NULL*/);
+
 /* ------------------------------------------------------------ platform */
 
 /* HIP device init for the stack's net_plat_init hook (plat/net_plat.c:7):

@@ -38,6 +38,31 @@ using tcsum::Geometry;
 constexpr int kMaxDev = 16;
 constexpr int kHostStreams = 3;
 
+// Grow-only pinned, coherent host buffer with its device-side address.
+struct Pinned {
+    uint8_t *h = nullptr;
+    uint8_t *d = nullptr;
+    size_t cap = 0;
+    bool reserve(size_t bytes)
+    {
+        if (bytes <= cap)
+            return true;
+        size_t c = 1 << 16;
+        while (c < bytes)
+            c <<= 1;
+        if (h)
+            (void)hipHostFree(h);
+        h = d = nullptr;
+        cap = 0;
+        if (hipHostMalloc(reinterpret_cast<void **>(&h), c, hipHostMallocCoherent) != hipSuccess)
+            return false;
+        if (hipHostGetDevicePointer(reinterpret_cast<void **>(&d), h, 0) != hipSuccess)
+            return false;
+        cap = c;
+        return true;
+    }
+};
+
 struct Ctx {
     std::mutex mu;
     bool ready = false;
@@ -59,6 +84,9 @@ struct Ctx {
     size_t d_descs_cap = 0;
     uint16_t *d_out = nullptr;
     size_t d_out_cap = 0;
+    // host-queue batches: pinned, fine-grained descriptors / results / a copy
+    // of a pageable arena, all read and written by the kernel over PCIe
+    Pinned q_desc, q_res, q_arena;
 };
 
 Ctx g_ctx[kMaxDev];
@@ -466,6 +494,120 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         if (hipStreamSynchronize(s) != hipSuccess)
             return TCSUM_ERR_SYS;
     return TCSUM_OK;
+}
+
+// ------------------------------------------------------ host-queue batches
+
+namespace {
+
+// Device-side address of host memory the kernel may read/write in place
+// (pinned by hipHostMalloc / hipHostRegister), or nullptr for pageable memory.
+uint8_t *mapped_host(const void *p)
+{
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost)
+        return nullptr;
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, const_cast<void *>(p), 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return static_cast<uint8_t *>(d);
+}
+
+// IPv4 batch over packets in host memory (the stack's netif queues): pinned
+// arenas are read -- and for tx written -- in place by the kernel over PCIe;
+// a pageable arena is first copied into pinned staging (and copied back after
+// a tx fill).  Descriptors and results travel through pinned staging too.
+int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes, const tcsum_pkt_t *pkts,
+              uint32_t n, int8_t *verdict, uint32_t *out, uint8_t *flags)
+{
+    if (n == 0)
+        return TCSUM_OK;
+    if (!host_arena || !pkts || device < 0 || device >= kMaxDev || (ip_mode == 2 && !verdict))
+        return TCSUM_ERR_PARAM;
+    uint64_t lo = UINT64_MAX, hi = 0, total = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (pkts[i].offset > arena_bytes || pkts[i].len > arena_bytes - pkts[i].offset)
+            return TCSUM_ERR_PARAM;
+        if (pkts[i].len == 0)
+            continue;
+        lo = pkts[i].offset < lo ? pkts[i].offset : lo;
+        hi = pkts[i].offset + pkts[i].len > hi ? pkts[i].offset + pkts[i].len : hi;
+        total += pkts[i].len;
+    }
+    Ctx &c = g_ctx[device];
+    std::lock_guard<std::mutex> lk(c.mu);
+    int rc = ctx_init(c, device);
+    if (rc != TCSUM_OK)
+        return rc;
+    if (hipSetDevice(device) != hipSuccess)
+        return TCSUM_ERR_SYS;
+
+    uint8_t *d_arena = mapped_host(host_arena);
+    const bool staged = d_arena == nullptr;
+    constexpr uint64_t kPad = 16; // aligned over-reads around [lo, hi) stay inside the staging buffer
+    if (staged) {
+        if (hi <= lo)
+            lo = hi = 0;
+        if (!c.q_arena.reserve(hi - lo + 2 * kPad))
+            return TCSUM_ERR_MEM;
+        memcpy(c.q_arena.h + kPad, host_arena + lo, hi - lo);
+        d_arena = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(c.q_arena.d) + kPad - lo);
+    }
+    if (!c.q_desc.reserve(sizeof(tcsum_pkt_t) * n) || !c.q_res.reserve(6ull * n + 64))
+        return TCSUM_ERR_MEM;
+    memcpy(c.q_desc.h, pkts, sizeof(tcsum_pkt_t) * n);
+    // results: out u32[n] | flags u8[n] | verdict i8[n]
+    uint32_t *d_out = out ? reinterpret_cast<uint32_t *>(c.q_res.d) : nullptr;
+    uint8_t *d_flags = flags ? c.q_res.d + 4ull * n : nullptr;
+    int8_t *d_verdict = verdict ? reinterpret_cast<int8_t *>(c.q_res.d + 5ull * n) : nullptr;
+    hipError_t e = tcsum::launch_ipv4(ip_mode, tcsum::pick_geometry(mean_of(total, n)), d_arena,
+                                      reinterpret_cast<const tcsum_pkt_t *>(c.q_desc.d), n, d_out, d_flags,
+                                      d_verdict, c.stream);
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(c.stream);
+    if (e != hipSuccess)
+        return TCSUM_ERR_SYS;
+    if (out)
+        memcpy(out, c.q_res.h, 4ull * n);
+    if (flags)
+        memcpy(flags, c.q_res.h + 4ull * n, n);
+    if (verdict)
+        memcpy(verdict, c.q_res.h + 5ull * n, n);
+    if (staged && ip_mode == 1)
+        memcpy(host_arena + lo, c.q_arena.h + kPad, hi - lo);
+    return TCSUM_OK;
+}
+
+} // namespace
+
+int tcsum_host_batch_ipv4(int device, const void *host_arena, uint64_t arena_bytes, const tcsum_pkt_t *pkts,
+                          uint32_t n, uint32_t *out, uint8_t *flags)
+{
+    if (n && !out)
+        return TCSUM_ERR_PARAM;
+    return host_ipv4(0, device, const_cast<uint8_t *>(static_cast<const uint8_t *>(host_arena)), arena_bytes,
+                     pkts, n, nullptr, out, flags);
+}
+
+int tcsum_host_batch_ipv4_tx_fill(int device, void *host_arena, uint64_t arena_bytes, const tcsum_pkt_t *pkts,
+                                  uint32_t n, uint32_t *out, uint8_t *flags)
+{
+    return host_ipv4(1, device, static_cast<uint8_t *>(host_arena), arena_bytes, pkts, n, nullptr, out, flags);
+}
+
+int tcsum_host_batch_ipv4_rx_verify(int device, const void *host_arena, uint64_t arena_bytes,
+                                    const tcsum_pkt_t *pkts, uint32_t n, int8_t *verdict, uint32_t *out,
+                                    uint8_t *flags)
+{
+    // the kernel never writes the arena in this mode
+    return host_ipv4(2, device, const_cast<uint8_t *>(static_cast<const uint8_t *>(host_arena)), arena_bytes,
+                     pkts, n, verdict, out, flags);
 }
 
 // ================================================== drop-in legacy symbols

@@ -149,6 +149,74 @@ def host_batch_peso(host_arena: np.ndarray, segs: np.ndarray, device: int = 0) -
     return out
 
 
+class HostArena:
+    """Pinned host memory from tcsum_host_alloc (the plat/ pinned pool), viewed
+    as a numpy u8 array; the kernels read and write it in place."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        self._ptr = _lib.lib().tcsum_host_alloc(max(self.nbytes, 1))
+        if not self._ptr:
+            raise MemoryError(f"tcsum_host_alloc({nbytes}) failed")
+        buf = (ctypes.c_uint8 * max(self.nbytes, 1)).from_address(self._ptr)
+        self.array = np.ctypeslib.as_array(buf)[: self.nbytes]
+
+    def free(self):
+        if self._ptr:
+            self.array = None
+            _lib.lib().tcsum_host_free(self._ptr)
+            self._ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def _host_arena_args(host_arena):
+    arr = host_arena.array if isinstance(host_arena, HostArena) else host_arena
+    assert arr.dtype == np.uint8 and arr.flags["C_CONTIGUOUS"]
+    return arr.ctypes.data, arr.nbytes
+
+
+def host_batch_ipv4(host_arena, pkts: np.ndarray, device: int = 0):
+    """(out u32 = ip | l4 << 16, flags) for packets in host memory (tcsum_host_batch_ipv4)."""
+    assert pkts.dtype == PKT_DTYPE
+    pkts = np.ascontiguousarray(pkts)
+    out = np.zeros(pkts.size, np.uint32)
+    flags = np.zeros(pkts.size, np.uint8)
+    p, nb = _host_arena_args(host_arena)
+    _lib.check(_lib.lib().tcsum_host_batch_ipv4(device, p, nb, pkts.ctypes.data, pkts.size, out.ctypes.data,
+                                                flags.ctypes.data), "tcsum_host_batch_ipv4")
+    return out, flags
+
+
+def host_batch_ipv4_tx_fill(host_arena, pkts: np.ndarray, device: int = 0):
+    """Fill the checksum fields of packets in host memory in place; returns flags."""
+    assert pkts.dtype == PKT_DTYPE
+    pkts = np.ascontiguousarray(pkts)
+    flags = np.zeros(pkts.size, np.uint8)
+    p, nb = _host_arena_args(host_arena)
+    _lib.check(_lib.lib().tcsum_host_batch_ipv4_tx_fill(device, p, nb, pkts.ctypes.data, pkts.size, None,
+                                                        flags.ctypes.data), "tcsum_host_batch_ipv4_tx_fill")
+    return flags
+
+
+def host_batch_ipv4_rx_verify(host_arena, pkts: np.ndarray, device: int = 0):
+    """(verdict int8 net_err_t, out, flags) for packets in host memory."""
+    assert pkts.dtype == PKT_DTYPE
+    pkts = np.ascontiguousarray(pkts)
+    verdict = np.zeros(pkts.size, np.int8)
+    out = np.zeros(pkts.size, np.uint32)
+    flags = np.zeros(pkts.size, np.uint8)
+    p, nb = _host_arena_args(host_arena)
+    _lib.check(_lib.lib().tcsum_host_batch_ipv4_rx_verify(device, p, nb, pkts.ctypes.data, pkts.size,
+                                                          verdict.ctypes.data, out.ctypes.data, flags.ctypes.data),
+               "tcsum_host_batch_ipv4_rx_verify")
+    return verdict, out, flags
+
+
 def synth_fill(arena, nbytes: int | None = None, byte_base: int = 0, seed: int = 20240807, stream=None):
     n = arena.numel() if nbytes is None else nbytes
     _lib.check(_lib.lib().tcsum_synth_fill(arena.data_ptr(), n, byte_base, seed, _stream_ptr(stream)),

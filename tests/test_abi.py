@@ -134,6 +134,20 @@ def test_batch_argument_errors_without_device(libpath):
     out = np.zeros(1, np.uint16)
     rc = L.tcsum_host_batch_peso(0, host.ctypes.data, host.nbytes, seg.ctypes.data, 1, out.ctypes.data)
     assert rc == _lib.ERR_PARAM  # segment past the arena
+    from tcp_amd import PKT_DTYPE
+    pk = np.zeros(2, PKT_DTYPE)
+    pk["offset"], pk["len"] = (0, 60), (20, 5)  # the second ends past a 64-byte arena
+    out32, fl, vd = np.zeros(2, np.uint32), np.zeros(2, np.uint8), np.zeros(2, np.int8)
+    a = host.ctypes.data
+    assert L.tcsum_host_batch_ipv4(0, a, 64, pk.ctypes.data, 2, out32.ctypes.data, None) == _lib.ERR_PARAM
+    assert L.tcsum_host_batch_ipv4_tx_fill(0, a, 64, pk.ctypes.data, 2, None, None) == _lib.ERR_PARAM
+    assert L.tcsum_host_batch_ipv4_rx_verify(0, a, 64, pk.ctypes.data, 2, vd.ctypes.data, None,
+                                             None) == _lib.ERR_PARAM
+    assert L.tcsum_host_batch_ipv4_rx_verify(0, a, 64, pk.ctypes.data, 1, None, None, None) == _lib.ERR_PARAM
+    assert L.tcsum_host_batch_ipv4(0, a, 64, pk.ctypes.data, 1, None, fl.ctypes.data) == _lib.ERR_PARAM
+    assert L.tcsum_host_batch_ipv4_tx_fill(-1, a, 64, pk.ctypes.data, 1, None, None) == _lib.ERR_PARAM
+    assert L.tcsum_host_batch_ipv4_tx_fill(0, a, 64, pk.ctypes.data, 0, None, None) == _lib.OK
+    assert (host == 0).all()  # nothing touched
     assert L.tcsum_plat_init(99) == _lib.ERR_PARAM
 
 

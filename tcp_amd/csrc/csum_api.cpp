@@ -628,7 +628,7 @@ uint16_t checksum16(int offset, void *buf, uint16_t len, uint32_t pre_sum, int c
     d->offset = par;
     d->len = len;
     d->pre_sum = pre_sum;
-    const hipError_t e = tcsum::launch_segments(tcsum::MODE_EXACT, Geometry{64, 8, 0} /* unused for MODE_EXACT */, c.d_stage, c.d_desc,
+    const hipError_t e = tcsum::launch_segments(tcsum::MODE_EXACT, Geometry{64, 8, 0, 1} /* unused for MODE_EXACT */, c.d_stage, c.d_desc,
                                                 1, c.d_result, (complement ? 1u : 0u) | (par << 1), c.stream);
     run_sync(c, e);
     return *c.result;

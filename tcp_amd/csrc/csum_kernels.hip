@@ -160,6 +160,27 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t x)
     return x;
 }
 
+// XCD-grouped block order.  The dispatcher hands consecutive workgroups to
+// the 8 XCDs round-robin (MI355X_MICROARCH.md, workgroup dispatch), so with the
+// identity map the results of neighbouring packets -- one 128-byte line of
+// `out` -- are written by 4..16 workgroups on different XCDs, each L2 writing
+// its own partial copy of the line back to HBM, and the 16-byte chunk two
+// packed packets share is fetched by two L2s.  Remapped, every run of `xg`
+// consecutive logical blocks sits on one XCD (hardware blocks b, b+8, ...),
+// while the set of blocks in flight -- the HBM window the chip streams
+// through -- stays the same.  Bijective: a last, incomplete group of 8*xg
+// blocks keeps the identity map.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t xg)
+{
+    if (xg <= 1)
+        return b;
+    const uint32_t sg = 8u * xg;
+    if (b >= nb - nb % sg)
+        return b;
+    const uint32_t r = b % sg;
+    return b - r + (r & 7u) * xg + (r >> 3);
+}
+
 // ---------------------------------------------------------------- segments
 //
 // One descriptor per range.  MODE_SEG: pktbuf_checksum16 (u16 pre_sum);
@@ -327,11 +348,12 @@ __device__ __forceinline__ uint16_t finalize(uint32_t acc, uintptr_t start, cons
 template <int G, int U, int MODE>
 __global__ __launch_bounds__(256) void k_segments(const uint8_t *__restrict__ arena,
                                                   const void *__restrict__ descs, uint32_t n,
-                                                  uint16_t *__restrict__ out, uint32_t aux)
+                                                  uint16_t *__restrict__ out, uint32_t aux, uint32_t xg)
 {
     static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G");
     const uint32_t gl = threadIdx.x & (G - 1);
-    const uint32_t seg = blockIdx.x * (256u / G) + threadIdx.x / G; // no 32-bit wrap for any n
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    const uint32_t seg = blk * (256u / G) + threadIdx.x / G; // no 32-bit wrap for any n
     const bool live = seg < n;
     const SegDesc d = load_desc<MODE>(descs, seg, live);
     uint32_t acc = sum_range<G, U, MODE == MODE_EXACT>(arena, d.off, d.len, gl, [] {});
@@ -475,10 +497,11 @@ template <int G, int U, int IPM>
 __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                               uint32_t n, uint32_t *__restrict__ out,
                                               uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
-                                              uint32_t diag)
+                                              uint32_t diag, uint32_t xg)
 {
     const uint32_t gl = threadIdx.x & (G - 1);
-    const uint32_t pk = blockIdx.x * (256u / G) + threadIdx.x / G; // no 32-bit wrap for any n
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    const uint32_t pk = blk * (256u / G) + threadIdx.x / G; // no 32-bit wrap for any n
     const bool live = pk < n;
 
     // unconditional loads throughout (dead lanes read descriptor 0 / the zero chunk)
@@ -739,9 +762,9 @@ __global__ __launch_bounds__(256) void k_synth_ipv4(uint8_t *__restrict__ arena,
 // happens if the fold hits a magic value.
 template <int U>
 __global__ __launch_bounds__(256) void k_probe_read(const u32x4 *__restrict__ p, uint64_t nchunks,
-                                                    uint32_t *__restrict__ sink)
+                                                    uint32_t *__restrict__ sink, uint32_t xg)
 {
-    const uint64_t wave = (blockIdx.x * 256ull + threadIdx.x) >> 6;
+    const uint64_t wave = (xcd_block(blockIdx.x, gridDim.x, xg) * 256ull + threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t base = wave * 64ull * U;
     uint32_t acc = 0;
@@ -766,15 +789,18 @@ hipError_t launch_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, hip
     int U = 8;
     if (const char *s = getenv("TCSUM_PROBE_U"))
         U = atoi(s);
+    uint32_t xg = 1; // dispatch order: measured faster for the plain read (profiles/r01/xcd_tune.txt)
+    if (const char *s = getenv("TCSUM_PROBE_XCD"))
+        xg = (uint32_t)atoi(s);
     const uint64_t per_block = 4ull * 64 * (uint64_t)U;
     const dim3 grid((uint32_t)((nchunks + per_block - 1) / per_block));
     const u32x4 *q = static_cast<const u32x4 *>(p);
     switch (U) {
-    case 1: hipLaunchKernelGGL(k_probe_read<1>, grid, dim3(256), 0, stream, q, nchunks, sink); break;
-    case 2: hipLaunchKernelGGL(k_probe_read<2>, grid, dim3(256), 0, stream, q, nchunks, sink); break;
-    case 4: hipLaunchKernelGGL(k_probe_read<4>, grid, dim3(256), 0, stream, q, nchunks, sink); break;
-    case 16: hipLaunchKernelGGL(k_probe_read<16>, grid, dim3(256), 0, stream, q, nchunks, sink); break;
-    default: hipLaunchKernelGGL(k_probe_read<8>, grid, dim3(256), 0, stream, q, nchunks, sink); break;
+    case 1: hipLaunchKernelGGL(k_probe_read<1>, grid, dim3(256), 0, stream, q, nchunks, sink, xg); break;
+    case 2: hipLaunchKernelGGL(k_probe_read<2>, grid, dim3(256), 0, stream, q, nchunks, sink, xg); break;
+    case 4: hipLaunchKernelGGL(k_probe_read<4>, grid, dim3(256), 0, stream, q, nchunks, sink, xg); break;
+    case 16: hipLaunchKernelGGL(k_probe_read<16>, grid, dim3(256), 0, stream, q, nchunks, sink, xg); break;
+    default: hipLaunchKernelGGL(k_probe_read<8>, grid, dim3(256), 0, stream, q, nchunks, sink, xg); break;
     }
     return hipGetLastError();
 }
@@ -812,7 +838,9 @@ static uint32_t resident_blocks(K kernel)
 // The resident-grid variants (persist 1, 2) measured slower on all three.
 Geometry pick_geometry(uint64_t mean_len)
 {
-    Geometry g{32, 4, 0};
+    // xcd: 64 workgroups per XCD run (scripts/xcd_tune.py, profiles/r01/xcd_tune.txt:
+    // 2-4 % on every config, flat from 32 to 512)
+    Geometry g{32, 4, 0, 64};
     const uint64_t chunks = mean_len / 16 + 1;
     const uint64_t interior = chunks > 2 ? chunks - 2 : 0;
     if (chunks >= 2048) {
@@ -838,11 +866,13 @@ Geometry pick_geometry(uint64_t mean_len)
         g.loads = atoi(s);
     if (const char *s = getenv("TCSUM_P"))
         g.persist = atoi(s);
+    if (const char *s = getenv("TCSUM_XCD"))
+        g.xcd = atoi(s);
     return g;
 }
 
 template <int MODE>
-static hipError_t seg_u(int G, int U, int persist, uint32_t n, const void *arena, const void *descs,
+static hipError_t seg_u(int G, int U, int persist, uint32_t xg, uint32_t n, const void *arena, const void *descs,
                         uint16_t *out, uint32_t aux, hipStream_t s)
 {
 #define TCSUM_SEG(GG, UU)                                                                            \
@@ -861,7 +891,7 @@ static hipError_t seg_u(int G, int U, int persist, uint32_t n, const void *arena
                                aux);                                                               \
         } else {                                                                                   \
             hipLaunchKernelGGL((k_segments<GG, UU, MODE>), dim3(blocks), dim3(256), 0, s,          \
-                               static_cast<const uint8_t *>(arena), descs, n, out, aux);           \
+                               static_cast<const uint8_t *>(arena), descs, n, out, aux, xg);       \
         }                                                                                          \
         return hipGetLastError();                                                                  \
     }
@@ -905,22 +935,23 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
     }
     if (mode == MODE_EXACT) {
         hipLaunchKernelGGL((k_segments<64, 8, MODE_EXACT>), dim3((n + 3) / 4), dim3(256), 0, stream,
-                           static_cast<const uint8_t *>(arena), descs, n, out, aux);
+                           static_cast<const uint8_t *>(arena), descs, n, out, aux, 1u);
         return hipGetLastError();
     }
     if (mode == MODE_SEG)
-        return seg_u<MODE_SEG>(g.lanes, g.loads, g.persist, n, arena, descs, out, aux, stream);
-    return seg_u<MODE_PESO>(g.lanes, g.loads, g.persist, n, arena, descs, out, aux, stream);
+        return seg_u<MODE_SEG>(g.lanes, g.loads, g.persist, (uint32_t)g.xcd, n, arena, descs, out, aux, stream);
+    return seg_u<MODE_PESO>(g.lanes, g.loads, g.persist, (uint32_t)g.xcd, n, arena, descs, out, aux, stream);
 }
 
 template <int IPM>
 static hipError_t ipv4_u(int G, int U, dim3 grid, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
-                         uint32_t *out, uint8_t *flags, int8_t *verdict, uint32_t diag, hipStream_t s)
+                         uint32_t *out, uint8_t *flags, int8_t *verdict, uint32_t diag, uint32_t xg,
+                         hipStream_t s)
 {
 #define TCSUM_IP(GG, UU)                                                                             \
     if (G == GG && U == UU) {                                                                      \
         hipLaunchKernelGGL((k_ipv4<GG, UU, IPM>), grid, dim3(256), 0, s, arena, pkts, n, out, flags, \
-                           verdict, diag);                                                         \
+                           verdict, diag, xg);                                                     \
         return hipGetLastError();                                                                  \
     }
 #define TCSUM_IP_U(GG)                                                                               \
@@ -959,11 +990,11 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
     const uint32_t diag = getenv("TCSUM_DIAG") ? (uint32_t)atoi(getenv("TCSUM_DIAG")) : 0u;
     switch (ip_mode) {
     case IP_TX:
-        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, stream);
+        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, (uint32_t)g.xcd, stream);
     case IP_RX:
-        return ipv4_u<IP_RX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, stream);
+        return ipv4_u<IP_RX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, (uint32_t)g.xcd, stream);
     default:
-        return ipv4_u<IP_SUMS>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, stream);
+        return ipv4_u<IP_SUMS>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, (uint32_t)g.xcd, stream);
     }
 }
 

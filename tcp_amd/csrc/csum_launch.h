@@ -21,6 +21,7 @@ struct Geometry {
     int loads; // U: 16-byte loads in flight per lane per pass
     int persist; // 0: one pass per wave; 1: resident grid + descriptor prefetch;
                  // 2: resident grid, two ranges in flight per wave (k_segments_pp)
+    int xcd;     // consecutive workgroups kept on one XCD (1: dispatch order)
 };
 
 Geometry pick_geometry(uint64_t mean_len);

@@ -169,6 +169,32 @@ def test_batch_peso_golden(tc, torch, geometry, g, u, p):
     np.testing.assert_array_equal(out.cpu().numpy(), cases["expected"].astype(np.uint16))
 
 
+
+@pytest.mark.parametrize("xg", [1, 2, 3, 5, 64])
+def test_xcd_block_order_golden(tc, torch, geometry, monkeypatch, xg):
+    """The XCD-grouped workgroup order (TCSUM_XCD) is a bijection on the grid:
+    with groups small enough that the golden batches hold whole 8*xg groups
+    AND a tail group, every segment / packet still gets exactly its own result."""
+    monkeypatch.setenv("TCSUM_XCD", str(xg))
+    geometry(4, 4)
+    pool = G.pool()
+    cases, _ = G.peso_cases()
+    d = peso_descs(tc, cases)
+    out = torch.empty(d.size, dtype=torch.uint16, device="cuda")
+    out.view(torch.int16).fill_(-0x5556)  # 0xAAAA: a result nobody wrote shows up
+    tc.batch_peso(to_dev(torch, pool), tc.descs_to_device(d), d.size, out=out)
+    np.testing.assert_array_equal(out.cpu().numpy(), cases["expected"].astype(np.uint16))
+    geometry(16, 4)
+    cases, ipool = G.ipv4_rx_cases()
+    pk = G.pkt_descs(cases, tc.PKT_DTYPE)
+    verdict, flags = tc.batch_ipv4_rx_verify(to_dev(torch, ipool), tc.descs_to_device(pk), cases.size)
+    np.testing.assert_array_equal(verdict.cpu().numpy(), cases["verdict"])
+    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+    cases, pin, pout = G.ipv4_tx_cases()
+    arena = to_dev(torch, pin)
+    tc.batch_ipv4_tx_fill(arena, tc.descs_to_device(G.pkt_descs(cases, tc.PKT_DTYPE)), cases.size)
+    np.testing.assert_array_equal(arena.cpu().numpy()[: pout.size], pout)
+
 @pytest.mark.parametrize("p", [0, 1, 2])
 def test_batch_segments_golden(tc, torch, geometry, p):
     """pktbuf_checksum16 cases (from the cursor) and even-offset checksum16 cases

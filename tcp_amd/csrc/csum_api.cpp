@@ -4,11 +4,13 @@
 // kernels in csum_kernels.hip; nothing here sums bytes.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <mutex>
 #include <stddef.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <thread>
 #include <vector>
 
 #include "csum_launch.h"
@@ -519,6 +521,47 @@ uint8_t *mapped_host(const void *p)
     return static_cast<uint8_t *>(d);
 }
 
+// f(begin, end) over [0, n) split across host threads, at least `min_per`
+// items each (one core moves ~10-20 GB/s through memcpy; the PCIe link takes
+// ~55).  TCSUM_COPY_THREADS caps the count (default 16, the box's CPU share).
+extern "C++" {
+template <class F>
+void parallel_for(size_t n, size_t min_per, F &&f)
+{
+    static const unsigned cap = [] {
+        const char *s = getenv("TCSUM_COPY_THREADS");
+        const int v = s ? atoi(s) : 16;
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        return std::max(1u, std::min(hw, (unsigned)(v > 0 ? v : 1)));
+    }();
+    size_t k = std::min<size_t>(cap, min_per ? n / min_per : cap);
+    if (k <= 1) {
+        f(size_t(0), n);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(k - 1);
+    const size_t per = (n + k - 1) / k;
+    for (size_t i = 1; i < k; ++i) {
+        const size_t b = std::min(n, i * per), e = std::min(n, b + per);
+        th.emplace_back([&f, b, e] { f(b, e); });
+    }
+    f(size_t(0), std::min(n, per));
+    for (auto &t : th)
+        t.join();
+}
+}
+
+void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n)
+{
+    parallel_for(n, size_t(16) << 20, [=](size_t b, size_t e) { memcpy(dst + b, src + b, e - b); });
+}
+
+// The bytes of a packet a tx fill may write: the IPv4 header checksum at
+// 10..11 and the L4 checksum at hl + fld .. +1 with hl <= 60 (IHL <= 15) and
+// fld <= 16 (tcp.h:71): all below byte 78 of the packet.
+constexpr uint64_t kTxWindow = 78;
+
 // IPv4 batch over packets in host memory (the stack's netif queues): pinned
 // arenas are read -- and for tx written -- in place by the kernel over PCIe;
 // a pageable arena is first copied into pinned staging (and copied back after
@@ -556,7 +599,7 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
             lo = hi = 0;
         if (!c.q_arena.reserve(hi - lo + 2 * kPad))
             return TCSUM_ERR_MEM;
-        memcpy(c.q_arena.h + kPad, host_arena + lo, hi - lo);
+        par_memcpy(c.q_arena.h + kPad, host_arena + lo, hi - lo);
         d_arena = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(c.q_arena.d) + kPad - lo);
     }
     if (!c.q_desc.reserve(sizeof(tcsum_pkt_t) * n) || !c.q_res.reserve(6ull * n + 64))
@@ -579,8 +622,19 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
         memcpy(flags, c.q_res.h + 4ull * n, n);
     if (verdict)
         memcpy(verdict, c.q_res.h + 5ull * n, n);
-    if (staged && ip_mode == 1)
-        memcpy(host_arena + lo, c.q_arena.h + kPad, hi - lo);
+    if (staged && ip_mode == 1) {
+        // copy back only what the fill may have written: each packet's first
+        // kTxWindow bytes (staging holds the final state of every byte, so
+        // overlapping packets copy consistent values)
+        const uint8_t *st = c.q_arena.h + kPad;
+        parallel_for(n, size_t(1) << 16, [=](size_t b, size_t e) {
+            for (size_t i = b; i < e; ++i) {
+                const uint64_t w = pkts[i].len < kTxWindow ? pkts[i].len : kTxWindow;
+                if (w)
+                    memcpy(host_arena + pkts[i].offset, st + (pkts[i].offset - lo), w);
+            }
+        });
+    }
     return TCSUM_OK;
 }
 

@@ -76,8 +76,9 @@ def test_host_rx_verify_golden(tc, oracle, where, shift):
     np.testing.assert_array_equal(view[: pool.size], pool)  # rx never writes
 
 
-@pytest.mark.parametrize("n", [1, 50, 4096, 50])
-def test_host_queue_matches_device(tc, oracle, n):
+@pytest.mark.parametrize("n,where", [(1, "pinned"), (50, "pinned"), (4096, "pinned"), (50, "pageable"),
+                                     (70000, "pageable")])
+def test_host_queue_matches_device(tc, oracle, n, where):
     """A netif-queue-sized batch (NETIF_INQ_SIZE = 50, net_cfg.h:39) and a
     larger one, mixed 64-9000 B frames packed at odd offsets: host tx fill ->
     host rx verify (all OK) -> one corrupted byte per frame -> BROKEN; the
@@ -87,18 +88,23 @@ def test_host_queue_matches_device(tc, oracle, n):
     b = workload.make_batch("mixed_tx", n=n)
     arena, descs = workload.materialize(b)  # unfilled frames, generated on the GPU
     raw = arena.cpu().numpy()
-    ha = tc.HostArena(raw.size)
-    ha.array[:] = raw
-    tc.host_batch_ipv4_tx_fill(ha, b.descs)
+    # pinned: read/written in place; pageable (> 16 MiB and > 64K packets at the
+    # largest n): threaded staging copy, header windows copied back
+    ha = tc.HostArena(raw.size) if where == "pinned" else None
+    arg = ha if ha is not None else raw.copy()
+    view = ha.array if ha is not None else arg
+    view[:] = raw
+    tc.host_batch_ipv4_tx_fill(arg, b.descs)
     tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes)
     torch.cuda.synchronize()
-    np.testing.assert_array_equal(ha.array, arena.cpu().numpy())
-    verdict, _, _ = tc.host_batch_ipv4_rx_verify(ha, b.descs)
+    np.testing.assert_array_equal(view, arena.cpu().numpy())
+    verdict, _, _ = tc.host_batch_ipv4_rx_verify(arg, b.descs)
     assert (verdict == 0).all()
     pos = (b.descs["offset"] + 20 + (np.arange(n) * 7919) % (b.descs["len"] - 20)).astype(np.int64)
-    ha.array[pos] ^= 0x10
-    verdict, _, _ = tc.host_batch_ipv4_rx_verify(ha, b.descs)
-    ev, _ = oracle.batch_ipv4_rx_verify(ha.array, b.descs)
+    view[pos] ^= 0x10
+    verdict, _, _ = tc.host_batch_ipv4_rx_verify(arg, b.descs)
+    ev, _ = oracle.batch_ipv4_rx_verify(view, b.descs)
     np.testing.assert_array_equal(verdict, ev)
     assert (verdict == -13).mean() > 0.95
-    ha.free()
+    if ha is not None:
+        ha.free()

@@ -554,7 +554,7 @@ void parallel_for(size_t n, size_t min_per, F &&f)
 
 void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n)
 {
-    parallel_for(n, size_t(16) << 20, [=](size_t b, size_t e) { memcpy(dst + b, src + b, e - b); });
+    parallel_for(n, size_t(8) << 20, [=](size_t b, size_t e) { memcpy(dst + b, src + b, e - b); });
 }
 
 // The bytes of a packet a tx fill may write: the IPv4 header checksum at
@@ -599,7 +599,6 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
             lo = hi = 0;
         if (!c.q_arena.reserve(hi - lo + 2 * kPad))
             return TCSUM_ERR_MEM;
-        par_memcpy(c.q_arena.h + kPad, host_arena + lo, hi - lo);
         d_arena = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(c.q_arena.d) + kPad - lo);
     }
     if (!c.q_desc.reserve(sizeof(tcsum_pkt_t) * n) || !c.q_res.reserve(6ull * n + 64))
@@ -609,9 +608,51 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     uint32_t *d_out = out ? reinterpret_cast<uint32_t *>(c.q_res.d) : nullptr;
     uint8_t *d_flags = flags ? c.q_res.d + 4ull * n : nullptr;
     int8_t *d_verdict = verdict ? reinterpret_cast<int8_t *>(c.q_res.d + 5ull * n) : nullptr;
-    hipError_t e = tcsum::launch_ipv4(ip_mode, tcsum::pick_geometry(mean_of(total, n)), d_arena,
-                                      reinterpret_cast<const tcsum_pkt_t *>(c.q_desc.d), n, d_out, d_flags,
-                                      d_verdict, c.stream);
+    const tcsum_pkt_t *d_pkts = reinterpret_cast<const tcsum_pkt_t *>(c.q_desc.d);
+    auto launch = [&](uint32_t i0, uint32_t i1, uint64_t bytes) {
+        return tcsum::launch_ipv4(ip_mode, tcsum::pick_geometry(mean_of(bytes, i1 - i0)), d_arena, d_pkts + i0,
+                                  i1 - i0, d_out ? d_out + i0 : nullptr, d_flags ? d_flags + i0 : nullptr,
+                                  d_verdict ? d_verdict + i0 : nullptr, c.stream);
+    };
+    hipError_t e = hipSuccess;
+    uint8_t *const st = c.q_arena.h + kPad; // staging byte of arena offset x: st[x - lo]
+    bool in_order = staged;
+    for (uint32_t i = 1, last = 0; in_order && i < n; ++i)
+        if (pkts[i].len) {
+            in_order = pkts[i].offset >= pkts[last].offset;
+            last = i;
+        }
+    if (!staged) {
+        e = launch(0, n, total);
+    } else if (!in_order) {
+        par_memcpy(st, host_arena + lo, hi - lo);
+        e = launch(0, n, total);
+    } else {
+        // packets in offset order: stage 1/16 of the bytes (32..256 MiB) at a time and launch
+        // on each piece as soon as it is staged, so the host copy of the next
+        // piece overlaps the kernel's PCIe reads of this one.  `staged_hi`: every
+        // byte below it is in staging; no byte is copied twice (a tx fill may
+        // already have written it).
+        const uint64_t kPiece = std::min<uint64_t>(256ull << 20, std::max<uint64_t>(32ull << 20, (hi - lo) / 16));
+        uint64_t staged_hi = lo;
+        for (uint32_t i0 = 0; i0 < n && e == hipSuccess;) {
+            uint32_t i1 = i0;
+            uint64_t bytes = 0, end = staged_hi;
+            while (i1 < n && (i1 == i0 || bytes < kPiece)) {
+                if (pkts[i1].len) {
+                    bytes += pkts[i1].len;
+                    end = std::max<uint64_t>(end, pkts[i1].offset + pkts[i1].len);
+                }
+                ++i1;
+            }
+            if (end > staged_hi) {
+                par_memcpy(st + (staged_hi - lo), host_arena + staged_hi, end - staged_hi);
+                staged_hi = end;
+            }
+            e = launch(i0, i1, bytes);
+            i0 = i1;
+        }
+    }
     if (e == hipSuccess)
         e = hipStreamSynchronize(c.stream);
     if (e != hipSuccess)
@@ -626,7 +667,6 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
         // copy back only what the fill may have written: each packet's first
         // kTxWindow bytes (staging holds the final state of every byte, so
         // overlapping packets copy consistent values)
-        const uint8_t *st = c.q_arena.h + kPad;
         parallel_for(n, size_t(1) << 16, [=](size_t b, size_t e) {
             for (size_t i = b; i < e; ++i) {
                 const uint64_t w = pkts[i].len < kTxWindow ? pkts[i].len : kTxWindow;

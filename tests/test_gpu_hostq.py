@@ -108,3 +108,16 @@ def test_host_queue_matches_device(tc, oracle, n, where):
     assert (verdict == -13).mean() > 0.95
     if ha is not None:
         ha.free()
+
+
+@pytest.mark.parametrize("where", ["pinned", "pageable"])
+def test_host_tx_fill_any_descriptor_order(tc, where):
+    """Descriptors out of offset order take the one-launch staging path (the
+    pipelined one needs offset order): same bytes as the reference's tx path."""
+    cases, pin, pout = G.ipv4_tx_cases()
+    arg, view, keep = host_copy(tc, pin, where, 5)
+    pk = G.pkt_descs(cases, tc.PKT_DTYPE)
+    perm = np.random.default_rng(7).permutation(pk.size)
+    flags = tc.host_batch_ipv4_tx_fill(arg, pk[perm])
+    np.testing.assert_array_equal(view[: pout.size], pout)
+    np.testing.assert_array_equal(flags, cases["flags"][perm])

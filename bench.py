@@ -158,6 +158,11 @@ def pmc_traffic(config: str):
         except (subprocess.SubprocessError, OSError) as e:
             return None, f"rocprofv3 {counter} pass failed: {type(e).__name__}"
         files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        keep = os.environ.get("TCSUM_PMC_KEEP")  # directory to keep the raw counter CSVs in
+        if keep:
+            os.makedirs(keep, exist_ok=True)
+            for i, f in enumerate(files):
+                shutil.copy(f, os.path.join(keep, f"pmc_{counter.lower()}_{config}{'_%d' % i if i else ''}.csv"))
         per = []
         for f in files:
             with open(f) as fh:
@@ -184,17 +189,34 @@ def cpu_baseline(torch, r, seconds):
     import numpy as np
     pyoracle.build()
     b = r["batch"]
-    n = min(b.n, 65536 if b.config == "mtu" else 2048)
+    n = min(b.n, 65536 if b.config == "mtu" else 2048 if b.kind == "peso" else 16384)
     end = int(b.descs["offset"][n - 1] + b.descs["len"][n - 1])
     host = r["arena"][: end + 16].cpu().numpy()
-    segs = b.descs[:n].copy()
-    want = int(r["out"][:n].to(torch.int64).sum().item())
+    what = "segments"
+    if b.kind == "peso":
+        segs = b.descs[:n].copy()
+        want = int(r["out"][:n].to(torch.int64).sum().item())
+    else:
+        # IPv4 packets: the reference's per-packet cost is checksum_peso over
+        # the L4 bytes (tcp_in.c:80 / udp.c:410) plus checksum16 over the
+        # 20-byte header (ipv4.c:243, ~0.5 % of the bytes, not timed); the
+        # synthetic packets are IHL 5 with total_len == frame length
+        off = b.descs["offset"][:n].astype(np.int64)
+        hdr = host[off[:, None] + np.arange(20)[None, :]]
+        segs = np.zeros(n, pyoracle.PESO_DTYPE)
+        segs["offset"] = off + 20
+        segs["len"] = b.descs["len"][:n] - 20
+        segs["src"] = hdr[:, 12:16]
+        segs["dst"] = hdr[:, 16:20]
+        segs["protocol"] = hdr[:, 9]
+        want = int((r["out"][:n].to(torch.int64) >> 16).sum().item())
+        what = "packets' L4 ranges"
     rate1, kind, cs1 = pyoracle.time_peso(host, segs, 1, seconds, use_reference=True)
     threads = min(16, os.cpu_count() or 1)
     rateN, _, csN = pyoracle.time_peso(host, segs, threads, seconds / 2, use_reference=True)
     return {
         "value": round(rate1 / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
-        "sample": f"first {n} segments of the {b.config} batch ({n * int(segs['len'][0]) / 1e6:.0f} MB), "
+        "sample": f"first {n} {what} of the {b.config} batch ({int(segs['len'].sum()) / 1e6:.0f} MB), "
                   f"re-summed for >= {seconds:.0f} s",
         "multi": {"value": round(rateN / GIB, 3), "cores": threads},
         "parity": bool(cs1 == want and csN == want),

@@ -9,8 +9,7 @@
  * (net/net/net_cfg.h:31) point straight into the segment -- the layout the
  * stack's own pktbuf_alloc produces, without a copy -- so the time measured
  * is the reference's block walk + checksum16 loop, as it runs in-stack
- * (tcp_out.c:20, udp.c:321).  The chain is cached per thread and only re-aimed
- * when the next segment has the same length.
+ * (tcp_out.c:20, udp.c:321).  One chain per thread, re-aimed per segment.
  */
 #include <string.h>
 
@@ -23,32 +22,40 @@
 
 static __thread pktblk_t shim_blks[SHIM_MAX_BLKS];
 static __thread pktbuf_t shim_buf;
-static __thread int shim_len = -1;
+static __thread int shim_ready;
 
+/* Aim the thread's block chain at `seg`: the first ceil(len/127) blocks get
+ * their size/data and are linked, the list is cut after the last one.  Only
+ * the fields the stack's own pktbuf_alloc would have set are written, so
+ * re-aiming costs a few stores per block for any mix of lengths (the payload
+ * arrays are never touched: data points into the segment). */
 static pktbuf_t *aim_chain(const uint8_t *seg, int len)
 {
-    if (len != shim_len) {
-        memset(&shim_buf, 0, sizeof shim_buf);
-        list_init(&shim_buf.blk_list);
-        shim_buf.ref = 1;
-        int left = len, i = 0;
-        while (left > 0 && i < SHIM_MAX_BLKS) {
-            int take = left > PKTBUF_BLK_SIZE ? PKTBUF_BLK_SIZE : left;
-            pktblk_t *b = &shim_blks[i++];
-            memset(b, 0, sizeof *b);
-            b->size = take;
-            list_insert_last(&shim_buf.blk_list, &b->node);
-            shim_buf.total_size += take;
-            left -= take;
-        }
-        shim_len = len;
+    if (!shim_ready) {
+        memset(shim_blks, 0, sizeof shim_blks);
+        for (int i = 1; i < SHIM_MAX_BLKS; ++i)
+            shim_blks[i].node.pre = &shim_blks[i - 1].node;
+        shim_ready = 1;
     }
-    int off = 0;
-    for (node_t *n = list_first(&shim_buf.blk_list); n; n = list_node_next(n)) {
-        pktblk_t *b = list_node_parent(n, pktblk_t, node);
-        b->data = (uint8_t *)seg + off;
-        off += b->size;
+    int left = len, k = 0;
+    while (left > 0 && k < SHIM_MAX_BLKS) {
+        int take = left > PKTBUF_BLK_SIZE ? PKTBUF_BLK_SIZE : left;
+        pktblk_t *b = &shim_blks[k];
+        b->size = take;
+        b->data = (uint8_t *)seg + (len - left);
+        b->node.next = k + 1 < SHIM_MAX_BLKS ? &shim_blks[k + 1].node : (node_t *)0;
+        left -= take;
+        ++k;
     }
+    memset(&shim_buf, 0, sizeof shim_buf);
+    if (k) {
+        shim_blks[k - 1].node.next = (node_t *)0;
+        shim_buf.blk_list.first = &shim_blks[0].node;
+        shim_buf.blk_list.last = &shim_blks[k - 1].node;
+    }
+    shim_buf.blk_list.count = k;
+    shim_buf.total_size = len - left;
+    shim_buf.ref = 1;
     return &shim_buf;
 }
 

@@ -166,6 +166,18 @@ int tcsum_host_batch_ipv4_rx_verify(int device, const void *host_arena, uint64_t
                                     const tcsum_pkt_t *pkts /*[host]*/, uint32_t n, int8_t *verdict /*[host]*/,
                                     uint32_t *out /*[host] or NULL*/, uint8_t *flags /*[host] or NULL*/);
 
+/* Queue server for small host-queue batches (the stack's <= 50-frame netif
+ * queues, NETIF_INQ_SIZE net_cfg.h:39): with enable != 0, the
+ * tcsum_host_batch_ipv4* calls on `device` with n <= $TCSUM_SERVER_MAX
+ * (default 65536) frames are served by a resident grid that polls pinned
+ * memory for the next job, instead of one kernel launch and one stream sync
+ * per call (same results, same arguments).  The grid leaves by itself after
+ * $TCSUM_SERVER_IDLE_MS (default 10) without a job and is relaunched by the
+ * next call; while it is up, a device-wide synchronisation
+ * (hipDeviceSynchronize) waits for it to leave.  enable == 0 stops it (bounded
+ * wait).  Returns TCSUM_OK, TCSUM_ERR_NOT_SUPPORT without a gfx950 device. */
+int tcsum_queue_server(int device, int enable);
+
 /* ------------------------------------------------------------ platform */
 
 /* HIP device init for the stack's net_plat_init hook (plat/net_plat.c:7):

@@ -13,6 +13,8 @@ import tcp_amd as tc  # noqa: E402
 from tcp_amd import workload  # noqa: E402
 
 tc.plat_init(0)
+if os.environ.get("TCSUM_PROBE_SERVER") == "1":  # serve the calls from the resident grid
+    tc.queue_server(True)
 sizes = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 50, 1024, 65536, 1 << 20]
 for n in sizes:
     b = workload.make_batch("mixed_tx", n=n)
@@ -37,3 +39,5 @@ for n in sizes:
             print(f"n={n:8d} {mem:8s} {op}: {t*1e6:10.1f} us/call  {b.total_bytes/t/2**30:8.2f} GiB/s"
                   f"  ({b.total_bytes} B)", flush=True)
     ha.free()
+if os.environ.get("TCSUM_PROBE_SERVER") == "1":
+    tc.queue_server(False)  # TCSUM_SERVER_TRACE=1: prints the grid's phase timings

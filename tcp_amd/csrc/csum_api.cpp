@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
 #include <stddef.h>
 #include <stdio.h>
@@ -89,6 +90,16 @@ struct Ctx {
     // host-queue batches: pinned, fine-grained descriptors / results / a copy
     // of a pageable arena, all read and written by the kernel over PCIe
     Pinned q_desc, q_res, q_arena;
+    // queue server (tcsum_queue_server): a resident grid serving host-queue
+    // jobs posted through pinned memory, instead of a launch + sync per job
+    bool srv_on = false;      // enabled for this device
+    bool srv_running = false; // a grid was launched and not yet seen to finish
+    hipStream_t srv_stream = nullptr;
+    tcsum::SrvHost *srv_h = nullptr;  // pinned, coherent: host address
+    tcsum::SrvHost *srv_hd = nullptr; // ... and the device's address of it
+    tcsum::SrvCtl *srv_d = nullptr;
+    uint32_t srv_seq = 0; // last job posted (0 = none)
+    uint64_t *srv_trace = nullptr; // TCSUM_SERVER_TRACE stamps (host address)
 };
 
 Ctx g_ctx[kMaxDev];
@@ -562,6 +573,164 @@ void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n)
 // fld <= 16 (tcp.h:71): all below byte 78 of the packet.
 constexpr uint64_t kTxWindow = 78;
 
+// ---- queue server (k_server, csum_kernels.hip) ----
+
+int env_int(const char *name, int dflt)
+{
+    const char *s = getenv(name);
+    return s && *s ? atoi(s) : dflt;
+}
+
+// Largest host-queue batch handed to the server (bigger ones are bandwidth
+// work: a launch per batch costs nothing there).
+uint32_t srv_max_packets() { return (uint32_t)env_int("TCSUM_SERVER_MAX", 65536); }
+
+int srv_setup(Ctx &c)
+{
+    if (c.srv_h)
+        return TCSUM_OK;
+    if (hipStreamCreateWithFlags(&c.srv_stream, hipStreamNonBlocking) != hipSuccess)
+        return TCSUM_ERR_SYS;
+    if (hipHostMalloc(reinterpret_cast<void **>(&c.srv_h), sizeof(tcsum::SrvHost), hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void **>(&c.srv_hd), c.srv_h, 0) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&c.srv_d), sizeof(tcsum::SrvCtl)) != hipSuccess) {
+        c.srv_h = nullptr;
+        return TCSUM_ERR_MEM;
+    }
+    memset(c.srv_h, 0, sizeof(tcsum::SrvHost));
+    if (env_int("TCSUM_SERVER_TRACE", 0)) { // phase stamps, printed by srv_stop (measurement only)
+        uint64_t *t = nullptr, *td = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void **>(&t), 256 * 8 * sizeof(uint64_t), hipHostMallocCoherent) ==
+                hipSuccess &&
+            hipHostGetDevicePointer(reinterpret_cast<void **>(&td), t, 0) == hipSuccess) {
+            memset(t, 0, 256 * 8 * sizeof(uint64_t));
+            c.srv_trace = t;
+            c.srv_h->trace = reinterpret_cast<uint64_t>(td);
+        }
+    }
+    return TCSUM_OK;
+}
+
+// Mean phase durations over the traced jobs (TCSUM_SERVER_TRACE=1), in us.
+void srv_print_trace(const Ctx &c)
+{
+    const uint64_t *t = c.srv_trace;
+    if (!t)
+        return;
+    static const char *names[6] = {"seen->bcast", "bcast->wg1 seen", "bcast->wg0 summed", "wg0 release fence",
+                                   "wg0 release->last arrival", "last arrival->done stored"};
+    const int from[6] = {0, 1, 1, 3, 4, 5}, to[6] = {1, 2, 3, 4, 5, 6};
+    double sum[6] = {0};
+    int cnt[6] = {0};
+    for (int j = 0; j < 256; ++j)
+        for (int k = 0; k < 6; ++k) {
+            const uint64_t a = t[j * 8 + from[k]], b = t[j * 8 + to[k]];
+            if (a && b && b >= a && b - a < 100000000ull) {
+                sum[k] += (double)(b - a) / 100.0;
+                ++cnt[k];
+            }
+        }
+    for (int k = 0; k < 6; ++k)
+        if (cnt[k])
+            fprintf(stderr, "tcsum server trace: %-28s %8.2f us (%d jobs)\n", names[k], sum[k] / cnt[k], cnt[k]);
+}
+
+int srv_launch(Ctx &c, uint32_t last)
+{
+    const uint64_t idle_ticks = 100000ull * (uint64_t)std::max(1, env_int("TCSUM_SERVER_IDLE_MS", 10)); // 100 MHz
+    if (tcsum::launch_server(c.srv_hd, c.srv_d, last, idle_ticks, std::max(1, env_int("TCSUM_SERVER_WGS", 64)),
+                             c.srv_stream) != hipSuccess)
+        return TCSUM_ERR_SYS;
+    c.srv_running = true;
+    return TCSUM_OK;
+}
+
+// Ask the grid to leave and wait (bounded) until its stream is idle.
+int srv_stop(Ctx &c)
+{
+    if (!c.srv_h)
+        return TCSUM_OK;
+    __atomic_store_n(&c.srv_h->quit, 1u, __ATOMIC_SEQ_CST);
+    int rc = TCSUM_OK;
+    if (c.srv_running) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t q = hipStreamQuery(c.srv_stream);
+            if (q == hipSuccess)
+                break;
+            if (q != hipErrorNotReady || std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+                rc = TCSUM_ERR_SYS;
+                break;
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(100));
+        }
+        if (rc == TCSUM_OK)
+            c.srv_running = false;
+    }
+    if (rc == TCSUM_OK)
+        __atomic_store_n(&c.srv_h->quit, 0u, __ATOMIC_SEQ_CST);
+    srv_print_trace(c);
+    return rc;
+}
+
+// Post one job and wait for it.  A grid that left (idle, or a job posted
+// while it was leaving) is relaunched; it serves any job with req != last.
+int srv_submit(Ctx &c, int op, uint8_t *d_arena, const tcsum_pkt_t *d_pkts, uint32_t n, uint32_t *d_out,
+               uint8_t *d_flags, int8_t *d_verdict)
+{
+    int rc = srv_setup(c);
+    if (rc != TCSUM_OK)
+        return rc;
+    tcsum::SrvHost *h = c.srv_h;
+    const uint32_t prev = c.srv_seq;
+    const uint32_t seq = prev + 1u ? prev + 1u : 1u; // never 0
+    h->op = (uint32_t)op;
+    h->n = n;
+    h->ptr[0] = reinterpret_cast<uint64_t>(d_arena);
+    h->ptr[1] = reinterpret_cast<uint64_t>(d_pkts);
+    h->ptr[2] = reinterpret_cast<uint64_t>(d_out);
+    h->ptr[3] = reinterpret_cast<uint64_t>(d_flags);
+    h->ptr[4] = reinterpret_cast<uint64_t>(d_verdict);
+    __atomic_store_n(&h->req, seq, __ATOMIC_SEQ_CST); // after the job fields
+    c.srv_seq = seq;
+    if (!c.srv_running && (rc = srv_launch(c, prev)) != TCSUM_OK)
+        return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spins = 1;; ++spins) {
+        if (__atomic_load_n(&h->done, __ATOMIC_ACQUIRE) == seq)
+            return TCSUM_OK;
+        if ((spins & 255u) == 0) {
+            if (c.srv_running) {
+                const hipError_t q = hipStreamQuery(c.srv_stream);
+                if (q == hipSuccess)
+                    c.srv_running = false;
+                else if (q != hipErrorNotReady)
+                    return TCSUM_ERR_SYS;
+            }
+            if (!c.srv_running) {
+                if (__atomic_load_n(&h->done, __ATOMIC_ACQUIRE) == seq)
+                    return TCSUM_OK;
+                if ((rc = srv_launch(c, prev)) != TCSUM_OK)
+                    return rc;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+                return TCSUM_ERR_SYS;
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+// At unload: ask every live server grid to leave (bounded wait).
+struct SrvReaper {
+    ~SrvReaper()
+    {
+        for (auto &c : g_ctx)
+            if (c.srv_running)
+                (void)srv_stop(c);
+    }
+} g_srv_reaper;
+
 // IPv4 batch over packets in host memory (the stack's netif queues): pinned
 // arenas are read -- and for tx written -- in place by the kernel over PCIe;
 // a pageable arena is first copied into pinned staging (and copied back after
@@ -616,6 +785,15 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     };
     hipError_t e = hipSuccess;
     uint8_t *const st = c.q_arena.h + kPad; // staging byte of arena offset x: st[x - lo]
+    if (c.srv_on && n <= srv_max_packets()) { // small queue: the resident grid, no launch
+        if (staged)
+            par_memcpy(st, host_arena + lo, hi - lo);
+        rc = srv_submit(c, ip_mode, d_arena, d_pkts, n, d_out, d_flags, d_verdict);
+        if (rc != TCSUM_OK)
+            return rc;
+        goto results;
+    }
+    {
     bool in_order = staged;
     for (uint32_t i = 1, last = 0; in_order && i < n; ++i)
         if (pkts[i].len) {
@@ -657,6 +835,8 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
         e = hipStreamSynchronize(c.stream);
     if (e != hipSuccess)
         return TCSUM_ERR_SYS;
+    }
+results:
     if (out)
         memcpy(out, c.q_res.h, 4ull * n);
     if (flags)
@@ -702,6 +882,27 @@ int tcsum_host_batch_ipv4_rx_verify(int device, const void *host_arena, uint64_t
     // the kernel never writes the arena in this mode
     return host_ipv4(2, device, const_cast<uint8_t *>(static_cast<const uint8_t *>(host_arena)), arena_bytes,
                      pkts, n, verdict, out, flags);
+}
+
+int tcsum_queue_server(int device, int enable)
+{
+    if (device < 0 || device >= kMaxDev)
+        return TCSUM_ERR_PARAM;
+    Ctx &c = g_ctx[device];
+    std::lock_guard<std::mutex> lk(c.mu);
+    int rc = ctx_init(c, device);
+    if (rc != TCSUM_OK)
+        return rc;
+    if (hipSetDevice(device) != hipSuccess)
+        return TCSUM_ERR_SYS;
+    if (enable) {
+        rc = srv_setup(c);
+        if (rc == TCSUM_OK)
+            c.srv_on = true;
+        return rc;
+    }
+    c.srv_on = false;
+    return srv_stop(c);
 }
 
 // ================================================== drop-in legacy symbols

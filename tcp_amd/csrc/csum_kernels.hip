@@ -493,15 +493,16 @@ __device__ __forceinline__ uint32_t l4_field(uint32_t proto, uint32_t &min_len)
     return proto == 6 ? 16u : proto == 17 ? 6u : proto == 1 ? 2u : 0u;
 }
 
+// Packet `pk` (one per G-lane group; pk >= n: a dead group that reads
+// descriptor 0 and writes nothing).  Every lane of the wave must call it: the
+// group reduction crosses lanes.
 template <int G, int U, int IPM>
-__global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
-                                              uint32_t n, uint32_t *__restrict__ out,
-                                              uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
-                                              uint32_t diag, uint32_t xg)
+__device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
+                                            uint32_t pk, uint32_t n, uint32_t *__restrict__ out,
+                                            uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
+                                            uint32_t diag)
 {
     const uint32_t gl = threadIdx.x & (G - 1);
-    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
-    const uint32_t pk = blk * (256u / G) + threadIdx.x / G; // no 32-bit wrap for any n
     const bool live = pk < n;
 
     // unconditional loads throughout (dead lanes read descriptor 0 / the zero chunk)
@@ -692,6 +693,150 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const
             out[pk] = ip | (l4 << 16);
         if (flags_out)
             flags_out[pk] = (uint8_t)fl;
+    }
+}
+
+template <int G, int U, int IPM>
+__global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
+                                              uint32_t n, uint32_t *__restrict__ out,
+                                              uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
+                                              uint32_t diag, uint32_t xg)
+{
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    ipv4_packet<G, U, IPM>(arena, pkts, blk * (256u / G) + threadIdx.x / G, n, out, flags_out, verdict_out,
+                           diag); // no 32-bit wrap for any n
+}
+
+// ---------------------------------------------------------------- queue server
+//
+// A resident grid that serves small host-queue batches without a launch and
+// a stream sync per batch (tcsum_queue_server, include/tcsum.h).  The host
+// posts one job at a time into pinned, coherent memory (SrvHost: job fields,
+// then `req`); workgroup 0 polls `req` over PCIe with one lane and s_sleep,
+// copies the job into device memory (SrvCtl, agent-scope atomics) and bumps
+// SrvCtl::seq; the other workgroups poll that word (relaxed, s_sleep), take
+// ONE system-scope acquire (their L1/L2 may hold host lines from the last
+// job), and every workgroup sums its share of the packets.  Each workgroup
+// drains its stores, releases them at system scope (results and tx bytes live
+// in host memory) and adds to SrvCtl::arrivals; the last arriver writes
+// SrvHost::done.  Exit: workgroup 0 alone decides -- host `quit`, or no job
+// for `idle_ticks` of the 100 MHz real-time clock -- and publishes
+// SrvCtl::quit; every other workgroup also gives up after 8x that without a
+// word, so every wave reaches an exit.  A job posted while the grid is
+// leaving is never lost: the host sees the stream idle with done != req and
+// relaunches (csum_api.cpp).
+template <int G, int U>
+__global__ __launch_bounds__(256) void k_server(SrvHost *__restrict__ h, SrvCtl *__restrict__ d, uint32_t last,
+                                                uint64_t idle_ticks)
+{
+    __shared__ uint32_t s_go;
+    const bool lead = threadIdx.x == 0;
+    uint32_t jobs = 0;
+    uint64_t t_last = __builtin_amdgcn_s_memrealtime();
+    // phase stamps (100 MHz) of job j in tr[(j % 256) * 8 + k], measurement only
+    uint64_t *tr = reinterpret_cast<uint64_t *>(__hip_atomic_load(&h->trace, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    auto stamp = [&](int k) {
+        if (tr)
+            __hip_atomic_store(tr + (jobs % 256u) * 8u + k, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    };
+    for (;;) {
+        if (lead) {
+            uint32_t go = 0;
+            if (blockIdx.x == 0) {
+                for (;;) {
+                    const uint32_t r = __hip_atomic_load(&h->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (r != last) {
+                        stamp(0);
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // system: the host's job and data
+                        // all job words in flight together: one PCIe round trip, not seven
+                        const uint32_t jop = __hip_atomic_load(&h->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        const uint32_t jn = __hip_atomic_load(&h->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        uint64_t jp[5];
+#pragma unroll
+                        for (int k = 0; k < 5; ++k)
+                            jp[k] = __hip_atomic_load(&h->ptr[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __hip_atomic_store(&d->op, jop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&d->n, jn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                        for (int k = 0; k < 5; ++k)
+                            __hip_atomic_store(&d->ptr[k], jp[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        __hip_atomic_store(&d->seq, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        stamp(1);
+                        go = r;
+                        break;
+                    }
+                    if (__hip_atomic_load(&h->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                        __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) {
+                        __hip_atomic_store(&d->quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(4);
+                }
+            } else {
+                for (;;) {
+                    const uint32_t sq = __hip_atomic_load(&d->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (sq != 0u && sq != last) { // 0: zeroed at launch, nothing posted yet
+                        if (blockIdx.x == 1)
+                            stamp(2);
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // system: SrvCtl + the host's data
+                        go = sq;
+                        break;
+                    }
+                    if (__hip_atomic_load(&d->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+                        __builtin_amdgcn_s_memrealtime() - t_last > 8 * idle_ticks)
+                        break;
+                    __builtin_amdgcn_s_sleep(8);
+                }
+            }
+            s_go = go;
+        }
+        __syncthreads();
+        const uint32_t go = s_go;
+        if (!go)
+            return;
+        const uint32_t op = __hip_atomic_load(&d->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t n = __hip_atomic_load(&d->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t q[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            q[k] = __hip_atomic_load(&d->ptr[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint8_t *arena = reinterpret_cast<uint8_t *>(q[0]);
+        const tcsum_pkt_t *pkts = reinterpret_cast<const tcsum_pkt_t *>(q[1]);
+        uint32_t *out = reinterpret_cast<uint32_t *>(q[2]);
+        uint8_t *flags = reinterpret_cast<uint8_t *>(q[3]);
+        int8_t *verdict = reinterpret_cast<int8_t *>(q[4]);
+        constexpr uint32_t PER = 256u / G;
+        const uint32_t stride = gridDim.x * PER;
+        for (uint32_t first = blockIdx.x * PER; first < n; first += stride) { // workgroup-uniform
+            const uint32_t pk = first + threadIdx.x / G;
+            if (op == IP_TX)
+                ipv4_packet<G, U, IP_TX>(arena, pkts, pk, n, out, flags, verdict, 0u);
+            else if (op == IP_RX)
+                ipv4_packet<G, U, IP_RX>(arena, pkts, pk, n, out, flags, verdict, 0u);
+            else
+                ipv4_packet<G, U, IP_SUMS>(arena, pkts, pk, n, out, flags, verdict, 0u);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // every storing wave drains
+        __syncthreads();
+        if (lead) {
+            if (blockIdx.x == 0)
+                stamp(3);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // system: this workgroup's results / tx bytes
+            if (blockIdx.x == 0)
+                stamp(4);
+            const uint32_t old = __hip_atomic_fetch_add(&d->arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (old == (jobs + 1u) * gridDim.x - 1u) {
+                stamp(5);
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
+                __hip_atomic_store(&h->done, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                stamp(6);
+            }
+            ++jobs;
+        }
+        last = go;
+        t_last = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -996,6 +1141,18 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
     default:
         return ipv4_u<IP_SUMS>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, (uint32_t)g.xcd, stream);
     }
+}
+
+hipError_t launch_server(SrvHost *h, SrvCtl *d, uint32_t last, uint64_t idle_ticks, int wgs, hipStream_t stream)
+{
+    hipError_t e = hipMemsetAsync(d, 0, sizeof(SrvCtl), stream); // re-initialise every polled word
+    if (e != hipSuccess)
+        return e;
+    // 64 lanes x 16 loads per frame: a frame of up to 16 KiB is one pass -- one
+    // PCIe round trip for its bytes (the server's frames live in host memory)
+    hipLaunchKernelGGL((k_server<64, 16>), dim3((uint32_t)(wgs > 0 ? wgs : 1)), dim3(256), 0, stream, h, d, last,
+                       idle_ticks);
+    return hipGetLastError();
 }
 
 hipError_t launch_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, uint64_t seed,

@@ -34,6 +34,30 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
 hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
                        uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream);
 
+// Queue server (k_server): one job at a time.  SrvHost lives in pinned,
+// coherent host memory (the host writes the job, then `req`, and reads `done`);
+// SrvCtl in device memory (zeroed before every launch).
+struct SrvHost {
+    uint32_t req;  // host: sequence number of the posted job (never 0)
+    uint32_t quit; // host: ask the grid to leave
+    uint32_t op;   // IP_SUMS / IP_TX / IP_RX
+    uint32_t n;    // packets
+    uint64_t ptr[5]; // device-visible: arena, pkts, out, flags, verdict (0 = none)
+    uint64_t trace;  // device-visible u64[256 * 8] of phase stamps, or 0 (TCSUM_SERVER_TRACE)
+    uint32_t pad[2];
+    alignas(64) uint32_t done; // device: last completed job
+};
+struct SrvCtl {
+    uint32_t seq, quit, op, n;
+    uint64_t ptr[5];
+    uint32_t arrivals;
+    uint32_t pad;
+};
+static_assert(sizeof(SrvCtl) % 16 == 0, "SrvCtl is memset whole");
+
+hipError_t launch_server(SrvHost *h /*device-visible address*/, SrvCtl *d, uint32_t last, uint64_t idle_ticks,
+                         int wgs, hipStream_t stream);
+
 hipError_t launch_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, uint64_t seed,
                              hipStream_t stream);
 

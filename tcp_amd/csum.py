@@ -251,3 +251,8 @@ def device_count() -> int:
 
 def plat_init(device: int = 0) -> None:
     _lib.check(_lib.lib().tcsum_plat_init(device), "tcsum_plat_init")
+
+
+def queue_server(enable: bool, device: int = 0) -> None:
+    """Serve small host-queue batches from a resident grid (tcsum_queue_server)."""
+    _lib.check(_lib.lib().tcsum_queue_server(device, 1 if enable else 0), "tcsum_queue_server")

@@ -21,9 +21,18 @@ arena, descs = workload.materialize(b)
 out = torch.empty(b.n, dtype=torch.uint16 if b.kind == "peso" else torch.uint32, device="cuda")
 
 
+verdict = torch.empty(b.n, dtype=torch.int8, device="cuda")
+if cfg == "mixed_tx":  # fill once so every timed launch rewrites the same values
+    tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
+
+
 def run():
     if b.kind == "peso":
         tc.batch_peso(arena, descs, b.n, b.total_bytes, out=out)
+    elif cfg == "mixed_tx":
+        tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, out=out, want_flags=False)
+    elif cfg == "mixed_rx":
+        tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes, verdict=verdict, out=out, want_flags=False)
     else:
         tc.batch_ipv4(arena, descs, b.n, b.total_bytes, out=out, want_flags=False)
 

@@ -977,8 +977,8 @@ static uint32_t resident_blocks(K kernel)
 //   c <= ~136 (<= ~2 KiB, e.g. MTU): 16 lanes, U = ceil(c/16) loads -> one
 //       pass with almost no idle slots (1500 B: G=16, U=6, 95% of the read
 //       probe on the same bytes);
-//   ~2 KiB .. 32 KiB (mixed 64-9000 B, mean 4.5 KiB): 32 lanes x 4 loads,
-//       several passes (93-96% of the probe);
+//   ~2 KiB .. 32 KiB (mixed 64-9000 B, mean 4.5 KiB): 32 lanes x 6 loads,
+//       several passes (95-97% of the probe; re-measured with the XCD order);
 //   >= 32 KiB (TSO): one range per wave, 16 loads per lane (98-100%).
 // The resident-grid variants (persist 1, 2) measured slower on all three.
 Geometry pick_geometry(uint64_t mean_len)
@@ -993,7 +993,7 @@ Geometry pick_geometry(uint64_t mean_len)
         g.loads = 16;
     } else if (interior > 128) {
         g.lanes = 32;
-        g.loads = 4;
+        g.loads = 6; // 1.0-1.5 % over 4 and 8 on every mixed variant (profiles/r01/geom_tune_mixed.txt)
     } else if (interior > 32) {
         g.lanes = 16;
         const uint64_t u = (interior + 15) / 16; // 3..8

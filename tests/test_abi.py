@@ -91,7 +91,7 @@ def test_pktbuf_cursor_walk_on_host():
 def test_geometry_choice(libpath):
     from tcp_amd import pick_geometry
     assert pick_geometry(1500) == (16, 6)
-    assert pick_geometry(4500) == (32, 4)
+    assert pick_geometry(4500) == (32, 6)
     assert pick_geometry(65536) == (64, 16)
     assert pick_geometry(64) == (4, 1)
     for n in range(0, 70000, 37):  # every choice is an instantiated kernel

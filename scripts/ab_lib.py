@@ -1,0 +1,71 @@
+"""A/B two builds of libtcsum.so in ONE process (box-to-box spread is larger
+than the effects measured): interleaved rounds, median ms per launch, and the
+outputs of every build must be identical.
+
+  python scripts/ab_lib.py LIB_A LIB_B [configs]   (configs: mtu,tso,mixed,mixed_tx,mixed_rx)
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import tcp_amd as tc  # noqa: E402
+from tcp_amd import _lib, workload  # noqa: E402
+
+
+def load(path):
+    L = ctypes.CDLL(os.path.abspath(path))
+    for name, (res, args) in _lib.SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+    return L
+
+
+libs = [load(p) for p in sys.argv[1:3]]
+configs = sys.argv[3].split(",") if len(sys.argv) > 3 else ["mtu", "tso", "mixed", "mixed_tx", "mixed_rx"]
+rounds, reps = 5, 10
+for cfg in configs:
+    base = cfg.split("_")[0] if cfg in ("mixed_tx", "mixed_rx") else cfg
+    b = workload.make_batch(base)
+    arena, descs = workload.materialize(b)
+    peso = b.kind == "peso"
+    outs = [torch.empty(b.n, dtype=torch.uint16 if peso else torch.uint32, device="cuda") for _ in libs]
+    verdict = torch.empty(b.n, dtype=torch.int8, device="cuda")
+    if cfg == "mixed_tx":  # fill once: every timed launch rewrites the same values
+        tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
+
+    def run(i):
+        _lib._lib = libs[i]
+        if peso:
+            tc.batch_peso(arena, descs, b.n, b.total_bytes, out=outs[i])
+        elif cfg == "mixed_tx":
+            tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, out=outs[i], want_flags=False)
+        elif cfg == "mixed_rx":
+            tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes, verdict=verdict, out=outs[i],
+                                    want_flags=False)
+        else:
+            tc.batch_ipv4(arena, descs, b.n, b.total_bytes, out=outs[i], want_flags=False)
+
+    times = [[] for _ in libs]
+    for r in range(rounds):
+        for i in range(len(libs)):
+            run(i)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                run(i)
+            e1.record()
+            torch.cuda.synchronize()
+            times[i].append(e0.elapsed_time(e1) / reps)
+    same = all(torch.equal(outs[0], o) for o in outs[1:])
+    print(f"== {cfg} n={b.n} bytes={b.total_bytes} identical={same}", flush=True)
+    for i, p in enumerate(sys.argv[1:3]):
+        med = float(np.median(times[i]))
+        print(f"  {os.path.basename(p):24s} {med * 1e3:8.1f} us  {b.total_bytes / med / 1e6:8.1f} GB/s payload"
+              f"  (min {min(times[i]) * 1e3:.1f})", flush=True)
+    assert same, cfg
+    del arena, descs, outs
+    torch.cuda.empty_cache()

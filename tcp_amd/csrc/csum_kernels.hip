@@ -30,6 +30,14 @@
 namespace tcsum {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Minimum waves per SIMD asked of the register allocator for the streaming
+// kernels with U <= 8 loads per lane (TCSUM_WAVES_U8; 0 = the compiler's
+// choice).  Experiment knob; see pick_geometry.
+#ifndef TCSUM_WAVES_U8
+#define TCSUM_WAVES_U8 0
+#endif
+#define TCSUM_OCC(U) __attribute__((amdgpu_waves_per_eu((U) <= 8 && TCSUM_WAVES_U8 ? TCSUM_WAVES_U8 : 1)))
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 // a.lo + a.hi + acc in one VALU op (v_dot2_u32_u16 with {1,1}).
@@ -274,22 +282,31 @@ __device__ __forceinline__ uint32_t frame_consume(Frame<U> &f, uint32_t gl)
         const int hi = f.has_edge ? (int)(f.e - c < 16 ? f.e - c : 16) : 0;
         acc = chunk_sum_masked(0u, f.ev, lo, hi);
     }
-    for (uint32_t b0 = 0; b0 < f.ni;) {
+    // pass 0: the loads frame_issue put in flight
+    {
+        uint32_t part = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            part = chunk_sum_w(part, f.v[u], (uint32_t)(u * G) + gl < f.ni ? 0x00010001u : 0u);
+        acc = EXACT ? acc + part : fold_step(acc + part);
+    }
+    // later passes load and sum inside one iteration: nothing vector-sized is
+    // carried around the loop, so its registers are pass 0's (a loop-carried
+    // f.v made hipcc keep two copies: 68 -> 52 VGPRs at U=6, 8 waves/SIMD)
+    for (uint32_t b0 = G * U; b0 < f.ni; b0 += G * U) {
+        u32x4 w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = b0 + u * G + gl;
+            w[u] = load16<true>(f.ibase + (j < f.ni ? j : f.ilast));
+        }
         uint32_t part = 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t j = b0 + u * G + gl;
-            part = chunk_sum_w(part, f.v[u], j < f.ni ? 0x00010001u : 0u);
+            part = chunk_sum_w(part, w[u], j < f.ni ? 0x00010001u : 0u);
         }
         acc = EXACT ? acc + part : fold_step(acc + part);
-        b0 += G * U;
-        if (b0 >= f.ni)
-            break;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t j = b0 + u * G + gl;
-            f.v[u] = load16<true>(f.ibase + (j < f.ni ? j : f.ilast));
-        }
     }
     return acc;
 }
@@ -346,7 +363,7 @@ __device__ __forceinline__ uint16_t finalize(uint32_t acc, uintptr_t start, cons
 
 // One wave-slice of packets per wave, one launch-wide pass.
 template <int G, int U, int MODE>
-__global__ __launch_bounds__(256) void k_segments(const uint8_t *__restrict__ arena,
+__global__ __launch_bounds__(256) TCSUM_OCC(U) void k_segments(const uint8_t *__restrict__ arena,
                                                   const void *__restrict__ descs, uint32_t n,
                                                   uint16_t *__restrict__ out, uint32_t aux, uint32_t xg)
 {
@@ -591,7 +608,10 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     const int i0 = (int)s0 + 10; // IPv4 header checksum field
 
     uint32_t acc_h = 0, acc_l = 0, acc_f = 0;
-    for (uint32_t b0 = 0; b0 < nch;) {
+    // one pass of U chunks per lane starting at chunk b0 (pass 0: the loads
+    // already in flight; later passes load and sum inside one iteration, so
+    // no vector registers are carried around the loop -- see frame_consume)
+    auto pass = [&](const u32x4 (&vv)[U], uint32_t b0) {
         uint32_t ph = 0, pl = 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -600,32 +620,35 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
             const int c = (int)(16u * idx);
             const bool inner = valid && c >= h_end && c + 16 <= l_end && (f0 + 2 <= c || f0 >= c + 16);
             if (valid && !inner) { // header chunks, the field chunk(s), the last chunk: rare
-                uint32_t th = region_sum(v[u], c, (int)s0, h_end);
-                uint32_t tl4 = region_sum(v[u], c, h_end, l_end);
+                uint32_t th = region_sum(vv[u], c, (int)s0, h_end);
+                uint32_t tl4 = region_sum(vv[u], c, h_end, l_end);
                 if (field_on) {
-                    const uint32_t tf = region_sum(v[u], c, f0, f0 + 2);
+                    const uint32_t tf = region_sum(vv[u], c, f0, f0 + 2);
                     if (IPM == IP_TX)
                         tl4 -= tf; // tcp_out.c:19 / udp.c:320 / icmpv4.c:58 zero it first
                     else
                         acc_f += tf;
                 }
                 if (IPM == IP_TX)
-                    th -= region_sum(v[u], c, i0, i0 + 2); // ipv4.c:643
+                    th -= region_sum(vv[u], c, i0, i0 + 2); // ipv4.c:643
                 ph += th;
                 pl += tl4;
             }
-            pl = chunk_sum_w(pl, v[u], inner ? 0x00010001u : 0u);
+            pl = chunk_sum_w(pl, vv[u], inner ? 0x00010001u : 0u);
         }
         acc_h += ph; // header <= 60 bytes: no overflow
         acc_l = fold_step(acc_l + pl);
-        b0 += G * U;
-        if (b0 >= nch)
-            break;
+    };
+    if (nch)
+        pass(v, 0u);
+    for (uint32_t b0 = G * U; b0 < nch; b0 += G * U) {
+        u32x4 w[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t idx = b0 + u * G + gl;
-            v[u] = load16<true>(dbase + (idx < nch ? idx : dlast));
+            w[u] = load16<true>(dbase + (idx < nch ? idx : dlast));
         }
+        pass(w, b0);
     }
     acc_h = group_sum<G>(acc_h);
     acc_l = group_sum<G>(acc_l);
@@ -697,7 +720,7 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
 }
 
 template <int G, int U, int IPM>
-__global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
+__global__ __launch_bounds__(256) TCSUM_OCC(U) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                               uint32_t n, uint32_t *__restrict__ out,
                                               uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
                                               uint32_t diag, uint32_t xg)

@@ -493,6 +493,34 @@ def test_host_batch_end_to_end(tc, oracle):
     np.testing.assert_array_equal(out, oracle.batch_peso(host, d, nthreads=8))
 
 
+@pytest.mark.parametrize("shift", [0, 7])
+def test_host_batch_pinned(tc, oracle, shift):
+    """A pinned arena (tcsum_host_alloc), ragged segments in any order, at an
+    odd arena base too: same results as the oracle."""
+    import ctypes
+    from tcp_amd import _lib, workload
+    b = workload.make_batch("mtu", n=20000)
+    L = _lib.lib()
+    nbytes = b.alloc_bytes + shift
+    p = L.tcsum_host_alloc(nbytes)
+    assert p
+    try:
+        host = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p))[shift:]
+        host[:] = oracle.synth_fill(b.byte_base, b.alloc_bytes, b.seed)
+        rng = np.random.default_rng(5)
+        segs = np.zeros(b.n, tc.PESO_DTYPE)
+        segs["offset"] = b.descs["offset"]
+        segs["len"] = rng.integers(0, 1501, b.n)  # ragged, inside each 1500-B slot
+        segs["src"] = rng.integers(0, 256, (b.n, 4))
+        segs["dst"] = rng.integers(0, 256, (b.n, 4))
+        segs["protocol"] = rng.choice([6, 17], b.n)
+        segs = segs[rng.permutation(b.n)]
+        out = tc.host_batch_peso(host, segs)
+        np.testing.assert_array_equal(out, oracle.batch_peso(np.array(host), segs, nthreads=8))
+    finally:
+        L.tcsum_host_free(p)
+
+
 # --------------------------------------------------- full BASELINE sizes
 
 def test_full_mtu_batch_exact(tc, torch, oracle):

@@ -181,6 +181,16 @@ def pmc_traffic(config: str):
 
 # ------------------------------------------------------------ CPU baseline
 
+def cpu_model():
+    """The GPU box's host CPU as /proc/cpuinfo names it (and its logical CPUs)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            names = [ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")]
+        return f"{names[0]} ({len(names)} logical CPUs on the host)" if names else None
+    except OSError:
+        return None
+
+
 def cpu_baseline(torch, r, seconds):
     """The reference's checksum_peso (oracle/_ref/libtcpref.so, compiled from
     /root/reference; else the oracle port) on a bounded sample of the same
@@ -219,6 +229,7 @@ def cpu_baseline(torch, r, seconds):
         "sample": f"first {n} {what} of the {b.config} batch ({int(segs['len'].sum()) / 1e6:.0f} MB), "
                   f"re-summed for >= {seconds:.0f} s",
         "multi": {"value": round(rateN / GIB, 3), "cores": threads},
+        "host_cpu": cpu_model(),
         "parity": bool(cs1 == want and csN == want),
     }
 

@@ -66,6 +66,6 @@ for cfg in configs:
         med = float(np.median(times[i]))
         print(f"  {os.path.basename(p):24s} {med * 1e3:8.1f} us  {b.total_bytes / med / 1e6:8.1f} GB/s payload"
               f"  (min {min(times[i]) * 1e3:.1f})", flush=True)
-    assert same, cfg
+    assert same or os.environ.get("AB_ALLOW_DIFF") == "1", cfg
     del arena, descs, outs
     torch.cuda.empty_cache()

@@ -16,8 +16,8 @@ TCSUM_PMC_KEEP="$out" timeout -k 10 300 python -u bench.py > "$out/bench.json"
 echo "== rocprof ($(date +%T))"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/rocprof" -o bench \
     -- python -u bench.py --no-pmc > "$out/bench_under_rocprof.json"
-trace=$(find "$out/rocprof" -name 'bench_kernel_trace.csv' | head -n 1)
-stats=$(find "$out/rocprof" -name 'bench_kernel_stats.csv' | head -n 1)
+trace=$(find "$out/rocprof" -name 'bench_kernel_trace.csv' -print -quit)
+stats=$(find "$out/rocprof" -name 'bench_kernel_stats.csv' -print -quit)
 cp "$trace" "$out/bench_kernel_trace.csv"
 cp "$stats" "$out/bench_kernel_stats.csv"
 python scripts/group_trace.py "$out/bench_kernel_trace.csv" \

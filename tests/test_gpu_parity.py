@@ -538,7 +538,7 @@ def test_full_mixed_batch_exact(tc, torch, oracle):
 
 
 def test_full_tso_batch_properties(tc, torch, oracle):
-    """configs[2] at full size (256K x 64 KiB = 16 GiB): a sampled exact check,
+    """configs[2] at full size (256K x 64 KiB = 16 GiB): every segment exact,
     run-to-run determinism, geometry invariance, and the RFC 1624 incremental
     update on every segment (changing one 16-bit word m -> m' turns checksum
     HC into ~(~HC + ~m + m'))."""
@@ -556,7 +556,12 @@ def test_full_tso_batch_properties(tc, torch, oracle):
     finally:
         del os.environ["TCSUM_G"], os.environ["TCSUM_U"], os.environ["TCSUM_P"]
     np.testing.assert_array_equal(hc, out3.cpu().numpy())
-    # sampled exact parity
+    # every segment exact: the 16 GiB arena copied to the host once, the
+    # oracle over all 262,144 segments on 16 threads
+    host = arena.cpu().numpy()
+    np.testing.assert_array_equal(hc, oracle.batch_peso(host, b.descs, nthreads=16))
+    del host
+    # sampled exact parity through the single-segment oracle entry point
     rng = np.random.default_rng(11)
     idx = np.sort(rng.choice(b.n, 512, replace=False))
     for i in idx:

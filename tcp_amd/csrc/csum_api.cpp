@@ -466,7 +466,9 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; ++i)
         total += segs[i].len;
-    const uint64_t target = 32ull << 20;
+    uint64_t target = 32ull << 20; // bytes per chunk; TCSUM_E2E_CHUNK_MB overrides (measurement)
+    if (const char *v = getenv("TCSUM_E2E_CHUNK_MB"))
+        target = (uint64_t)std::max(1, atoi(v)) << 20;
     uint32_t per = (uint32_t)(total ? ((uint64_t)n * target + total - 1) / total : n);
     if (per == 0)
         per = 1;

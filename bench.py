@@ -260,8 +260,20 @@ def e2e(torch, tc, r):
             out = tc.host_batch_peso(host, b.descs)
         dt = (time.perf_counter() - t0) / reps
         same = bool((out == r["out"].cpu().numpy()).all())
+        # the host link itself: one plain pinned -> device copy of the same bytes
+        src = torch.from_numpy(host)
+        dst = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        link = nbytes / ((time.perf_counter() - t0) / reps) / GIB
+        del dst
         return {"gib_s": round(b.total_bytes / dt / GIB, 2), "ms_per_batch": round(dt * 1e3, 3),
                 "path": "pinned host -> hipMemcpyAsync H2D (32 MiB chunks, 3 streams) -> kernel -> D2H",
+                "h2d_copy_gib_s": round(link, 2),
                 "matches_device_resident": same}
     finally:
         L.tcsum_host_free(p)

@@ -289,16 +289,24 @@ def legacy_latency(tc):
     buf = tc.PktBuf([seg[i: i + 127] for i in range(0, 1500, 127)])
     d, s_ = tc.IpAddr.v4([192, 168, 74, 3]), tc.IpAddr.v4([192, 168, 74, 2])
     res = {}
-    for name, fn in (("checksum16_20B_us", lambda: tc.checksum16(0, hdr, 20, 0, 1)),
-                     ("checksum_peso_1500B_us", lambda: tc.checksum_peso(buf, d, s_, 6))):
-        for _ in range(20):
-            fn()
-        t0 = time.perf_counter()
-        reps = 2000
-        for _ in range(reps):
-            fn()
-        res[name] = round((time.perf_counter() - t0) / reps * 1e6, 2)
-    res["note"] = "one launch + one sync per call: use the batch API for throughput"
+    for served in (False, True):  # one launch + sync per call / the call server's resident wave
+        if served:
+            tc.call_server(True)
+        try:
+            for name, fn in (("checksum16_20B_us", lambda: tc.checksum16(0, hdr, 20, 0, 1)),
+                             ("checksum_peso_1500B_us", lambda: tc.checksum_peso(buf, d, s_, 6))):
+                for _ in range(20):
+                    fn()
+                t0 = time.perf_counter()
+                reps = 2000
+                for _ in range(reps):
+                    fn()
+                res[("served_" if served else "") + name] = round((time.perf_counter() - t0) / reps * 1e6, 2)
+        finally:
+            if served:
+                tc.call_server(False)
+    res["note"] = ("plain: one launch + one sync per call; served_: tcsum_call_server (one resident wave "
+                   "polling pinned memory). Use the batch API for throughput")
     return res
 
 

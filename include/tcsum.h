@@ -178,6 +178,19 @@ int tcsum_host_batch_ipv4_rx_verify(int device, const void *host_arena, uint64_t
  * wait).  Returns TCSUM_OK, TCSUM_ERR_NOT_SUPPORT without a gfx950 device. */
 int tcsum_queue_server(int device, int enable);
 
+/* Call server for the three synchronous drop-in symbols (checksum16,
+ * pktbuf_checksum16, checksum_peso; tcsum_legacy.h): with enable != 0 their
+ * calls on `device` (the legacy device, tcsum_plat_init / $TCSUM_DEVICE) are
+ * served by one resident wave that polls a pinned job box, instead of one
+ * kernel launch and one stream sync per call (same results, same side
+ * effects).  Ranges over 64 KiB still take the launch path.  The wave leaves
+ * by itself after $TCSUM_SERVER_IDLE_MS (default 10) without a call and the
+ * next call relaunches it; while it is up, a device-wide synchronisation
+ * waits for it to leave.  $TCSUM_CALL_SERVER=1 turns it on at the first
+ * legacy call without a code change.  enable == 0 stops it (bounded wait).
+ * Returns TCSUM_OK, TCSUM_ERR_NOT_SUPPORT without a gfx950 device. */
+int tcsum_call_server(int device, int enable);
+
 /* ------------------------------------------------------------ platform */
 
 /* HIP device init for the stack's net_plat_init hook (plat/net_plat.c:7):

@@ -35,6 +35,7 @@ SIGNATURES = {
     "tcsum_host_batch_ipv4_tx_fill": (_I, [_I, _V, _U64, _V, _U32, _V, _V]),
     "tcsum_host_batch_ipv4_rx_verify": (_I, [_I, _V, _U64, _V, _U32, _V, _V, _V]),
     "tcsum_queue_server": (_I, [_I, _I]),
+    "tcsum_call_server": (_I, [_I, _I]),
     "tcsum_plat_init": (_I, [_I]),
     "tcsum_host_alloc": (_V, [_SZ]),
     "tcsum_host_free": (None, [_V]),

@@ -100,7 +100,21 @@ struct Ctx {
     tcsum::SrvCtl *srv_d = nullptr;
     uint32_t srv_seq = 0; // last job posted (0 = none)
     uint64_t *srv_trace = nullptr; // TCSUM_SERVER_TRACE stamps (host address)
+    // call server (tcsum_call_server): one resident wave serving the three
+    // synchronous drop-in symbols, instead of a launch + sync per call
+    bool cs_on = false;      // enabled for this device
+    bool cs_running = false; // the wave was launched and not yet seen to finish
+    hipStream_t cs_stream = nullptr;
+    tcsum::CallBox *cs_h = nullptr;  // pinned, coherent: host address
+    tcsum::CallBox *cs_hd = nullptr; // ... and the device's address of it
+    uint8_t *cs_stage = nullptr;     // pinned staging for the call's bytes
+    uint8_t *cs_stage_d = nullptr;
+    uint32_t cs_seq = 0; // last job posted (0 = none)
 };
+
+// Bytes one served call may carry (checksum16's len is a u16; longer pktbuf
+// ranges take the launch path).
+constexpr size_t kCallStageMax = 1u << 16;
 
 Ctx g_ctx[kMaxDev];
 std::mutex g_default_mu;
@@ -173,6 +187,9 @@ Ctx &legacy_ctx()
         if (rc != TCSUM_OK)
             die(rc == TCSUM_ERR_NOT_SUPPORT ? "finding a gfx950 device" : "device init",
                 rc == TCSUM_ERR_NOT_SUPPORT ? hipErrorNoDevice : hipErrorOutOfMemory);
+        const char *cs = getenv("TCSUM_CALL_SERVER"); // drop-in users: no code change needed
+        if (cs && atoi(cs) != 0)
+            c.cs_on = true;
     }
     const hipError_t e = hipSetDevice(c.device); // HIP's current device is per thread
     if (e != hipSuccess)
@@ -747,13 +764,121 @@ int srv_submit(Ctx &c, int op, uint8_t *d_arena, const tcsum_pkt_t *d_pkts, uint
     }
 }
 
-// At unload: ask every live server grid to leave (bounded wait).
+// ---- call server (k_call, csum_kernels.hip) ----
+
+int cs_setup(Ctx &c)
+{
+    if (c.cs_h)
+        return TCSUM_OK;
+    if (!c.cs_stream && hipStreamCreateWithFlags(&c.cs_stream, hipStreamNonBlocking) != hipSuccess)
+        return TCSUM_ERR_SYS;
+    tcsum::CallBox *h = nullptr, *hd = nullptr;
+    uint8_t *st = nullptr, *std_ = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void **>(&h), sizeof(tcsum::CallBox), hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void **>(&hd), h, 0) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&st), kCallStageMax + 64, hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void **>(&std_), st, 0) != hipSuccess)
+        return TCSUM_ERR_MEM;
+    memset(h, 0, sizeof(tcsum::CallBox));
+    memset(st, 0, kCallStageMax + 64);
+    c.cs_stage = st;
+    c.cs_stage_d = std_;
+    c.cs_hd = hd;
+    c.cs_h = h;
+    return TCSUM_OK;
+}
+
+void cs_launch(Ctx &c, uint32_t last)
+{
+    const uint64_t idle_ticks = 100000ull * (uint64_t)std::max(1, env_int("TCSUM_SERVER_IDLE_MS", 10)); // 100 MHz
+    const hipError_t e = tcsum::launch_call_server(c.cs_hd, c.cs_stage_d, last, idle_ticks, c.cs_stream);
+    if (e != hipSuccess)
+        die("call server launch", e);
+    c.cs_running = true;
+}
+
+// Post one job (its bytes already in cs_stage) and spin until the wave has
+// answered; a wave that left (idle, or leaving while the job was posted) is
+// relaunched and serves the job (it takes any seq != last).
+uint32_t cs_post(Ctx &c, uint32_t ctl, uint32_t len, uint32_t pre, uint32_t src, uint32_t dst, uint32_t proto)
+{
+    tcsum::CallBox *h = c.cs_h;
+    const uint32_t prev = c.cs_seq;
+    const uint32_t seq = prev + 1u ? prev + 1u : 1u; // never 0
+    h->w0[1] = ctl;
+    h->w0[2] = len;
+    h->w0[3] = pre;
+    h->w1[0] = src;
+    h->w1[1] = dst;
+    h->w1[2] = proto;
+    __atomic_thread_fence(__ATOMIC_SEQ_CST); // the staged bytes and fields before the sequence words
+    __atomic_store_n(&h->w1[3], seq, __ATOMIC_RELEASE);
+    __atomic_store_n(&h->w0[0], seq, __ATOMIC_RELEASE);
+    c.cs_seq = seq;
+    if (!c.cs_running)
+        cs_launch(c, prev);
+    const auto t0 = std::chrono::steady_clock::now();
+    auto check = t0 + std::chrono::microseconds(100);
+    for (unsigned spins = 1;; ++spins) {
+        const uint64_t r = __atomic_load_n(&h->res, __ATOMIC_ACQUIRE);
+        if ((uint32_t)r == seq)
+            return (uint32_t)(r >> 32);
+        if ((spins & 1023u) == 0) {
+            const auto now = std::chrono::steady_clock::now();
+            if (now >= check) {
+                if (c.cs_running) {
+                    const hipError_t q = hipStreamQuery(c.cs_stream);
+                    if (q == hipSuccess)
+                        c.cs_running = false;
+                    else if (q != hipErrorNotReady)
+                        die("call server", q);
+                }
+                if (!c.cs_running && (uint32_t)__atomic_load_n(&h->res, __ATOMIC_ACQUIRE) != seq)
+                    cs_launch(c, prev);
+                if (now - t0 > std::chrono::seconds(10))
+                    die("call server (no answer in 10 s)", hipErrorLaunchTimeOut);
+                check = now + std::chrono::microseconds(100);
+            }
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+// Ask the wave to leave and wait (bounded) until its stream is idle.
+int cs_stop(Ctx &c)
+{
+    if (!c.cs_h || !c.cs_running)
+        return TCSUM_OK;
+    tcsum::CallBox *h = c.cs_h;
+    const uint32_t seq = c.cs_seq + 1u ? c.cs_seq + 1u : 1u;
+    h->w0[1] = tcsum::CALL_QUIT;
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    __atomic_store_n(&h->w1[3], seq, __ATOMIC_RELEASE);
+    __atomic_store_n(&h->w0[0], seq, __ATOMIC_RELEASE);
+    c.cs_seq = seq;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipStreamQuery(c.cs_stream);
+        if (q == hipSuccess)
+            break;
+        if (q != hipErrorNotReady || std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
+            return TCSUM_ERR_SYS;
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+    c.cs_running = false;
+    return TCSUM_OK;
+}
+
+// At unload: ask every live server grid / wave to leave (bounded wait).
 struct SrvReaper {
     ~SrvReaper()
     {
-        for (auto &c : g_ctx)
+        for (auto &c : g_ctx) {
             if (c.srv_running)
                 (void)srv_stop(c);
+            if (c.cs_running)
+                (void)cs_stop(c);
+        }
     }
 } g_srv_reaper;
 
@@ -931,6 +1056,27 @@ int tcsum_queue_server(int device, int enable)
     return srv_stop(c);
 }
 
+int tcsum_call_server(int device, int enable)
+{
+    if (device < 0 || device >= kMaxDev)
+        return TCSUM_ERR_PARAM;
+    Ctx &c = g_ctx[device];
+    std::lock_guard<std::mutex> lk(c.mu);
+    int rc = ctx_init(c, device);
+    if (rc != TCSUM_OK)
+        return rc;
+    if (hipSetDevice(device) != hipSuccess)
+        return TCSUM_ERR_SYS;
+    if (enable) {
+        rc = cs_setup(c);
+        if (rc == TCSUM_OK)
+            c.cs_on = true;
+        return rc;
+    }
+    c.cs_on = false;
+    return cs_stop(c);
+}
+
 // ================================================== drop-in legacy symbols
 
 // net/src/tools.c:24-54
@@ -938,10 +1084,17 @@ uint16_t checksum16(int offset, void *buf, uint16_t len, uint32_t pre_sum, int c
 {
     Ctx &c = legacy_ctx();
     std::lock_guard<std::mutex> lk(c.mu);
-    ensure_stage(c, len);
     // place the bytes so that address parity == logical parity: the kernel
     // then has the exact u32 word sum for the reference's u32 wrap
     const uint32_t par = (uint32_t)offset & 1u;
+    if (c.cs_on && cs_setup(c) == TCSUM_OK) {
+        if (len)
+            memcpy(c.cs_stage + par, buf, len);
+        return (uint16_t)cs_post(c, tcsum::MODE_EXACT | (complement ? tcsum::CALL_COMPLEMENT : 0u) |
+                                        (par ? tcsum::CALL_ODD : 0u),
+                                 len, pre_sum, 0u, 0u, 0u);
+    }
+    ensure_stage(c, len);
     uint8_t *dst = c.stage + par;
     if (len)
         memcpy(dst, buf, len);
@@ -966,6 +1119,11 @@ uint16_t pktbuf_checksum16(tcsum_pktbuf_t *buf, int len, int pre_sum, int comple
         len = 0; // loop not entered: the kernel returns (uint16_t)pre_sum, complemented or not
     Ctx &c = legacy_ctx();
     std::lock_guard<std::mutex> lk(c.mu);
+    if (c.cs_on && (size_t)len <= kCallStageMax && cs_setup(c) == TCSUM_OK) {
+        gather(buf, len, c.cs_stage);
+        return (uint16_t)cs_post(c, tcsum::MODE_SEG | (complement ? tcsum::CALL_COMPLEMENT : 0u), (uint32_t)len,
+                                 (uint32_t)pre_sum, 0u, 0u, 0u);
+    }
     ensure_stage(c, (size_t)len);
     gather(buf, len, c.stage);
     tcsum_seg_t *d = static_cast<tcsum_seg_t *>(c.desc);
@@ -987,6 +1145,14 @@ uint16_t checksum_peso(tcsum_pktbuf_t *buf, const tcsum_ipaddr_t *dest, const tc
     const int total = buf->total_size;
     Ctx &c = legacy_ctx();
     std::lock_guard<std::mutex> lk(c.mu);
+    if (c.cs_on && (total <= 0 || (size_t)total <= kCallStageMax) && cs_setup(c) == TCSUM_OK) {
+        if (total > 0)
+            gather(buf, total, c.cs_stage); // leaves the cursor at the end, like tools.c:73
+        uint32_t s32, d32;
+        memcpy(&s32, src->addr, 4);
+        memcpy(&d32, dest->addr, 4);
+        return (uint16_t)cs_post(c, tcsum::MODE_PESO, total > 0 ? (uint32_t)total : 0u, 0u, s32, d32, protocol);
+    }
     ensure_stage(c, total > 0 ? (size_t)total : 0);
     if (total > 0)
         gather(buf, total, c.stage); // leaves the cursor at the end, like tools.c:73

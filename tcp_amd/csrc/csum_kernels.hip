@@ -863,6 +863,84 @@ __global__ __launch_bounds__(256) void k_server(SrvHost *__restrict__ h, SrvCtl 
     }
 }
 
+// ---------------------------------------------------------------- call server
+//
+// One resident wave serving the synchronous drop-in calls (csum_api.cpp,
+// tcsum_call_server): instead of a kernel launch plus a stream sync per call
+// (~17 us), the host copies the call's bytes into pinned staging, writes the
+// job into a pinned CallBox and spins on the result word; the wave polls the
+// box (both 16-byte job words in one PCIe round trip, s_sleep between polls),
+// sums the range with all 64 lanes exactly like k_segments, and stores
+// result << 32 | seq with one system-scope release.  A job is taken only when
+// both job words carry its sequence number: the host stores them last, w1
+// before w0, so a read that sees the new number in both saw every field.
+// Exit: a QUIT job, or no job for idle_ticks of the 100 MHz clock -- every
+// path leaves the loop, so the wave always finishes.
+
+// The box's two 16-byte job words, system-scope loads both in flight (one
+// PCIe round trip)
+__device__ __forceinline__ void load_job(const CallBox *p, u32x4 &a, u32x4 &b)
+{
+    asm volatile("global_load_dwordx4 %0, %2, off sc0 sc1\n\t"
+                 "global_load_dwordx4 %1, %2, off offset:16 sc0 sc1\n\t"
+                 "s_waitcnt vmcnt(0)"
+                 : "=&v"(a), "=&v"(b)
+                 : "v"(p)
+                 : "memory");
+}
+
+__global__ __launch_bounds__(64) void k_call(CallBox *__restrict__ box, const uint8_t *__restrict__ stage,
+                                             uint32_t last, uint64_t idle_ticks)
+{
+    constexpr int G = 64, U = 16; // 16 KiB per pass: a 1500-B call is one PCIe round trip
+    const uint32_t gl = threadIdx.x;
+    uint64_t t_last = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        u32x4 a, b;
+        for (;;) {
+            load_job(box, a, b);
+            const uint32_t sa = __builtin_amdgcn_readfirstlane(a.x), sb = __builtin_amdgcn_readfirstlane(b.w);
+            if (sa != last && sa != 0u && sa == sb)
+                break;
+            if (__builtin_amdgcn_s_memrealtime() - t_last > idle_ticks)
+                return;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // system: the staged bytes
+        last = __builtin_amdgcn_readfirstlane(a.x);
+        const uint32_t ctl = __builtin_amdgcn_readfirstlane(a.y);
+        if (ctl & CALL_QUIT)
+            return;
+        SegDesc d;
+        d.off = (ctl & CALL_ODD) ? 1u : 0u;
+        d.len = __builtin_amdgcn_readfirstlane(a.z);
+        d.pre = __builtin_amdgcn_readfirstlane(a.w);
+        d.src = __builtin_amdgcn_readfirstlane(b.x);
+        d.dst = __builtin_amdgcn_readfirstlane(b.y);
+        d.proto = __builtin_amdgcn_readfirstlane(b.z) & 0xFFu;
+        const uint32_t mode = ctl & CALL_MODE_MASK;
+        uint32_t acc;
+        if (mode == MODE_EXACT)
+            acc = sum_range<G, U, true>(stage, d.off, d.len, gl, [] {});
+        else
+            acc = sum_range<G, U, false>(stage, d.off, d.len, gl, [] {});
+        acc = group_sum<G>(acc);
+        if (gl == 0) {
+            const uintptr_t start = reinterpret_cast<uintptr_t>(stage + d.off);
+            const uint32_t comp = (ctl & CALL_COMPLEMENT) ? 1u : 0u;
+            uint16_t r;
+            if (mode == MODE_EXACT)
+                r = finalize<MODE_EXACT>(acc, start, d, comp | ((uint32_t)d.off << 1));
+            else if (mode == MODE_PESO)
+                r = finalize<MODE_PESO>(acc, start, d, 0u);
+            else
+                r = finalize<MODE_SEG>(acc, start, d, comp);
+            __hip_atomic_store(&box->res, ((uint64_t)r << 32) | last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        t_last = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
 // ---------------------------------------------------------------- synthetic
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
@@ -1175,6 +1253,13 @@ hipError_t launch_server(SrvHost *h, SrvCtl *d, uint32_t last, uint64_t idle_tic
     // PCIe round trip for its bytes (the server's frames live in host memory)
     hipLaunchKernelGGL((k_server<64, 16>), dim3((uint32_t)(wgs > 0 ? wgs : 1)), dim3(256), 0, stream, h, d, last,
                        idle_ticks);
+    return hipGetLastError();
+}
+
+hipError_t launch_call_server(CallBox *box, const uint8_t *stage, uint32_t last, uint64_t idle_ticks,
+                              hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_call, dim3(1), dim3(64), 0, stream, box, stage, last, idle_ticks);
     return hipGetLastError();
 }
 

@@ -58,6 +58,28 @@ static_assert(sizeof(SrvCtl) % 16 == 0, "SrvCtl is memset whole");
 hipError_t launch_server(SrvHost *h /*device-visible address*/, SrvCtl *d, uint32_t last, uint64_t idle_ticks,
                          int wgs, hipStream_t stream);
 
+// Call server (k_call): one resident wave serving the synchronous drop-in
+// calls (checksum16 / pktbuf_checksum16 / checksum_peso) posted through
+// pinned, coherent host memory.  The wave reads the two 16-byte job words in
+// one poll and takes the job only when both carry the new sequence number
+// (the host stores every field, then w1[3], then w0[0]).
+enum CallCtl : uint32_t {
+    CALL_MODE_MASK = 3u,    // a Mode
+    CALL_COMPLEMENT = 4u,   // MODE_SEG / MODE_EXACT: complement the result
+    CALL_ODD = 8u,          // MODE_EXACT: the bytes start at stage + 1 (offset parity)
+    CALL_QUIT = 1u << 31,   // leave
+};
+struct CallBox {
+    uint32_t w0[4]; // seq, ctl, len, pre_sum
+    uint32_t w1[4]; // src, dst (as in memory), protocol, seq
+    uint32_t pad[8];
+    alignas(64) uint64_t res; // device: result << 32 | seq of the finished job
+};
+static_assert(sizeof(CallBox) == 128, "CallBox: job line + result line");
+
+hipError_t launch_call_server(CallBox *box /*device-visible address*/, const uint8_t *stage /*device-visible*/,
+                              uint32_t last, uint64_t idle_ticks, hipStream_t stream);
+
 hipError_t launch_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, uint64_t seed,
                              hipStream_t stream);
 

@@ -256,3 +256,8 @@ def plat_init(device: int = 0) -> None:
 def queue_server(enable: bool, device: int = 0) -> None:
     """Serve small host-queue batches from a resident grid (tcsum_queue_server)."""
     _lib.check(_lib.lib().tcsum_queue_server(device, 1 if enable else 0), "tcsum_queue_server")
+
+
+def call_server(enable: bool, device: int = 0) -> None:
+    """Serve the synchronous drop-in calls from one resident wave (tcsum_call_server)."""
+    _lib.check(_lib.lib().tcsum_call_server(device, 1 if enable else 0), "tcsum_call_server")

@@ -679,8 +679,11 @@ void srv_print_trace(const Ctx &c)
             fprintf(stderr, "tcsum server trace: %-28s %8.2f us (%d jobs)\n", names[k], sum[k] / cnt[k], cnt[k]);
 }
 
+void reap_at_exit();
+
 int srv_launch(Ctx &c, uint32_t last)
 {
+    reap_at_exit();
     const uint64_t idle_ticks = 100000ull * (uint64_t)std::max(1, env_int("TCSUM_SERVER_IDLE_MS", 10)); // 100 MHz
     if (tcsum::launch_server(c.srv_hd, c.srv_d, last, idle_ticks, std::max(1, env_int("TCSUM_SERVER_WGS", 64)),
                              c.srv_stream) != hipSuccess)
@@ -790,6 +793,7 @@ int cs_setup(Ctx &c)
 
 void cs_launch(Ctx &c, uint32_t last)
 {
+    reap_at_exit();
     const uint64_t idle_ticks = 100000ull * (uint64_t)std::max(1, env_int("TCSUM_SERVER_IDLE_MS", 10)); // 100 MHz
     const hipError_t e = tcsum::launch_call_server(c.cs_hd, c.cs_stage_d, last, idle_ticks, c.cs_stream);
     if (e != hipSuccess)
@@ -869,18 +873,25 @@ int cs_stop(Ctx &c)
     return TCSUM_OK;
 }
 
-// At unload: ask every live server grid / wave to leave (bounded wait).
-struct SrvReaper {
-    ~SrvReaper()
-    {
-        for (auto &c : g_ctx) {
-            if (c.srv_running)
-                (void)srv_stop(c);
-            if (c.cs_running)
-                (void)cs_stop(c);
-        }
+// At exit: ask every live server grid / wave to leave (bounded wait) while
+// the HIP runtime is still up -- registered with atexit at the first server
+// launch, i.e. after the runtime's own initialisation, so it runs before the
+// runtime's teardown; the static destructor below is the fallback for a
+// dlclose'd library.
+void reap_servers()
+{
+    for (auto &c : g_ctx) {
+        if (c.srv_running)
+            (void)srv_stop(c);
+        if (c.cs_running)
+            (void)cs_stop(c);
     }
+}
+struct SrvReaper {
+    ~SrvReaper() { reap_servers(); }
 } g_srv_reaper;
+std::once_flag g_reap_once;
+void reap_at_exit() { std::call_once(g_reap_once, [] { atexit(reap_servers); }); }
 
 // IPv4 batch over packets in host memory (the stack's netif queues): pinned
 // arenas are read -- and for tx written -- in place by the kernel over PCIe;

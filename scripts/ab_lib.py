@@ -19,8 +19,9 @@ from tcp_amd import _lib, workload  # noqa: E402
 def load(path):
     L = ctypes.CDLL(os.path.abspath(path))
     for name, (res, args) in _lib.SIGNATURES.items():
-        f = getattr(L, name)
-        f.restype, f.argtypes = res, args
+        f = getattr(L, name, None)  # an older build may lack newer symbols
+        if f is not None:
+            f.restype, f.argtypes = res, args
     return L
 
 

@@ -804,11 +804,23 @@ void cs_launch(Ctx &c, uint32_t last)
 // Post one job (its bytes already in cs_stage) and spin until the wave has
 // answered; a wave that left (idle, or leaving while the job was posted) is
 // relaunched and serves the job (it takes any seq != last).
-uint32_t cs_post(Ctx &c, uint32_t ctl, uint32_t len, uint32_t pre, uint32_t src, uint32_t dst, uint32_t proto)
+// `small`: the call's bytes (len + parity <= kCallInline) travel in the job
+// line itself instead of cs_stage -- one PCIe round trip less for the
+// 20-byte IPv4 header checks (ipv4.c:243, 656).
+uint32_t cs_post(Ctx &c, uint32_t ctl, uint32_t len, uint32_t pre, uint32_t src, uint32_t dst, uint32_t proto,
+                 const uint8_t *small = nullptr)
 {
     tcsum::CallBox *h = c.cs_h;
     const uint32_t prev = c.cs_seq;
     const uint32_t seq = prev + 1u ? prev + 1u : 1u; // never 0
+    if (small) {
+        uint8_t b[tcsum::kCallInline] = {};
+        if (len)
+            memcpy(b + ((ctl & tcsum::CALL_ODD) ? 1 : 0), small, len);
+        memcpy(h->w2, b, 12);
+        memcpy(h->w3, b + 12, 12);
+        ctl |= tcsum::CALL_INLINE;
+    }
     h->w0[1] = ctl;
     h->w0[2] = len;
     h->w0[3] = pre;
@@ -816,6 +828,8 @@ uint32_t cs_post(Ctx &c, uint32_t ctl, uint32_t len, uint32_t pre, uint32_t src,
     h->w1[1] = dst;
     h->w1[2] = proto;
     __atomic_thread_fence(__ATOMIC_SEQ_CST); // the staged bytes and fields before the sequence words
+    __atomic_store_n(&h->w3[3], seq, __ATOMIC_RELEASE);
+    __atomic_store_n(&h->w2[3], seq, __ATOMIC_RELEASE);
     __atomic_store_n(&h->w1[3], seq, __ATOMIC_RELEASE);
     __atomic_store_n(&h->w0[0], seq, __ATOMIC_RELEASE);
     c.cs_seq = seq;
@@ -857,6 +871,8 @@ int cs_stop(Ctx &c)
     const uint32_t seq = c.cs_seq + 1u ? c.cs_seq + 1u : 1u;
     h->w0[1] = tcsum::CALL_QUIT;
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    __atomic_store_n(&h->w3[3], seq, __ATOMIC_RELEASE);
+    __atomic_store_n(&h->w2[3], seq, __ATOMIC_RELEASE);
     __atomic_store_n(&h->w1[3], seq, __ATOMIC_RELEASE);
     __atomic_store_n(&h->w0[0], seq, __ATOMIC_RELEASE);
     c.cs_seq = seq;
@@ -1099,11 +1115,12 @@ uint16_t checksum16(int offset, void *buf, uint16_t len, uint32_t pre_sum, int c
     // then has the exact u32 word sum for the reference's u32 wrap
     const uint32_t par = (uint32_t)offset & 1u;
     if (c.cs_on && cs_setup(c) == TCSUM_OK) {
-        if (len)
-            memcpy(c.cs_stage + par, buf, len);
-        return (uint16_t)cs_post(c, tcsum::MODE_EXACT | (complement ? tcsum::CALL_COMPLEMENT : 0u) |
-                                        (par ? tcsum::CALL_ODD : 0u),
-                                 len, pre_sum, 0u, 0u, 0u);
+        const uint32_t ctl = tcsum::MODE_EXACT | (complement ? tcsum::CALL_COMPLEMENT : 0u) |
+                             (par ? tcsum::CALL_ODD : 0u);
+        if (len + par <= tcsum::kCallInline)
+            return (uint16_t)cs_post(c, ctl, len, pre_sum, 0u, 0u, 0u, static_cast<const uint8_t *>(buf));
+        memcpy(c.cs_stage + par, buf, len);
+        return (uint16_t)cs_post(c, ctl, len, pre_sum, 0u, 0u, 0u);
     }
     ensure_stage(c, len);
     uint8_t *dst = c.stage + par;
@@ -1131,9 +1148,14 @@ uint16_t pktbuf_checksum16(tcsum_pktbuf_t *buf, int len, int pre_sum, int comple
     Ctx &c = legacy_ctx();
     std::lock_guard<std::mutex> lk(c.mu);
     if (c.cs_on && (size_t)len <= kCallStageMax && cs_setup(c) == TCSUM_OK) {
+        const uint32_t ctl = tcsum::MODE_SEG | (complement ? tcsum::CALL_COMPLEMENT : 0u);
+        if ((uint32_t)len <= tcsum::kCallInline) {
+            uint8_t small[tcsum::kCallInline];
+            gather(buf, len, small);
+            return (uint16_t)cs_post(c, ctl, (uint32_t)len, (uint32_t)pre_sum, 0u, 0u, 0u, small);
+        }
         gather(buf, len, c.cs_stage);
-        return (uint16_t)cs_post(c, tcsum::MODE_SEG | (complement ? tcsum::CALL_COMPLEMENT : 0u), (uint32_t)len,
-                                 (uint32_t)pre_sum, 0u, 0u, 0u);
+        return (uint16_t)cs_post(c, ctl, (uint32_t)len, (uint32_t)pre_sum, 0u, 0u, 0u);
     }
     ensure_stage(c, (size_t)len);
     gather(buf, len, c.stage);

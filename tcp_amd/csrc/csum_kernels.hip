@@ -877,14 +877,16 @@ __global__ __launch_bounds__(256) void k_server(SrvHost *__restrict__ h, SrvCtl 
 // Exit: a QUIT job, or no job for idle_ticks of the 100 MHz clock -- every
 // path leaves the loop, so the wave always finishes.
 
-// The box's two 16-byte job words, system-scope loads both in flight (one
+// The box's four 16-byte job words, system-scope loads all in flight (one
 // PCIe round trip)
-__device__ __forceinline__ void load_job(const CallBox *p, u32x4 &a, u32x4 &b)
+__device__ __forceinline__ void load_job(const CallBox *p, u32x4 &a, u32x4 &b, u32x4 &c, u32x4 &e)
 {
-    asm volatile("global_load_dwordx4 %0, %2, off sc0 sc1\n\t"
-                 "global_load_dwordx4 %1, %2, off offset:16 sc0 sc1\n\t"
+    asm volatile("global_load_dwordx4 %0, %4, off sc0 sc1\n\t"
+                 "global_load_dwordx4 %1, %4, off offset:16 sc0 sc1\n\t"
+                 "global_load_dwordx4 %2, %4, off offset:32 sc0 sc1\n\t"
+                 "global_load_dwordx4 %3, %4, off offset:48 sc0 sc1\n\t"
                  "s_waitcnt vmcnt(0)"
-                 : "=&v"(a), "=&v"(b)
+                 : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(e)
                  : "v"(p)
                  : "memory");
 }
@@ -896,11 +898,12 @@ __global__ __launch_bounds__(64) void k_call(CallBox *__restrict__ box, const ui
     const uint32_t gl = threadIdx.x;
     uint64_t t_last = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-        u32x4 a, b;
+        u32x4 a, b, c, e;
         for (;;) {
-            load_job(box, a, b);
-            const uint32_t sa = __builtin_amdgcn_readfirstlane(a.x), sb = __builtin_amdgcn_readfirstlane(b.w);
-            if (sa != last && sa != 0u && sa == sb)
+            load_job(box, a, b, c, e);
+            const uint32_t sa = __builtin_amdgcn_readfirstlane(a.x), sb = __builtin_amdgcn_readfirstlane(b.w),
+                           sc = __builtin_amdgcn_readfirstlane(c.w), se = __builtin_amdgcn_readfirstlane(e.w);
+            if (sa != last && sa != 0u && sa == sb && sa == sc && sa == se)
                 break;
             if (__builtin_amdgcn_s_memrealtime() - t_last > idle_ticks)
                 return;
@@ -920,13 +923,27 @@ __global__ __launch_bounds__(64) void k_call(CallBox *__restrict__ box, const ui
         d.proto = __builtin_amdgcn_readfirstlane(b.z) & 0xFFu;
         const uint32_t mode = ctl & CALL_MODE_MASK;
         uint32_t acc;
-        if (mode == MODE_EXACT)
-            acc = sum_range<G, U, true>(stage, d.off, d.len, gl, [] {});
-        else
-            acc = sum_range<G, U, false>(stage, d.off, d.len, gl, [] {});
-        acc = group_sum<G>(acc);
+        uintptr_t start = reinterpret_cast<uintptr_t>(stage + d.off);
+        if (ctl & CALL_INLINE) {
+            // <= 24 bytes that came with the job: the host zeroed the rest of
+            // w2/w3 and put the bytes at offset (ctl & CALL_ODD), so the
+            // exact word sum of the six dwords is the range's (no PCIe trip)
+            acc = 0;
+            acc = dot_halves(acc, __builtin_amdgcn_readfirstlane(c.x), 0x00010001u);
+            acc = dot_halves(acc, __builtin_amdgcn_readfirstlane(c.y), 0x00010001u);
+            acc = dot_halves(acc, __builtin_amdgcn_readfirstlane(c.z), 0x00010001u);
+            acc = dot_halves(acc, __builtin_amdgcn_readfirstlane(e.x), 0x00010001u);
+            acc = dot_halves(acc, __builtin_amdgcn_readfirstlane(e.y), 0x00010001u);
+            acc = dot_halves(acc, __builtin_amdgcn_readfirstlane(e.z), 0x00010001u);
+            start = d.off; // the byte parity the sum was taken at
+        } else {
+            if (mode == MODE_EXACT)
+                acc = sum_range<G, U, true>(stage, d.off, d.len, gl, [] {});
+            else
+                acc = sum_range<G, U, false>(stage, d.off, d.len, gl, [] {});
+            acc = group_sum<G>(acc);
+        }
         if (gl == 0) {
-            const uintptr_t start = reinterpret_cast<uintptr_t>(stage + d.off);
             const uint32_t comp = (ctl & CALL_COMPLEMENT) ? 1u : 0u;
             uint16_t r;
             if (mode == MODE_EXACT)

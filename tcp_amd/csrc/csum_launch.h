@@ -60,19 +60,22 @@ hipError_t launch_server(SrvHost *h /*device-visible address*/, SrvCtl *d, uint3
 
 // Call server (k_call): one resident wave serving the synchronous drop-in
 // calls (checksum16 / pktbuf_checksum16 / checksum_peso) posted through
-// pinned, coherent host memory.  The wave reads the two 16-byte job words in
-// one poll and takes the job only when both carry the new sequence number
-// (the host stores every field, then w1[3], then w0[0]).
+// pinned, coherent host memory.  The wave reads the four 16-byte job words in
+// one poll and takes the job only when all carry the new sequence number
+// (the host stores every field, then w3[3], w2[3], w1[3] and w0[0] last).
 enum CallCtl : uint32_t {
     CALL_MODE_MASK = 3u,    // a Mode
     CALL_COMPLEMENT = 4u,   // MODE_SEG / MODE_EXACT: complement the result
     CALL_ODD = 8u,          // MODE_EXACT: the bytes start at stage + 1 (offset parity)
+    CALL_INLINE = 16u,      // the bytes are in w2/w3 (<= kCallInline with the parity byte), not in stage
     CALL_QUIT = 1u << 31,   // leave
 };
+constexpr uint32_t kCallInline = 24; // bytes carried in the job line itself
 struct CallBox {
     uint32_t w0[4]; // seq, ctl, len, pre_sum
     uint32_t w1[4]; // src, dst (as in memory), protocol, seq
-    uint32_t pad[8];
+    uint32_t w2[4]; // inline bytes 0..11, seq
+    uint32_t w3[4]; // inline bytes 12..23, seq
     alignas(64) uint64_t res; // device: result << 32 | seq of the finished job
 };
 static_assert(sizeof(CallBox) == 128, "CallBox: job line + result line");

@@ -264,7 +264,13 @@ __device__ __forceinline__ void frame_issue(Frame<U> &f, const uint8_t *__restri
     const u32x4 *ebase = nch ? base : &g_zero_chunk;
     f.ibase = f.ni ? base + 1 : &g_zero_chunk;
     f.ilast = f.ni ? f.ni - 1u : 0u;
-    f.ev = load16<true>(ebase + (nch ? f.eidx : 0u));
+    // the edge chunks with the DEFAULT policy, the interior nontemporal: a
+    // packed range shares its first and last 128-B line with its neighbours,
+    // and a line fetched by a default-policy load stays in L2 until the
+    // neighbour's wave (same XCD, xcd_block) reads it -- configs[1] fetched
+    // 1.2 % more than the algorithmic bytes with nt edges, 0.05 % without,
+    // and ran 5 % faster (profiles/r01/ab_edge_policy.txt)
+    f.ev = load16<false>(ebase + (nch ? f.eidx : 0u));
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t j = u * G + gl;

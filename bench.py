@@ -271,10 +271,21 @@ def e2e(torch, tc, r):
         torch.cuda.synchronize()
         link = nbytes / ((time.perf_counter() - t0) / reps) / GIB
         del dst
-        return {"gib_s": round(b.total_bytes / dt / GIB, 2), "ms_per_batch": round(dt * 1e3, 3),
-                "path": "pinned host -> hipMemcpyAsync H2D (32 MiB chunks, 3 streams) -> kernel -> D2H",
-                "h2d_copy_gib_s": round(link, 2),
-                "matches_device_resident": same}
+        res = {"gib_s": round(b.total_bytes / dt / GIB, 2), "ms_per_batch": round(dt * 1e3, 3),
+               "path": "pinned host -> hipMemcpyAsync H2D (32 MiB chunks, 3 streams) -> kernel -> D2H",
+               "h2d_copy_gib_s": round(link, 2),
+               "matches_device_resident": same}
+        ndev = torch.cuda.device_count()
+        if ndev > 1:  # the same host batch sharded over every GPU of the node
+            devs = list(range(ndev))
+            out = tc.host_batch_peso_multi(host, b.descs, devs)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                out = tc.host_batch_peso_multi(host, b.descs, devs)
+            dt = (time.perf_counter() - t0) / reps
+            res["multi_device"] = {"gpus": ndev, "gib_s": round(b.total_bytes / dt / GIB, 2),
+                                   "matches_device_resident": bool((out == r["out"].cpu().numpy()).all())}
+        return res
     finally:
         L.tcsum_host_free(p)
 

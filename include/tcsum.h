@@ -144,6 +144,14 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
                           const tcsum_peso_t *segs /*[host]*/, uint32_t n,
                           uint16_t *out /*[host]*/);
 
+/* tcsum_host_batch_peso over several GPUs of this node: the segments are cut
+ * into contiguous shards balanced by bytes, one per entry of devices[] (a
+ * device may repeat; its shards then run one after the other), each shard
+ * moved over its own GPU's host link and summed in its HBM by one host thread
+ * per device.  Results land in out[] in segment order.  No collective. */
+int tcsum_host_batch_peso_multi(const int *devices, int ndev, const void *host_arena, uint64_t arena_bytes,
+                                const tcsum_peso_t *segs /*[host]*/, uint32_t n, uint16_t *out /*[host]*/);
+
 /* Host-queue IPv4 batches: the frames of a netif
  * in_q / out_q (net/src/netif.c:339-349, exmsg.c:89-112) as they sit in host
  * memory.  Same semantics as the device-resident calls above; every pointer

@@ -449,9 +449,18 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         return TCSUM_OK;
     if (!host_arena || !segs || !out || device < 0 || device >= kMaxDev)
         return TCSUM_ERR_PARAM;
-    for (uint32_t i = 0; i < n; ++i)
+    uint64_t glo = UINT64_MAX, ghi = 0; // the span the segments touch
+    for (uint32_t i = 0; i < n; ++i) {
         if (segs[i].offset > arena_bytes || segs[i].len > arena_bytes - segs[i].offset)
             return TCSUM_ERR_PARAM;
+        if (segs[i].len) {
+            glo = segs[i].offset < glo ? segs[i].offset : glo;
+            ghi = segs[i].offset + segs[i].len > ghi ? segs[i].offset + segs[i].len : ghi;
+        }
+    }
+    if (ghi == 0)
+        glo = 0;
+    glo &= ~uint64_t(15);
     Ctx &c = g_ctx[device];
     std::lock_guard<std::mutex> lk(c.mu);
     int rc = ctx_init(c, device);
@@ -460,9 +469,11 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     if (hipSetDevice(device) != hipSuccess)
         return TCSUM_ERR_SYS;
 
-    // device buffers (grow-only; the arena keeps a 16-byte tail so the last
-    // aligned chunk is in bounds)
-    const size_t need_arena = ((arena_bytes + 15) & ~size_t(15)) + 16;
+    // device buffers (grow-only).  Only the span [glo, ghi) the segments touch
+    // lives in HBM (a shard of a multi-device batch holds its own part only),
+    // plus a 16-byte tail so the last aligned chunk is in bounds; `dbase` is
+    // the device address arena offset 0 would have.
+    const size_t need_arena = ((ghi - glo + 15) & ~size_t(15)) + 16;
     if (need_arena > c.d_arena_cap) {
         if (c.d_arena)
             (void)hipFree(c.d_arena);
@@ -512,6 +523,7 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
             return TCSUM_ERR_MEM;
         hout = reinterpret_cast<uint16_t *>(c.q_res.h);
     }
+    uint8_t *const dbase = c.d_arena - glo;
     int k = 0;
     for (uint32_t i0 = 0; i0 < n; i0 += per, ++k) {
         const uint32_t i1 = i0 + per < n ? i0 + per : n;
@@ -530,14 +542,14 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
             hi = (hi + 15) & ~uint64_t(15);
             if (hi > arena_bytes)
                 hi = arena_bytes;
-            if (hipMemcpyAsync(c.d_arena + lo, h + lo, hi - lo, hipMemcpyHostToDevice, s) != hipSuccess)
+            if (hipMemcpyAsync(dbase + lo, h + lo, hi - lo, hipMemcpyHostToDevice, s) != hipSuccess)
                 return TCSUM_ERR_SYS;
         }
         if (hipMemcpyAsync(c.d_descs + i0, hsegs + i0, sizeof(tcsum_peso_t) * (i1 - i0),
                            hipMemcpyHostToDevice, s) != hipSuccess)
             return TCSUM_ERR_SYS;
         const hipError_t e = tcsum::launch_segments(tcsum::MODE_PESO, tcsum::pick_geometry(mean_of(bytes, i1 - i0)),
-                                                    c.d_arena, c.d_descs + i0, i1 - i0, c.d_out + i0, 0u, s);
+                                                    dbase, c.d_descs + i0, i1 - i0, c.d_out + i0, 0u, s);
         if (e != hipSuccess)
             return TCSUM_ERR_SYS;
         if (hipMemcpyAsync(hout + i0, c.d_out + i0, sizeof(uint16_t) * (i1 - i0), hipMemcpyDeviceToHost, s) !=
@@ -549,6 +561,49 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
             return TCSUM_ERR_SYS;
     if (hout != out)
         memcpy(out, hout, sizeof(uint16_t) * n);
+    return TCSUM_OK;
+}
+
+// One host batch over several GPUs: contiguous shards balanced by bytes
+// (SURVEY §8(e)), one host thread per device, each shard through its own
+// device's host link and HBM; no collective.
+int tcsum_host_batch_peso_multi(const int *devices, int ndev, const void *host_arena, uint64_t arena_bytes,
+                                const tcsum_peso_t *segs, uint32_t n, uint16_t *out)
+{
+    if (n == 0)
+        return TCSUM_OK;
+    if (!devices || ndev <= 0 || ndev > kMaxDev || !host_arena || !segs || !out)
+        return TCSUM_ERR_PARAM;
+    for (int d = 0; d < ndev; ++d)
+        if (devices[d] < 0 || devices[d] >= kMaxDev)
+            return TCSUM_ERR_PARAM;
+    if (ndev == 1)
+        return tcsum_host_batch_peso(devices[0], host_arena, arena_bytes, segs, n, out);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        total += segs[i].len;
+    std::vector<uint32_t> cut((size_t)ndev + 1, n);
+    cut[0] = 0;
+    uint64_t acc = 0;
+    int k = 1;
+    for (uint32_t i = 0; i < n && k < ndev; ++i) {
+        acc += segs[i].len;
+        while (k < ndev && acc * (uint64_t)ndev >= total * (uint64_t)k) // shard k starts after byte quantile k
+            cut[k++] = i + 1;
+    }
+    std::vector<int> rc((size_t)ndev, TCSUM_OK);
+    std::vector<std::thread> th;
+    for (int d = 0; d < ndev; ++d)
+        if (cut[d + 1] > cut[d])
+            th.emplace_back([&, d] {
+                rc[d] = tcsum_host_batch_peso(devices[d], host_arena, arena_bytes, segs + cut[d], cut[d + 1] - cut[d],
+                                              out + cut[d]);
+            });
+    for (auto &t : th)
+        t.join();
+    for (int r : rc)
+        if (r != TCSUM_OK)
+            return r;
     return TCSUM_OK;
 }
 

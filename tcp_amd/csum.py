@@ -149,6 +149,18 @@ def host_batch_peso(host_arena: np.ndarray, segs: np.ndarray, device: int = 0) -
     return out
 
 
+def host_batch_peso_multi(host_arena: np.ndarray, segs: np.ndarray, devices) -> np.ndarray:
+    """tcsum_host_batch_peso_multi: one host batch sharded by bytes over `devices`."""
+    assert segs.dtype == PESO_DTYPE
+    devs = np.ascontiguousarray(np.asarray(list(devices), dtype=np.int32))
+    out = np.zeros(segs.size, np.uint16)
+    rc = _lib.lib().tcsum_host_batch_peso_multi(devs.ctypes.data, devs.size, host_arena.ctypes.data,
+                                                host_arena.nbytes, np.ascontiguousarray(segs).ctypes.data,
+                                                segs.size, out.ctypes.data)
+    _lib.check(rc, "tcsum_host_batch_peso_multi")
+    return out
+
+
 class HostArena:
     """Pinned host memory from tcsum_host_alloc (the plat/ pinned pool), viewed
     as a numpy u8 array; the kernels read and write it in place."""

@@ -521,6 +521,30 @@ def test_host_batch_pinned(tc, oracle, shift):
         L.tcsum_host_free(p)
 
 
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0, 0]])
+def test_host_batch_multi_device(tc, oracle, devices):
+    """tcsum_host_batch_peso_multi: byte-balanced shards over a device list
+    (one GPU here, listed repeatedly: every shard boundary and the span-only
+    device arena are exercised), ragged segments in any order, results in
+    segment order; also fewer segments than devices."""
+    rng = np.random.default_rng(31)
+    host = rng.integers(0, 256, 12 << 20, dtype=np.uint8)
+    n = 30000
+    p = np.zeros(n, tc.PESO_DTYPE)
+    p["len"] = rng.integers(0, 9000, n)
+    p["offset"] = rng.integers(0, host.size - 9000, n)
+    p["src"] = rng.integers(0, 256, (n, 4))
+    p["dst"] = rng.integers(0, 256, (n, 4))
+    p["protocol"] = rng.choice([6, 17], n)
+    out = tc.host_batch_peso_multi(host, p, devices)
+    np.testing.assert_array_equal(out, oracle.batch_peso(host, p, nthreads=8))
+    few = p[:2].copy()
+    few["offset"] = [host.size - 100, 5]  # the span is not in offset order
+    few["len"] = [100, 51]
+    np.testing.assert_array_equal(tc.host_batch_peso_multi(host, few, devices),
+                                  oracle.batch_peso(host, few, nthreads=1))
+
+
 # --------------------------------------------------- full BASELINE sizes
 
 def test_full_mtu_batch_exact(tc, torch, oracle):

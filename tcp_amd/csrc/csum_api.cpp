@@ -797,26 +797,33 @@ int srv_submit(Ctx &c, int op, uint8_t *d_arena, const tcsum_pkt_t *d_pkts, uint
     c.srv_seq = seq;
     if (!c.srv_running && (rc = srv_launch(c, prev)) != TCSUM_OK)
         return rc;
+    // spin on `done`; only every 100 us ask the runtime whether the grid left
+    // (a hipStreamQuery in the spin loop itself delays noticing `done`)
     const auto t0 = std::chrono::steady_clock::now();
+    auto check = t0 + std::chrono::microseconds(100);
     for (unsigned spins = 1;; ++spins) {
         if (__atomic_load_n(&h->done, __ATOMIC_ACQUIRE) == seq)
             return TCSUM_OK;
-        if ((spins & 255u) == 0) {
-            if (c.srv_running) {
-                const hipError_t q = hipStreamQuery(c.srv_stream);
-                if (q == hipSuccess)
-                    c.srv_running = false;
-                else if (q != hipErrorNotReady)
+        if ((spins & 1023u) == 0) {
+            const auto now = std::chrono::steady_clock::now();
+            if (now >= check) {
+                if (c.srv_running) {
+                    const hipError_t q = hipStreamQuery(c.srv_stream);
+                    if (q == hipSuccess)
+                        c.srv_running = false;
+                    else if (q != hipErrorNotReady)
+                        return TCSUM_ERR_SYS;
+                }
+                if (!c.srv_running) {
+                    if (__atomic_load_n(&h->done, __ATOMIC_ACQUIRE) == seq)
+                        return TCSUM_OK;
+                    if ((rc = srv_launch(c, prev)) != TCSUM_OK)
+                        return rc;
+                }
+                if (now - t0 > std::chrono::seconds(10))
                     return TCSUM_ERR_SYS;
+                check = now + std::chrono::microseconds(100);
             }
-            if (!c.srv_running) {
-                if (__atomic_load_n(&h->done, __ATOMIC_ACQUIRE) == seq)
-                    return TCSUM_OK;
-                if ((rc = srv_launch(c, prev)) != TCSUM_OK)
-                    return rc;
-            }
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
-                return TCSUM_ERR_SYS;
         }
         __builtin_ia32_pause();
     }

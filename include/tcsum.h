@@ -212,6 +212,17 @@ int tcsum_plat_init(int device);
 void *tcsum_host_alloc(size_t bytes);
 void tcsum_host_free(void *p);
 
+/* Pin memory the stack already owns, in place (hipHostRegister, mapped): a
+ * frame ring the capture path fills (a libpcap / PACKET_MMAP ring, the tx
+ * arena of INTEGRATION.md §4a, or the reference's static block pool
+ * `block_buffer`, net/src/pktbuf.c:13) becomes DMA-able without moving it,
+ * and the host-queue batches then read -- and tx fill writes -- its frames in
+ * place instead of staging them.  Returns TCSUM_OK, TCSUM_ERR_PARAM, or
+ * TCSUM_ERR_SYS when the runtime refuses.  Unregister before the memory goes
+ * away. */
+int tcsum_host_register(void *p, size_t bytes);
+int tcsum_host_unregister(void *p);
+
 /* Number of usable gfx950 devices (0 when none); never aborts. */
 int tcsum_device_count(void);
 

@@ -40,6 +40,8 @@ SIGNATURES = {
     "tcsum_plat_init": (_I, [_I]),
     "tcsum_host_alloc": (_V, [_SZ]),
     "tcsum_host_free": (None, [_V]),
+    "tcsum_host_register": (_I, [_V, _SZ]),
+    "tcsum_host_unregister": (_I, [_V]),
     "tcsum_device_count": (_I, []),
     "tcsum_pick_geometry": (None, [_U64, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "tcsum_version": (ctypes.c_char_p, []),

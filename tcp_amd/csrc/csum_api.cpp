@@ -340,6 +340,28 @@ void tcsum_host_free(void *p)
         (void)hipHostFree(p);
 }
 
+int tcsum_host_register(void *p, size_t bytes)
+{
+    if (!p || bytes == 0)
+        return TCSUM_ERR_PARAM;
+    if (hipHostRegister(p, bytes, hipHostRegisterMapped) != hipSuccess) {
+        (void)hipGetLastError();
+        return TCSUM_ERR_SYS;
+    }
+    return TCSUM_OK;
+}
+
+int tcsum_host_unregister(void *p)
+{
+    if (!p)
+        return TCSUM_ERR_PARAM;
+    if (hipHostUnregister(p) != hipSuccess) {
+        (void)hipGetLastError();
+        return TCSUM_ERR_SYS;
+    }
+    return TCSUM_OK;
+}
+
 static uint64_t mean_of(uint64_t total, uint32_t n) { return total && n ? total / n : 1500; }
 
 int tcsum_batch_segments(const void *arena, const tcsum_seg_t *segs, uint32_t n, uint16_t *out,

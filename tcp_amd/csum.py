@@ -186,6 +186,15 @@ class HostArena:
             pass
 
 
+def host_register(arr: np.ndarray) -> None:
+    """Pin an existing u8 array in place (tcsum_host_register)."""
+    _lib.check(_lib.lib().tcsum_host_register(arr.ctypes.data, arr.nbytes), "tcsum_host_register")
+
+
+def host_unregister(arr: np.ndarray) -> None:
+    _lib.check(_lib.lib().tcsum_host_unregister(arr.ctypes.data), "tcsum_host_unregister")
+
+
 def _host_arena_args(host_arena):
     arr = host_arena.array if isinstance(host_arena, HostArena) else host_arena
     assert arr.dtype == np.uint8 and arr.flags["C_CONTIGUOUS"]

@@ -23,9 +23,32 @@ def tc():
     return tcp_amd
 
 
+class _Registered:
+    """Pageable memory pinned in place with tcsum_host_register (the way the
+    stack would pin its static block pool, pktbuf.c:13); unpinned on release."""
+
+    def __init__(self, tc, n):
+        self.tc = tc
+        self.raw = np.zeros(n + 8192, np.uint8)
+        a0 = (-self.raw.ctypes.data) % 4096
+        self.region = self.raw[a0: a0 + (n + 4095) // 4096 * 4096]
+        tc.host_register(self.region)
+
+    def __del__(self):
+        try:
+            self.tc.host_unregister(self.region)
+        except Exception:
+            pass
+
+
 def host_copy(tc, data: np.ndarray, where: str, shift: int = 0):
     """(arena argument, its numpy view) holding `data` at byte `shift`."""
     n = data.size + shift + 64
+    if where == "registered":
+        reg = _Registered(tc, n)
+        view = reg.region[shift:]
+        view[: data.size] = data
+        return view, view, reg
     if where == "pinned":
         ha = tc.HostArena(n)
         ha.array[:] = 0
@@ -37,7 +60,7 @@ def host_copy(tc, data: np.ndarray, where: str, shift: int = 0):
     return view, view, None
 
 
-WHERE = [("pinned", 0), ("pinned", 7), ("pageable", 0), ("pageable", 3)]
+WHERE = [("pinned", 0), ("pinned", 7), ("pageable", 0), ("pageable", 3), ("registered", 0), ("registered", 5)]
 
 
 @pytest.mark.parametrize("where,shift", WHERE)

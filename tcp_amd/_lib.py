@@ -66,6 +66,13 @@ def lib() -> ctypes.CDLL:
             raise RuntimeError(
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                 " (there is no CPU fallback)")
+        # PyTorch ships its own HIP runtime under the same SONAME
+        # (libamdhip64.so.7): load it first so this library binds to that one
+        # copy -- loaded the other way round, torch's own init fails
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)

@@ -99,6 +99,7 @@ struct Ctx {
     tcsum::SrvHost *srv_hd = nullptr; // ... and the device's address of it
     tcsum::SrvCtl *srv_d = nullptr;
     uint32_t srv_seq = 0; // last job posted (0 = none)
+    uint64_t *srv_trace = nullptr; // TCSUM_SERVER_TRACE stamps (host address)
     // call server (tcsum_call_server): one resident wave serving the three
     // synchronous drop-in symbols, instead of a launch + sync per call
     bool cs_on = false;      // enabled for this device
@@ -718,7 +719,41 @@ int srv_setup(Ctx &c)
         return TCSUM_ERR_MEM;
     }
     memset(c.srv_h, 0, sizeof(tcsum::SrvHost));
+    if (env_int("TCSUM_SERVER_TRACE", 0)) { // phase stamps, printed by srv_stop (measurement only)
+        uint64_t *t = nullptr, *td = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void **>(&t), 256 * 8 * sizeof(uint64_t), hipHostMallocCoherent) ==
+                hipSuccess &&
+            hipHostGetDevicePointer(reinterpret_cast<void **>(&td), t, 0) == hipSuccess) {
+            memset(t, 0, 256 * 8 * sizeof(uint64_t));
+            c.srv_trace = t;
+            c.srv_h->trace = reinterpret_cast<uint64_t>(td);
+        }
+    }
     return TCSUM_OK;
+}
+
+// Mean phase durations over the traced jobs (TCSUM_SERVER_TRACE=1), in us.
+void srv_print_trace(const Ctx &c)
+{
+    const uint64_t *t = c.srv_trace;
+    if (!t)
+        return;
+    static const char *names[6] = {"seen->bcast", "bcast->wg1 seen", "bcast->wg0 summed", "wg0 release fence",
+                                   "wg0 release->last arrival", "last arrival->done stored"};
+    const int from[6] = {0, 1, 1, 3, 4, 5}, to[6] = {1, 2, 3, 4, 5, 6};
+    double sum[6] = {0};
+    int cnt[6] = {0};
+    for (int j = 0; j < 256; ++j)
+        for (int k = 0; k < 6; ++k) {
+            const uint64_t a = t[j * 8 + from[k]], b = t[j * 8 + to[k]];
+            if (a && b && b >= a && b - a < 100000000ull) {
+                sum[k] += (double)(b - a) / 100.0;
+                ++cnt[k];
+            }
+        }
+    for (int k = 0; k < 6; ++k)
+        if (cnt[k])
+            fprintf(stderr, "tcsum server trace: %-28s %8.2f us (%d jobs)\n", names[k], sum[k] / cnt[k], cnt[k]);
 }
 
 void reap_at_exit();
@@ -727,7 +762,7 @@ int srv_launch(Ctx &c, uint32_t last)
 {
     reap_at_exit();
     const uint64_t idle_ticks = 100000ull * (uint64_t)std::max(1, env_int("TCSUM_SERVER_IDLE_MS", 10)); // 100 MHz
-    if (tcsum::launch_server(c.srv_hd, c.srv_d, last, idle_ticks, std::max(1, env_int("TCSUM_SERVER_WGS", 16)),
+    if (tcsum::launch_server(c.srv_hd, c.srv_d, last, idle_ticks, std::max(1, env_int("TCSUM_SERVER_WGS", 64)),
                              c.srv_stream) != hipSuccess)
         return TCSUM_ERR_SYS;
     c.srv_running = true;
@@ -739,7 +774,7 @@ int srv_stop(Ctx &c)
 {
     if (!c.srv_h)
         return TCSUM_OK;
-    __atomic_store_n(&c.srv_h->w[0][2], 1u, __ATOMIC_SEQ_CST); // the quit word every poll reads
+    __atomic_store_n(&c.srv_h->quit, 1u, __ATOMIC_SEQ_CST);
     int rc = TCSUM_OK;
     if (c.srv_running) {
         const auto t0 = std::chrono::steady_clock::now();
@@ -757,7 +792,8 @@ int srv_stop(Ctx &c)
             c.srv_running = false;
     }
     if (rc == TCSUM_OK)
-        __atomic_store_n(&c.srv_h->w[0][2], 0u, __ATOMIC_SEQ_CST);
+        __atomic_store_n(&c.srv_h->quit, 0u, __ATOMIC_SEQ_CST);
+    srv_print_trace(c);
     return rc;
 }
 
@@ -772,27 +808,14 @@ int srv_submit(Ctx &c, int op, uint8_t *d_arena, const tcsum_pkt_t *d_pkts, uint
     tcsum::SrvHost *h = c.srv_h;
     const uint32_t prev = c.srv_seq;
     const uint32_t seq = prev + 1u ? prev + 1u : 1u; // never 0
-    const uint64_t p[5] = {reinterpret_cast<uint64_t>(d_arena), reinterpret_cast<uint64_t>(d_pkts),
-                           reinterpret_cast<uint64_t>(d_out), reinterpret_cast<uint64_t>(d_flags),
-                           reinterpret_cast<uint64_t>(d_verdict)};
-    h->w[0][0] = (uint32_t)op;
-    h->w[0][1] = n;
-    h->w[1][0] = (uint32_t)p[0];
-    h->w[1][1] = (uint32_t)(p[0] >> 32);
-    h->w[1][2] = (uint32_t)p[1];
-    h->w[2][0] = (uint32_t)(p[1] >> 32);
-    h->w[2][1] = (uint32_t)p[2];
-    h->w[2][2] = (uint32_t)(p[2] >> 32);
-    h->w[3][0] = (uint32_t)p[3];
-    h->w[3][1] = (uint32_t)(p[3] >> 32);
-    h->w[3][2] = (uint32_t)p[4];
-    h->w[4][0] = (uint32_t)(p[4] >> 32);
-    // every field (and the staged frames / descriptors) before the sequence
-    // words; w[0][3] last, so a poll that sees it in all five saw a whole job
-    __atomic_thread_fence(__ATOMIC_SEQ_CST);
-    for (int k = 4; k >= 1; --k)
-        __atomic_store_n(&h->w[k][3], seq, __ATOMIC_RELEASE);
-    __atomic_store_n(&h->w[0][3], seq, __ATOMIC_RELEASE);
+    h->op = (uint32_t)op;
+    h->n = n;
+    h->ptr[0] = reinterpret_cast<uint64_t>(d_arena);
+    h->ptr[1] = reinterpret_cast<uint64_t>(d_pkts);
+    h->ptr[2] = reinterpret_cast<uint64_t>(d_out);
+    h->ptr[3] = reinterpret_cast<uint64_t>(d_flags);
+    h->ptr[4] = reinterpret_cast<uint64_t>(d_verdict);
+    __atomic_store_n(&h->req, seq, __ATOMIC_SEQ_CST); // after the job fields
     c.srv_seq = seq;
     if (!c.srv_running && (rc = srv_launch(c, prev)) != TCSUM_OK)
         return rc;

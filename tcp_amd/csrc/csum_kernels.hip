@@ -740,93 +740,102 @@ __global__ __launch_bounds__(256) TCSUM_OCC(U) void k_ipv4(uint8_t *__restrict__
 //
 // A resident grid that serves small host-queue batches without a launch and
 // a stream sync per batch (tcsum_queue_server, include/tcsum.h).  The host
-// posts one job at a time into pinned, coherent memory (SrvHost: five 16-byte
-// job words, each ending in the job's sequence number, the first stored
-// last).  Wave 0 of EVERY workgroup polls the box itself -- all five words in
-// one PCIe round trip, s_sleep between polls -- and takes the job only when
-// all five carry the same new number, so there is no relay through device
-// memory.  The workgroup shares the job through LDS, takes ONE system-scope
-// acquire (its L1/L2 may hold host lines from the last job), sums its share
-// of the packets, drains its stores, releases them at system scope (results
-// and tx bytes live in host memory) and adds to SrvCtl::arrivals; the last
-// arriver stores SrvHost::done.  Exit: the host's quit word (w0.z) seen in a
-// poll; or workgroup 0 alone decides after idle_ticks of the 100 MHz clock
-// without a job and publishes SrvCtl::quit; every other workgroup also gives
-// up after 8x that -- every wave reaches an exit.  A job posted while the
-// grid is leaving is never lost: the host sees the stream idle with done !=
-// seq and relaunches (SrvCtl zeroed, csum_api.cpp); workgroups that took it
-// before leaving wrote the same bytes a relaunched grid writes again.
-
-// The box's five 16-byte job words, system-scope loads all in flight
-__device__ __forceinline__ void load_srv_job(const SrvHost *h, u32x4 (&w)[5])
-{
-    asm volatile("global_load_dwordx4 %0, %5, off sc0 sc1\n\t"
-                 "global_load_dwordx4 %1, %5, off offset:16 sc0 sc1\n\t"
-                 "global_load_dwordx4 %2, %5, off offset:32 sc0 sc1\n\t"
-                 "global_load_dwordx4 %3, %5, off offset:48 sc0 sc1\n\t"
-                 "global_load_dwordx4 %4, %5, off offset:64 sc0 sc1\n\t"
-                 "s_waitcnt vmcnt(0)"
-                 : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4])
-                 : "v"(h)
-                 : "memory");
-}
-
+// posts one job at a time into pinned, coherent memory (SrvHost: job fields,
+// then `req`); workgroup 0 polls `req` over PCIe with one lane and s_sleep,
+// copies the job into device memory (SrvCtl, agent-scope atomics) and bumps
+// SrvCtl::seq; the other workgroups poll that word (relaxed, s_sleep), take
+// ONE system-scope acquire (their L1/L2 may hold host lines from the last
+// job), and every workgroup sums its share of the packets.  Each workgroup
+// drains its stores, releases them at system scope (results and tx bytes live
+// in host memory) and adds to SrvCtl::arrivals; the last arriver writes
+// SrvHost::done.  Exit: workgroup 0 alone decides -- host `quit`, or no job
+// for `idle_ticks` of the 100 MHz real-time clock -- and publishes
+// SrvCtl::quit; every other workgroup also gives up after 8x that without a
+// word, so every wave reaches an exit.  A job posted while the grid is
+// leaving is never lost: the host sees the stream idle with done != req and
+// relaunches (csum_api.cpp).
 template <int G, int U>
 __global__ __launch_bounds__(256) void k_server(SrvHost *__restrict__ h, SrvCtl *__restrict__ d, uint32_t last,
                                                 uint64_t idle_ticks)
 {
-    __shared__ uint32_t s_go, s_op, s_n;
-    __shared__ uint64_t s_ptr[5];
+    __shared__ uint32_t s_go;
+    const bool lead = threadIdx.x == 0;
     uint32_t jobs = 0;
     uint64_t t_last = __builtin_amdgcn_s_memrealtime();
+    // phase stamps (100 MHz) of job j in tr[(j % 256) * 8 + k], measurement only
+    uint64_t *tr = reinterpret_cast<uint64_t *>(__hip_atomic_load(&h->trace, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    auto stamp = [&](int k) {
+        if (tr)
+            __hip_atomic_store(tr + (jobs % 256u) * 8u + k, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    };
     for (;;) {
-        if (threadIdx.x < 64) { // wave 0 polls
+        if (lead) {
             uint32_t go = 0;
-            u32x4 w[5];
-            for (;;) {
-                load_srv_job(h, w);
-                const uint32_t sq = __builtin_amdgcn_readfirstlane(w[0].w);
-                if (sq != last && sq != 0u && sq == __builtin_amdgcn_readfirstlane(w[1].w) &&
-                    sq == __builtin_amdgcn_readfirstlane(w[2].w) && sq == __builtin_amdgcn_readfirstlane(w[3].w) &&
-                    sq == __builtin_amdgcn_readfirstlane(w[4].w)) {
-                    go = sq;
-                    break;
+            if (blockIdx.x == 0) {
+                for (;;) {
+                    const uint32_t r = __hip_atomic_load(&h->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (r != last) {
+                        stamp(0);
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // system: the host's job and data
+                        // all job words in flight together: one PCIe round trip, not seven
+                        const uint32_t jop = __hip_atomic_load(&h->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        const uint32_t jn = __hip_atomic_load(&h->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        uint64_t jp[5];
+#pragma unroll
+                        for (int k = 0; k < 5; ++k)
+                            jp[k] = __hip_atomic_load(&h->ptr[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __hip_atomic_store(&d->op, jop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&d->n, jn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                        for (int k = 0; k < 5; ++k)
+                            __hip_atomic_store(&d->ptr[k], jp[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        __hip_atomic_store(&d->seq, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        stamp(1);
+                        go = r;
+                        break;
+                    }
+                    if (__hip_atomic_load(&h->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                        __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) {
+                        __hip_atomic_store(&d->quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(4);
                 }
-                if (__builtin_amdgcn_readfirstlane(w[0].z)) // the host's quit word
-                    break;
-                if (__hip_atomic_load(&d->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                    break;
-                const uint64_t idle = __builtin_amdgcn_s_memrealtime() - t_last;
-                if (blockIdx.x == 0 && idle > idle_ticks) {
-                    __hip_atomic_store(&d->quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
+            } else {
+                for (;;) {
+                    const uint32_t sq = __hip_atomic_load(&d->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (sq != 0u && sq != last) { // 0: zeroed at launch, nothing posted yet
+                        if (blockIdx.x == 1)
+                            stamp(2);
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // system: SrvCtl + the host's data
+                        go = sq;
+                        break;
+                    }
+                    if (__hip_atomic_load(&d->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+                        __builtin_amdgcn_s_memrealtime() - t_last > 8 * idle_ticks)
+                        break;
+                    __builtin_amdgcn_s_sleep(8);
                 }
-                if (idle > 8 * idle_ticks)
-                    break;
-                __builtin_amdgcn_s_sleep(2);
             }
-            if (threadIdx.x == 0) {
-                s_go = go;
-                s_op = w[0].x;
-                s_n = w[0].y;
-                s_ptr[0] = (uint64_t)w[1].x | ((uint64_t)w[1].y << 32); // arena
-                s_ptr[1] = (uint64_t)w[1].z | ((uint64_t)w[2].x << 32); // pkts
-                s_ptr[2] = (uint64_t)w[2].y | ((uint64_t)w[2].z << 32); // out
-                s_ptr[3] = (uint64_t)w[3].x | ((uint64_t)w[3].y << 32); // flags
-                s_ptr[4] = (uint64_t)w[3].z | ((uint64_t)w[4].x << 32); // verdict
-            }
+            s_go = go;
         }
         __syncthreads();
         const uint32_t go = s_go;
         if (!go)
             return;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // system: the host's frames and descriptors
-        const uint32_t op = s_op, n = s_n;
-        uint8_t *arena = reinterpret_cast<uint8_t *>(s_ptr[0]);
-        const tcsum_pkt_t *pkts = reinterpret_cast<const tcsum_pkt_t *>(s_ptr[1]);
-        uint32_t *out = reinterpret_cast<uint32_t *>(s_ptr[2]);
-        uint8_t *flags = reinterpret_cast<uint8_t *>(s_ptr[3]);
-        int8_t *verdict = reinterpret_cast<int8_t *>(s_ptr[4]);
+        const uint32_t op = __hip_atomic_load(&d->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t n = __hip_atomic_load(&d->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t q[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            q[k] = __hip_atomic_load(&d->ptr[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint8_t *arena = reinterpret_cast<uint8_t *>(q[0]);
+        const tcsum_pkt_t *pkts = reinterpret_cast<const tcsum_pkt_t *>(q[1]);
+        uint32_t *out = reinterpret_cast<uint32_t *>(q[2]);
+        uint8_t *flags = reinterpret_cast<uint8_t *>(q[3]);
+        int8_t *verdict = reinterpret_cast<int8_t *>(q[4]);
         constexpr uint32_t PER = 256u / G;
         const uint32_t stride = gridDim.x * PER;
         for (uint32_t first = blockIdx.x * PER; first < n; first += stride) { // workgroup-uniform
@@ -839,16 +848,22 @@ __global__ __launch_bounds__(256) void k_server(SrvHost *__restrict__ h, SrvCtl 
                 ipv4_packet<G, U, IP_SUMS>(arena, pkts, pk, n, out, flags, verdict, 0u);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // every storing wave drains
-        __syncthreads(); // also: every wave has read s_* before wave 0 polls again
-        if (threadIdx.x == 0) {
+        __syncthreads();
+        if (lead) {
+            if (blockIdx.x == 0)
+                stamp(3);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // system: this workgroup's results / tx bytes
+            if (blockIdx.x == 0)
+                stamp(4);
             const uint32_t old = __hip_atomic_fetch_add(&d->arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (old == (jobs + 1u) * gridDim.x - 1u) {
+                stamp(5);
                 __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
                 __hip_atomic_store(&h->done, go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                stamp(6);
             }
+            ++jobs;
         }
-        ++jobs;
         last = go;
         t_last = __builtin_amdgcn_s_memrealtime();
     }

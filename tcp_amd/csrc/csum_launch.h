@@ -35,22 +35,23 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
                        uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream);
 
 // Queue server (k_server): one job at a time.  SrvHost lives in pinned,
-// coherent host memory: five 16-byte job words, each ending in the job's
-// sequence number (the host stores every field, then w[4..1][3], w[0][3]
-// last), and the `done` word the grid stores; SrvCtl in device memory
-// (zeroed before every launch).
+// coherent host memory (the host writes the job, then `req`, and reads `done`);
+// SrvCtl in device memory (zeroed before every launch).
 struct SrvHost {
-    uint32_t w[5][4]; // w0 {op, n, quit, seq}  w1 {arena lo, arena hi, pkts lo, seq}
-                      // w2 {pkts hi, out lo, out hi, seq}  w3 {flags lo, flags hi, verdict lo, seq}
-                      // w4 {verdict hi, 0, 0, seq}   (device-visible addresses; 0 = none)
-    uint32_t pad[12];
+    uint32_t req;  // host: sequence number of the posted job (never 0)
+    uint32_t quit; // host: ask the grid to leave
+    uint32_t op;   // IP_SUMS / IP_TX / IP_RX
+    uint32_t n;    // packets
+    uint64_t ptr[5]; // device-visible: arena, pkts, out, flags, verdict (0 = none)
+    uint64_t trace;  // device-visible u64[256 * 8] of phase stamps, or 0 (TCSUM_SERVER_TRACE)
+    uint32_t pad[2];
     alignas(64) uint32_t done; // device: last completed job
 };
-static_assert(sizeof(SrvHost) == 192, "SrvHost: job lines + done line");
 struct SrvCtl {
-    uint32_t quit;     // workgroup 0 decided to leave (idle)
-    uint32_t arrivals; // workgroups done, cumulative over the launch
-    uint32_t pad[2];
+    uint32_t seq, quit, op, n;
+    uint64_t ptr[5];
+    uint32_t arrivals;
+    uint32_t pad;
 };
 static_assert(sizeof(SrvCtl) % 16 == 0, "SrvCtl is memset whole");
 

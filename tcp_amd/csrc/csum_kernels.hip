@@ -1029,7 +1029,7 @@ __global__ __launch_bounds__(256) void k_synth_ipv4(uint8_t *__restrict__ arena,
 // bytes with the same load shape (nontemporal dwordx4, one contiguous
 // 64*U-chunk tile per wave), XOR-folded so the loads stay live; a store only
 // happens if the fold hits a magic value.
-template <int U>
+template <int U, bool NT = true>
 __global__ __launch_bounds__(256) void k_probe_read(const u32x4 *__restrict__ p, uint64_t nchunks,
                                                     uint32_t *__restrict__ sink, uint32_t xg)
 {
@@ -1041,7 +1041,7 @@ __global__ __launch_bounds__(256) void k_probe_read(const u32x4 *__restrict__ p,
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t idx = base + u * 64ull + lane;
-        v[u] = idx < nchunks ? load16<true>(p + idx) : u32x4(0u);
+        v[u] = idx < nchunks ? load16<NT>(p + idx) : u32x4(0u);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -1064,6 +1064,14 @@ hipError_t launch_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, hip
     const uint64_t per_block = 4ull * 64 * (uint64_t)U;
     const dim3 grid((uint32_t)((nchunks + per_block - 1) / per_block));
     const u32x4 *q = static_cast<const u32x4 *>(p);
+    if (const char *s = getenv("TCSUM_PROBE_NT"); s && atoi(s) == 0) { // measurement: default-policy loads
+        switch (U) {
+        case 4: hipLaunchKernelGGL((k_probe_read<4, false>), grid, dim3(256), 0, stream, q, nchunks, sink, xg); break;
+        case 16: hipLaunchKernelGGL((k_probe_read<16, false>), grid, dim3(256), 0, stream, q, nchunks, sink, xg); break;
+        default: hipLaunchKernelGGL((k_probe_read<8, false>), grid, dim3(256), 0, stream, q, nchunks, sink, xg); break;
+        }
+        return hipGetLastError();
+    }
     switch (U) {
     case 1: hipLaunchKernelGGL(k_probe_read<1>, grid, dim3(256), 0, stream, q, nchunks, sink, xg); break;
     case 2: hipLaunchKernelGGL(k_probe_read<2>, grid, dim3(256), 0, stream, q, nchunks, sink, xg); break;

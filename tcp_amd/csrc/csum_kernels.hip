@@ -385,6 +385,30 @@ __global__ __launch_bounds__(256) TCSUM_OCC(U) void k_segments(const uint8_t *__
         out[seg] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + d.off), d, aux);
 }
 
+// One range per workgroup: all four waves on one range (G = 256), for ranges
+// of tens of KiB (TSO).  Each wave's share of a 64-KiB range is one pass of
+// U loads per lane -- the short-lived, one-pass shape of the fastest plain
+// read (profiles/r01/probe_variants.txt) -- and the waves' sums meet in LDS.
+template <int U, int MODE>
+__global__ __launch_bounds__(256) void k_segments_wg(const uint8_t *__restrict__ arena,
+                                                     const void *__restrict__ descs, uint32_t n,
+                                                     uint16_t *__restrict__ out, uint32_t aux, uint32_t xg)
+{
+    __shared__ uint32_t part[4];
+    const uint32_t gl = threadIdx.x;
+    const uint32_t seg = xcd_block(blockIdx.x, gridDim.x, xg); // grid == n: one range per workgroup
+    const bool live = seg < n;
+    const SegDesc d = load_desc<MODE>(descs, seg, live);
+    uint32_t acc = sum_range<256, U, MODE == MODE_EXACT>(arena, d.off, d.len, gl, [] {});
+    acc = group_sum<64>(acc); // < 2^23 (folded lanes) or exact
+    if ((gl & 63u) == 0)
+        part[gl >> 6] = acc;
+    __syncthreads();
+    if (gl == 0 && live)
+        out[seg] = finalize<MODE>(part[0] + part[1] + part[2] + part[3], reinterpret_cast<uintptr_t>(arena + d.off),
+                                  d, aux);
+}
+
 // Persistent form: a resident grid walks the batch; each wave prefetches its
 // next descriptor while the current packets' bytes are in flight, so the
 // descriptor -> data dependence costs one latency per wave, not per packet.
@@ -1182,6 +1206,17 @@ static hipError_t seg_u(int G, int U, int persist, uint32_t xg, uint32_t n, cons
     TCSUM_SEG_U(64)
 #undef TCSUM_SEG_U
 #undef TCSUM_SEG
+    if (G == 256) { // one range per workgroup
+        const dim3 grid(n);
+        const uint8_t *a = static_cast<const uint8_t *>(arena);
+        switch (U) {
+        case 4: hipLaunchKernelGGL((k_segments_wg<4, MODE>), grid, dim3(256), 0, s, a, descs, n, out, aux, xg); break;
+        case 8: hipLaunchKernelGGL((k_segments_wg<8, MODE>), grid, dim3(256), 0, s, a, descs, n, out, aux, xg); break;
+        case 16: hipLaunchKernelGGL((k_segments_wg<16, MODE>), grid, dim3(256), 0, s, a, descs, n, out, aux, xg); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     return hipErrorInvalidValue;
 }
 

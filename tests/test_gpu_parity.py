@@ -17,7 +17,8 @@ import golden_io as G
 
 pytestmark = pytest.mark.gpu
 
-GEOMS_SEG = [(g, u, p) for g in (4, 8, 16, 32, 64) for u in (1, 3, 4, 16) for p in (0, 1, 2)]
+GEOMS_SEG = [(g, u, p) for g in (4, 8, 16, 32, 64) for u in (1, 3, 4, 16) for p in (0, 1, 2)] + \
+    [(256, u, 0) for u in (4, 8, 16)]  # one range per workgroup (k_segments_wg)
 GEOMS_IP = [(g, u) for g in (16, 32, 64) for u in (1, 2, 3, 4, 6, 8, 16)]
 
 

@@ -1135,7 +1135,9 @@ static uint32_t resident_blocks(K kernel)
 //       probe on the same bytes);
 //   ~2 KiB .. 32 KiB (mixed 64-9000 B, mean 4.5 KiB): 32 lanes x 6 loads,
 //       several passes (95-97% of the probe; re-measured with the XCD order);
-//   >= 32 KiB (TSO): one range per wave, 16 loads per lane (98-100%).
+//   >= 32 KiB (TSO): one range per WORKGROUP, 16 loads per lane -- a 64-KiB
+//       range is one pass of every wave (profiles/r01/tso_wg.txt: 2343 us
+//       against 2385 us for one range per wave, 1.02x the read probe).
 // The resident-grid variants (persist 1, 2) measured slower on all three.
 Geometry pick_geometry(uint64_t mean_len)
 {
@@ -1145,7 +1147,7 @@ Geometry pick_geometry(uint64_t mean_len)
     const uint64_t chunks = mean_len / 16 + 1;
     const uint64_t interior = chunks > 2 ? chunks - 2 : 0;
     if (chunks >= 2048) {
-        g.lanes = 64;
+        g.lanes = 256; // one range per workgroup (k_segments_wg): 1.8 % over G=64 on configs[2]
         g.loads = 16;
     } else if (interior > 128) {
         g.lanes = 32;

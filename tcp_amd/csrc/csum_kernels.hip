@@ -1079,7 +1079,7 @@ hipError_t launch_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, hip
     const uint64_t nchunks = nbytes / 16;
     if (nchunks == 0)
         return hipSuccess;
-    int U = 8;
+    int U = 4; // the fastest plain read of those measured (profiles/r01/probe_variants.txt)
     if (const char *s = getenv("TCSUM_PROBE_U"))
         U = atoi(s);
     uint32_t xg = 1; // dispatch order: measured faster for the plain read (profiles/r01/xcd_tune.txt)

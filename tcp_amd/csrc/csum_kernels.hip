@@ -1286,6 +1286,8 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
         return hipSuccess;
     if (g.lanes < 16)
         g.lanes = 16;
+    if (g.lanes > 64) // k_ipv4 keeps a packet inside one wave (no workgroup-per-packet form)
+        g.lanes = 64;
     const uint64_t per_launch = kMaxBlocks * (256u / (uint32_t)g.lanes);
     if (n > per_launch) { // see kMaxBlocks
         for (uint64_t i0 = 0; i0 < n; i0 += per_launch) {

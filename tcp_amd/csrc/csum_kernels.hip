@@ -31,13 +31,6 @@ namespace tcsum {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// Minimum waves per SIMD asked of the register allocator for the streaming
-// kernels with U <= 8 loads per lane (TCSUM_WAVES_U8; 0 = the compiler's
-// choice).  Experiment knob; see pick_geometry.
-#ifndef TCSUM_WAVES_U8
-#define TCSUM_WAVES_U8 0
-#endif
-#define TCSUM_OCC(U) __attribute__((amdgpu_waves_per_eu((U) <= 8 && TCSUM_WAVES_U8 ? TCSUM_WAVES_U8 : 1)))
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 // a.lo + a.hi + acc in one VALU op (v_dot2_u32_u16 with {1,1}).
@@ -369,7 +362,7 @@ __device__ __forceinline__ uint16_t finalize(uint32_t acc, uintptr_t start, cons
 
 // One wave-slice of packets per wave, one launch-wide pass.
 template <int G, int U, int MODE>
-__global__ __launch_bounds__(256) TCSUM_OCC(U) void k_segments(const uint8_t *__restrict__ arena,
+__global__ __launch_bounds__(256) void k_segments(const uint8_t *__restrict__ arena,
                                                   const void *__restrict__ descs, uint32_t n,
                                                   uint16_t *__restrict__ out, uint32_t aux, uint32_t xg)
 {
@@ -750,7 +743,7 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
 }
 
 template <int G, int U, int IPM>
-__global__ __launch_bounds__(256) TCSUM_OCC(U) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
+__global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                               uint32_t n, uint32_t *__restrict__ out,
                                               uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
                                               uint32_t diag, uint32_t xg)

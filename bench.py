@@ -43,7 +43,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=50,
+                    help="untimed launches first: ~10 ms of load brings the GPU out of its idle clocks "
+                         "(scripts/drift_probe.py: the first ~40 configs[1] launches run 6 %% slower)")
     ap.add_argument("--config", default="mtu", help="headline workload (mtu|tso|mixed|mixed_aligned)")
     ap.add_argument("--secondary", default="tso,mixed,mixed_aligned,mixed_tx,mixed_rx",
                     help="extra configs measured at N=1")

@@ -532,13 +532,11 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     // caller's arrays are pinned already: a hipMemcpyAsync from/to pageable
     // memory is staged by the runtime per call and cost ~100 us per chunk
     // (e2e 45.8 -> 49.5 GiB/s only by making chunks 16x larger).
-    // (staged chunk by chunk inside the loop below, so the host copy of chunk
-    // k+1's descriptors overlaps the DMA of chunk k)
     const tcsum_peso_t *hsegs = segs;
-    const bool stage_descs = !mapped_host(segs);
-    if (stage_descs) {
+    if (!mapped_host(segs)) {
         if (!c.q_desc.reserve(sizeof(tcsum_peso_t) * n))
             return TCSUM_ERR_MEM;
+        par_memcpy(c.q_desc.h, reinterpret_cast<const uint8_t *>(segs), sizeof(tcsum_peso_t) * n);
         hsegs = reinterpret_cast<const tcsum_peso_t *>(c.q_desc.h);
     }
     uint16_t *hout = out;
@@ -569,8 +567,6 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
             if (hipMemcpyAsync(dbase + lo, h + lo, hi - lo, hipMemcpyHostToDevice, s) != hipSuccess)
                 return TCSUM_ERR_SYS;
         }
-        if (stage_descs)
-            memcpy(c.q_desc.h + sizeof(tcsum_peso_t) * i0, segs + i0, sizeof(tcsum_peso_t) * (i1 - i0));
         if (hipMemcpyAsync(c.d_descs + i0, hsegs + i0, sizeof(tcsum_peso_t) * (i1 - i0),
                            hipMemcpyHostToDevice, s) != hipSuccess)
             return TCSUM_ERR_SYS;

@@ -144,3 +144,18 @@ def test_host_tx_fill_any_descriptor_order(tc, where):
     flags = tc.host_batch_ipv4_tx_fill(arg, pk[perm])
     np.testing.assert_array_equal(view[: pout.size], pout)
     np.testing.assert_array_equal(flags, cases["flags"][perm])
+
+
+def test_c_netif_queue_demo(tc):
+    """tests/c/queue_demo.c: INTEGRATION.md §4a in plain C -- 50-frame netif
+    queues (Ethernet + IPv4 + TCP/UDP/ICMP) in a tcsum_host_alloc arena, tx
+    fill == the oracle's bytes, rx verdicts == the oracle's after damaging
+    random frames; per-queue launches and the queue server."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "c", "build",
+                       "queue_demo")
+    assert os.path.exists(exe), "built by __graft_entry__.build() (make -C tests/c)"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "queue server: 200 queues" in r.stdout

@@ -47,7 +47,7 @@ def parse():
                     help="untimed launches first: ~10 ms of load brings the GPU out of its idle clocks "
                          "(scripts/drift_probe.py: the first ~40 configs[1] launches run 6 %% slower)")
     ap.add_argument("--config", default="mtu", help="headline workload (mtu|tso|mixed|mixed_aligned)")
-    ap.add_argument("--secondary", default="tso,mixed,mixed_aligned,mixed_tx,mixed_rx",
+    ap.add_argument("--secondary", default="tso,mixed,mixed_aligned,mixed_tx,mixed_txo,mixed_rx",
                     help="extra configs measured at N=1")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -61,19 +61,22 @@ def algorithmic_bytes(batch) -> int:
     """Bytes one launch must move: every packet byte once, its descriptor, its result.
 
     peso: 24-B descriptor + 2-B result; ipv4 sums: 16-B descriptor + 4-B result;
-    tx fill: 16 B + 4 B written into the packet; rx verify: 16 B + 1-B verdict."""
+    tx fill: 16 B + 4 B written into the packet; rx verify: 16 B + 1-B verdict;
+    tx offload: 16 B + 4-B value + 1-B flags."""
     if batch.kind == "peso":
         per = 24 + 2
     else:
-        per = {"sums": 16 + 4, "tx": 16 + 4, "rx": 16 + 1}[batch.op]
+        per = {"sums": 16 + 4, "tx": 16 + 4, "rx": 16 + 1, "txo": 16 + 4 + 1}[batch.op]
     return batch.total_bytes + per * batch.n
 
 
-def launch(tc, batch, arena, descs, out):
+def launch(tc, batch, arena, descs, out, flags=None):
     if batch.kind == "peso":
         tc.batch_peso(arena, descs, batch.n, batch.total_bytes, out=out)
     elif batch.op == "tx":
         tc.batch_ipv4_tx_fill(arena, descs, batch.n, batch.total_bytes, want_flags=False)
+    elif batch.op == "txo":
+        tc.batch_ipv4_tx_offload(arena, descs, batch.n, batch.total_bytes, out=out, flags=flags)
     elif batch.op == "rx":
         tc.batch_ipv4_rx_verify(arena, descs, batch.n, batch.total_bytes, verdict=out, want_flags=False)
     else:
@@ -85,8 +88,9 @@ def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None):
     arena, descs = workload.materialize(batch)
     dt = torch.uint16 if batch.kind == "peso" else torch.int8 if batch.op == "rx" else torch.uint32
     out = torch.empty(batch.n, dtype=dt, device=arena.device)
+    flags = torch.empty(batch.n, dtype=torch.uint8, device=arena.device) if batch.op == "txo" else None
     for _ in range(warmup):
-        launch(tc, batch, arena, descs, out)
+        launch(tc, batch, arena, descs, out, flags)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -97,7 +101,7 @@ def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None):
     wall0 = time.perf_counter()
     t0.record(stream)
     for _ in range(steps):
-        launch(tc, batch, arena, descs, out)
+        launch(tc, batch, arena, descs, out, flags)
     t1.record(stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - wall0

@@ -120,6 +120,27 @@ int tcsum_batch_ipv4_tx_fill(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[d
                              uint32_t *out /*[dev] or NULL*/, uint8_t *flags /*[dev] or NULL*/,
                              uint64_t total_bytes_hint, void *stream);
 
+/* Batched tx offload (NIC checksum-offload style): the
+ * values tcsum_batch_ipv4_tx_fill would store -- out[i] = ip | l4 << 16, with
+ * the checksum fields read as zero -- and flags[i], WITHOUT writing the
+ * packets (the arena is read-only here).  The host applies them with
+ * tcsum_tx_apply where it touches the frame anyway (the pcap tx thread's copy
+ * of each frame, netif_pcap.c:42-67), which skips the scattered in-place
+ * writes of the fill.  tcsum_tx_apply on every packet of a batch leaves the
+ * bytes tcsum_batch_ipv4_tx_fill leaves.  out and flags are required. */
+int tcsum_batch_ipv4_tx_offload(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,
+                                uint32_t *out /*[dev]*/, uint8_t *flags /*[dev]*/,
+                                uint64_t total_bytes_hint, void *stream);
+
+/* Host side of the offload: store csums (one out[] word) into the IPv4 frame
+ * of len bytes at `frame` [host] exactly as the fill would -- header checksum
+ * always, the TCP/UDP/ICMP field unless flags says fragment / short L4 /
+ * other protocol, nothing for a SHORT / BAD_* packet.  Plain CPU stores. */
+int tcsum_tx_apply(void *frame /*[host]*/, uint32_t len, uint32_t csums, uint8_t flags);
+/* tcsum_tx_apply over a batch in a host arena (bounds checked first). */
+int tcsum_tx_apply_batch(void *arena /*[host]*/, uint64_t arena_bytes, const tcsum_pkt_t *pkts /*[host]*/,
+                         uint32_t n, const uint32_t *csums /*[host]*/, const uint8_t *flags /*[host]*/);
+
 /* Batched rx verify: verdict[i] = the net_err_t the
  * reference's receive path returns from its size and checksum gates, in its
  * order: frame < 20 -> SIZE; version != 4 -> NOT_SUPPORT; IHL/total length ->

@@ -30,6 +30,9 @@ SIGNATURES = {
     "tcsum_batch_ipv4": (_I, [_V, _V, _U32, _V, _V, _U64, _V]),
     "tcsum_batch_ipv4_tx_fill": (_I, [_V, _V, _U32, _V, _V, _U64, _V]),
     "tcsum_batch_ipv4_rx_verify": (_I, [_V, _V, _U32, _V, _V, _V, _U64, _V]),
+    "tcsum_batch_ipv4_tx_offload": (_I, [_V, _V, _U32, _V, _V, _U64, _V]),
+    "tcsum_tx_apply": (_I, [_V, _U32, _U32, ctypes.c_uint8]),
+    "tcsum_tx_apply_batch": (_I, [_V, _U64, _V, _U32, _V, _V]),
     "tcsum_host_batch_peso": (_I, [_I, _V, _U64, _V, _U32, _V]),
     "tcsum_host_batch_peso_multi": (_I, [_V, _I, _V, _U64, _V, _U32, _V]),
     "tcsum_host_batch_ipv4": (_I, [_I, _V, _U64, _V, _U32, _V, _V]),

@@ -415,6 +415,62 @@ int tcsum_batch_ipv4_tx_fill(void *arena, const tcsum_pkt_t *pkts, uint32_t n, u
     return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
 }
 
+int tcsum_batch_ipv4_tx_offload(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
+                                uint8_t *flags, uint64_t total_bytes_hint, void *stream)
+{
+    if (n == 0)
+        return TCSUM_OK;
+    if (!arena || !pkts || !out || !flags)
+        return TCSUM_ERR_PARAM;
+    // the kernel never writes the arena in this mode
+    const hipError_t e = tcsum::launch_ipv4(3, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
+                                            const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts,
+                                            n, out, flags, nullptr, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
+}
+
+// Host side of the offload contract: the stores k_ipv4<IP_TX> makes, driven
+// by the flags it computed (so no header gate is restated here).
+int tcsum_tx_apply(void *frame, uint32_t len, uint32_t csums, uint8_t flags)
+{
+    if (!frame)
+        return TCSUM_ERR_PARAM;
+    if (flags & (TCSUM_PKT_SHORT | TCSUM_PKT_BAD_VERSION | TCSUM_PKT_BAD_HDRLEN | TCSUM_PKT_BAD_TOTLEN))
+        return TCSUM_OK; // the fill writes nothing into a rejected packet
+    if (len < 20)
+        return TCSUM_ERR_PARAM; // flags that do not belong to this frame
+    uint8_t *p = static_cast<uint8_t *>(frame);
+    p[10] = (uint8_t)csums; // ipv4.c:643,656, host order like the struct field
+    p[11] = (uint8_t)(csums >> 8);
+    if (flags & (TCSUM_PKT_FRAGMENT | TCSUM_PKT_L4_SHORT | TCSUM_PKT_PROTO_OTHER))
+        return TCSUM_OK;
+    const uint32_t hl = (uint32_t)(p[0] & 0xFu) << 2;
+    const uint32_t fld = p[9] == 6 ? 16u : p[9] == 17 ? 6u : p[9] == 1 ? 2u : 0u; // tcp.h:71 udp.h:24 icmpv4.h:28
+    if (!fld || hl + fld + 2 > len)
+        return TCSUM_ERR_PARAM;
+    p[hl + fld] = (uint8_t)(csums >> 16); // tcp_out.c:19-20 / udp.c:320-321 / icmpv4.c:45-58
+    p[hl + fld + 1] = (uint8_t)(csums >> 24);
+    return TCSUM_OK;
+}
+
+int tcsum_tx_apply_batch(void *arena, uint64_t arena_bytes, const tcsum_pkt_t *pkts, uint32_t n,
+                         const uint32_t *csums, const uint8_t *flags)
+{
+    if (n == 0)
+        return TCSUM_OK;
+    if (!arena || !pkts || !csums || !flags)
+        return TCSUM_ERR_PARAM;
+    for (uint32_t i = 0; i < n; ++i)
+        if (pkts[i].offset > arena_bytes || pkts[i].len > arena_bytes - pkts[i].offset)
+            return TCSUM_ERR_PARAM;
+    int rc = TCSUM_OK;
+    for (uint32_t i = 0; i < n; ++i) {
+        const int r = tcsum_tx_apply(static_cast<uint8_t *>(arena) + pkts[i].offset, pkts[i].len, csums[i], flags[i]);
+        rc = rc == TCSUM_OK ? r : rc;
+    }
+    return rc;
+}
+
 int tcsum_batch_ipv4_rx_verify(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, int8_t *verdict,
                                uint32_t *out, uint8_t *flags, uint64_t total_bytes_hint, void *stream)
 {

@@ -494,7 +494,8 @@ __global__ __launch_bounds__(256) void k_segments_pp(const uint8_t *__restrict__
 //            icmpv4.c:36) and is_pkt_ok flags;
 //   IP_TX    the stack's tx fill, in place: checksum fields read as zero,
 //            values stored into them (ipv4.c:643,656, tcp_out.c:19-20,
-//            udp.c:320-321, icmpv4.c:45-58);
+//            udp.c:320-321, icmpv4.c:45-58); with IP_OPT_NO_STORE the same
+//            values go to `out` only (tx offload: the host applies them);
 //   IP_RX    the stack's rx gates: net_err_t verdict per packet
 //            (ipv4.c:475-515, is_pkt_ok ipv4.c:220-250, tcp_in.c:69-85,
 //            udp.c:386-415, icmpv4.c:29-43,71-77).
@@ -502,6 +503,10 @@ __global__ __launch_bounds__(256) void k_segments_pp(const uint8_t *__restrict__
 // with v_alignbyte; the data pass splits every chunk between the header range
 // [0,hl), the L4 range [hl,end) and the 2-byte checksum fields.
 enum IpMode : int { IP_SUMS = 0, IP_TX = 1, IP_RX = 2 };
+// k_ipv4 `opts` bits (runtime, uniform over the grid)
+constexpr uint32_t IP_OPT_NO_STORE = 1u; // IP_TX: compute the fill's values, leave the packets alone
+// launch_ipv4 mode 3: IP_TX kernels with IP_OPT_NO_STORE
+constexpr int IP_TX_OFFLOAD = 3;
 
 // x[k] = w[q + k] for k < 6, q in 0..3: two stages of selects, no branches.
 __device__ __forceinline__ void pick6(uint32_t q, const uint32_t w[12], uint32_t x[6])
@@ -540,7 +545,7 @@ template <int G, int U, int IPM>
 __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                             uint32_t pk, uint32_t n, uint32_t *__restrict__ out,
                                             uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
-                                            uint32_t diag)
+                                            uint32_t opts)
 {
     const uint32_t gl = threadIdx.x & (G - 1);
     const bool live = pk < n;
@@ -704,7 +709,7 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
             }
         }
         if constexpr (IPM == IP_TX) {
-            if (!bad && !(diag & 1u)) { // stored in host order, like the struct fields
+            if (!bad && !(opts & IP_OPT_NO_STORE)) { // stored in host order, like the struct fields
                 pp[10] = (uint8_t)ip;
                 pp[11] = (uint8_t)(ip >> 8);
                 if (field_on) {
@@ -746,11 +751,11 @@ template <int G, int U, int IPM>
 __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                               uint32_t n, uint32_t *__restrict__ out,
                                               uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
-                                              uint32_t diag, uint32_t xg)
+                                              uint32_t opts, uint32_t xg)
 {
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
     ipv4_packet<G, U, IPM>(arena, pkts, blk * (256u / G) + threadIdx.x / G, n, out, flags_out, verdict_out,
-                           diag); // no 32-bit wrap for any n
+                           opts); // no 32-bit wrap for any n
 }
 
 // ---------------------------------------------------------------- queue server
@@ -1252,13 +1257,13 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
 
 template <int IPM>
 static hipError_t ipv4_u(int G, int U, dim3 grid, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
-                         uint32_t *out, uint8_t *flags, int8_t *verdict, uint32_t diag, uint32_t xg,
+                         uint32_t *out, uint8_t *flags, int8_t *verdict, uint32_t opts, uint32_t xg,
                          hipStream_t s)
 {
 #define TCSUM_IP(GG, UU)                                                                             \
     if (G == GG && U == UU) {                                                                      \
         hipLaunchKernelGGL((k_ipv4<GG, UU, IPM>), grid, dim3(256), 0, s, arena, pkts, n, out, flags, \
-                           verdict, diag, xg);                                                     \
+                           verdict, opts, xg);                                                     \
         return hipGetLastError();                                                                  \
     }
 #define TCSUM_IP_U(GG)                                                                               \
@@ -1294,16 +1299,17 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
     }
     const uint64_t per_block = 256u / (uint32_t)g.lanes;
     const dim3 grid((uint32_t)((n + per_block - 1) / per_block));
-    // TCSUM_DIAG=1: tx fill computes but does not store (measurement only,
-    // scripts/tx_probe.py)
-    const uint32_t diag = getenv("TCSUM_DIAG") ? (uint32_t)atoi(getenv("TCSUM_DIAG")) : 0u;
+    const uint32_t xg = (uint32_t)g.xcd;
     switch (ip_mode) {
     case IP_TX:
-        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, (uint32_t)g.xcd, stream);
+        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, 0u, xg, stream);
+    case IP_TX_OFFLOAD: // the tx values into `out` only; the packets are not written
+        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, IP_OPT_NO_STORE, xg,
+                             stream);
     case IP_RX:
-        return ipv4_u<IP_RX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, (uint32_t)g.xcd, stream);
+        return ipv4_u<IP_RX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, 0u, xg, stream);
     default:
-        return ipv4_u<IP_SUMS>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, diag, (uint32_t)g.xcd, stream);
+        return ipv4_u<IP_SUMS>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, 0u, xg, stream);
     }
 }
 

@@ -224,6 +224,33 @@ def host_batch_ipv4_tx_fill(host_arena, pkts: np.ndarray, device: int = 0):
     return flags
 
 
+def batch_ipv4_tx_offload(arena, pkts, n: int, total_bytes: int = 0, out=None, flags=None, stream=None):
+    """(out u32 = ip | l4 << 16, flags): the values batch_ipv4_tx_fill would
+    store, the packets left untouched (NIC-offload contract; apply on the host
+    with tx_apply / tx_apply_batch)."""
+    torch = _torch()
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint32, device=arena.device)
+    if flags is None:
+        flags = torch.empty(n, dtype=torch.uint8, device=arena.device)
+    rc = _lib.lib().tcsum_batch_ipv4_tx_offload(arena.data_ptr(), pkts.data_ptr(), n, out.data_ptr(),
+                                                flags.data_ptr(), total_bytes, _stream_ptr(stream))
+    _lib.check(rc, "tcsum_batch_ipv4_tx_offload")
+    return out, flags
+
+
+def tx_apply_batch(host_arena: np.ndarray, pkts: np.ndarray, out: np.ndarray, flags: np.ndarray) -> None:
+    """Store the offloaded tx values into host frames (tcsum_tx_apply_batch), in place."""
+    assert pkts.dtype == PKT_DTYPE
+    pkts = np.ascontiguousarray(pkts)
+    out = np.ascontiguousarray(out, dtype=np.uint32)
+    flags = np.ascontiguousarray(flags, dtype=np.uint8)
+    assert out.size == pkts.size and flags.size == pkts.size
+    p, nb = _host_arena_args(host_arena)
+    _lib.check(_lib.lib().tcsum_tx_apply_batch(p, nb, pkts.ctypes.data, pkts.size, out.ctypes.data,
+                                               flags.ctypes.data), "tcsum_tx_apply_batch")
+
+
 def host_batch_ipv4_rx_verify(host_arena, pkts: np.ndarray, device: int = 0):
     """(verdict int8 net_err_t, out, flags) for packets in host memory."""
     assert pkts.dtype == PKT_DTYPE

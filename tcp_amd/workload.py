@@ -31,6 +31,7 @@ CONFIGS = {
     # the same packets through the tx fill / rx verify entry points
     "mixed_tx": dict(n=1 << 20, lo=64, hi=9000, kind="ipv4", aligned=False, op="tx"),
     "mixed_rx": dict(n=1 << 20, lo=64, hi=9000, kind="ipv4", aligned=False, op="rx"),
+    "mixed_txo": dict(n=1 << 20, lo=64, hi=9000, kind="ipv4", aligned=False, op="txo"),
 }
 CONFIG_NAMES = {
     "mtu": "1M x 1500 B TCP segments (MTU), device-resident",
@@ -39,6 +40,7 @@ CONFIG_NAMES = {
     "mixed_aligned": "1M mixed IPv4 TCP/UDP packets, uniform 64-9000 B, 16-B aligned starts",
     "mixed_tx": "1M mixed IPv4 packets: batched tx fill (checksums written in place)",
     "mixed_rx": "1M mixed IPv4 packets: batched rx verify (net_err_t verdict per packet)",
+    "mixed_txo": "1M mixed IPv4 packets: batched tx offload (the fill's values + flags out, packets untouched)",
 }
 
 

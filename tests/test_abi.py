@@ -172,3 +172,40 @@ def test_no_cpu_fallback(libpath):
     rc = L.tcsum_host_batch_peso(0, host.ctypes.data, host.nbytes, seg.ctypes.data, 1, out.ctypes.data)
     assert rc == _lib.ERR_NOT_SUPPORT
     assert L.tcsum_plat_init(0) == _lib.ERR_NOT_SUPPORT
+
+
+def test_tx_apply_reproduces_the_reference_fill(libpath):
+    """tcsum_tx_apply (the host half of the tx offload) stores exactly what the
+    reference's tx path stores: the values are read back from the reference's
+    filled frames (ipv4_tx_out.bin), the flags are the fixture's, and applying
+    them to the unfilled frames must give the filled pool byte for byte --
+    which fields are written, where, and for which packets not at all."""
+    import golden_io as G
+    from tcp_amd import PKT_DTYPE, tx_apply_batch
+    from tcp_amd import _lib
+    cases, pin, pout = G.ipv4_tx_cases()
+    pk = G.pkt_descs(cases, PKT_DTYPE)
+    off = pk["offset"].astype(np.int64)
+    ln = pk["len"].astype(np.int64)
+    ihl4 = np.where(ln >= 20, (pout[np.minimum(off, pout.size - 1)] & 0xF).astype(np.int64) * 4, 0)
+    proto = pout[np.minimum(off + 9, pout.size - 1)]
+    fld = np.select([proto == 6, proto == 17, proto == 1], [16, 6, 2], 0)
+
+    def u16(pos):
+        pos = np.clip(pos, 0, pout.size - 2)
+        return pout[pos].astype(np.uint32) | (pout[pos + 1].astype(np.uint32) << 8)
+
+    csums = u16(off + 10) | (u16(off + ihl4 + fld) << 16)
+    host = pin.copy()
+    tx_apply_batch(host, pk, csums, cases["flags"].astype(np.uint8))
+    np.testing.assert_array_equal(host[: pout.size], pout)
+    L = _lib.lib()
+    assert L.tcsum_tx_apply(None, 20, 0, 0) == _lib.ERR_PARAM
+    assert L.tcsum_batch_ipv4_tx_offload(None, None, 4, None, None, 0, None) == _lib.ERR_PARAM
+    assert L.tcsum_batch_ipv4_tx_offload(None, None, 0, None, None, 0, None) == _lib.OK
+    bad = np.zeros(1, PKT_DTYPE)
+    bad["offset"], bad["len"] = host.size - 4, 20  # past the arena: nothing is touched
+    before = host.copy()
+    rc = L.tcsum_tx_apply_batch(host.ctypes.data, host.nbytes, bad.ctypes.data, 1,
+                                np.zeros(1, np.uint32).ctypes.data, np.zeros(1, np.uint8).ctypes.data)
+    assert rc == _lib.ERR_PARAM and (host == before).all()

@@ -290,6 +290,39 @@ def test_batch_ipv4_tx_fill_golden(tc, torch, geometry, g, u):
     np.testing.assert_array_equal(arena.cpu().numpy()[: pout.size], pout)
 
 
+@pytest.mark.parametrize("g,u", [(16, 1), (32, 4), (64, 2), (64, 16)])
+def test_batch_ipv4_tx_offload_golden(tc, torch, geometry, g, u):
+    """tx offload: the packets stay untouched on the device, and the host
+    applying out/flags gives the reference's filled frames byte for byte;
+    out is the word tx fill reports for the same packets."""
+    geometry(g, u)
+    cases, pin, pout = G.ipv4_tx_cases()
+    arena = to_dev(torch, pin)
+    d = tc.descs_to_device(G.pkt_descs(cases, tc.PKT_DTYPE))
+    out, flags = tc.batch_ipv4_tx_offload(arena, d, cases.size, int(cases["frame_len"].sum()))
+    np.testing.assert_array_equal(arena.cpu().numpy()[: pin.size], pin)
+    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+    host = pin.copy()
+    tc.tx_apply_batch(host, G.pkt_descs(cases, tc.PKT_DTYPE), out.cpu().numpy(), flags.cpu().numpy())
+    np.testing.assert_array_equal(host[: pout.size], pout)
+    fill_out = torch.empty(cases.size, dtype=torch.uint32, device="cuda")
+    tc.batch_ipv4_tx_fill(arena, d, cases.size, out=fill_out)
+    np.testing.assert_array_equal(out.cpu().numpy(), fill_out.cpu().numpy())
+
+
+def test_tx_offload_full_mixed(tc, torch):
+    """configs[3] at full size: offload + host apply == in-place fill, every byte."""
+    from tcp_amd import workload
+    b = workload.make_batch("mixed")
+    arena, descs = workload.materialize(b)
+    out, flags = tc.batch_ipv4_tx_offload(arena, descs, b.n, b.total_bytes)
+    host = arena.cpu().numpy()
+    tc.tx_apply_batch(host, b.descs, out.cpu().numpy(), flags.cpu().numpy())
+    tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
+    torch.cuda.synchronize()
+    assert torch.equal(arena, torch.from_numpy(host).to(arena.device))
+
+
 @pytest.mark.parametrize("g,u", [(16, 1), (16, 4), (32, 3), (32, 4), (64, 2), (64, 16)])
 def test_batch_ipv4_rx_verify_golden(tc, torch, oracle, geometry, g, u):
     geometry(g, u)

@@ -329,7 +329,8 @@ int tcsum_plat_init(int device)
 void *tcsum_host_alloc(size_t bytes)
 {
     void *p = nullptr;
-    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
+    // portable: a multi-device host batch reads it from every GPU's link
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess)
         return nullptr;
     return p;
 }

@@ -4,7 +4,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
 One "step" = one batched checksum pass (one kernel launch) over the whole
-synthetic batch already resident in HBM.  The headline workload is
+synthetic batch already resident in HBM.  Before the K timed steps: W untimed
+warm-up steps, continued (untimed) until --settle-ms have passed, so the GPU
+clocks are out of idle whatever W the caller picks.  The headline workload is
 BASELINE.json configs[1]: 1,048,576 x 1500 B TCP segments per GPU, checksummed
 exactly as checksum_peso (net/src/tools.c:56-75) does, pseudo-header built
 in-kernel.  With N GPUs every rank holds its own 1M-segment slice of one
@@ -49,6 +51,9 @@ def parse():
     ap.add_argument("--config", default="mtu", help="headline workload (mtu|tso|mixed|mixed_aligned)")
     ap.add_argument("--secondary", default="tso,mixed,mixed_aligned,mixed_tx,mixed_txo,mixed_rx",
                     help="extra configs measured at N=1")
+    ap.add_argument("--settle-ms", type=float, default=30.0,
+                    help="untimed: the warm-up also lasts at least this long (GPU clocks out of idle "
+                         "whatever W is; 0 = exactly W launches)")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -83,6 +88,9 @@ def launch(tc, batch, arena, descs, out, flags=None):
         tc.batch_ipv4(arena, descs, batch.n, batch.total_bytes, out=out, want_flags=False)
 
 
+SETTLE_MS = 30.0  # set from --settle-ms in main()
+
+
 def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None):
     batch = workload.make_batch(config, rank=rank)
     arena, descs = workload.materialize(batch)
@@ -92,6 +100,14 @@ def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None):
     for _ in range(warmup):
         launch(tc, batch, arena, descs, out, flags)
     torch.cuda.synchronize()
+    # untimed: keep warming until SETTLE_MS have passed (after idle the first
+    # ~13 ms of launches run ~6 % slow while the clocks ramp,
+    # profiles/r01/drift_probe.txt), so a small W does not time the ramp
+    settle0 = time.perf_counter()
+    while (time.perf_counter() - settle0) * 1e3 < SETTLE_MS:
+        for _ in range(4):
+            launch(tc, batch, arena, descs, out, flags)
+        torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -350,6 +366,8 @@ def main():
     torch.cuda.set_device(dev)
     dist = D.init(backend, dev)  # barrier + max-time only; no data-path collective
 
+    global SETTLE_MS
+    SETTLE_MS = 0.0 if args.pmc_child else max(0.0, args.settle_ms)
     if args.pmc_child:
         time_config(torch, tc, workload, args.config, 0, args.steps, args.warmup)
         return
@@ -374,6 +392,7 @@ def main():
         "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
+        "settle_ms": SETTLE_MS,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
         "scaling": "weak",

@@ -39,7 +39,8 @@ namespace {
 using tcsum::Geometry;
 
 constexpr int kMaxDev = 16;
-constexpr int kHostStreams = 3;
+constexpr int kHostStreams = 2; // host batches: one copy stream, one kernel stream
+constexpr int kHostEvents = 8; // ring of copy-done events (host batches)
 
 // Grow-only pinned, coherent host buffer with its device-side address.
 struct Pinned {
@@ -81,6 +82,7 @@ struct Ctx {
     uint16_t *d_result = nullptr;
     // host-resident batches
     hipStream_t hs[kHostStreams] = {};
+    hipEvent_t hev[kHostEvents] = {};
     uint8_t *d_arena = nullptr;
     size_t d_arena_cap = 0;
     tcsum_peso_t *d_descs = nullptr;
@@ -151,6 +153,9 @@ int ctx_init(Ctx &c, int dev)
         return TCSUM_ERR_SYS;
     for (auto &s : c.hs)
         if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+            return TCSUM_ERR_SYS;
+    for (auto &e : c.hev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
             return TCSUM_ERR_SYS;
     if (hipHostMalloc(&c.desc, 64, hipHostMallocCoherent) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void **>(&c.result), 64, hipHostMallocCoherent) != hipSuccess)
@@ -519,6 +524,23 @@ int tcsum_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, void *strea
 namespace { // defined with the host-queue batches below
 uint8_t *mapped_host(const void *p);
 void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n);
+extern "C++" {
+template <class F>
+void parallel_for(size_t n, size_t min_per, F &&f);
+}
+
+// Byte span [lo, hi) and byte count of a run of segments.
+struct HostSpan {
+    uint64_t lo = UINT64_MAX, hi = 0, bytes = 0;
+    bool bad = false;
+    void merge(const HostSpan &o)
+    {
+        lo = o.lo < lo ? o.lo : lo;
+        hi = o.hi > hi ? o.hi : hi;
+        bytes += o.bytes;
+        bad |= o.bad;
+    }
+};
 } // namespace
 
 int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_bytes,
@@ -528,18 +550,33 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         return TCSUM_OK;
     if (!host_arena || !segs || !out || device < 0 || device >= kMaxDev)
         return TCSUM_ERR_PARAM;
-    uint64_t glo = UINT64_MAX, ghi = 0; // the span the segments touch
-    for (uint32_t i = 0; i < n; ++i) {
-        if (segs[i].offset > arena_bytes || segs[i].len > arena_bytes - segs[i].offset)
-            return TCSUM_ERR_PARAM;
-        if (segs[i].len) {
-            glo = segs[i].offset < glo ? segs[i].offset : glo;
-            ghi = segs[i].offset + segs[i].len > ghi ? segs[i].offset + segs[i].len : ghi;
+    // One parallel pass over the descriptors: per block of kSpanBlock
+    // segments, validity and the byte span [lo, hi) its segments touch.
+    constexpr uint32_t kSpanBlock = 4096;
+    const uint32_t nblk = (n + kSpanBlock - 1) / kSpanBlock;
+    std::vector<HostSpan> blk(nblk);
+    parallel_for(nblk, 16, [&](size_t b, size_t e) {
+        for (size_t k = b; k < e; ++k) {
+            HostSpan sp;
+            const uint32_t i1 = (uint32_t)std::min<uint64_t>(n, (k + 1) * (uint64_t)kSpanBlock);
+            for (uint32_t i = (uint32_t)k * kSpanBlock; i < i1; ++i) {
+                const uint64_t o = segs[i].offset, l = segs[i].len;
+                sp.bad |= o > arena_bytes || l > arena_bytes - o;
+                if (l) {
+                    sp.lo = o < sp.lo ? o : sp.lo;
+                    sp.hi = o + l > sp.hi ? o + l : sp.hi;
+                    sp.bytes += l;
+                }
+            }
+            blk[k] = sp;
         }
-    }
-    if (ghi == 0)
-        glo = 0;
-    glo &= ~uint64_t(15);
+    });
+    HostSpan all;
+    for (const HostSpan &sp : blk)
+        all.merge(sp);
+    if (all.bad)
+        return TCSUM_ERR_PARAM;
+    const uint64_t glo = all.hi ? all.lo & ~uint64_t(15) : 0, ghi = all.hi;
     Ctx &c = g_ctx[device];
     std::lock_guard<std::mutex> lk(c.mu);
     int rc = ctx_init(c, device);
@@ -573,22 +610,48 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         c.d_descs_cap = c.d_out_cap = n;
     }
 
-    // chunks of ~32 MiB of packet bytes, round-robin over the streams:
-    // H2D(bytes, descriptors) -> kernel -> D2H(results)
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < n; ++i)
-        total += segs[i].len;
-    uint64_t target = 32ull << 20; // bytes per chunk; TCSUM_E2E_CHUNK_MB overrides (measurement)
+    // Chunks of >= ~64 MiB of packet bytes (whole span blocks).  All copies go
+    // in order on ONE copy stream, so the host link never idles between
+    // chunks and no two copies compete for it; each chunk's kernel waits on
+    // its copy's event on the kernel stream and runs under the next copy.
+    uint64_t target = 64ull << 20; // TCSUM_E2E_CHUNK_MB overrides (measurement)
     if (const char *v = getenv("TCSUM_E2E_CHUNK_MB"))
         target = (uint64_t)std::max(1, atoi(v)) << 20;
-    uint32_t per = (uint32_t)(total ? ((uint64_t)n * target + total - 1) / total : n);
-    if (per == 0)
-        per = 1;
+    std::vector<uint32_t> cut{0}; // chunk k = span blocks [cut[k], cut[k+1])
+    std::vector<HostSpan> ch;
+    for (uint32_t k = 0; k < nblk; ++k) {
+        if (ch.empty() || ch.back().bytes >= target) {
+            ch.emplace_back();
+            if (k)
+                cut.push_back(k);
+        }
+        ch.back().merge(blk[k]);
+    }
+    cut.push_back(nblk);
+    // segments in no particular order: every chunk's span covers most of the
+    // batch's, so copy the batch's span once and run one kernel on it
+    uint64_t spans = 0;
+    for (const HostSpan &sp : ch)
+        spans += sp.hi > sp.lo ? sp.hi - sp.lo : 0;
+    if (ch.size() > 1 && spans > (ghi - glo) + (ghi - glo) / 4) {
+        ch.assign(1, all);
+        cut.assign({0u, nblk});
+    }
     const uint8_t *h = static_cast<const uint8_t *>(host_arena);
-    // Descriptors in and results out through pinned staging unless the
-    // caller's arrays are pinned already: a hipMemcpyAsync from/to pageable
-    // memory is staged by the runtime per call and cost ~100 us per chunk
-    // (e2e 45.8 -> 49.5 GiB/s only by making chunks 16x larger).
+    uint8_t *const dbase = c.d_arena - glo;
+    hipStream_t cs = c.hs[0], ks = c.hs[1];
+    auto copy_bytes = [&](const HostSpan &sp) {
+        if (sp.hi <= sp.lo)
+            return hipSuccess;
+        const uint64_t lo = sp.lo & ~uint64_t(15), hi = std::min(arena_bytes, (sp.hi + 15) & ~uint64_t(15));
+        return hipMemcpyAsync(dbase + lo, h + lo, hi - lo, hipMemcpyHostToDevice, cs);
+    };
+    // the first chunk's bytes start crossing the link before the host stages
+    // the descriptors: a hipMemcpyAsync from pageable memory is staged by the
+    // runtime per call (~100 us per chunk), so they go through pinned staging
+    // unless the caller's array is pinned already
+    if (copy_bytes(ch[0]) != hipSuccess)
+        return TCSUM_ERR_SYS;
     const tcsum_peso_t *hsegs = segs;
     if (!mapped_host(segs)) {
         if (!c.q_desc.reserve(sizeof(tcsum_peso_t) * n))
@@ -602,42 +665,25 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
             return TCSUM_ERR_MEM;
         hout = reinterpret_cast<uint16_t *>(c.q_res.h);
     }
-    uint8_t *const dbase = c.d_arena - glo;
-    int k = 0;
-    for (uint32_t i0 = 0; i0 < n; i0 += per, ++k) {
-        const uint32_t i1 = i0 + per < n ? i0 + per : n;
-        uint64_t lo = UINT64_MAX, hi = 0, bytes = 0;
-        for (uint32_t i = i0; i < i1; ++i) {
-            if (segs[i].len == 0)
-                continue;
-            lo = segs[i].offset < lo ? segs[i].offset : lo;
-            const uint64_t end = segs[i].offset + segs[i].len;
-            hi = end > hi ? end : hi;
-            bytes += segs[i].len;
-        }
-        hipStream_t s = c.hs[k % kHostStreams];
-        if (hi > lo) {
-            lo &= ~uint64_t(15);
-            hi = (hi + 15) & ~uint64_t(15);
-            if (hi > arena_bytes)
-                hi = arena_bytes;
-            if (hipMemcpyAsync(dbase + lo, h + lo, hi - lo, hipMemcpyHostToDevice, s) != hipSuccess)
-                return TCSUM_ERR_SYS;
-        }
-        if (hipMemcpyAsync(c.d_descs + i0, hsegs + i0, sizeof(tcsum_peso_t) * (i1 - i0),
-                           hipMemcpyHostToDevice, s) != hipSuccess)
+    if (hipMemcpyAsync(c.d_descs, hsegs, sizeof(tcsum_peso_t) * n, hipMemcpyHostToDevice, cs) != hipSuccess)
+        return TCSUM_ERR_SYS;
+    for (size_t k = 0; k < ch.size(); ++k) {
+        if (k && copy_bytes(ch[k]) != hipSuccess)
             return TCSUM_ERR_SYS;
-        const hipError_t e = tcsum::launch_segments(tcsum::MODE_PESO, tcsum::pick_geometry(mean_of(bytes, i1 - i0)),
-                                                    dbase, c.d_descs + i0, i1 - i0, c.d_out + i0, 0u, s);
+        hipEvent_t ev = c.hev[k % kHostEvents];
+        if (hipEventRecord(ev, cs) != hipSuccess || hipStreamWaitEvent(ks, ev, 0) != hipSuccess)
+            return TCSUM_ERR_SYS;
+        const uint32_t i0 = cut[k] * kSpanBlock;
+        const uint32_t i1 = (uint32_t)std::min<uint64_t>(n, (uint64_t)cut[k + 1] * kSpanBlock);
+        const hipError_t e = tcsum::launch_segments(tcsum::MODE_PESO,
+                                                    tcsum::pick_geometry(mean_of(ch[k].bytes, i1 - i0)), dbase,
+                                                    c.d_descs + i0, i1 - i0, c.d_out + i0, 0u, ks);
         if (e != hipSuccess)
             return TCSUM_ERR_SYS;
-        if (hipMemcpyAsync(hout + i0, c.d_out + i0, sizeof(uint16_t) * (i1 - i0), hipMemcpyDeviceToHost, s) !=
-            hipSuccess)
-            return TCSUM_ERR_SYS;
     }
-    for (auto &s : c.hs)
-        if (hipStreamSynchronize(s) != hipSuccess)
-            return TCSUM_ERR_SYS;
+    if (hipMemcpyAsync(hout, c.d_out, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, ks) != hipSuccess ||
+        hipStreamSynchronize(ks) != hipSuccess || hipStreamSynchronize(cs) != hipSuccess)
+        return TCSUM_ERR_SYS;
     if (hout != out)
         memcpy(out, hout, sizeof(uint16_t) * n);
     return TCSUM_OK;

@@ -516,13 +516,18 @@ def test_huge_batch_index_math(tc, torch, oracle, geometry):
     np.testing.assert_array_equal(out.cpu().numpy(), exp)
 
 
-def test_host_batch_end_to_end(tc, oracle):
-    """Pinned host arena -> H2D -> kernel -> D2H matches the device-resident path."""
+@pytest.mark.parametrize("order,chunk_mb", [("permuted", None), ("offset", None), ("offset", "1")])
+def test_host_batch_end_to_end(tc, oracle, monkeypatch, order, chunk_mb):
+    """Pinned host arena -> H2D -> kernel -> D2H matches the device-resident
+    path: descriptors in any order (one span copy) and in offset order (the
+    chunk pipeline; 1 MiB chunks = one per 4096-segment block, 11 chunks)."""
     from tcp_amd import workload
-    b = workload.make_batch("mtu", n=30000)
+    if chunk_mb:
+        monkeypatch.setenv("TCSUM_E2E_CHUNK_MB", chunk_mb)
+    b = workload.make_batch("mtu", n=43000)
     host = oracle.synth_fill(b.byte_base, b.alloc_bytes, b.seed)
     rng = np.random.default_rng(3)
-    d = b.descs[rng.permutation(b.n)]  # any order
+    d = b.descs[rng.permutation(b.n)] if order == "permuted" else b.descs
     out = tc.host_batch_peso(host, d)
     np.testing.assert_array_equal(out, oracle.batch_peso(host, d, nthreads=8))
 

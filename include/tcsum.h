@@ -157,10 +157,12 @@ int tcsum_batch_ipv4_rx_verify(const void *arena /*[dev]*/, const tcsum_pkt_t *p
 
 /* --------------------------------------------------- host-resident batches */
 
-/* End to end: host arena -> hipMemcpyAsync H2D (chunked, pipelined over
- * several streams) -> tcsum_batch_peso -> D2H of the results; returns after
- * the results are in host_out.  host_arena should come from tcsum_host_alloc
- * (pinned) for full PCIe rate.  Segments may be in any order. */
+/* End to end: host arena -> hipMemcpyAsync H2D (chunks in order on one copy
+ * stream; each chunk's kernel on a second stream behind that chunk's copy) ->
+ * tcsum_batch_peso -> D2H of the results; returns after the results are in
+ * host_out.  host_arena should come from tcsum_host_alloc (pinned) for full
+ * PCIe rate.  Segments may be in any order (in offset order the copies and
+ * kernels pipeline; otherwise the batch's byte span is copied once). */
 int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_bytes,
                           const tcsum_peso_t *segs /*[host]*/, uint32_t n,
                           uint16_t *out /*[host]*/);

@@ -646,43 +646,47 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         const uint64_t lo = sp.lo & ~uint64_t(15), hi = std::min(arena_bytes, (sp.hi + 15) & ~uint64_t(15));
         return hipMemcpyAsync(dbase + lo, h + lo, hi - lo, hipMemcpyHostToDevice, cs);
     };
-    // the first chunk's bytes start crossing the link before the host stages
-    // the descriptors: a hipMemcpyAsync from pageable memory is staged by the
-    // runtime per call (~100 us per chunk), so they go through pinned staging
-    // unless the caller's array is pinned already
+    // a hipMemcpyAsync from pageable memory is staged by the runtime per call
+    // (~100 us per chunk), so descriptors and results go through pinned
+    // staging unless the caller's arrays are pinned already
+    const bool stage_descs = !mapped_host(segs), stage_out = !mapped_host(out);
+    if ((stage_descs && !c.q_desc.reserve(sizeof(tcsum_peso_t) * n)) ||
+        (stage_out && !c.q_res.reserve(sizeof(uint16_t) * n + 64)))
+        return TCSUM_ERR_MEM;
+    const tcsum_peso_t *hsegs = stage_descs ? reinterpret_cast<const tcsum_peso_t *>(c.q_desc.h) : segs;
+    uint16_t *hout = stage_out ? reinterpret_cast<uint16_t *>(c.q_res.h) : out;
+    // once a copy is queued, an error return first drains both streams: no
+    // copy may still read the caller's memory after the call returns
+    auto fail = [&](int code) {
+        (void)hipStreamSynchronize(ks);
+        (void)hipStreamSynchronize(cs);
+        return code;
+    };
+    // the first chunk's bytes start crossing the link while the host stages
+    // the descriptors
     if (copy_bytes(ch[0]) != hipSuccess)
-        return TCSUM_ERR_SYS;
-    const tcsum_peso_t *hsegs = segs;
-    if (!mapped_host(segs)) {
-        if (!c.q_desc.reserve(sizeof(tcsum_peso_t) * n))
-            return TCSUM_ERR_MEM;
+        return fail(TCSUM_ERR_SYS);
+    if (stage_descs)
         par_memcpy(c.q_desc.h, reinterpret_cast<const uint8_t *>(segs), sizeof(tcsum_peso_t) * n);
-        hsegs = reinterpret_cast<const tcsum_peso_t *>(c.q_desc.h);
-    }
-    uint16_t *hout = out;
-    if (!mapped_host(out)) {
-        if (!c.q_res.reserve(sizeof(uint16_t) * n + 64))
-            return TCSUM_ERR_MEM;
-        hout = reinterpret_cast<uint16_t *>(c.q_res.h);
-    }
     if (hipMemcpyAsync(c.d_descs, hsegs, sizeof(tcsum_peso_t) * n, hipMemcpyHostToDevice, cs) != hipSuccess)
-        return TCSUM_ERR_SYS;
+        return fail(TCSUM_ERR_SYS);
     for (size_t k = 0; k < ch.size(); ++k) {
         if (k && copy_bytes(ch[k]) != hipSuccess)
-            return TCSUM_ERR_SYS;
+            return fail(TCSUM_ERR_SYS);
         hipEvent_t ev = c.hev[k % kHostEvents];
         if (hipEventRecord(ev, cs) != hipSuccess || hipStreamWaitEvent(ks, ev, 0) != hipSuccess)
-            return TCSUM_ERR_SYS;
+            return fail(TCSUM_ERR_SYS);
         const uint32_t i0 = cut[k] * kSpanBlock;
         const uint32_t i1 = (uint32_t)std::min<uint64_t>(n, (uint64_t)cut[k + 1] * kSpanBlock);
         const hipError_t e = tcsum::launch_segments(tcsum::MODE_PESO,
                                                     tcsum::pick_geometry(mean_of(ch[k].bytes, i1 - i0)), dbase,
                                                     c.d_descs + i0, i1 - i0, c.d_out + i0, 0u, ks);
         if (e != hipSuccess)
-            return TCSUM_ERR_SYS;
+            return fail(TCSUM_ERR_SYS);
     }
-    if (hipMemcpyAsync(hout, c.d_out, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, ks) != hipSuccess ||
-        hipStreamSynchronize(ks) != hipSuccess || hipStreamSynchronize(cs) != hipSuccess)
+    if (hipMemcpyAsync(hout, c.d_out, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, ks) != hipSuccess)
+        return fail(TCSUM_ERR_SYS);
+    if (hipStreamSynchronize(ks) != hipSuccess || hipStreamSynchronize(cs) != hipSuccess)
         return TCSUM_ERR_SYS;
     if (hout != out)
         memcpy(out, hout, sizeof(uint16_t) * n);
@@ -1196,9 +1200,10 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
             i0 = i1;
         }
     }
-    if (e == hipSuccess)
-        e = hipStreamSynchronize(c.stream);
-    if (e != hipSuccess)
+    // on a failed launch the pieces already launched still read the arena
+    // (and the staging the next call reuses): drain them before returning
+    const hipError_t se = hipStreamSynchronize(c.stream);
+    if (e != hipSuccess || se != hipSuccess)
         return TCSUM_ERR_SYS;
     }
 results:

@@ -10,12 +10,12 @@ from .csum import (PESO_DTYPE, PKT_DTYPE, SEG_DTYPE, batch_ipv4, batch_ipv4_rx_v
                    pick_geometry, pktbuf_checksum16, plat_init, probe_read, queue_server, call_server, synth_fill,
                    synth_ipv4)
 from .pktbuf import IpAddr, PktBuf
-from . import workload
+from . import pcap, workload
 
 __all__ = [
     "checksum16", "checksum_peso", "pktbuf_checksum16", "batch_segments", "batch_peso", "batch_ipv4",
     "batch_ipv4_tx_fill", "batch_ipv4_tx_offload", "tx_apply_batch", "batch_ipv4_rx_verify",
     "host_batch_peso", "host_batch_peso_multi", "HostArena", "host_register", "host_unregister", "host_batch_ipv4", "host_batch_ipv4_tx_fill", "host_batch_ipv4_rx_verify",
     "synth_fill", "synth_ipv4", "descs_to_device", "device_count", "pick_geometry",
-    "plat_init", "probe_read", "queue_server", "call_server", "PktBuf", "IpAddr", "SEG_DTYPE", "PESO_DTYPE", "PKT_DTYPE", "workload",
+    "plat_init", "probe_read", "queue_server", "call_server", "PktBuf", "IpAddr", "SEG_DTYPE", "PESO_DTYPE", "PKT_DTYPE", "pcap", "workload",
 ]

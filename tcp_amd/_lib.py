@@ -19,6 +19,7 @@ ERR_SIZE = -5
 ERR_PARAM = -7
 ERR_NOT_SUPPORT = -11
 ERR_BROKEN = -13
+PCAP_ARP = 1  # tcsum_pcap_index l2 verdict: the frame goes to arp_in
 
 # (name, restype, argtypes) for every symbol include/*.h declares
 _V, _U16, _U32, _U64, _I, _SZ = (ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64,
@@ -38,6 +39,7 @@ SIGNATURES = {
     "tcsum_host_batch_ipv4": (_I, [_I, _V, _U64, _V, _U32, _V, _V]),
     "tcsum_host_batch_ipv4_tx_fill": (_I, [_I, _V, _U64, _V, _U32, _V, _V]),
     "tcsum_host_batch_ipv4_rx_verify": (_I, [_I, _V, _U64, _V, _U32, _V, _V, _V]),
+    "tcsum_pcap_index": (_I, [_V, _U64, _V, _V, _U32, ctypes.POINTER(_U32)]),
     "tcsum_queue_server": (_I, [_I, _I]),
     "tcsum_call_server": (_I, [_I, _I]),
     "tcsum_plat_init": (_I, [_I]),

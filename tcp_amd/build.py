@@ -19,7 +19,8 @@ INCLUDE = os.path.join(ROOT, "include")
 LIB = os.path.join(PKG, "libtcsum.so")
 ARCH = "gfx950"
 
-SOURCES = [os.path.join(CSRC, "csum_kernels.hip"), os.path.join(CSRC, "csum_api.cpp")]
+SOURCES = [os.path.join(CSRC, "csum_kernels.hip"), os.path.join(CSRC, "csum_api.cpp"),
+           os.path.join(CSRC, "pcap_index.cpp")]
 HEADERS = [os.path.join(CSRC, "csum_launch.h")] + [
     os.path.join(INCLUDE, h) for h in ("tcsum.h", "tcsum_legacy.h", "tcsum_synth.h")]
 
@@ -44,7 +45,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}",
-           "-x", "hip", SOURCES[0], "-x", "hip", SOURCES[1], "-o", tmp]
+           "-x", "hip", SOURCES[0], "-x", "hip", SOURCES[1], "-x", "hip", SOURCES[2], "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

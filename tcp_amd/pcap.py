@@ -1,0 +1,53 @@
+"""Capture files on the rx path: a libpcap savefile's bytes are the arena.
+
+`index` wraps tcsum_pcap_index (include/tcsum.h): one descriptor per record,
+pointing at the record's IPv4 packet inside the file, plus what the stack's
+rx front end does with the frame before ipv4_in (plat/netif_pcap.c:9-38,
+net/src/ether.c:14-25,62-101).  `rx_verify` then runs the batched rx gates
+(tcsum_host_batch_ipv4_rx_verify, the GPU path) over the file in place and
+merges the two verdicts per frame.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .csum import PKT_DTYPE, host_batch_ipv4_rx_verify
+
+
+def _as_u8(buf) -> np.ndarray:
+    a = np.frombuffer(buf, dtype=np.uint8) if not isinstance(buf, np.ndarray) else buf
+    assert a.dtype == np.uint8 and a.ndim == 1 and a.flags.c_contiguous
+    return a
+
+
+def index(buf):
+    """(pkts PKT_DTYPE[frames], l2_verdict int8[frames]) for a savefile in
+    memory (bytes, mmap, or a u8 numpy array); raises on a file that is not
+    one, or that ends inside a record."""
+    a = _as_u8(buf)
+    L = _lib.lib()
+    n = ctypes.c_uint32(0)
+    rc = L.tcsum_pcap_index(a.ctypes.data, a.nbytes, None, None, 0, ctypes.byref(n))
+    if rc not in (_lib.OK, _lib.ERR_MEM):
+        _lib.check(rc, "tcsum_pcap_index")
+    pkts = np.zeros(n.value, PKT_DTYPE)
+    l2 = np.zeros(n.value, np.int8)
+    got = ctypes.c_uint32(0)
+    _lib.check(L.tcsum_pcap_index(a.ctypes.data, a.nbytes, pkts.ctypes.data, l2.ctypes.data, n.value,
+                                  ctypes.byref(got)), "tcsum_pcap_index")
+    assert got.value == n.value
+    return pkts, l2
+
+
+def rx_verify(buf, device: int = 0):
+    """Per frame of the capture: (verdict int8, l2 int8, out u32, flags u8).
+    verdict is the rx front end's (l2) where the frame does not reach
+    ipv4_in, else the rx gates' net_err_t (tcsum_batch_ipv4_rx_verify)."""
+    a = _as_u8(buf)
+    pkts, l2 = index(a)
+    verdict, out, flags = host_batch_ipv4_rx_verify(a, pkts, device)
+    verdict = np.where(l2 == _lib.OK, verdict, l2).astype(np.int8)
+    return verdict, l2, out, flags

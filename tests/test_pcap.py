@@ -1,0 +1,148 @@
+"""Capture files on the rx path (tcsum_pcap_index, tcp_amd.pcap).
+
+CPU: the index over savefiles written by tests/pcap_build.py (every link
+type, byte order and timestamp unit; FCS; truncated records and files) against
+the offsets the writer recorded, and the rx front end's per-frame decision
+(plat/netif_pcap.c:9-38, net/src/ether.c:14-25,62-101).
+GPU: the reference's own rx fixtures (tests/golden/ipv4_rx_*.bin, verdicts
+from the compiled reference stack) wrapped into captures and verified in
+place through tcsum_host_batch_ipv4_rx_verify.
+"""
+import numpy as np
+import pytest
+
+import golden_io as G
+import pcap_build as PB
+
+OK, SIZE, NOT_SUPPORT, PARAM, MEM, ARP = 0, -5, -11, -7, -2, 1
+
+
+def golden_frames():
+    cases, pool = G.ipv4_rx_cases()
+    frames = [pool[o: o + n].tobytes() for o, n in zip(cases["pool_off"], cases["frame_len"])]
+    return cases, frames
+
+
+@pytest.fixture(scope="module")
+def pcap():
+    from tcp_amd import pcap
+    return pcap
+
+
+@pytest.mark.parametrize("big_endian", [False, True])
+@pytest.mark.parametrize("nanosecond", [False, True])
+@pytest.mark.parametrize("link", [PB.ETHER, PB.RAW, PB.IPV4, PB.NULL, PB.SLL])
+def test_index_offsets(pcap, link, big_endian, nanosecond):
+    cases, frames = golden_frames()
+    frames = [f for f in frames if len(f) <= 1500]  # ether's is_pkt_ok bound for every link type here
+    buf, offs, lens = PB.build(frames, link, big_endian, nanosecond)
+    pkts, l2 = pcap.index(buf)
+    assert pkts.size == len(frames)
+    ipv4 = np.ones(len(frames), bool)  # raw links: every frame goes to ipv4_in, whose gates judge it
+    np.testing.assert_array_equal(l2[ipv4], OK)
+    np.testing.assert_array_equal(l2[~ipv4], NOT_SUPPORT)
+    np.testing.assert_array_equal(pkts["offset"][ipv4], offs[ipv4])
+    np.testing.assert_array_equal(pkts["len"][ipv4], lens[ipv4])
+    assert (pkts["len"][~ipv4] == 0).all()
+    for i in np.flatnonzero(ipv4)[:50]:  # the descriptor addresses the frame's own bytes
+        o, n = int(pkts["offset"][i]), int(pkts["len"][i])
+        assert buf[o: o + n] == frames[i]
+
+
+def test_ether_front_end_decisions(pcap):
+    """ether_in: is_pkt_ok size bounds (14..1514), ARP to arp_in, other types
+    NOT_SUPPORT (ether.c:14-25,75-97); an FCS the file declares is not L3."""
+    body = bytes(range(40))
+    frames = [body, body, body, b"", bytes(1500), bytes(1501), body]
+    types = [0x0800, 0x0806, 0x86DD, 0x0800, 0x0800, 0x0800, 0x8100]
+    buf, offs, lens = PB.build(frames, PB.ETHER, ethertypes=types, fcs_len=4)
+    pkts, l2 = pcap.index(buf)
+    np.testing.assert_array_equal(l2, [OK, ARP, NOT_SUPPORT, OK, OK, SIZE, NOT_SUPPORT])
+    np.testing.assert_array_equal(pkts["len"], [40, 0, 0, 0, 1500, 0, 0])
+    assert pkts["offset"][0] == offs[0] and pkts["offset"][4] == offs[4]
+    # a record shorter than an Ethernet header
+    buf, _, _ = PB.build([b""], PB.ETHER, caplen_cut=[10])
+    _, l2 = pcap.index(buf)
+    np.testing.assert_array_equal(l2, [SIZE])
+
+
+def test_truncated_records_are_the_captured_bytes(pcap):
+    body = bytes(range(200))
+    buf, offs, lens = PB.build([body, body], PB.ETHER, caplen_cut=[14 + 60, None])
+    pkts, l2 = pcap.index(buf)
+    np.testing.assert_array_equal(pkts["len"], [60, 200])
+    np.testing.assert_array_equal(l2, [OK, OK])
+
+
+def test_file_level_errors(pcap):
+    import ctypes
+    from tcp_amd import _lib
+    L = _lib.lib()
+    body = bytes(range(64))
+    buf, offs, _ = PB.build([body] * 5, PB.ETHER)
+    n = ctypes.c_uint32(0)
+    # count only
+    assert L.tcsum_pcap_index(buf, len(buf), None, None, 0, ctypes.byref(n)) == MEM and n.value == 5
+    # too small an output: the first max_frames are indexed
+    from tcp_amd import PKT_DTYPE
+    pk = np.zeros(3, PKT_DTYPE)
+    assert L.tcsum_pcap_index(buf, len(buf), pk.ctypes.data, None, 3, ctypes.byref(n)) == MEM
+    assert n.value == 5 and (pk["offset"] == offs[:3]).all()
+    # the file ends inside the last record / inside a record header
+    for cut in (len(buf) - 10, len(buf) - (14 + 64) - 8):
+        pk = np.zeros(5, pk.dtype)
+        assert L.tcsum_pcap_index(buf[:cut], cut, pk.ctypes.data, None, 5, ctypes.byref(n)) == SIZE
+        assert n.value == 4 and (pk["offset"][:4] == offs[:4]).all()
+    # empty capture (header only)
+    assert L.tcsum_pcap_index(buf[:24], 24, pk.ctypes.data, None, 5, ctypes.byref(n)) == OK and n.value == 0
+    # not a savefile / too short / pcapng / unsupported link type
+    assert L.tcsum_pcap_index(b"\0" * 64, 64, pk.ctypes.data, None, 5, ctypes.byref(n)) == PARAM
+    assert L.tcsum_pcap_index(buf, 20, pk.ctypes.data, None, 5, ctypes.byref(n)) == PARAM
+    assert L.tcsum_pcap_index(bytes.fromhex("0a0d0d0a") + buf[4:], len(buf), pk.ctypes.data, None, 5,
+                              ctypes.byref(n)) == PARAM
+    other = bytearray(buf)
+    other[20:24] = (105).to_bytes(4, "little")  # IEEE 802.11
+    assert L.tcsum_pcap_index(bytes(other), len(other), pk.ctypes.data, None, 5, ctypes.byref(n)) == NOT_SUPPORT
+    assert L.tcsum_pcap_index(None, 0, None, None, 0, ctypes.byref(n)) == PARAM
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("link", [PB.RAW, PB.ETHER, PB.SLL])
+def test_capture_rx_verify_golden(pcap, link):
+    """The reference's rx verdicts, from a capture file verified in place:
+    frames ether's is_pkt_ok rejects (> 1500 B of L3) get NET_ERR_SIZE
+    before ipv4_in; every other frame the fixture's verdict, bit for bit."""
+    cases, frames = golden_frames()
+    buf, _, _ = PB.build(frames, link)
+    verdict, l2, out, flags = pcap.rx_verify(np.frombuffer(buf, np.uint8))
+    want = cases["verdict"].astype(np.int8)
+    if link == PB.ETHER:
+        want = np.where(cases["frame_len"] > 1500, SIZE, want).astype(np.int8)
+    np.testing.assert_array_equal(verdict, want)
+    reached = l2 == OK
+    np.testing.assert_array_equal(flags[reached], cases["flags"][reached])
+
+
+@pytest.mark.gpu
+def test_capture_rx_verify_mixed_vs_oracle(pcap, oracle):
+    """A 20,000-frame capture of configs[3]-style packets (tx-filled, then a
+    few corrupted): verdicts equal the oracle's on the same L3 bytes."""
+    from tcp_amd import workload
+    b = workload.make_batch("mixed", n=20000)
+    host = oracle.synth_fill(b.byte_base, b.alloc_bytes, b.seed)
+    arena = np.array(host)
+    oracle.batch_ipv4_tx_fill(arena, b.descs)
+    rng = np.random.default_rng(11)
+    frames = [arena[o: o + n].tobytes() for o, n in zip(b.descs["offset"], b.descs["len"])]
+    for i in rng.choice(len(frames), 300, replace=False):
+        f = bytearray(frames[i])
+        f[rng.integers(0, len(f))] ^= 0x5A
+        frames[i] = bytes(f)
+    buf, offs, lens = PB.build(frames, PB.RAW, big_endian=True)
+    verdict, l2, out, flags = pcap.rx_verify(np.frombuffer(buf, np.uint8))
+    from tcp_amd import PKT_DTYPE
+    pk = np.zeros(len(frames), PKT_DTYPE)
+    pk["offset"], pk["len"] = offs, lens
+    ev, ef = oracle.batch_ipv4_rx_verify(np.frombuffer(buf, np.uint8), pk, nthreads=8)
+    np.testing.assert_array_equal(verdict, ev)
+    assert (verdict == -13).sum() > 200  # the corruptions are seen

@@ -106,6 +106,46 @@ def test_file_level_errors(pcap):
     assert L.tcsum_pcap_index(None, 0, None, None, 0, ctypes.byref(n)) == PARAM
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_parallel_walk_equals_sequential(pcap, monkeypatch, seed):
+    """Large files are walked in pieces that find their own record boundary:
+    with 1-4 KiB pieces (as many walkers as the host has, up to 16) the index
+    equals the one-piece walk, also when payloads are full of fake record
+    headers and when the file ends inside a record."""
+    rng = np.random.default_rng(seed)
+    n = 3000
+    lens = rng.integers(0, 600, n)
+    frames = []
+    for i, L in enumerate(lens):
+        f = bytearray(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        if seed % 2 and L >= 32:  # plant chains of plausible record headers in the payload
+            for k in range(0, L - 16, 16):
+                f[k: k + 16] = np.array([i, 7, (L - k) % 33, 40], "<u4").tobytes()
+        frames.append(bytes(f))
+    buf, offs, lens_exp = PB.build(frames, [PB.ETHER, PB.RAW, PB.NULL, PB.SLL][seed], big_endian=seed == 2)
+    one = pcap.index(buf)
+    np.testing.assert_array_equal(one[0]["offset"][one[1] == OK], offs[one[1] == OK])
+    for kb in ("1", "2", "4"):
+        monkeypatch.setenv("TCSUM_PCAP_PIECE_KB", kb)
+        many = pcap.index(buf)
+        np.testing.assert_array_equal(many[0], one[0])
+        np.testing.assert_array_equal(many[1], one[1])
+    # the file ends inside a record: the whole records before it, SIZE
+    import ctypes
+    from tcp_amd import _lib, PKT_DTYPE
+    cut = int(offs[n // 2]) + 3
+    for kb in (None, "1"):
+        if kb:
+            monkeypatch.setenv("TCSUM_PCAP_PIECE_KB", kb)
+        else:
+            monkeypatch.delenv("TCSUM_PCAP_PIECE_KB", raising=False)
+        pk = np.zeros(n, PKT_DTYPE)
+        got = ctypes.c_uint32(0)
+        rc = _lib.lib().tcsum_pcap_index(buf[:cut], cut, pk.ctypes.data, None, n, ctypes.byref(got))
+        assert rc == SIZE and got.value == n // 2
+        np.testing.assert_array_equal(pk[: n // 2], one[0][: n // 2])
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("link", [PB.RAW, PB.ETHER, PB.SLL])
 def test_capture_rx_verify_golden(pcap, link):
@@ -128,10 +168,9 @@ def test_capture_rx_verify_mixed_vs_oracle(pcap, oracle):
     """A 20,000-frame capture of configs[3]-style packets (tx-filled, then a
     few corrupted): verdicts equal the oracle's on the same L3 bytes."""
     from tcp_amd import workload
-    b = workload.make_batch("mixed", n=20000)
-    host = oracle.synth_fill(b.byte_base, b.alloc_bytes, b.seed)
-    arena = np.array(host)
-    oracle.batch_ipv4_tx_fill(arena, b.descs)
+    b = workload.make_batch("mixed_rx", n=20000)
+    dev, _ = workload.materialize(b)  # IPv4 packets generated in HBM, tx-filled like a sender
+    arena = dev.cpu().numpy()
     rng = np.random.default_rng(11)
     frames = [arena[o: o + n].tobytes() for o, n in zip(b.descs["offset"], b.descs["len"])]
     for i in rng.choice(len(frames), 300, replace=False):

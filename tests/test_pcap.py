@@ -185,3 +185,25 @@ def test_capture_rx_verify_mixed_vs_oracle(pcap, oracle):
     ev, ef = oracle.batch_ipv4_rx_verify(np.frombuffer(buf, np.uint8), pk, nthreads=8)
     np.testing.assert_array_equal(verdict, ev)
     assert (verdict == -13).sum() > 200  # the corruptions are seen
+
+
+@pytest.mark.gpu
+def test_c_pcap_verify(tmp_path):
+    """tests/c/pcap_verify.c (INTEGRATION.md §4b in plain C) on a capture of
+    the reference's rx fixtures: the per-frame verdicts it writes are the
+    fixture's (Ethernet: frames over 1514 B get ether's NET_ERR_SIZE)."""
+    import os
+    import subprocess
+    cases, frames = golden_frames()
+    buf, _, _ = PB.build(frames, PB.ETHER)
+    cap, res = tmp_path / "rx.pcap", tmp_path / "verdicts.bin"
+    cap.write_bytes(buf)
+    here = os.path.dirname(os.path.abspath(__file__))
+    exe = os.path.join(here, "c", "build", "pcap_verify")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(here, "c")], check=True)
+    r = subprocess.run([exe, str(cap), str(res)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    want = np.where(cases["frame_len"] > 1500, SIZE, cases["verdict"]).astype(np.int8)
+    np.testing.assert_array_equal(np.fromfile(res, np.int8), want)
+    assert r.stdout.startswith(f"{len(frames)} frames:")

@@ -55,7 +55,7 @@ for _ in range(5):
     t.append(time.perf_counter() - t0)
 assert (pk["offset"] == descs["offset"]).all() and (pk["len"] == descs["len"]).all() and (l2 == 0).all()
 ti = float(np.median(t))
-print(f"tcsum_pcap_index (host, <= 16 walkers) {ti * 1e3:8.2f} ms   {n / ti / 1e6:7.1f} Mframes/s", flush=True)
+print(f"tcsum_pcap_index (16 thr x 4 chains) {ti * 1e3:8.2f} ms   {n / ti / 1e6:7.1f} Mframes/s", flush=True)
 
 v, _, _, _ = pcap.rx_verify(buf)  # warm (staging, contexts)
 t = []

@@ -30,7 +30,8 @@ constexpr uint32_t kEtherHdr = 14;   // ether_hdr_t (ether.h:20-25)
 constexpr uint32_t kEtherMtu = 1500; // ETHER_MTU (ether.h:14)
 constexpr uint32_t kMaxCap = 262144;  // libpcap's largest snapshot length
 constexpr int kSyncRun = 8;           // consecutive plausible headers that make a sync point
-constexpr uint64_t kPieceMin = 64ull << 20; // bytes per walker, at least
+constexpr uint64_t kPieceMin = 16ull << 20; // bytes per piece, at least
+constexpr unsigned kChains = 4;             // pieces one walker thread interleaves
 
 inline uint32_t rd32(const uint8_t *p, bool swap)
 {
@@ -121,8 +122,9 @@ extern "C" int tcsum_pcap_index(const void *file, uint64_t file_bytes, tcsum_pkt
 
     // The records form a chain (each header gives the next one's position),
     // and walking it is one dependent cache + TLB miss per frame (~0.45 us
-    // over a multi-GiB file).  Large files are cut into K pieces; the walker
-    // of piece t > 0 first finds a record boundary at or after the piece's
+    // over a multi-GiB file).  Large files are cut into K pieces, kChains of
+    // them per walker thread, interleaved; the walker of piece t > 0 first
+    // finds a record boundary at or after the piece's
     // start by looking for kSyncRun consecutive plausible headers, then walks
     // to the piece's end.  The stitch below accepts a piece only if its sync
     // point is exactly where the exact walk of the pieces before it ended, and
@@ -134,28 +136,55 @@ extern "C" int tcsum_pcap_index(const void *file, uint64_t file_bytes, tcsum_pkt
         int rc = TCSUM_OK;
         bool synced = false;
     };
-    auto walk = [&](Piece &pc, uint64_t pos, uint64_t stop) {
-        pc.begin = pos;
-        pc.pk.clear();
-        pc.v.clear();
-        pc.rc = TCSUM_OK;
-        while (pos < stop && pos < file_bytes) {
-            if (file_bytes - pos < kRecHdr) {
-                pc.rc = TCSUM_ERR_SIZE; // a partial record header at the end
-                break;
-            }
-            const uint32_t caplen = rd32(f + pos + 8, swap);
-            const uint64_t data = pos + kRecHdr;
-            if (caplen > file_bytes - data) {
-                pc.rc = TCSUM_ERR_SIZE; // the last record's bytes are cut short
-                break;
-            }
-            tcsum_pkt_t d;
-            pc.v.push_back(classify(data, caplen, d));
-            pc.pk.push_back(d);
-            pos = data + caplen;
+    // Walk pieces [a, b) to their ends with their chains interleaved, one
+    // record of each per round: the misses of different chains overlap.
+    auto walk = [&](Piece *pcs, const uint64_t *start, const uint64_t *stop, unsigned a, unsigned b) {
+        uint64_t pos[kChains];
+        bool live[kChains];
+        unsigned left = 0;
+        for (unsigned j = a; j < b; ++j) {
+            Piece &pc = pcs[j];
+            pc.begin = pos[j - a] = start[j];
+            pc.pk.clear();
+            pc.v.clear();
+            pc.rc = TCSUM_OK;
+            live[j - a] = pc.synced;
+            left += pc.synced;
+            if (!pc.synced)
+                pc.end = pc.begin;
         }
-        pc.end = pos;
+        while (left) {
+            for (unsigned j = a; j < b; ++j) {
+                if (!live[j - a])
+                    continue;
+                Piece &pc = pcs[j];
+                uint64_t &q = pos[j - a];
+                bool done = q >= stop[j] || q >= file_bytes;
+                if (!done && file_bytes - q < kRecHdr) {
+                    pc.rc = TCSUM_ERR_SIZE; // a partial record header at the end
+                    done = true;
+                }
+                if (!done) {
+                    const uint32_t caplen = rd32(f + q + 8, swap);
+                    const uint64_t data = q + kRecHdr;
+                    if (caplen > file_bytes - data) {
+                        pc.rc = TCSUM_ERR_SIZE; // the last record's bytes are cut short
+                        done = true;
+                    } else {
+                        tcsum_pkt_t d;
+                        pc.v.push_back(classify(data, caplen, d));
+                        pc.pk.push_back(d);
+                        q = data + caplen;
+                        __builtin_prefetch(f + std::min(q + 8, file_bytes - 1));
+                    }
+                }
+                if (done) {
+                    pc.end = q;
+                    live[j - a] = false;
+                    --left;
+                }
+            }
+        }
     };
     const uint32_t frac_max = ns ? 1000000000u : 1000000u;
     auto plausible = [&](uint64_t pos) {
@@ -163,7 +192,9 @@ extern "C" int tcsum_pcap_index(const void *file, uint64_t file_bytes, tcsum_pkt
             return false;
         const uint32_t frac = rd32(f + pos + 4, swap), cap = rd32(f + pos + 8, swap),
                        orig = rd32(f + pos + 12, swap);
-        return frac < frac_max && cap <= kMaxCap && orig >= cap && orig <= kMaxCap &&
+        // cap >= 1: runs of zero bytes (padding, zeroed payloads) would
+        // otherwise read as chains of empty records
+        return frac < frac_max && cap >= 1 && cap <= kMaxCap && orig >= cap && orig <= kMaxCap &&
                cap <= file_bytes - pos - kRecHdr;
     };
     auto sync = [&](uint64_t from, uint64_t limit, uint64_t &at) {
@@ -187,22 +218,23 @@ extern "C" int tcsum_pcap_index(const void *file, uint64_t file_bytes, tcsum_pkt
     if (const char *e = getenv("TCSUM_PCAP_PIECE_KB"))
         piece_min = std::max<uint64_t>(1, strtoull(e, nullptr, 10)) << 10;
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const unsigned K = (unsigned)std::min<uint64_t>(std::min(16u, hw), std::max<uint64_t>(1, body / piece_min));
-    std::vector<uint64_t> cut(K + 1);
+    const unsigned T0 = std::min(16u, hw);
+    const unsigned K = (unsigned)std::min<uint64_t>(T0 * kChains, std::max<uint64_t>(1, body / piece_min));
+    const unsigned T = (K + kChains - 1) / kChains; // walker threads, kChains pieces each
+    std::vector<uint64_t> cut(K + 1), start(K, kFileHdr);
     for (unsigned t = 0; t <= K; ++t)
         cut[t] = kFileHdr + body * t / K;
     std::vector<Piece> pcs(K);
     {
         std::vector<std::thread> th;
-        for (unsigned t = 0; t < K; ++t) {
+        for (unsigned t = 0; t < T; ++t) {
             auto job = [&, t] {
-                Piece &pc = pcs[t];
-                uint64_t at = kFileHdr;
-                pc.synced = t == 0 || sync(cut[t], cut[t + 1], at);
-                if (pc.synced)
-                    walk(pc, at, cut[t + 1]);
+                const unsigned a = t * kChains, b = std::min(K, a + kChains);
+                for (unsigned j = a; j < b; ++j)
+                    pcs[j].synced = j == 0 || sync(cut[j], cut[j + 1], start[j]);
+                walk(pcs.data(), start.data(), cut.data() + 1, a, b);
             };
-            if (t + 1 < K)
+            if (t + 1 < T)
                 th.emplace_back(job);
             else
                 job();
@@ -216,8 +248,11 @@ extern "C" int tcsum_pcap_index(const void *file, uint64_t file_bytes, tcsum_pkt
     int rc = pcs[0].rc;
     for (unsigned t = 1; t < K && rc == TCSUM_OK; ++t) {
         Piece &pc = pcs[t];
-        if (!(pc.synced && pc.begin == pos))
-            walk(pc, pos, cut[t + 1]); // a false or missing sync point: walk it exactly
+        if (!(pc.synced && pc.begin == pos)) { // a false or missing sync point: walk it exactly
+            pc.synced = true;
+            start[t] = pos;
+            walk(pcs.data(), start.data(), cut.data() + 1, t, t + 1);
+        }
         pos = pc.end;
         rc = pc.rc;
     }

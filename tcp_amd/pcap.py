@@ -5,7 +5,8 @@ pointing at the record's IPv4 packet inside the file, plus what the stack's
 rx front end does with the frame before ipv4_in (plat/netif_pcap.c:9-38,
 net/src/ether.c:14-25,62-101).  `rx_verify` then runs the batched rx gates
 (tcsum_host_batch_ipv4_rx_verify, the GPU path) over the file in place and
-merges the two verdicts per frame.
+merges the two verdicts per frame; `tx_fill` fills a capture's checksums in
+place by the stack's tx rules.
 """
 from __future__ import annotations
 
@@ -14,7 +15,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from .csum import PKT_DTYPE, host_batch_ipv4_rx_verify
+from .csum import PKT_DTYPE, host_batch_ipv4_rx_verify, host_batch_ipv4_tx_fill
 
 
 def _as_u8(buf) -> np.ndarray:
@@ -51,3 +52,16 @@ def rx_verify(buf, device: int = 0):
     verdict, out, flags = host_batch_ipv4_rx_verify(a, pkts, device)
     verdict = np.where(l2 == _lib.OK, verdict, l2).astype(np.int8)
     return verdict, l2, out, flags
+
+
+def tx_fill(buf, device: int = 0):
+    """Fill the IPv4 header and L4 checksums of every frame of a capture that
+    reaches ipv4_in, in place, by the stack's tx rules (ipv4.c:643,656,
+    tcp_out.c:19-20, udp.c:320-321, icmpv4.c:45-58): a capture's checksums
+    fixed the way the stack would have sent them.  Frames the front end does
+    not hand to ipv4_in are left alone.  Returns (l2 int8, flags u8)."""
+    a = _as_u8(buf)
+    assert a.flags.writeable, "tx_fill writes the capture in place"
+    pkts, l2 = index(a)
+    flags = host_batch_ipv4_tx_fill(a, pkts, device)
+    return l2, flags

@@ -207,3 +207,26 @@ def test_c_pcap_verify(tmp_path):
     want = np.where(cases["frame_len"] > 1500, SIZE, cases["verdict"]).astype(np.int8)
     np.testing.assert_array_equal(np.fromfile(res, np.int8), want)
     assert r.stdout.startswith(f"{len(frames)} frames:")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("link", [PB.RAW, PB.ETHER])
+def test_capture_tx_fill_golden(pcap, link):
+    """A capture of the reference's tx fixture packets (tests/golden/ipv4_tx_*):
+    filled in place, every frame that reaches ipv4_in holds exactly the bytes
+    the reference's tx path produced; the others (Ethernet frames over 1514 B)
+    and every record header are untouched."""
+    cases, pin, pout = G.ipv4_tx_cases()
+    before = [pin[o: o + n].tobytes() for o, n in zip(cases["pool_off"], cases["frame_len"])]
+    after = [pout[o: o + n].tobytes() for o, n in zip(cases["pool_off"], cases["frame_len"])]
+    buf, offs, lens = PB.build(before, link)
+    a = np.frombuffer(bytearray(buf), np.uint8)
+    l2, flags = pcap.tx_fill(a)
+    filled = l2 == OK
+    if link == PB.RAW:
+        assert filled.all()
+    else:
+        np.testing.assert_array_equal(filled, cases["frame_len"] <= 1500)
+    np.testing.assert_array_equal(flags[filled], cases["flags"][filled])
+    want, _, _ = PB.build([after[i] if filled[i] else before[i] for i in range(len(before))], link)
+    assert a.tobytes() == want

@@ -226,6 +226,24 @@ int tcsum_host_batch_ipv4_rx_verify(int device, const void *host_arena, uint64_t
 int tcsum_pcap_index(const void *file /*[host]*/, uint64_t file_bytes, tcsum_pkt_t *pkts /*[host]*/,
                      int8_t *l2_verdict /*[host] or NULL*/, uint32_t max_frames, uint32_t *n_frames);
 
+/* The three host-queue batches over several GPUs of this node: contiguous
+ * shards balanced by bytes, one per entry of devices[] (a device may repeat;
+ * its shards then run one after the other), each an ordinary host batch on
+ * its device -- pinned frames (tcsum_host_alloc is portable: every GPU maps
+ * it) read and, tx, written in place over that GPU's own host link.  Same
+ * results, in packet order, as the one-device calls.  For the tx fill, packets
+ * of different shards must not overlap. */
+int tcsum_host_batch_ipv4_multi(const int *devices, int ndev, const void *host_arena, uint64_t arena_bytes,
+                                const tcsum_pkt_t *pkts /*[host]*/, uint32_t n, uint32_t *out /*[host]*/,
+                                uint8_t *flags /*[host] or NULL*/);
+int tcsum_host_batch_ipv4_tx_fill_multi(const int *devices, int ndev, void *host_arena, uint64_t arena_bytes,
+                                        const tcsum_pkt_t *pkts /*[host]*/, uint32_t n,
+                                        uint32_t *out /*[host] or NULL*/, uint8_t *flags /*[host] or NULL*/);
+int tcsum_host_batch_ipv4_rx_verify_multi(const int *devices, int ndev, const void *host_arena,
+                                          uint64_t arena_bytes, const tcsum_pkt_t *pkts /*[host]*/, uint32_t n,
+                                          int8_t *verdict /*[host]*/, uint32_t *out /*[host] or NULL*/,
+                                          uint8_t *flags /*[host] or NULL*/);
+
 /* Queue server for small host-queue batches (the stack's <= 50-frame netif
  * queues, NETIF_INQ_SIZE net_cfg.h:39): with enable != 0, the
  * tcsum_host_batch_ipv4* calls on `device` with n <= $TCSUM_SERVER_MAX

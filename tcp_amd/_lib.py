@@ -39,6 +39,9 @@ SIGNATURES = {
     "tcsum_host_batch_ipv4": (_I, [_I, _V, _U64, _V, _U32, _V, _V]),
     "tcsum_host_batch_ipv4_tx_fill": (_I, [_I, _V, _U64, _V, _U32, _V, _V]),
     "tcsum_host_batch_ipv4_rx_verify": (_I, [_I, _V, _U64, _V, _U32, _V, _V, _V]),
+    "tcsum_host_batch_ipv4_multi": (_I, [_V, _I, _V, _U64, _V, _U32, _V, _V]),
+    "tcsum_host_batch_ipv4_tx_fill_multi": (_I, [_V, _I, _V, _U64, _V, _U32, _V, _V]),
+    "tcsum_host_batch_ipv4_rx_verify_multi": (_I, [_V, _I, _V, _U64, _V, _U32, _V, _V, _V]),
     "tcsum_pcap_index": (_I, [_V, _U64, _V, _V, _U32, ctypes.POINTER(_U32)]),
     "tcsum_queue_server": (_I, [_I, _I]),
     "tcsum_call_server": (_I, [_I, _I]),

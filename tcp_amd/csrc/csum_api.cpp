@@ -693,6 +693,29 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     return TCSUM_OK;
 }
 
+extern "C++" {
+// Contiguous shards of a descriptor array balanced by bytes:
+// shard d is [cut[d], cut[d+1]).
+template <class D>
+std::vector<uint32_t> byte_shards(const D *descs, uint32_t n, int ndev)
+{
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        total += descs[i].len;
+    std::vector<uint32_t> cut((size_t)ndev + 1, n);
+    cut[0] = 0;
+    uint64_t acc = 0;
+    int k = 1;
+    for (uint32_t i = 0; i < n && k < ndev; ++i) {
+        acc += descs[i].len;
+        while (k < ndev && acc * (uint64_t)ndev >= total * (uint64_t)k) // shard k starts after byte quantile k
+            cut[k++] = i + 1;
+    }
+    return cut;
+}
+
+}
+
 // One host batch over several GPUs: contiguous shards balanced by bytes
 // (SURVEY §8(e)), one host thread per device, each shard through its own
 // device's host link and HBM; no collective.
@@ -708,18 +731,7 @@ int tcsum_host_batch_peso_multi(const int *devices, int ndev, const void *host_a
             return TCSUM_ERR_PARAM;
     if (ndev == 1)
         return tcsum_host_batch_peso(devices[0], host_arena, arena_bytes, segs, n, out);
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < n; ++i)
-        total += segs[i].len;
-    std::vector<uint32_t> cut((size_t)ndev + 1, n);
-    cut[0] = 0;
-    uint64_t acc = 0;
-    int k = 1;
-    for (uint32_t i = 0; i < n && k < ndev; ++i) {
-        acc += segs[i].len;
-        while (k < ndev && acc * (uint64_t)ndev >= total * (uint64_t)k) // shard k starts after byte quantile k
-            cut[k++] = i + 1;
-    }
+    const std::vector<uint32_t> cut = byte_shards(segs, n, ndev);
     std::vector<int> rc((size_t)ndev, TCSUM_OK);
     std::vector<std::thread> th;
     for (int d = 0; d < ndev; ++d)
@@ -1252,6 +1264,67 @@ int tcsum_host_batch_ipv4_rx_verify(int device, const void *host_arena, uint64_t
     // the kernel never writes the arena in this mode
     return host_ipv4(2, device, const_cast<uint8_t *>(static_cast<const uint8_t *>(host_arena)), arena_bytes,
                      pkts, n, verdict, out, flags);
+}
+
+// The host-queue batches over several GPUs (tcsum_host_batch_peso_multi's
+// split): each shard is an ordinary host batch on its device -- pinned
+// frames read (and, tx, written) in place over that GPU's own host link,
+// pageable ones staged by that device's context.
+static int host_ipv4_multi(int ip_mode, const int *devices, int ndev, uint8_t *host_arena, uint64_t arena_bytes,
+                           const tcsum_pkt_t *pkts, uint32_t n, int8_t *verdict, uint32_t *out, uint8_t *flags)
+{
+    if (n == 0)
+        return TCSUM_OK;
+    if (!devices || ndev <= 0 || ndev > kMaxDev || !host_arena || !pkts)
+        return TCSUM_ERR_PARAM;
+    for (int d = 0; d < ndev; ++d)
+        if (devices[d] < 0 || devices[d] >= kMaxDev)
+            return TCSUM_ERR_PARAM;
+    if (ndev == 1)
+        return host_ipv4(ip_mode, devices[0], host_arena, arena_bytes, pkts, n, verdict, out, flags);
+    const std::vector<uint32_t> cut = byte_shards(pkts, n, ndev);
+    std::vector<int> rc((size_t)ndev, TCSUM_OK);
+    std::vector<std::thread> th;
+    for (int d = 0; d < ndev; ++d)
+        if (cut[d + 1] > cut[d])
+            th.emplace_back([&, d] {
+                const uint32_t i0 = cut[d];
+                rc[d] = host_ipv4(ip_mode, devices[d], host_arena, arena_bytes, pkts + i0, cut[d + 1] - i0,
+                                  verdict ? verdict + i0 : nullptr, out ? out + i0 : nullptr,
+                                  flags ? flags + i0 : nullptr);
+            });
+    for (auto &t : th)
+        t.join();
+    for (int r : rc)
+        if (r != TCSUM_OK)
+            return r;
+    return TCSUM_OK;
+}
+
+int tcsum_host_batch_ipv4_multi(const int *devices, int ndev, const void *host_arena, uint64_t arena_bytes,
+                                const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out, uint8_t *flags)
+{
+    if (n && !out)
+        return TCSUM_ERR_PARAM;
+    return host_ipv4_multi(0, devices, ndev, const_cast<uint8_t *>(static_cast<const uint8_t *>(host_arena)),
+                           arena_bytes, pkts, n, nullptr, out, flags);
+}
+
+int tcsum_host_batch_ipv4_tx_fill_multi(const int *devices, int ndev, void *host_arena, uint64_t arena_bytes,
+                                        const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out, uint8_t *flags)
+{
+    return host_ipv4_multi(1, devices, ndev, static_cast<uint8_t *>(host_arena), arena_bytes, pkts, n, nullptr, out,
+                           flags);
+}
+
+int tcsum_host_batch_ipv4_rx_verify_multi(const int *devices, int ndev, const void *host_arena,
+                                          uint64_t arena_bytes, const tcsum_pkt_t *pkts, uint32_t n,
+                                          int8_t *verdict, uint32_t *out, uint8_t *flags)
+{
+    if (n && !verdict)
+        return TCSUM_ERR_PARAM;
+    return host_ipv4_multi(2, devices, ndev, const_cast<uint8_t *>(static_cast<const uint8_t *>(host_arena)),
+                           arena_bytes, pkts, n, verdict, out, flags);
 }
 
 int tcsum_queue_server(int device, int enable)

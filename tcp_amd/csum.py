@@ -201,26 +201,46 @@ def _host_arena_args(host_arena):
     return arr.ctypes.data, arr.nbytes
 
 
-def host_batch_ipv4(host_arena, pkts: np.ndarray, device: int = 0):
-    """(out u32 = ip | l4 << 16, flags) for packets in host memory (tcsum_host_batch_ipv4)."""
+def _devices(devices):
+    d = np.ascontiguousarray(np.asarray(list(devices), dtype=np.int32))
+    return d.ctypes.data, d.size, d
+
+
+def host_batch_ipv4(host_arena, pkts: np.ndarray, device: int = 0, devices=None):
+    """(out u32 = ip | l4 << 16, flags) for packets in host memory
+    (tcsum_host_batch_ipv4; with `devices`, sharded by bytes over those GPUs:
+    tcsum_host_batch_ipv4_multi)."""
     assert pkts.dtype == PKT_DTYPE
     pkts = np.ascontiguousarray(pkts)
     out = np.zeros(pkts.size, np.uint32)
     flags = np.zeros(pkts.size, np.uint8)
     p, nb = _host_arena_args(host_arena)
-    _lib.check(_lib.lib().tcsum_host_batch_ipv4(device, p, nb, pkts.ctypes.data, pkts.size, out.ctypes.data,
-                                                flags.ctypes.data), "tcsum_host_batch_ipv4")
+    if devices is None:
+        rc = _lib.lib().tcsum_host_batch_ipv4(device, p, nb, pkts.ctypes.data, pkts.size, out.ctypes.data,
+                                              flags.ctypes.data)
+    else:
+        dp, nd, _keep = _devices(devices)
+        rc = _lib.lib().tcsum_host_batch_ipv4_multi(dp, nd, p, nb, pkts.ctypes.data, pkts.size, out.ctypes.data,
+                                                    flags.ctypes.data)
+    _lib.check(rc, "tcsum_host_batch_ipv4")
     return out, flags
 
 
-def host_batch_ipv4_tx_fill(host_arena, pkts: np.ndarray, device: int = 0):
-    """Fill the checksum fields of packets in host memory in place; returns flags."""
+def host_batch_ipv4_tx_fill(host_arena, pkts: np.ndarray, device: int = 0, devices=None):
+    """Fill the checksum fields of packets in host memory in place; returns
+    flags (with `devices`: tcsum_host_batch_ipv4_tx_fill_multi)."""
     assert pkts.dtype == PKT_DTYPE
     pkts = np.ascontiguousarray(pkts)
     flags = np.zeros(pkts.size, np.uint8)
     p, nb = _host_arena_args(host_arena)
-    _lib.check(_lib.lib().tcsum_host_batch_ipv4_tx_fill(device, p, nb, pkts.ctypes.data, pkts.size, None,
-                                                        flags.ctypes.data), "tcsum_host_batch_ipv4_tx_fill")
+    if devices is None:
+        rc = _lib.lib().tcsum_host_batch_ipv4_tx_fill(device, p, nb, pkts.ctypes.data, pkts.size, None,
+                                                      flags.ctypes.data)
+    else:
+        dp, nd, _keep = _devices(devices)
+        rc = _lib.lib().tcsum_host_batch_ipv4_tx_fill_multi(dp, nd, p, nb, pkts.ctypes.data, pkts.size, None,
+                                                            flags.ctypes.data)
+    _lib.check(rc, "tcsum_host_batch_ipv4_tx_fill")
     return flags
 
 
@@ -251,17 +271,24 @@ def tx_apply_batch(host_arena: np.ndarray, pkts: np.ndarray, out: np.ndarray, fl
                                                flags.ctypes.data), "tcsum_tx_apply_batch")
 
 
-def host_batch_ipv4_rx_verify(host_arena, pkts: np.ndarray, device: int = 0):
-    """(verdict int8 net_err_t, out, flags) for packets in host memory."""
+def host_batch_ipv4_rx_verify(host_arena, pkts: np.ndarray, device: int = 0, devices=None):
+    """(verdict int8 net_err_t, out, flags) for packets in host memory (with
+    `devices`: tcsum_host_batch_ipv4_rx_verify_multi)."""
     assert pkts.dtype == PKT_DTYPE
     pkts = np.ascontiguousarray(pkts)
     verdict = np.zeros(pkts.size, np.int8)
     out = np.zeros(pkts.size, np.uint32)
     flags = np.zeros(pkts.size, np.uint8)
     p, nb = _host_arena_args(host_arena)
-    _lib.check(_lib.lib().tcsum_host_batch_ipv4_rx_verify(device, p, nb, pkts.ctypes.data, pkts.size,
-                                                          verdict.ctypes.data, out.ctypes.data, flags.ctypes.data),
-               "tcsum_host_batch_ipv4_rx_verify")
+    if devices is None:
+        rc = _lib.lib().tcsum_host_batch_ipv4_rx_verify(device, p, nb, pkts.ctypes.data, pkts.size,
+                                                        verdict.ctypes.data, out.ctypes.data, flags.ctypes.data)
+    else:
+        dp, nd, _keep = _devices(devices)
+        rc = _lib.lib().tcsum_host_batch_ipv4_rx_verify_multi(dp, nd, p, nb, pkts.ctypes.data, pkts.size,
+                                                              verdict.ctypes.data, out.ctypes.data,
+                                                              flags.ctypes.data)
+    _lib.check(rc, "tcsum_host_batch_ipv4_rx_verify")
     return verdict, out, flags
 
 

@@ -43,18 +43,19 @@ def index(buf):
     return pkts, l2
 
 
-def rx_verify(buf, device: int = 0):
+def rx_verify(buf, device: int = 0, devices=None):
     """Per frame of the capture: (verdict int8, l2 int8, out u32, flags u8).
     verdict is the rx front end's (l2) where the frame does not reach
-    ipv4_in, else the rx gates' net_err_t (tcsum_batch_ipv4_rx_verify)."""
+    ipv4_in, else the rx gates' net_err_t (tcsum_batch_ipv4_rx_verify).
+    `devices`: shard the frames by bytes over those GPUs."""
     a = _as_u8(buf)
     pkts, l2 = index(a)
-    verdict, out, flags = host_batch_ipv4_rx_verify(a, pkts, device)
+    verdict, out, flags = host_batch_ipv4_rx_verify(a, pkts, device, devices)
     verdict = np.where(l2 == _lib.OK, verdict, l2).astype(np.int8)
     return verdict, l2, out, flags
 
 
-def tx_fill(buf, device: int = 0):
+def tx_fill(buf, device: int = 0, devices=None):
     """Fill the IPv4 header and L4 checksums of every frame of a capture that
     reaches ipv4_in, in place, by the stack's tx rules (ipv4.c:643,656,
     tcp_out.c:19-20, udp.c:320-321, icmpv4.c:45-58): a capture's checksums
@@ -63,5 +64,5 @@ def tx_fill(buf, device: int = 0):
     a = _as_u8(buf)
     assert a.flags.writeable, "tx_fill writes the capture in place"
     pkts, l2 = index(a)
-    flags = host_batch_ipv4_tx_fill(a, pkts, device)
+    flags = host_batch_ipv4_tx_fill(a, pkts, device, devices)
     return l2, flags

@@ -159,3 +159,34 @@ def test_c_netif_queue_demo(tc):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "queue server: 200 queues" in r.stdout
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0, 0, 0]])
+@pytest.mark.parametrize("where,shift", [("pinned", 0), ("pinned", 7), ("pageable", 3)])
+def test_host_multi_device_golden(tc, oracle, devices, where, shift):
+    """tcsum_host_batch_ipv4{,_tx_fill,_rx_verify}_multi: byte-balanced shards
+    over a device list (one GPU here, listed repeatedly, so every shard
+    boundary is crossed) give the reference's sums, tx bytes and rx verdicts
+    in packet order; also fewer packets than devices."""
+    cases, pool = G.ipv4_cases()
+    arg, view, keep = host_copy(tc, pool, where, shift)
+    out, flags = tc.host_batch_ipv4(arg, G.pkt_descs(cases, tc.PKT_DTYPE), devices=devices)
+    np.testing.assert_array_equal(out & 0xFFFF, cases["ip"])
+    np.testing.assert_array_equal(out >> 16, cases["l4"])
+    np.testing.assert_array_equal(flags, cases["flags"])
+
+    cases, pin, pout = G.ipv4_tx_cases()
+    arg, view, keep = host_copy(tc, pin, where, shift)
+    flags = tc.host_batch_ipv4_tx_fill(arg, G.pkt_descs(cases, tc.PKT_DTYPE), devices=devices)
+    np.testing.assert_array_equal(view[: pout.size], pout)
+    np.testing.assert_array_equal(flags, cases["flags"])
+
+    cases, pool = G.ipv4_rx_cases()
+    arg, view, keep = host_copy(tc, pool, where, shift)
+    pk = G.pkt_descs(cases, tc.PKT_DTYPE)
+    verdict, out, flags = tc.host_batch_ipv4_rx_verify(arg, pk, devices=devices)
+    np.testing.assert_array_equal(verdict, cases["verdict"])
+    np.testing.assert_array_equal(flags, cases["flags"])
+    few = pk[:2]
+    v2, _, _ = tc.host_batch_ipv4_rx_verify(arg, few, devices=devices)
+    np.testing.assert_array_equal(v2, cases["verdict"][:2])

@@ -179,6 +179,8 @@ def test_capture_rx_verify_mixed_vs_oracle(pcap, oracle):
         frames[i] = bytes(f)
     buf, offs, lens = PB.build(frames, PB.RAW, big_endian=True)
     verdict, l2, out, flags = pcap.rx_verify(np.frombuffer(buf, np.uint8))
+    v3, _, _, _ = pcap.rx_verify(np.frombuffer(buf, np.uint8), devices=[0, 0, 0])  # sharded
+    np.testing.assert_array_equal(v3, verdict)
     from tcp_amd import PKT_DTYPE
     pk = np.zeros(len(frames), PKT_DTYPE)
     pk["offset"], pk["len"] = offs, lens

@@ -199,8 +199,11 @@ int tcsum_host_batch_ipv4_rx_verify(int device, const void *host_arena, uint64_t
 
 /* ------------------------------------------------------- capture files */
 
-/* A classic libpcap savefile already in memory (mmap'd, read, or copied to
- * HBM as is) indexed into IPv4 batch descriptors that point INTO the file:
+/* A libpcap savefile -- classic, or pcapng (Enhanced / Simple / obsolete
+ * Packet Blocks; link type and FCS length per interface; any number of
+ * sections, each in its own byte order) -- already in memory (mmap'd, read,
+ * or copied to HBM as is) indexed into IPv4 batch descriptors that point INTO
+ * the file:
  * the file is the arena, no bytes move.  Host code, no GPU needed.
  *   pkts[i]       frame i's IPv4 packet: offset = record data + link header,
  *                 len = captured bytes after it (an FCS the file declares is
@@ -221,7 +224,8 @@ int tcsum_host_batch_ipv4_rx_verify(int device, const void *host_arena, uint64_t
  * max_frames < records (the first max_frames are indexed; max_frames 0 and
  * pkts NULL = count only); TCSUM_ERR_SIZE when the file ends inside a record
  * (the whole records before it are indexed); TCSUM_ERR_PARAM for a file that
- * is not a savefile; TCSUM_ERR_NOT_SUPPORT for another link type. */
+ * is not a savefile (or a corrupt pcapng block); TCSUM_ERR_NOT_SUPPORT for
+ * another link type (pcapng: that interface's frames get it as l2_verdict). */
 #define TCSUM_PCAP_ARP 1
 int tcsum_pcap_index(const void *file /*[host]*/, uint64_t file_bytes, tcsum_pkt_t *pkts /*[host]*/,
                      int8_t *l2_verdict /*[host] or NULL*/, uint32_t max_frames, uint32_t *n_frames);

@@ -1,4 +1,4 @@
-// Capture-file side of the rx path: a classic libpcap savefile in memory ->
+// Capture-file side of the rx path: a libpcap savefile (classic or pcapng) in memory ->
 // IPv4 batch descriptors that point INTO the file, so the file's bytes are
 // the arena (mmap it and hand it to tcsum_host_batch_ipv4_rx_verify, or copy
 // it to HBM as is and call tcsum_batch_ipv4_rx_verify).
@@ -42,6 +42,175 @@ inline uint32_t rd32(const uint8_t *p, bool swap)
 
 inline uint16_t be16(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
 
+inline uint16_t rd16(const uint8_t *p, bool swap)
+{
+    uint16_t v;
+    memcpy(&v, p, 2);
+    return swap ? __builtin_bswap16(v) : v;
+}
+
+enum Link { L_ETHER, L_RAW, L_NULL, L_SLL, L_OTHER };
+
+// LINKTYPE_* value -> the kinds read here
+Link link_kind(uint32_t type)
+{
+    switch (type) {
+    case 1: // LINKTYPE_ETHERNET: what netif_pcap opens (pcap_open_live on a NIC)
+        return L_ETHER;
+    case 101: // LINKTYPE_RAW
+    case 228: // LINKTYPE_IPV4: the IPv4 header is the first byte
+        return L_RAW;
+    case 0: // LINKTYPE_NULL: 4-byte address family in the writer's byte order
+        return L_NULL;
+    case 113: // LINKTYPE_LINUX_SLL: 16-byte cooked header, protocol at 14..15
+        return L_SLL;
+    default:
+        return L_OTHER;
+    }
+}
+
+// One captured frame (`caplen` bytes at file offset `data`, `fcs` trailing
+// FCS bytes) -> its IPv4 descriptor and the rx front end's decision.
+int8_t classify(const uint8_t *f, uint64_t data, uint32_t caplen, Link kind, uint32_t fcs, bool swap,
+                tcsum_pkt_t &d)
+{
+    // the frame as the capture holds it (recv_thread copies pkthdr->len
+    // bytes, netif_pcap.c:23-30; only caplen of them exist in a record)
+    const uint32_t frame = caplen >= fcs ? caplen - fcs : 0u;
+    const uint8_t *p = f + data;
+    uint32_t l2 = 0;
+    int v = TCSUM_OK;
+    switch (kind) {
+    case L_ETHER:
+        l2 = kEtherHdr;
+        if (frame < kEtherHdr || frame > kEtherHdr + kEtherMtu)
+            v = TCSUM_ERR_SIZE; // is_pkt_ok, ether.c:14-25
+        else if (be16(p + 12) == 0x0806)
+            v = TCSUM_PCAP_ARP; // arp_in, ether.c:76-84: not this path
+        else if (be16(p + 12) != 0x0800)
+            v = TCSUM_ERR_NOT_SUPPORT; // ether.c:95-97
+        break;
+    case L_RAW: // every frame goes to ipv4_in, whose gates sort out short
+        break;  // frames (SIZE) and IPv6 (NOT_SUPPORT, ipv4.c:222)
+    case L_NULL:
+        l2 = 4;
+        if (frame < 4)
+            v = TCSUM_ERR_SIZE;
+        else if (rd32(p, swap) != 2u) // AF_INET
+            v = TCSUM_ERR_NOT_SUPPORT;
+        break;
+    case L_SLL:
+        l2 = 16;
+        if (frame < 16)
+            v = TCSUM_ERR_SIZE;
+        else if (be16(p + 14) == 0x0806)
+            v = TCSUM_PCAP_ARP;
+        else if (be16(p + 14) != 0x0800)
+            v = TCSUM_ERR_NOT_SUPPORT;
+        break;
+    case L_OTHER: // a pcapng interface of a link type not read here
+        v = TCSUM_ERR_NOT_SUPPORT;
+        break;
+    }
+    d.offset = data + (v == TCSUM_OK ? l2 : 0u);
+    d.len = v == TCSUM_OK ? frame - l2 : 0u;
+    d.rsv = 0;
+    return (int8_t)v;
+}
+
+// pcapng (block types: pcapng spec) -- one sequential walk over the blocks:
+// a Section Header Block sets the byte order and clears the interface table,
+// Interface Description Blocks add link type + FCS length, and Enhanced /
+// Simple / obsolete Packet Blocks are frames; other blocks are skipped.
+constexpr uint32_t kShb = 0x0A0D0D0Au, kIdb = 1, kPb = 2, kSpb = 3, kEpb = 6;
+
+struct Iface {
+    Link kind;
+    uint32_t fcs, snaplen;
+};
+
+int pcapng_index(const uint8_t *f, uint64_t file_bytes, tcsum_pkt_t *pkts, int8_t *l2_verdict,
+                 uint32_t max_frames, uint32_t *n_frames)
+{
+    bool swap = false;
+    std::vector<Iface> ifs;
+    uint64_t pos = 0, count = 0;
+    int rc = TCSUM_OK;
+    while (pos < file_bytes) {
+        if (file_bytes - pos < 12) {
+            rc = TCSUM_ERR_SIZE; // the file ends inside a block header
+            break;
+        }
+        uint32_t type;
+        memcpy(&type, f + pos, 4); // the SHB type is a palindrome: no byte order needed
+        if (type == kShb) {
+            const uint32_t bom = rd32(f + pos + 8, false);
+            if (bom == 0x1A2B3C4Du)
+                swap = false;
+            else if (bom == 0x4D3C2B1Au)
+                swap = true;
+            else
+                return TCSUM_ERR_PARAM;
+            ifs.clear();
+        } else if (pos == 0) {
+            return TCSUM_ERR_PARAM;
+        }
+        type = rd32(f + pos, swap);
+        const uint32_t len = rd32(f + pos + 4, swap);
+        if (len < 12 || (len & 3u))
+            return TCSUM_ERR_PARAM; // not a pcapng block
+        if (len > file_bytes - pos) {
+            rc = TCSUM_ERR_SIZE; // the file ends inside this block
+            break;
+        }
+        if (rd32(f + pos + len - 4, swap) != len)
+            return TCSUM_ERR_PARAM; // leading and trailing lengths differ: corrupt
+        const uint8_t *b = f + pos;
+        if (type == kIdb && len >= 20) {
+            Iface in{link_kind(rd16(b + 8, swap)), 0, rd32(b + 12, swap)};
+            for (uint64_t o = 16; o + 4 <= (uint64_t)len - 4;) { // options: code, length, value (4-byte padded)
+                const uint16_t code = rd16(b + o, swap), olen = rd16(b + o + 2, swap);
+                if (code == 0)
+                    break;
+                if (code == 13 && olen >= 1 && o + 4 + olen <= (uint64_t)len - 4) // if_fcslen: bits in
+                    in.fcs = b[o + 4] >= 8 ? b[o + 4] / 8u : b[o + 4]; // the spec (16, 32); writers using bytes give 2, 4
+                o += 4 + ((olen + 3u) & ~3u);
+            }
+            ifs.push_back(in);
+        } else if (type == kEpb || type == kPb || type == kSpb) {
+            uint32_t iface = 0, caplen;
+            uint64_t data;
+            if (type == kSpb) {
+                data = pos + 12;
+                const uint32_t orig = len >= 16 ? rd32(b + 8, swap) : 0u;
+                caplen = std::min<uint32_t>(orig, len - 16);
+                if (!ifs.empty() && ifs[0].snaplen)
+                    caplen = std::min(caplen, ifs[0].snaplen);
+            } else {
+                if (len < 32)
+                    return TCSUM_ERR_PARAM;
+                iface = type == kEpb ? rd32(b + 8, swap) : rd16(b + 8, swap);
+                caplen = rd32(b + 20, swap);
+                data = pos + 28;
+                if (caplen > len - 32)
+                    return TCSUM_ERR_PARAM;
+            }
+            if (count < max_frames) {
+                const Iface in = iface < ifs.size() ? ifs[iface] : Iface{L_OTHER, 0, 0};
+                const int8_t v = classify(f, data, caplen, in.kind, in.fcs, swap, pkts[count]);
+                if (l2_verdict)
+                    l2_verdict[count] = v;
+            }
+            ++count;
+        }
+        pos += len;
+    }
+    *n_frames = (uint32_t)std::min<uint64_t>(count, UINT32_MAX);
+    if (rc == TCSUM_OK && count > max_frames)
+        rc = TCSUM_ERR_MEM;
+    return rc;
+}
+
 } // namespace
 
 extern "C" int tcsum_pcap_index(const void *file, uint64_t file_bytes, tcsum_pkt_t *pkts, int8_t *l2_verdict,
@@ -56,6 +225,8 @@ extern "C" int tcsum_pcap_index(const void *file, uint64_t file_bytes, tcsum_pkt
         return TCSUM_ERR_PARAM;
     uint32_t magic;
     memcpy(&magic, f, 4);
+    if (magic == kShb)
+        return pcapng_index(f, file_bytes, pkts, l2_verdict, max_frames, n_frames);
     const bool swap = magic == __builtin_bswap32(kMagicUs) || magic == __builtin_bswap32(kMagicNs);
     const bool ns = magic == kMagicNs || magic == __builtin_bswap32(kMagicNs);
     if (!swap && magic != kMagicUs && magic != kMagicNs)
@@ -65,59 +236,11 @@ extern "C" int tcsum_pcap_index(const void *file, uint64_t file_bytes, tcsum_pkt
     const uint32_t link = rd32(f + 20, swap);
     const uint32_t type = link & 0xFFFFu;
     const uint32_t fcs = (link & (1u << 26)) ? 2u * (link >> 28) : 0u;
-    enum { ETHER, RAW, NUL, SLL } kind;
-    if (type == 1)
-        kind = ETHER; // LINKTYPE_ETHERNET: what netif_pcap opens (pcap_open_live on a NIC)
-    else if (type == 101 || type == 228)
-        kind = RAW; // LINKTYPE_RAW / LINKTYPE_IPV4: the IPv4 header is the first byte
-    else if (type == 0)
-        kind = NUL; // LINKTYPE_NULL: 4-byte address family in the writer's byte order
-    else if (type == 113)
-        kind = SLL; // LINKTYPE_LINUX_SLL: 16-byte cooked header, protocol at 14..15
-    else
+    const Link kind = link_kind(type);
+    if (kind == L_OTHER)
         return TCSUM_ERR_NOT_SUPPORT;
-
-    // one frame's descriptor and front-end decision
-    auto classify = [&](uint64_t data, uint32_t caplen, tcsum_pkt_t &d) -> int8_t {
-        // the frame as the capture holds it (recv_thread copies pkthdr->len
-        // bytes, netif_pcap.c:23-30; only caplen of them exist in a record)
-        const uint32_t frame = caplen >= fcs ? caplen - fcs : 0u;
-        const uint8_t *p = f + data;
-        uint32_t l2 = 0;
-        int v = TCSUM_OK;
-        switch (kind) {
-        case ETHER:
-            l2 = kEtherHdr;
-            if (frame < kEtherHdr || frame > kEtherHdr + kEtherMtu)
-                v = TCSUM_ERR_SIZE; // is_pkt_ok, ether.c:14-25
-            else if (be16(p + 12) == 0x0806)
-                v = TCSUM_PCAP_ARP; // arp_in, ether.c:76-84: not this path
-            else if (be16(p + 12) != 0x0800)
-                v = TCSUM_ERR_NOT_SUPPORT; // ether.c:95-97
-            break;
-        case RAW: // every frame goes to ipv4_in, whose gates sort out short
-            break; // frames (SIZE) and IPv6 (NOT_SUPPORT, ipv4.c:222)
-        case NUL:
-            l2 = 4;
-            if (frame < 4)
-                v = TCSUM_ERR_SIZE;
-            else if (rd32(p, swap) != 2u) // AF_INET
-                v = TCSUM_ERR_NOT_SUPPORT;
-            break;
-        case SLL:
-            l2 = 16;
-            if (frame < 16)
-                v = TCSUM_ERR_SIZE;
-            else if (be16(p + 14) == 0x0806)
-                v = TCSUM_PCAP_ARP;
-            else if (be16(p + 14) != 0x0800)
-                v = TCSUM_ERR_NOT_SUPPORT;
-            break;
-        }
-        d.offset = data + (v == TCSUM_OK ? l2 : 0u);
-        d.len = v == TCSUM_OK ? frame - l2 : 0u;
-        d.rsv = 0;
-        return (int8_t)v;
+    auto cls = [&](uint64_t data, uint32_t caplen, tcsum_pkt_t &d) {
+        return classify(f, data, caplen, kind, fcs, swap, d);
     };
 
     // The records form a chain (each header gives the next one's position),
@@ -172,7 +295,7 @@ extern "C" int tcsum_pcap_index(const void *file, uint64_t file_bytes, tcsum_pkt
                         done = true;
                     } else {
                         tcsum_pkt_t d;
-                        pc.v.push_back(classify(data, caplen, d));
+                        pc.v.push_back(cls(data, caplen, d));
                         pc.pk.push_back(d);
                         q = data + caplen;
                         __builtin_prefetch(f + std::min(q + 8, file_bytes - 1));

@@ -95,7 +95,7 @@ def test_file_level_errors(pcap):
         assert n.value == 4 and (pk["offset"][:4] == offs[:4]).all()
     # empty capture (header only)
     assert L.tcsum_pcap_index(buf[:24], 24, pk.ctypes.data, None, 5, ctypes.byref(n)) == OK and n.value == 0
-    # not a savefile / too short / pcapng / unsupported link type
+    # not a savefile / too short / a pcapng SHB type on a classic body / unsupported link type
     assert L.tcsum_pcap_index(b"\0" * 64, 64, pk.ctypes.data, None, 5, ctypes.byref(n)) == PARAM
     assert L.tcsum_pcap_index(buf, 20, pk.ctypes.data, None, 5, ctypes.byref(n)) == PARAM
     assert L.tcsum_pcap_index(bytes.fromhex("0a0d0d0a") + buf[4:], len(buf), pk.ctypes.data, None, 5,
@@ -232,3 +232,62 @@ def test_capture_tx_fill_golden(pcap, link):
     np.testing.assert_array_equal(flags[filled], cases["flags"][filled])
     want, _, _ = PB.build([after[i] if filled[i] else before[i] for i in range(len(before))], link)
     assert a.tobytes() == want
+
+
+@pytest.mark.parametrize("big_endian", [False, True])
+@pytest.mark.parametrize("block", ["epb", "spb", "pb"])
+def test_pcapng_index(pcap, big_endian, block):
+    """pcapng: Enhanced / Simple / obsolete Packet Blocks, either byte order,
+    other block types skipped; descriptors point at each frame's IPv4 bytes."""
+    cases, frames = golden_frames()
+    frames = [f for f in frames if len(f) <= 1500]
+    buf, offs, lens = PB.build_ng(frames, (PB.ETHER,), big_endian=big_endian, block=block)
+    pkts, l2 = pcap.index(buf)
+    np.testing.assert_array_equal(l2, OK)
+    np.testing.assert_array_equal(pkts["offset"], offs)
+    np.testing.assert_array_equal(pkts["len"], lens)
+
+
+def test_pcapng_interfaces_sections_fcs(pcap):
+    """Per-interface link types (Ethernet, raw, cooked, an unsupported one),
+    several sections (each resets the interface table), an FCS length option
+    in bits (if_fcslen)."""
+    body = bytes(range(60))
+    n = 40
+    iface = [i % 4 for i in range(n)]
+    links = (PB.ETHER, PB.RAW, PB.SLL, 105)  # 105: IEEE 802.11, not read here
+    buf, offs, lens = PB.build_ng([body] * n, links, iface_of=iface, sections=3, fcs_bits=32)
+    pkts, l2 = pcap.index(buf)
+    want = np.array([NOT_SUPPORT if i == 3 else OK for i in iface], np.int8)
+    np.testing.assert_array_equal(l2, want)
+    ok = want == OK
+    np.testing.assert_array_equal(pkts["offset"][ok], offs[ok])
+    np.testing.assert_array_equal(pkts["len"][ok], 60)
+
+
+def test_pcapng_errors(pcap):
+    import ctypes
+    from tcp_amd import _lib, PKT_DTYPE
+    L = _lib.lib()
+    body = bytes(range(64))
+    buf, offs, _ = PB.build_ng([body] * 5, (PB.ETHER,), extra_blocks=False)
+    pk = np.zeros(5, PKT_DTYPE)
+    n = ctypes.c_uint32(0)
+    assert L.tcsum_pcap_index(buf, len(buf), None, None, 0, ctypes.byref(n)) == MEM and n.value == 5
+    assert L.tcsum_pcap_index(buf[:-6], len(buf) - 6, pk.ctypes.data, None, 5, ctypes.byref(n)) == SIZE
+    assert n.value == 4 and (pk["offset"][:4] == offs[:4]).all()
+    bad = bytearray(buf)
+    bad[-1] ^= 0x40  # trailing block length differs from the leading one
+    assert L.tcsum_pcap_index(bytes(bad), len(bad), pk.ctypes.data, None, 5, ctypes.byref(n)) == PARAM
+    bad = bytearray(buf)
+    bad[8:12] = b"\0\0\0\0"  # byte-order magic
+    assert L.tcsum_pcap_index(bytes(bad), len(bad), pk.ctypes.data, None, 5, ctypes.byref(n)) == PARAM
+
+
+@pytest.mark.gpu
+def test_pcapng_rx_verify_golden(pcap):
+    """The reference's rx verdicts from a pcapng capture (raw-IPv4 interface)."""
+    cases, frames = golden_frames()
+    buf, _, _ = PB.build_ng(frames, (PB.RAW,))
+    verdict, l2, out, flags = pcap.rx_verify(np.frombuffer(buf, np.uint8))
+    np.testing.assert_array_equal(verdict, cases["verdict"].astype(np.int8))

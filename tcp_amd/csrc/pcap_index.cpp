@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -118,6 +119,179 @@ int8_t classify(const uint8_t *f, uint64_t data, uint32_t caplen, Link kind, uin
     return (int8_t)v;
 }
 
+// ------------------------------------------------------------ parallel walk
+//
+// A capture is a chain of records (classic) or blocks (pcapng): each header
+// gives the next one's position, and walking it is one dependent cache + TLB
+// miss per record (~0.45 us over a multi-GiB file).  Large files are cut into
+// K pieces, kChains of them per walker thread, walked with their chains
+// interleaved (their misses overlap); the walker of piece t > 0 first finds a
+// record boundary at or after the piece's start by looking for kSyncRun
+// consecutive plausible headers.  The stitch accepts a piece only if its sync
+// point is exactly where the exact walk of the pieces before it ended, and
+// re-walks it from there otherwise, so the result is the sequential walk's.
+enum StepResult { S_FRAME, S_SKIP, S_TRUNC, S_BAD, S_SEQ };
+
+struct Frame {
+    uint64_t data = 0, next = 0;
+    uint32_t caplen = 0, iface = 0;
+};
+
+constexpr int kNeedSeq = 100; // a piece met a block only a sequential walk may interpret
+
+struct Walker {
+    const uint8_t *f = nullptr;
+    uint64_t file_bytes = 0, body = 0; // records start at `body`
+    std::function<StepResult(uint64_t, Frame &)> step;
+    std::function<bool(uint64_t, uint64_t &)> plausible;
+    std::function<int8_t(const Frame &, tcsum_pkt_t &)> classify;
+
+    struct Piece {
+        uint64_t begin = 0, end = 0; // first record walked / first record at or past the piece end
+        std::vector<tcsum_pkt_t> pk;
+        std::vector<int8_t> v;
+        int rc = TCSUM_OK;
+        bool synced = false;
+    };
+
+    // Walk pieces [a, b) to their ends, one record of each per round.
+    void walk(Piece *pcs, const uint64_t *start, const uint64_t *stop, unsigned a, unsigned b) const
+    {
+        uint64_t pos[kChains];
+        bool live[kChains];
+        unsigned left = 0;
+        for (unsigned j = a; j < b; ++j) {
+            Piece &pc = pcs[j];
+            pc.begin = pos[j - a] = start[j];
+            pc.pk.clear();
+            pc.v.clear();
+            pc.rc = TCSUM_OK;
+            live[j - a] = pc.synced;
+            left += pc.synced;
+            if (!pc.synced)
+                pc.end = pc.begin;
+        }
+        while (left) {
+            for (unsigned j = a; j < b; ++j) {
+                if (!live[j - a])
+                    continue;
+                Piece &pc = pcs[j];
+                uint64_t &q = pos[j - a];
+                bool done = q >= stop[j] || q >= file_bytes;
+                if (!done) {
+                    Frame fr;
+                    const StepResult r = step(q, fr);
+                    if (r == S_FRAME || r == S_SKIP) {
+                        if (r == S_FRAME) {
+                            tcsum_pkt_t d;
+                            pc.v.push_back(classify(fr, d));
+                            pc.pk.push_back(d);
+                        }
+                        q = fr.next;
+                        __builtin_prefetch(f + std::min(q + 8, file_bytes - 1));
+                    } else {
+                        pc.rc = r == S_TRUNC ? TCSUM_ERR_SIZE : r == S_BAD ? TCSUM_ERR_PARAM : kNeedSeq;
+                        done = true;
+                    }
+                }
+                if (done) {
+                    pc.end = q;
+                    live[j - a] = false;
+                    --left;
+                }
+            }
+        }
+    }
+
+    bool sync(uint64_t from, uint64_t limit, uint64_t &at) const
+    {
+        for (uint64_t p = from; p < limit && p < file_bytes; ++p) {
+            uint64_t q = p, next = 0;
+            int k = 0;
+            while (k < kSyncRun && q < file_bytes && plausible(q, next)) {
+                q = next;
+                ++k;
+            }
+            if (k == kSyncRun || (k > 0 && q == file_bytes)) {
+                at = p;
+                return true;
+            }
+        }
+        return false;
+    }
+
+    int run(tcsum_pkt_t *pkts, int8_t *l2_verdict, uint32_t max_frames, uint32_t *n_frames) const
+    {
+        const uint64_t span = file_bytes > body ? file_bytes - body : 0;
+        uint64_t piece_min = kPieceMin; // TCSUM_PCAP_PIECE_KB overrides (tests: many pieces on small files)
+        if (const char *e = getenv("TCSUM_PCAP_PIECE_KB"))
+            piece_min = std::max<uint64_t>(1, strtoull(e, nullptr, 10)) << 10;
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        const unsigned T0 = std::min(16u, hw);
+        const unsigned K = (unsigned)std::min<uint64_t>(T0 * kChains, std::max<uint64_t>(1, span / piece_min));
+        const unsigned T = (K + kChains - 1) / kChains; // walker threads, kChains pieces each
+        std::vector<uint64_t> cut(K + 1), start(K, body);
+        for (unsigned t = 0; t <= K; ++t)
+            cut[t] = body + span * t / K;
+        std::vector<Piece> pcs(K);
+        {
+            std::vector<std::thread> th;
+            for (unsigned t = 0; t < T; ++t) {
+                auto job = [&, t] {
+                    const unsigned a = t * kChains, b = std::min(K, a + kChains);
+                    for (unsigned j = a; j < b; ++j)
+                        pcs[j].synced = j == 0 || sync(cut[j], cut[j + 1], start[j]);
+                    walk(pcs.data(), start.data(), cut.data() + 1, a, b);
+                };
+                if (t + 1 < T)
+                    th.emplace_back(job);
+                else
+                    job();
+            }
+            for (auto &x : th)
+                x.join();
+        }
+        // stitch: piece 0 is exact; each later piece must start where the
+        // exact walk so far ended
+        uint64_t pos = pcs[0].end;
+        int rc = pcs[0].rc;
+        for (unsigned t = 1; t < K && rc == TCSUM_OK; ++t) {
+            Piece &pc = pcs[t];
+            if (!(pc.synced && pc.begin == pos)) { // a false or missing sync point: walk it exactly
+                pc.synced = true;
+                start[t] = pos;
+                walk(pcs.data(), start.data(), cut.data() + 1, t, t + 1);
+            }
+            pos = pc.end;
+            rc = pc.rc;
+        }
+        if (rc == TCSUM_ERR_PARAM || rc == kNeedSeq)
+            return rc;
+        uint64_t count = 0;
+        unsigned last = K;
+        for (unsigned t = 0; t < K; ++t) {
+            count += pcs[t].pk.size();
+            if (pcs[t].rc != TCSUM_OK) {
+                last = t + 1; // the file ends inside this piece's last record
+                break;
+            }
+        }
+        uint64_t i = 0;
+        for (unsigned t = 0; t < last && i < max_frames; ++t) {
+            const Piece &pc = pcs[t];
+            const size_t m = (size_t)std::min<uint64_t>(pc.pk.size(), max_frames - i);
+            memcpy(pkts + i, pc.pk.data(), m * sizeof(tcsum_pkt_t));
+            if (l2_verdict)
+                memcpy(l2_verdict + i, pc.v.data(), m);
+            i += m;
+        }
+        *n_frames = (uint32_t)std::min<uint64_t>(count, UINT32_MAX);
+        if (rc == TCSUM_OK && count > max_frames)
+            rc = TCSUM_ERR_MEM; // *n_frames = records in the file; max_frames of them indexed
+        return rc;
+    }
+};
+
 // pcapng (block types: pcapng spec) -- one sequential walk over the blocks:
 // a Section Header Block sets the byte order and clears the interface table,
 // Interface Description Blocks add link type + FCS length, and Enhanced /
@@ -129,8 +303,8 @@ struct Iface {
     uint32_t fcs, snaplen;
 };
 
-int pcapng_index(const uint8_t *f, uint64_t file_bytes, tcsum_pkt_t *pkts, int8_t *l2_verdict,
-                 uint32_t max_frames, uint32_t *n_frames)
+int pcapng_index_seq(const uint8_t *f, uint64_t file_bytes, tcsum_pkt_t *pkts, int8_t *l2_verdict,
+                     uint32_t max_frames, uint32_t *n_frames)
 {
     bool swap = false;
     std::vector<Iface> ifs;
@@ -211,6 +385,110 @@ int pcapng_index(const uint8_t *f, uint64_t file_bytes, tcsum_pkt_t *pkts, int8_
     return rc;
 }
 
+// Large single-section files: the header blocks (SHB, IDBs) are read first;
+// from the first packet block on, the blocks are walked in parallel pieces
+// (a block's leading and trailing lengths must agree, so a sync point is
+// hard to fake).  A piece that meets another SHB or IDB hands the whole file
+// to the sequential walk, which interprets them in order.
+int pcapng_index(const uint8_t *f, uint64_t file_bytes, tcsum_pkt_t *pkts, int8_t *l2_verdict,
+                 uint32_t max_frames, uint32_t *n_frames)
+{
+    if (file_bytes < 28)
+        return pcapng_index_seq(f, file_bytes, pkts, l2_verdict, max_frames, n_frames);
+    const uint32_t bom = rd32(f + 8, false);
+    if (bom != 0x1A2B3C4Du && bom != 0x4D3C2B1Au)
+        return TCSUM_ERR_PARAM;
+    const bool swap = bom == 0x4D3C2B1Au;
+    std::vector<Iface> ifs;
+    uint64_t body = 0;
+    for (;;) { // header region: the SHB, then blocks up to the first packet block
+        if (file_bytes - body < 12)
+            return pcapng_index_seq(f, file_bytes, pkts, l2_verdict, max_frames, n_frames);
+        const uint32_t type = rd32(f + body, swap), len = rd32(f + body + 4, swap);
+        if (len < 12 || (len & 3u) || len > file_bytes - body || (body > 0 && type == kShb))
+            return pcapng_index_seq(f, file_bytes, pkts, l2_verdict, max_frames, n_frames);
+        if (type == kEpb || type == kPb || type == kSpb)
+            break;
+        if (type == kIdb && len >= 20) {
+            Iface in{link_kind(rd16(f + body + 8, swap)), 0, rd32(f + body + 12, swap)};
+            for (uint64_t o = 16; o + 4 <= (uint64_t)len - 4;) { // options: code, length, value (4-byte padded)
+                const uint16_t code = rd16(f + body + o, swap), olen = rd16(f + body + o + 2, swap);
+                if (code == 0)
+                    break;
+                if (code == 13 && olen >= 1 && o + 4 + olen <= (uint64_t)len - 4) // if_fcslen, as in the walk
+                    in.fcs = f[body + o + 4] >= 8 ? f[body + o + 4] / 8u : f[body + o + 4];
+                o += 4 + ((olen + 3u) & ~3u);
+            }
+            ifs.push_back(in);
+        }
+        body += len;
+    }
+    uint64_t piece_min = kPieceMin;
+    if (const char *e = getenv("TCSUM_PCAP_PIECE_KB"))
+        piece_min = std::max<uint64_t>(1, strtoull(e, nullptr, 10)) << 10;
+    if (file_bytes - body < 2 * piece_min) // small: one walk
+        return pcapng_index_seq(f, file_bytes, pkts, l2_verdict, max_frames, n_frames);
+    Walker w;
+    w.f = f;
+    w.file_bytes = file_bytes;
+    w.body = body;
+    w.step = [=](uint64_t q, Frame &fr) {
+        if (file_bytes - q < 12)
+            return S_TRUNC;
+        uint32_t raw;
+        memcpy(&raw, f + q, 4);
+        const uint32_t type = rd32(f + q, swap), len = rd32(f + q + 4, swap);
+        if (len < 12 || (len & 3u))
+            return S_BAD;
+        if (len > file_bytes - q)
+            return S_TRUNC;
+        if (rd32(f + q + len - 4, swap) != len)
+            return S_BAD;
+        if (raw == kShb || type == kIdb)
+            return S_SEQ;
+        fr.next = q + len;
+        if (type == kSpb) {
+            if (len < 16)
+                return S_BAD;
+            fr.data = q + 12;
+            fr.caplen = std::min<uint32_t>(rd32(f + q + 8, swap), len - 16);
+            if (!ifs.empty() && ifs[0].snaplen)
+                fr.caplen = std::min(fr.caplen, ifs[0].snaplen);
+            fr.iface = 0;
+            return S_FRAME;
+        }
+        if (type == kEpb || type == kPb) {
+            if (len < 32)
+                return S_BAD;
+            fr.iface = type == kEpb ? rd32(f + q + 8, swap) : rd16(f + q + 8, swap);
+            fr.caplen = rd32(f + q + 20, swap);
+            fr.data = q + 28;
+            return fr.caplen > len - 32 ? S_BAD : S_FRAME;
+        }
+        return S_SKIP;
+    };
+    w.plausible = [=](uint64_t q, uint64_t &next) {
+        if (file_bytes - q < 12)
+            return false;
+        const uint32_t type = rd32(f + q, swap), len = rd32(f + q + 4, swap);
+        if (!(type == kEpb || type == kSpb || type == kPb || type == 4 || type == 5) || len < 16 || (len & 3u) ||
+            len > file_bytes - q || rd32(f + q + len - 4, swap) != len)
+            return false;
+        if ((type == kEpb || type == kPb) && (len < 32 || rd32(f + q + 20, swap) > len - 32))
+            return false;
+        next = q + len;
+        return true;
+    };
+    w.classify = [&](const Frame &fr, tcsum_pkt_t &d) {
+        const Iface in = fr.iface < ifs.size() ? ifs[fr.iface] : Iface{L_OTHER, 0, 0};
+        return classify(f, fr.data, fr.caplen, in.kind, in.fcs, swap, d);
+    };
+    const int rc = w.run(pkts, l2_verdict, max_frames, n_frames);
+    if (rc == kNeedSeq)
+        return pcapng_index_seq(f, file_bytes, pkts, l2_verdict, max_frames, n_frames);
+    return rc;
+}
+
 } // namespace
 
 extern "C" int tcsum_pcap_index(const void *file, uint64_t file_bytes, tcsum_pkt_t *pkts, int8_t *l2_verdict,
@@ -239,166 +517,32 @@ extern "C" int tcsum_pcap_index(const void *file, uint64_t file_bytes, tcsum_pkt
     const Link kind = link_kind(type);
     if (kind == L_OTHER)
         return TCSUM_ERR_NOT_SUPPORT;
-    auto cls = [&](uint64_t data, uint32_t caplen, tcsum_pkt_t &d) {
-        return classify(f, data, caplen, kind, fcs, swap, d);
-    };
-
-    // The records form a chain (each header gives the next one's position),
-    // and walking it is one dependent cache + TLB miss per frame (~0.45 us
-    // over a multi-GiB file).  Large files are cut into K pieces, kChains of
-    // them per walker thread, interleaved; the walker of piece t > 0 first
-    // finds a record boundary at or after the piece's
-    // start by looking for kSyncRun consecutive plausible headers, then walks
-    // to the piece's end.  The stitch below accepts a piece only if its sync
-    // point is exactly where the exact walk of the pieces before it ended, and
-    // re-walks it from there otherwise, so the result is the sequential walk's.
-    struct Piece {
-        uint64_t begin = 0, end = 0; // first record walked / first record at or past the piece end
-        std::vector<tcsum_pkt_t> pk;
-        std::vector<int8_t> v;
-        int rc = TCSUM_OK;
-        bool synced = false;
-    };
-    // Walk pieces [a, b) to their ends with their chains interleaved, one
-    // record of each per round: the misses of different chains overlap.
-    auto walk = [&](Piece *pcs, const uint64_t *start, const uint64_t *stop, unsigned a, unsigned b) {
-        uint64_t pos[kChains];
-        bool live[kChains];
-        unsigned left = 0;
-        for (unsigned j = a; j < b; ++j) {
-            Piece &pc = pcs[j];
-            pc.begin = pos[j - a] = start[j];
-            pc.pk.clear();
-            pc.v.clear();
-            pc.rc = TCSUM_OK;
-            live[j - a] = pc.synced;
-            left += pc.synced;
-            if (!pc.synced)
-                pc.end = pc.begin;
-        }
-        while (left) {
-            for (unsigned j = a; j < b; ++j) {
-                if (!live[j - a])
-                    continue;
-                Piece &pc = pcs[j];
-                uint64_t &q = pos[j - a];
-                bool done = q >= stop[j] || q >= file_bytes;
-                if (!done && file_bytes - q < kRecHdr) {
-                    pc.rc = TCSUM_ERR_SIZE; // a partial record header at the end
-                    done = true;
-                }
-                if (!done) {
-                    const uint32_t caplen = rd32(f + q + 8, swap);
-                    const uint64_t data = q + kRecHdr;
-                    if (caplen > file_bytes - data) {
-                        pc.rc = TCSUM_ERR_SIZE; // the last record's bytes are cut short
-                        done = true;
-                    } else {
-                        tcsum_pkt_t d;
-                        pc.v.push_back(cls(data, caplen, d));
-                        pc.pk.push_back(d);
-                        q = data + caplen;
-                        __builtin_prefetch(f + std::min(q + 8, file_bytes - 1));
-                    }
-                }
-                if (done) {
-                    pc.end = q;
-                    live[j - a] = false;
-                    --left;
-                }
-            }
-        }
-    };
     const uint32_t frac_max = ns ? 1000000000u : 1000000u;
-    auto plausible = [&](uint64_t pos) {
-        if (file_bytes - pos < kRecHdr)
+    Walker w;
+    w.f = f;
+    w.file_bytes = file_bytes;
+    w.body = kFileHdr;
+    w.step = [=](uint64_t q, Frame &fr) {
+        if (file_bytes - q < kRecHdr)
+            return S_TRUNC; // a partial record header at the end
+        const uint32_t caplen = rd32(f + q + 8, swap);
+        if (caplen > file_bytes - q - kRecHdr)
+            return S_TRUNC; // the last record's bytes are cut short
+        fr.data = q + kRecHdr;
+        fr.caplen = caplen;
+        fr.next = fr.data + caplen;
+        return S_FRAME;
+    };
+    w.plausible = [=](uint64_t q, uint64_t &next) {
+        if (file_bytes - q < kRecHdr)
             return false;
-        const uint32_t frac = rd32(f + pos + 4, swap), cap = rd32(f + pos + 8, swap),
-                       orig = rd32(f + pos + 12, swap);
+        const uint32_t frac = rd32(f + q + 4, swap), cap = rd32(f + q + 8, swap), orig = rd32(f + q + 12, swap);
         // cap >= 1: runs of zero bytes (padding, zeroed payloads) would
         // otherwise read as chains of empty records
+        next = q + kRecHdr + cap;
         return frac < frac_max && cap >= 1 && cap <= kMaxCap && orig >= cap && orig <= kMaxCap &&
-               cap <= file_bytes - pos - kRecHdr;
+               cap <= file_bytes - q - kRecHdr;
     };
-    auto sync = [&](uint64_t from, uint64_t limit, uint64_t &at) {
-        for (uint64_t p = from; p < limit && p < file_bytes; ++p) {
-            uint64_t q = p;
-            int k = 0;
-            while (k < kSyncRun && q < file_bytes && plausible(q)) {
-                q += kRecHdr + rd32(f + q + 8, swap);
-                ++k;
-            }
-            if (k == kSyncRun || (k > 0 && q == file_bytes)) {
-                at = p;
-                return true;
-            }
-        }
-        return false;
-    };
-
-    const uint64_t body = file_bytes - kFileHdr;
-    uint64_t piece_min = kPieceMin; // TCSUM_PCAP_PIECE_KB overrides (tests: many pieces on small files)
-    if (const char *e = getenv("TCSUM_PCAP_PIECE_KB"))
-        piece_min = std::max<uint64_t>(1, strtoull(e, nullptr, 10)) << 10;
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const unsigned T0 = std::min(16u, hw);
-    const unsigned K = (unsigned)std::min<uint64_t>(T0 * kChains, std::max<uint64_t>(1, body / piece_min));
-    const unsigned T = (K + kChains - 1) / kChains; // walker threads, kChains pieces each
-    std::vector<uint64_t> cut(K + 1), start(K, kFileHdr);
-    for (unsigned t = 0; t <= K; ++t)
-        cut[t] = kFileHdr + body * t / K;
-    std::vector<Piece> pcs(K);
-    {
-        std::vector<std::thread> th;
-        for (unsigned t = 0; t < T; ++t) {
-            auto job = [&, t] {
-                const unsigned a = t * kChains, b = std::min(K, a + kChains);
-                for (unsigned j = a; j < b; ++j)
-                    pcs[j].synced = j == 0 || sync(cut[j], cut[j + 1], start[j]);
-                walk(pcs.data(), start.data(), cut.data() + 1, a, b);
-            };
-            if (t + 1 < T)
-                th.emplace_back(job);
-            else
-                job();
-        }
-        for (auto &x : th)
-            x.join();
-    }
-    // stitch: piece 0 is exact; each later piece must start where the exact
-    // walk so far ended
-    uint64_t pos = pcs[0].end;
-    int rc = pcs[0].rc;
-    for (unsigned t = 1; t < K && rc == TCSUM_OK; ++t) {
-        Piece &pc = pcs[t];
-        if (!(pc.synced && pc.begin == pos)) { // a false or missing sync point: walk it exactly
-            pc.synced = true;
-            start[t] = pos;
-            walk(pcs.data(), start.data(), cut.data() + 1, t, t + 1);
-        }
-        pos = pc.end;
-        rc = pc.rc;
-    }
-    uint64_t count = 0;
-    unsigned last = K;
-    for (unsigned t = 0; t < K; ++t) {
-        count += pcs[t].pk.size();
-        if (pcs[t].rc != TCSUM_OK) {
-            last = t + 1; // the file ends inside this piece's last record
-            break;
-        }
-    }
-    uint64_t i = 0;
-    for (unsigned t = 0; t < last && i < max_frames; ++t) {
-        const Piece &pc = pcs[t];
-        const size_t m = (size_t)std::min<uint64_t>(pc.pk.size(), max_frames - i);
-        memcpy(pkts + i, pc.pk.data(), m * sizeof(tcsum_pkt_t));
-        if (l2_verdict)
-            memcpy(l2_verdict + i, pc.v.data(), m);
-        i += m;
-    }
-    *n_frames = (uint32_t)std::min<uint64_t>(count, UINT32_MAX);
-    if (rc == TCSUM_OK && count > max_frames)
-        rc = TCSUM_ERR_MEM; // *n_frames = records in the file; max_frames of them indexed
-    return rc;
+    w.classify = [=](const Frame &fr, tcsum_pkt_t &d) { return classify(f, fr.data, fr.caplen, kind, fcs, swap, d); };
+    return w.run(pkts, l2_verdict, max_frames, n_frames);
 }

@@ -291,3 +291,37 @@ def test_pcapng_rx_verify_golden(pcap):
     buf, _, _ = PB.build_ng(frames, (PB.RAW,))
     verdict, l2, out, flags = pcap.rx_verify(np.frombuffer(buf, np.uint8))
     np.testing.assert_array_equal(verdict, cases["verdict"].astype(np.int8))
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_pcapng_parallel_walk(pcap, monkeypatch, seed):
+    """Large pcapng files are walked in parallel pieces from the first packet
+    block on: with 1-4 KiB pieces the index equals the one-piece walk, with
+    fake blocks planted in payloads, with statistics blocks between packets,
+    and -- falling back to the sequential walk -- with several sections."""
+    import struct
+    rng = np.random.default_rng(100 + seed)
+    n = 2500
+    frames = []
+    for i in range(n):
+        L = int(rng.integers(0, 500))
+        f = bytearray(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        if seed % 2 and L > 48:  # a fake EPB (consistent lengths) inside the payload
+            fake = struct.pack("<IIIIIII", 6, 48, 0, 0, 0, 16, 16) + bytes(16) + struct.pack("<I", 48)
+            k = int(rng.integers(0, L - 48))
+            f[k: k + 48] = fake
+        frames.append(bytes(f))
+    links = (PB.ETHER, PB.RAW)
+    iface = [int(x) for x in rng.integers(0, 2, n)]
+    for sections in (1, 3):
+        buf, offs, lens = PB.build_ng(frames, links, iface_of=iface, big_endian=seed == 2,
+                                      block=["epb", "pb", "epb", "epb"][seed], sections=sections)
+        monkeypatch.delenv("TCSUM_PCAP_PIECE_KB", raising=False)
+        one = pcap.index(buf)
+        np.testing.assert_array_equal(one[0]["offset"], offs)
+        np.testing.assert_array_equal(one[0]["len"], lens)
+        for kb in ("1", "4"):
+            monkeypatch.setenv("TCSUM_PCAP_PIECE_KB", kb)
+            many = pcap.index(buf)
+            np.testing.assert_array_equal(many[0], one[0])
+            np.testing.assert_array_equal(many[1], one[1])

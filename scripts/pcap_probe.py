@@ -18,12 +18,19 @@ GIB = 1 << 30
 n = int(os.environ.get("PCAP_FRAMES", 1 << 20))
 b = workload.make_batch("mixed_rx", n=n)
 lens = b.descs["len"].astype(np.uint64)
+NG = os.environ.get("PCAP_NG") == "1"  # pcapng: SHB + IDB, then one Enhanced Packet Block per frame
+if NG:
+    blen = np.uint64(32) + (lens + np.uint64(3)) // np.uint64(4) * np.uint64(4)
+    head, data_at = 48, 28
+else:
+    blen = lens + np.uint64(16)
+    head, data_at = 24, 16
 rec = np.zeros(n, np.uint64)
-np.cumsum(lens[:-1] + np.uint64(16), out=rec[1:])
-rec += np.uint64(24)
-file_bytes = int(rec[-1] + np.uint64(16) + lens[-1])
+np.cumsum(blen[:-1], out=rec[1:])
+rec += np.uint64(head)
+file_bytes = int(rec[-1] + blen[-1])
 descs = np.zeros(n, tc.PKT_DTYPE)
-descs["offset"] = rec + np.uint64(16)
+descs["offset"] = rec + np.uint64(data_at)
 descs["len"] = lens
 
 # packets generated in HBM where the capture holds them, filled like a sender
@@ -36,16 +43,32 @@ torch.cuda.synchronize()
 host = tc.HostArena(file_bytes)
 host.array[:] = dev[:file_bytes].cpu().numpy()
 # savefile header (LINKTYPE_RAW) and record headers, written around the packets
-host.array[:24] = np.frombuffer(np.array([0xA1B2C3D4, 0x00040002, 0, 0, 262144, 101], "<u4").tobytes(), np.uint8)
-hdr = np.zeros((n, 4), "<u4")
-hdr[:, 0] = np.arange(n)
-hdr[:, 2] = lens
-hdr[:, 3] = lens
-idx = rec[:, None].astype(np.int64) + np.arange(16)
-host.array[idx] = hdr.view(np.uint8).reshape(n, 16)
+if NG:
+    host.array[:48] = np.frombuffer(np.array([0x0A0D0D0A, 28, 0x1A2B3C4D, 1, 0xFFFFFFFF, 0xFFFFFFFF, 28,
+                                              1, 20, 101, 262144, 20], "<u4").tobytes(), np.uint8)
+    hdr = np.zeros((n, 7), "<u4")
+    hdr[:, 0] = 6
+    hdr[:, 1] = blen
+    hdr[:, 4] = np.arange(n)
+    hdr[:, 5] = lens
+    hdr[:, 6] = lens
+    idx = rec[:, None].astype(np.int64) + np.arange(28)
+    host.array[idx] = hdr.view(np.uint8).reshape(n, 28)
+    tail = (rec + blen - np.uint64(4))[:, None].astype(np.int64) + np.arange(4)
+    host.array[tail] = blen.astype("<u4").view(np.uint8).reshape(n, 4)
+else:
+    host.array[:24] = np.frombuffer(np.array([0xA1B2C3D4, 0x00040002, 0, 0, 262144, 101], "<u4").tobytes(),
+                                    np.uint8)
+    hdr = np.zeros((n, 4), "<u4")
+    hdr[:, 0] = np.arange(n)
+    hdr[:, 2] = lens
+    hdr[:, 3] = lens
+    idx = rec[:, None].astype(np.int64) + np.arange(16)
+    host.array[idx] = hdr.view(np.uint8).reshape(n, 16)
 dev[:file_bytes].copy_(torch.from_numpy(host.array[:file_bytes]))
 total = int(lens.sum())
-print(f"capture: {n} frames, {file_bytes / GIB:.2f} GiB file, {total / GIB:.2f} GiB of IPv4", flush=True)
+print(f"{'pcapng' if NG else 'classic'} capture: {n} frames, {file_bytes / GIB:.2f} GiB file, "
+      f"{total / GIB:.2f} GiB of IPv4", flush=True)
 
 buf = host.array[:file_bytes]
 t = []

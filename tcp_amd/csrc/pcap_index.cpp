@@ -15,7 +15,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <functional>
 #include <thread>
 #include <vector>
 
@@ -139,12 +138,16 @@ struct Frame {
 
 constexpr int kNeedSeq = 100; // a piece met a block only a sequential walk may interpret
 
+// Step:      StepResult(uint64_t pos, Frame &)   one record at pos
+// Plausible: bool(uint64_t pos, uint64_t &next)   could a record start at pos?
+// Classify:  int8_t(const Frame &, tcsum_pkt_t &) descriptor + front-end verdict
+template <class Step, class Plausible, class Classify>
 struct Walker {
-    const uint8_t *f = nullptr;
-    uint64_t file_bytes = 0, body = 0; // records start at `body`
-    std::function<StepResult(uint64_t, Frame &)> step;
-    std::function<bool(uint64_t, uint64_t &)> plausible;
-    std::function<int8_t(const Frame &, tcsum_pkt_t &)> classify;
+    const uint8_t *f;
+    uint64_t file_bytes, body; // records start at `body`
+    Step step;
+    Plausible plausible;
+    Classify classify;
 
     struct Piece {
         uint64_t begin = 0, end = 0; // first record walked / first record at or past the piece end
@@ -292,6 +295,12 @@ struct Walker {
     }
 };
 
+template <class S, class P, class C>
+Walker<S, P, C> make_walker(const uint8_t *f, uint64_t file_bytes, uint64_t body, S step, P plausible, C classify)
+{
+    return Walker<S, P, C>{f, file_bytes, body, step, plausible, classify};
+}
+
 // pcapng (block types: pcapng spec) -- one sequential walk over the blocks:
 // a Section Header Block sets the byte order and clears the interface table,
 // Interface Description Blocks add link type + FCS length, and Enhanced /
@@ -428,11 +437,7 @@ int pcapng_index(const uint8_t *f, uint64_t file_bytes, tcsum_pkt_t *pkts, int8_
         piece_min = std::max<uint64_t>(1, strtoull(e, nullptr, 10)) << 10;
     if (file_bytes - body < 2 * piece_min) // small: one walk
         return pcapng_index_seq(f, file_bytes, pkts, l2_verdict, max_frames, n_frames);
-    Walker w;
-    w.f = f;
-    w.file_bytes = file_bytes;
-    w.body = body;
-    w.step = [=](uint64_t q, Frame &fr) {
+    auto step = [=](uint64_t q, Frame &fr) {
         if (file_bytes - q < 12)
             return S_TRUNC;
         uint32_t raw;
@@ -467,7 +472,7 @@ int pcapng_index(const uint8_t *f, uint64_t file_bytes, tcsum_pkt_t *pkts, int8_
         }
         return S_SKIP;
     };
-    w.plausible = [=](uint64_t q, uint64_t &next) {
+    auto plausible = [=](uint64_t q, uint64_t &next) {
         if (file_bytes - q < 12)
             return false;
         const uint32_t type = rd32(f + q, swap), len = rd32(f + q + 4, swap);
@@ -479,11 +484,11 @@ int pcapng_index(const uint8_t *f, uint64_t file_bytes, tcsum_pkt_t *pkts, int8_
         next = q + len;
         return true;
     };
-    w.classify = [&](const Frame &fr, tcsum_pkt_t &d) {
+    auto cls = [&](const Frame &fr, tcsum_pkt_t &d) {
         const Iface in = fr.iface < ifs.size() ? ifs[fr.iface] : Iface{L_OTHER, 0, 0};
         return classify(f, fr.data, fr.caplen, in.kind, in.fcs, swap, d);
     };
-    const int rc = w.run(pkts, l2_verdict, max_frames, n_frames);
+    const int rc = make_walker(f, file_bytes, body, step, plausible, cls).run(pkts, l2_verdict, max_frames, n_frames);
     if (rc == kNeedSeq)
         return pcapng_index_seq(f, file_bytes, pkts, l2_verdict, max_frames, n_frames);
     return rc;
@@ -518,11 +523,7 @@ extern "C" int tcsum_pcap_index(const void *file, uint64_t file_bytes, tcsum_pkt
     if (kind == L_OTHER)
         return TCSUM_ERR_NOT_SUPPORT;
     const uint32_t frac_max = ns ? 1000000000u : 1000000u;
-    Walker w;
-    w.f = f;
-    w.file_bytes = file_bytes;
-    w.body = kFileHdr;
-    w.step = [=](uint64_t q, Frame &fr) {
+    auto step = [=](uint64_t q, Frame &fr) {
         if (file_bytes - q < kRecHdr)
             return S_TRUNC; // a partial record header at the end
         const uint32_t caplen = rd32(f + q + 8, swap);
@@ -533,7 +534,7 @@ extern "C" int tcsum_pcap_index(const void *file, uint64_t file_bytes, tcsum_pkt
         fr.next = fr.data + caplen;
         return S_FRAME;
     };
-    w.plausible = [=](uint64_t q, uint64_t &next) {
+    auto plausible = [=](uint64_t q, uint64_t &next) {
         if (file_bytes - q < kRecHdr)
             return false;
         const uint32_t frac = rd32(f + q + 4, swap), cap = rd32(f + q + 8, swap), orig = rd32(f + q + 12, swap);
@@ -543,6 +544,6 @@ extern "C" int tcsum_pcap_index(const void *file, uint64_t file_bytes, tcsum_pkt
         return frac < frac_max && cap >= 1 && cap <= kMaxCap && orig >= cap && orig <= kMaxCap &&
                cap <= file_bytes - q - kRecHdr;
     };
-    w.classify = [=](const Frame &fr, tcsum_pkt_t &d) { return classify(f, fr.data, fr.caplen, kind, fcs, swap, d); };
-    return w.run(pkts, l2_verdict, max_frames, n_frames);
+    auto cls = [=](const Frame &fr, tcsum_pkt_t &d) { return classify(f, fr.data, fr.caplen, kind, fcs, swap, d); };
+    return make_walker(f, file_bytes, kFileHdr, step, plausible, cls).run(pkts, l2_verdict, max_frames, n_frames);
 }

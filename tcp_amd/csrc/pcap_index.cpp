@@ -283,6 +283,8 @@ struct Walker {
         for (unsigned t = 0; t < last && i < max_frames; ++t) {
             const Piece &pc = pcs[t];
             const size_t m = (size_t)std::min<uint64_t>(pc.pk.size(), max_frames - i);
+            if (!m)
+                continue;
             memcpy(pkts + i, pc.pk.data(), m * sizeof(tcsum_pkt_t));
             if (l2_verdict)
                 memcpy(l2_verdict + i, pc.v.data(), m);

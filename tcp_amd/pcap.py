@@ -66,3 +66,41 @@ def tx_fill(buf, device: int = 0, devices=None):
     pkts, l2 = index(a)
     flags = host_batch_ipv4_tx_fill(a, pkts, device, devices)
     return l2, flags
+
+
+def _main(argv=None) -> int:
+    """python -m tcp_amd.pcap FILE [--fill OUT] [--devices 0,1,...]: verify
+    every frame of a capture with the stack's rx rules on the GPU and print
+    one count per verdict; with --fill, also write a copy whose checksums are
+    filled by the stack's tx rules."""
+    import argparse
+    import collections
+
+    from . import csum
+    names = {0: "OK", -5: "SIZE", -11: "NOT_SUPPORT", -13: "BROKEN", _lib.PCAP_ARP: "ARP (not ipv4_in)"}
+    ap = argparse.ArgumentParser(prog="python -m tcp_amd.pcap")
+    ap.add_argument("file")
+    ap.add_argument("--fill", metavar="OUT")
+    ap.add_argument("--devices", default="0")
+    args = ap.parse_args(argv)
+    devices = [int(x) for x in args.devices.split(",")]
+    with open(args.file, "rb") as fh:
+        size = fh.seek(0, 2)
+        fh.seek(0)
+        arena = csum.HostArena(size)  # pinned: read in place by the GPU
+        fh.readinto(memoryview(arena.array))
+    try:
+        verdict, l2, _, _ = rx_verify(arena.array, devices[0], devices if len(devices) > 1 else None)
+        counts = collections.Counter(verdict.tolist())
+        print(f"{verdict.size} frames: " + ", ".join(f"{names.get(k, k)} {v}" for k, v in sorted(counts.items())))
+        if args.fill:
+            tx_fill(arena.array, devices[0], devices if len(devices) > 1 else None)
+            with open(args.fill, "wb") as out:
+                out.write(memoryview(arena.array))
+    finally:
+        arena.free()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(_main())

@@ -325,3 +325,25 @@ def test_pcapng_parallel_walk(pcap, monkeypatch, seed):
             many = pcap.index(buf)
             np.testing.assert_array_equal(many[0], one[0])
             np.testing.assert_array_equal(many[1], one[1])
+
+
+@pytest.mark.gpu
+def test_cli_verify_and_fill(tmp_path):
+    """python -m tcp_amd.pcap: counts per verdict; --fill writes the capture
+    with the reference's tx bytes."""
+    import os
+    import subprocess
+    import sys
+    cases, pin, pout = G.ipv4_tx_cases()
+    before = [pin[o: o + n].tobytes() for o, n in zip(cases["pool_off"], cases["frame_len"])]
+    after = [pout[o: o + n].tobytes() for o, n in zip(cases["pool_off"], cases["frame_len"])]
+    buf, _, _ = PB.build(before, PB.RAW)
+    src, dst = tmp_path / "in.pcap", tmp_path / "out.pcap"
+    src.write_bytes(buf)
+    r = subprocess.run([sys.executable, "-m", "tcp_amd.pcap", str(src), "--fill", str(dst)],
+                       capture_output=True, text=True, timeout=120,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith(f"{len(before)} frames: ")
+    want, _, _ = PB.build(after, PB.RAW)
+    assert dst.read_bytes() == want

@@ -1175,12 +1175,67 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
         goto results;
     }
     {
-    bool in_order = staged;
+    bool in_order = true;
     for (uint32_t i = 1, last = 0; in_order && i < n; ++i)
         if (pkts[i].len) {
             in_order = pkts[i].offset >= pkts[last].offset;
             last = i;
         }
+    // Large pinned batches that are only read (sums, rx) go through the copy
+    // engine instead of the kernel's own PCIe reads: pieces copied in order on
+    // one copy stream into HBM, each piece's kernel behind its copy's event
+    // (tcsum_host_batch_peso's pipeline): 50.7 against 49.3 GiB/s for 1M
+    // mixed frames (profiles/r01/hostq_dma.txt).  TCSUM_HOSTQ_DMA_KB: the
+    // span from which it is used (0 = never).
+    const uint64_t dma_min = (uint64_t)env_int("TCSUM_HOSTQ_DMA_KB", 256 << 10) << 10;
+    if (!staged && ip_mode != 1 && in_order && dma_min && hi > lo && hi - lo >= dma_min) {
+        const uint64_t alo = lo & ~uint64_t(15), ahi = std::min<uint64_t>(arena_bytes, (hi + 15) & ~uint64_t(15));
+        const size_t need = (size_t)(ahi - alo) + 32;
+        if (need > c.d_arena_cap) {
+            if (c.d_arena)
+                (void)hipFree(c.d_arena);
+            c.d_arena_cap = 0;
+            if (hipMalloc(reinterpret_cast<void **>(&c.d_arena), need) != hipSuccess)
+                return TCSUM_ERR_MEM;
+            c.d_arena_cap = need;
+        }
+        uint8_t *const dbase = c.d_arena + 16 - alo;
+        hipStream_t cs = c.hs[0], ks = c.hs[1];
+        const uint64_t kPiece = 64ull << 20;
+        uint64_t copied_hi = alo;
+        size_t k = 0;
+        for (uint32_t i0 = 0; i0 < n && e == hipSuccess; ++k) {
+            uint32_t i1 = i0;
+            uint64_t bytes = 0, end = copied_hi;
+            while (i1 < n && (i1 == i0 || bytes < kPiece)) {
+                if (pkts[i1].len) {
+                    bytes += pkts[i1].len;
+                    end = std::max<uint64_t>(end, pkts[i1].offset + pkts[i1].len);
+                }
+                ++i1;
+            }
+            end = std::min<uint64_t>(arena_bytes, (end + 15) & ~uint64_t(15));
+            if (end > copied_hi) {
+                e = hipMemcpyAsync(dbase + copied_hi, host_arena + copied_hi, end - copied_hi, hipMemcpyHostToDevice,
+                                   cs);
+                copied_hi = end;
+            }
+            hipEvent_t ev = c.hev[k % kHostEvents];
+            if (e == hipSuccess)
+                e = hipEventRecord(ev, cs);
+            if (e == hipSuccess)
+                e = hipStreamWaitEvent(ks, ev, 0);
+            if (e == hipSuccess)
+                e = tcsum::launch_ipv4(ip_mode, tcsum::pick_geometry(mean_of(bytes, i1 - i0)), dbase, d_pkts + i0,
+                                       i1 - i0, d_out ? d_out + i0 : nullptr, d_flags ? d_flags + i0 : nullptr,
+                                       d_verdict ? d_verdict + i0 : nullptr, ks);
+            i0 = i1;
+        }
+        const hipError_t s1 = hipStreamSynchronize(ks), s2 = hipStreamSynchronize(cs);
+        if (e != hipSuccess || s1 != hipSuccess || s2 != hipSuccess)
+            return TCSUM_ERR_SYS;
+        goto results;
+    }
     if (!staged) {
         e = launch(0, n, total);
     } else if (!in_order) {

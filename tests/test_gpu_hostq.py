@@ -190,3 +190,48 @@ def test_host_multi_device_golden(tc, oracle, devices, where, shift):
     few = pk[:2]
     v2, _, _ = tc.host_batch_ipv4_rx_verify(arg, few, devices=devices)
     np.testing.assert_array_equal(v2, cases["verdict"][:2])
+
+
+@pytest.mark.parametrize("mode", ["sums", "rx"])
+def test_host_pinned_copy_engine_path(tc, oracle, monkeypatch, mode):
+    """Large pinned read-only batches go through the copy engine into HBM in
+    64-MiB pieces (TCSUM_HOSTQ_DMA_KB lowered so a test-sized batch takes
+    that path): same results as the in-place path and as the oracle; the
+    reference's fixtures too."""
+    from tcp_amd import workload
+    monkeypatch.setenv("TCSUM_HOSTQ_DMA_KB", "1")
+    cases, pool = G.ipv4_rx_cases() if mode == "rx" else G.ipv4_cases()
+    arg, view, keep = host_copy(tc, pool, "pinned", 5)
+    pk = G.pkt_descs(cases, tc.PKT_DTYPE)
+    if mode == "rx":
+        verdict, out, flags = tc.host_batch_ipv4_rx_verify(arg, pk)
+        np.testing.assert_array_equal(verdict, cases["verdict"])
+    else:
+        out, flags = tc.host_batch_ipv4(arg, pk)
+        np.testing.assert_array_equal(out & 0xFFFF, cases["ip"])
+        np.testing.assert_array_equal(out >> 16, cases["l4"])
+    np.testing.assert_array_equal(flags, cases["flags"])
+    # a batch of several pieces (~140 MB), against the in-place path and the oracle
+    b = workload.make_batch("mixed_rx", n=30000)
+    dev, _ = workload.materialize(b)
+    ha = tc.HostArena(b.alloc_bytes)
+    try:
+        ha.array[:] = dev.cpu().numpy()
+        if mode == "rx":
+            v_dma, o_dma, f_dma = tc.host_batch_ipv4_rx_verify(ha, b.descs)
+            monkeypatch.setenv("TCSUM_HOSTQ_DMA_KB", "0")
+            v_in, o_in, f_in = tc.host_batch_ipv4_rx_verify(ha, b.descs)
+            ev, ef = oracle.batch_ipv4_rx_verify(ha.array, b.descs, nthreads=8)
+            np.testing.assert_array_equal(v_dma, ev)
+            np.testing.assert_array_equal(v_dma, v_in)
+        else:
+            o_dma, f_dma = tc.host_batch_ipv4(ha, b.descs)
+            monkeypatch.setenv("TCSUM_HOSTQ_DMA_KB", "0")
+            o_in, f_in = tc.host_batch_ipv4(ha, b.descs)
+            eo, ef = oracle.batch_ipv4(ha.array, b.descs, nthreads=8)
+            np.testing.assert_array_equal(o_dma, eo)
+        np.testing.assert_array_equal(o_dma, o_in)
+        np.testing.assert_array_equal(f_dma, f_in)
+    finally:
+        del keep
+        ha.free()

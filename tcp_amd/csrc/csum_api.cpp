@@ -1188,17 +1188,20 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     // mixed frames (profiles/r01/hostq_dma.txt).  TCSUM_HOSTQ_DMA_KB: the
     // span from which it is used (0 = never).
     const uint64_t dma_min = (uint64_t)env_int("TCSUM_HOSTQ_DMA_KB", 256 << 10) << 10;
-    if (!staged && ip_mode != 1 && in_order && dma_min && hi > lo && hi - lo >= dma_min) {
-        const uint64_t alo = lo & ~uint64_t(15), ahi = std::min<uint64_t>(arena_bytes, (hi + 15) & ~uint64_t(15));
-        const size_t need = (size_t)(ahi - alo) + 32;
-        if (need > c.d_arena_cap) {
-            if (c.d_arena)
-                (void)hipFree(c.d_arena);
-            c.d_arena_cap = 0;
-            if (hipMalloc(reinterpret_cast<void **>(&c.d_arena), need) != hipSuccess)
-                return TCSUM_ERR_MEM;
-            c.d_arena_cap = need;
-        }
+    const uint64_t alo = lo & ~uint64_t(15), ahi = std::min<uint64_t>(arena_bytes, (hi + 15) & ~uint64_t(15));
+    bool dma = !staged && ip_mode != 1 && in_order && dma_min && hi > lo && hi - lo >= dma_min;
+    if (dma && (size_t)(ahi - alo) + 32 > c.d_arena_cap) {
+        // no room in HBM for the span: the in-place path below needs none
+        if (c.d_arena)
+            (void)hipFree(c.d_arena);
+        c.d_arena = nullptr;
+        c.d_arena_cap = 0;
+        if (hipMalloc(reinterpret_cast<void **>(&c.d_arena), (size_t)(ahi - alo) + 32) == hipSuccess)
+            c.d_arena_cap = (size_t)(ahi - alo) + 32;
+        else
+            dma = false, (void)hipGetLastError();
+    }
+    if (dma) {
         uint8_t *const dbase = c.d_arena + 16 - alo;
         hipStream_t cs = c.hs[0], ks = c.hs[1];
         const uint64_t kPiece = 64ull << 20;

@@ -38,6 +38,7 @@ extern "C" {
 #define TCSUM_ERR_SIZE (-5)      /* NET_ERR_SIZE */
 #define TCSUM_ERR_PARAM (-7)     /* NET_ERR_PARAM: bad argument */
 #define TCSUM_ERR_BROKEN (-13)   /* NET_ERR_BROKEN: checksum mismatch (rx verdicts) */
+#define TCSUM_ERR_UNREACHABLE (-14) /* NET_ERR_UNREACHABLE: rx verdict, UDP to port 0 */
 #define TCSUM_ERR_NOT_SUPPORT (-11) /* NET_ERR_NOT_SUPPORT: no usable gfx950 device */
 
 /* ------------------------------------------------------------ descriptors */
@@ -142,15 +143,33 @@ int tcsum_tx_apply_batch(void *arena /*[host]*/, uint64_t arena_bytes, const tcs
                          uint32_t n, const uint32_t *csums /*[host]*/, const uint8_t *flags /*[host]*/);
 
 /* Batched rx verify: verdict[i] = the net_err_t the
- * reference's receive path returns from its size and checksum gates, in its
- * order: frame < 20 -> SIZE; version != 4 -> NOT_SUPPORT; IHL/total length ->
- * SIZE (ipv4.c:222-239); stored header checksum != 0 and wrong -> BROKEN
- * (ipv4.c:241-249); fragments -> OK (L4 is checked after reassembly);
- * L4 shorter than its header -> SIZE; stored TCP/UDP checksum != 0 and wrong
- * -> BROKEN (tcp_in.c:77-85, udp.c:407-415); ICMP -> OK unless total <= 21
- * (its checksum test cannot fail in the reference, icmpv4.c:31-43,71-77);
- * otherwise OK.  Socket lookup and routing are not modelled.  out and flags
- * may be NULL. */
+ * reference's receive path returns, gate by gate in its order, up to (not
+ * including) socket lookup and routing:
+ *   frame < 20                               SIZE        ipv4.c:475 (pktbuf_set_cont)
+ *   version != 4                             NOT_SUPPORT ipv4.c:222-226
+ *   IHL*4 < 20, total_len < 20 or > frame    SIZE        ipv4.c:228-240
+ *   stored header checksum != 0 and wrong    BROKEN      ipv4.c:241-249
+ *   fragment (MF or offset)                  OK          ipv4.c:506-509 (reassembly)
+ *   TCP  (after pktbuf_remove_header, ipv4.c:450-452)
+ *     segment < 20 bytes                     -1 (SYS)    tcp_in.c:70-74
+ *     stored checksum != 0 and wrong         BROKEN      tcp_in.c:77-85
+ *     segment < data offset * 4              SIZE        tcp_in.c:87-91
+ *     source or destination port 0           BROKEN      tcp_in.c:93-97
+ *     flag word (offset+flags) 0             BROKEN      tcp_in.c:99-103
+ *   UDP  datagram < 8 bytes                  SIZE        udp.c:386-391
+ *        destination port 0                  UNREACHABLE udp.c:337-340, 399-403
+ *        stored checksum != 0 and wrong      BROKEN      udp.c:407-415
+ *   ICMP message < 4 bytes                   SIZE        icmpv4.c:68-73 (its checksum
+ *                                                        test cannot fail, A10)
+ *   otherwise OK (other protocols: raw_in, no checksum).
+ * The verdicts equal the reference stack's own on every packet of
+ * tests/golden/ipv4_rx_* (oracle/stack_gen.c runs its ipv4_in/tcp_in/udp_in/
+ * icmpv4_in/raw_in) with a UDP socket bound to each port and the netif owning
+ * each destination.  Defined here where the reference is not: TCP with
+ * IHL*4 > total_len -> SIZE (the reference dereferences NULL in
+ * pktbuf_remove_header); a nonzero header checksum with IHL*4 past the frame
+ * is checked over the captured bytes only (the reference reads past them).
+ * out and flags may be NULL. */
 int tcsum_batch_ipv4_rx_verify(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/,
                                uint32_t n, int8_t *verdict /*[dev]*/, uint32_t *out /*[dev] or NULL*/,
                                uint8_t *flags /*[dev] or NULL*/, uint64_t total_bytes_hint, void *stream);

@@ -25,7 +25,10 @@ int tcsum_synth_fill(void *arena /*[dev]*/, uint64_t nbytes, uint64_t byte_base,
 
 /* Overwrite the first 20 bytes of every packet with an IPv4 header:
  * version 4, IHL 5, total_len = pkts[i].len, TTL 64, protocol TCP or UDP
- * (from the hash of seed and i), header checksum 0 (tx form), random src/dst.
+ * (from the hash of seed and i), header checksum 0 (tx form), random src/dst;
+ * and, in packets of >= 40 bytes, the L4 fields the receive gates read:
+ * nonzero ports, TCP data offset 5 with ACK (PSH half the time), UDP length.
+ * Checksum fields are left as stream bytes (the tx fill zeroes them).
  * Packets shorter than 20 bytes are left alone. */
 int tcsum_synth_ipv4(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,
                      uint64_t seed, void *stream);

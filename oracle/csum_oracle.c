@@ -124,9 +124,11 @@ uint16_t orc_checksum_peso(const uint8_t *seg, uint32_t len,
 #define F_L4_SHORT 0x40u
 
 /* net_err_t values (net/net/net_err.h) */
+#define E_SYS (-1)
 #define E_SIZE (-5)
 #define E_NOT_SUPPORT (-11)
 #define E_BROKEN (-13)
+#define E_UNREACHABLE (-14)
 
 /* L4 checksum field offset and minimum header, by protocol. */
 static int l4_field(uint8_t proto, uint32_t *field, uint32_t *min_len)
@@ -220,6 +222,11 @@ uint8_t orc_ipv4_tx_fill(uint8_t *pkt, uint32_t frame_len)
     return flags;
 }
 
+/* The receive path's verdict: the net_err_t of the first gate that rejects
+ * the packet, in the reference's order -- ipv4_in / is_pkt_ok, then the L4
+ * input function ip_normal_in dispatches to (ipv4.c:420-470) -- up to, not
+ * including, socket lookup and routing.  Pinned by tests/golden/ipv4_rx_*,
+ * the return values of the reference stack's own code (oracle/stack_gen.c). */
 int8_t orc_ipv4_rx_verify(const uint8_t *pkt, uint32_t frame_len, uint8_t *flags_out)
 {
     uint16_t ip, l4;
@@ -236,25 +243,47 @@ int8_t orc_ipv4_rx_verify(const uint8_t *pkt, uint32_t frame_len, uint8_t *flags
         return E_SIZE;
     if (tl < 20 || frame_len < tl) /* ipv4.c:236 */
         return E_SIZE;
-    if (ihl4 > tl) /* the reference would sum past the header (UB); defined here */
-        return E_SIZE;
-    if ((pkt[10] | pkt[11]) && ip != 0) /* ipv4.c:241-249 */
+    /* ipv4.c:241-249 (IHL*4 past the frame: the reference sums bytes it was
+     * not given; here only the captured ones count) */
+    if ((pkt[10] | pkt[11]) && ip != 0)
         return E_BROKEN;
-    if (flags & F_FRAGMENT) /* ipv4.c:506: reassembly first; L4 is checked per datagram */
+    if (flags & F_FRAGMENT) /* ipv4.c:506-509: reassembly first, ipv4_in returns OK */
         return 0;
     uint8_t proto = pkt[9];
-    uint32_t fld, minl;
-    if (!l4_field(proto, &fld, &minl))
-        return 0; /* raw_in: no checksum */
-    uint32_t l4len = tl - ihl4;
-    if (l4len < minl) /* pktbuf_set_cont: tcp_in.c:69, udp.c:386, icmpv4.c:68 */
-        return E_SIZE;
-    if (proto == 1)
-        return tl <= 21 ? E_SIZE : 0; /* icmpv4.c:31; the checksum test cannot fail (A10) */
-    const uint8_t *f = pkt + ihl4 + fld;
-    if ((f[0] | f[1]) && l4 != 0) /* tcp_in.c:77-85, udp.c:407-415 */
-        return E_BROKEN;
-    return 0;
+    const uint8_t *l4p = pkt + ihl4;
+    if (proto == 6) { /* ip_normal_in -> pktbuf_remove_header + tcp_in (ipv4.c:450-452) */
+        if (ihl4 > tl) /* the reference runs off the block list (pktbuf.c:264-281); defined here */
+            return E_SIZE;
+        uint32_t seg = tl - ihl4;
+        if (seg < 20) /* pktbuf_set_cont(buf, 20) fails: tcp_in returns -1, tcp_in.c:70-74 */
+            return E_SYS;
+        if ((l4p[16] | l4p[17]) && l4 != 0) /* tcp_in.c:77-85 */
+            return E_BROKEN;
+        if (seg < (uint32_t)(l4p[12] >> 4) * 4u) /* tcp_in.c:87-91 */
+            return E_SIZE;
+        if (!(l4p[0] | l4p[1]) || !(l4p[2] | l4p[3])) /* tcp_in.c:93-97 */
+            return E_BROKEN;
+        if (!(l4p[12] | l4p[13])) /* tcp_in.c:99-103 */
+            return E_BROKEN;
+        return 0; /* socket lookup (tcp_in.c:115) */
+    }
+    if (proto == 17) { /* udp_in (ipv4.c:436) */
+        if (tl < ihl4 + 8) /* pktbuf_set_cont(buf, 8 + ihl), udp.c:386-391 */
+            return E_SIZE;
+        if (!(l4p[2] | l4p[3])) /* port 0 matches no socket: udp.c:337-340, :399-403 */
+            return E_UNREACHABLE;
+        if ((l4p[6] | l4p[7]) && l4 != 0) /* udp.c:407-415 */
+            return E_BROKEN;
+        return 0; /* udp.c:373 cannot fail past the set_cont above */
+    }
+    if (proto == 1) { /* icmpv4_in (ipv4.c:427) */
+        if (tl < ihl4 + 4) /* pktbuf_set_cont(buf, ihl + 4), icmpv4.c:68-73 */
+            return E_SIZE;
+        /* icmpv4.c:31 (total <= 21) cannot fire past that, and the checksum
+         * test cannot fail (A10: len > remain, pktbuf.c:650-655) */
+        return 0;
+    }
+    return 0; /* raw_in: no checksum (ipv4.c:460-469) */
 }
 
 /* ---------------------------------------------------------------- batches */

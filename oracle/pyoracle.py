@@ -31,17 +31,16 @@ _lib = None
 
 def build(force: bool = False) -> None:
     """Compile liboracle.so with gcc (and oracle/_ref when /root/reference exists)."""
-    if force or not os.path.exists(LIB_PATH):
-        subprocess.run(["make", "-s", "-C", HERE, "all"], check=True)
+    subprocess.run(["make", "-s", "-C", HERE] + (["-B"] if force else []) + ["all"], check=True)
 
 
 def build_ref() -> bool:
-    """Compile oracle/_ref from the reference sources (golden generator, the
+    """Compile oracle/_ref from the reference sources (golden generators, the
     reference CPU baseline, and the drop-in link test against libtcsum.so);
     False when /root/reference is absent (the GPU box uses the prebuilt files)."""
     if not os.path.isdir("/root/reference/net/src"):
         return False
-    subprocess.run(["make", "-s", "-C", HERE, "ref", "dropin"], check=True)
+    subprocess.run(["make", "-s", "-C", HERE, "ref", "stack", "dropin"], check=True)
     return True
 
 

@@ -635,7 +635,7 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     const int f0 = field_on ? (int)(hl + fld) + (int)s0 : -64;
     const int i0 = (int)s0 + 10; // IPv4 header checksum field
 
-    uint32_t acc_h = 0, acc_l = 0, acc_f = 0;
+    uint32_t acc_h = 0, acc_l = 0, acc_f = 0, acc_pt = 0, acc_tw = 0;
     // one pass of U chunks per lane starting at chunk b0 (pass 0: the loads
     // already in flight; later passes load and sum inside one iteration, so
     // no vector registers are carried around the loop -- see frame_consume)
@@ -646,7 +646,9 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
             const uint32_t idx = b0 + u * G + gl;
             const bool valid = idx < nch;
             const int c = (int)(16u * idx);
-            const bool inner = valid && c >= h_end && c + 16 <= l_end && (f0 + 2 <= c || f0 >= c + 16);
+            // rx reads the first 14 L4 bytes too (ports, data offset, flags)
+            const bool inner = valid && c >= h_end && c + 16 <= l_end && (f0 + 2 <= c || f0 >= c + 16) &&
+                               (IPM != IP_RX || c >= h_end + 14);
             if (valid && !inner) { // header chunks, the field chunk(s), the last chunk: rare
                 uint32_t th = region_sum(vv[u], c, (int)s0, h_end);
                 uint32_t tl4 = region_sum(vv[u], c, h_end, l_end);
@@ -659,6 +661,15 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
                 }
                 if (IPM == IP_TX)
                     th -= region_sum(vv[u], c, i0, i0 + 2); // ipv4.c:643
+                if (IPM == IP_RX) {
+                    // L4 header words as byte sums (zero iff every byte is zero;
+                    // a 2-byte region sums to <= 0xFFFF): TCP/UDP ports at
+                    // +0/+2, the TCP data-offset byte and flag word at +12
+                    acc_pt += region_sum(vv[u], c, h_end, h_end + 2) +
+                              (region_sum(vv[u], c, h_end + 2, h_end + 4) << 16);
+                    acc_tw += region_sum(vv[u], c, h_end + 12, h_end + 14) +
+                              (region_sum(vv[u], c, h_end + 12, h_end + 13) << 16);
+                }
                 ph += th;
                 pl += tl4;
             }
@@ -680,8 +691,11 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     }
     acc_h = group_sum<G>(acc_h);
     acc_l = group_sum<G>(acc_l);
-    if (IPM == IP_RX)
+    if (IPM == IP_RX) {
         acc_f = group_sum<G>(acc_f);
+        acc_pt = group_sum<G>(acc_pt);
+        acc_tw = group_sum<G>(acc_tw);
+    }
 
     if (live && gl == 0) {
         uint32_t ip = 0, l4 = 0;
@@ -719,25 +733,52 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
             }
         }
         if constexpr (IPM == IP_RX) {
+            // The first gate that rejects, in the reference's order: ipv4_in /
+            // is_pkt_ok, then the L4 input ip_normal_in dispatches to
+            // (ipv4.c:420-470), up to socket lookup.  Pinned by the reference
+            // stack's own verdicts (tests/golden/ipv4_rx_*, oracle/stack_gen.c).
+            const uint32_t sport = acc_pt & 0xFFFFu, dport = acc_pt >> 16, fword = acc_tw & 0xFFFFu;
+            const uint32_t dob = (h_end + 12) & 1 ? (acc_tw >> 24) : ((acc_tw >> 16) & 0xFFu);
+            const uint32_t doff4 = (dob >> 4) << 2;
             int v8;
             if (!big_enough)
                 v8 = TCSUM_ERR_SIZE; // pktbuf_set_cont(buf, 20), ipv4.c:475
             else if (version != 4)
-                v8 = TCSUM_ERR_NOT_SUPPORT; // ipv4.c:222
-            else if (ihl4 < 20 || tl < 20 || frame < tl || ihl4 > tl)
-                v8 = TCSUM_ERR_SIZE; // ipv4.c:229-239 (ihl4 > tl: defined here, UB there)
+                v8 = TCSUM_ERR_NOT_SUPPORT; // ipv4.c:222-226
+            else if (ihl4 < 20 || tl < 20 || frame < tl)
+                v8 = TCSUM_ERR_SIZE; // ipv4.c:228-240
             else if (stored_ip != 0 && ip != 0)
                 v8 = TCSUM_ERR_BROKEN; // ipv4.c:241-249
-            else if (frag || !fld)
-                v8 = TCSUM_OK; // reassembly first (ipv4.c:506) / raw_in: no checksum
-            else if (tl - ihl4 < min_l4)
-                v8 = TCSUM_ERR_SIZE; // pktbuf_set_cont: tcp_in.c:69, udp.c:386, icmpv4.c:68
-            else if (proto == 1)
-                v8 = tl <= 21 ? TCSUM_ERR_SIZE : TCSUM_OK; // icmpv4.c:31; its sum test never fails (A10)
-            else if (acc_f != 0 && l4 != 0)
-                v8 = TCSUM_ERR_BROKEN; // tcp_in.c:77-85, udp.c:407-415
-            else
-                v8 = TCSUM_OK;
+            else if (frag)
+                v8 = TCSUM_OK; // ipv4.c:506-509: queued for reassembly
+            else if (proto == 6) { // pktbuf_remove_header + tcp_in, ipv4.c:450-452
+                if (ihl4 > tl)
+                    v8 = TCSUM_ERR_SIZE; // the reference runs off its block list (pktbuf.c:264-281)
+                else if (tl - ihl4 < 20)
+                    v8 = TCSUM_ERR_SYS; // pktbuf_set_cont fails: tcp_in returns -1, tcp_in.c:70-74
+                else if (acc_f != 0 && l4 != 0)
+                    v8 = TCSUM_ERR_BROKEN; // tcp_in.c:77-85
+                else if (tl - ihl4 < doff4)
+                    v8 = TCSUM_ERR_SIZE; // tcp_in.c:87-91
+                else if (sport == 0 || dport == 0 || fword == 0)
+                    v8 = TCSUM_ERR_BROKEN; // tcp_in.c:93-103
+                else
+                    v8 = TCSUM_OK;
+            } else if (proto == 17) { // udp_in, ipv4.c:436
+                if (tl < ihl4 + 8)
+                    v8 = TCSUM_ERR_SIZE; // pktbuf_set_cont(buf, 8 + ihl), udp.c:386-391
+                else if (dport == 0)
+                    v8 = TCSUM_ERR_UNREACHABLE; // no socket has port 0: udp.c:337-340, :399-403
+                else if (acc_f != 0 && l4 != 0)
+                    v8 = TCSUM_ERR_BROKEN; // udp.c:407-415
+                else
+                    v8 = TCSUM_OK;
+            } else if (proto == 1) { // icmpv4_in, ipv4.c:427
+                // pktbuf_set_cont(buf, ihl + 4), icmpv4.c:68; its checksum test cannot fail (A10)
+                v8 = tl < ihl4 + 4 ? TCSUM_ERR_SIZE : TCSUM_OK;
+            } else {
+                v8 = TCSUM_OK; // raw_in: no checksum, ipv4.c:460-469
+            }
             verdict_out[pk] = (int8_t)v8;
         }
         if (out)
@@ -1043,6 +1084,25 @@ __global__ __launch_bounds__(256) void k_synth_ipv4(uint8_t *__restrict__ arena,
 #pragma unroll
     for (int k = 0; k < 8; ++k)
         p[12 + k] = (uint8_t)(a >> (8 * k));
+    // L4 header fields the receive gates read (tcp_in.c:87-103, udp.c:337):
+    // nonzero ports; TCP data offset 5 with ACK (+ PSH half the time); UDP
+    // length.  The rest of the L4 bytes stay the synthetic stream.
+    if (len < 40u) // room for a TCP header (the configs start at 64 B)
+        return;
+    const uint64_t b = splitmix64(a);
+    const uint32_t sport = 1u + (uint32_t)(b % 65535u), dport = 1u + (uint32_t)((b >> 20) % 65535u);
+    p[20] = (uint8_t)(sport >> 8);
+    p[21] = (uint8_t)sport;
+    p[22] = (uint8_t)(dport >> 8);
+    p[23] = (uint8_t)dport;
+    if (p[9] == 6) {
+        p[32] = 0x50;
+        p[33] = (b >> 40) & 1u ? 0x18 : 0x10;
+    } else {
+        const uint32_t ul = tl - 20u;
+        p[24] = (uint8_t)(ul >> 8);
+        p[25] = (uint8_t)ul;
+    }
 }
 
 // ---------------------------------------------------------------- read probe

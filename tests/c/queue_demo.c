@@ -50,6 +50,14 @@ static uint32_t build_frame(uint8_t *f)
         ip[20 + 4] = (uint8_t)(l4 >> 8);
         ip[20 + 5] = (uint8_t)l4;
     }
+    if (proto != 1) { /* nonzero ports (tcp_in.c:93, udp.c:337) */
+        ip[20 + 0] |= 0x80;
+        ip[20 + 2] |= 0x80;
+    }
+    if (proto == 6) { /* data offset 5, ACK (tcp_in.c:87-103) */
+        ip[20 + 12] = 0x50;
+        ip[20 + 13] = 0x10;
+    }
     return L2 + total; /* checksum fields keep their random bytes: the fill zeroes them first */
 }
 

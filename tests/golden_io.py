@@ -1,10 +1,17 @@
 """Readers for the golden fixtures in tests/golden/.
 
-The fixtures were produced by the reference's own checksum16 /
-pktbuf_checksum16 / checksum_peso (net/src/tools.c:24-75,
-net/src/pktbuf.c:646-670), compiled from /root/reference by
-``make -C oracle golden`` (generator: oracle/golden_gen.c).  They are plain
-little-endian u32 records; the layouts below mirror golden_gen.c.
+The fixtures were produced by the reference compiled from /root/reference by
+``make -C oracle golden``:
+
+* oracle/golden_gen.c -- the reference's own checksum16 / pktbuf_checksum16 /
+  checksum_peso (net/src/tools.c:24-75, net/src/pktbuf.c:646-670) on recorded
+  inputs (flat, pktbuf, peso, ipv4 sums, ipv4_tx on malformed packets);
+* oracle/stack_gen.c -- the whole reference stack: frames its transmit path
+  built and checksummed (stack_tx_*), and the net_err_t its receive path
+  returns for each rx frame (ipv4_rx_*).
+
+They are plain little-endian u32 records; the layouts below mirror the
+generators.
 """
 from __future__ import annotations
 
@@ -28,7 +35,13 @@ IPV4 = np.dtype([("pool_off", "<u4"), ("frame_len", "<u4"), ("ip", "<u4"), ("l4"
                  ("flags", "<u4")])
 
 IPV4_TX = np.dtype([("pool_off", "<u4"), ("frame_len", "<u4"), ("flags", "<u4")])
-IPV4_RX = np.dtype([("pool_off", "<u4"), ("frame_len", "<u4"), ("verdict", "<i4"), ("flags", "<u4")])
+# gate & 0xFF: which reference function decided (1 ipv4_in's own checks,
+# 2 fragment queued for reassembly, 3 the L4 input tcp_in/udp_in/icmpv4_in/
+# raw_in); gate >> 8: the packet's protocol byte
+IPV4_RX = np.dtype([("pool_off", "<u4"), ("frame_len", "<u4"), ("verdict", "<i4"), ("flags", "<u4"),
+                    ("gate", "<u4")])
+# kind >> 8: protocol; kind & 1: a fragment (only its header checksum is filled)
+STACK_TX = np.dtype([("pool_off", "<u4"), ("frame_len", "<u4"), ("flags", "<u4"), ("kind", "<u4")])
 
 NO_BLOCK = 0xFFFFFFFF
 
@@ -60,6 +73,12 @@ def ipv4_cases():
 def ipv4_tx_cases():
     """(cases, pool before the fill, pool after the reference's fill)."""
     return _load("ipv4_tx_cases.bin", IPV4_TX), _load("ipv4_tx_in.bin"), _load("ipv4_tx_out.bin")
+
+
+def stack_tx_cases():
+    """Frames the reference stack transmitted: (cases, frames with the filled
+    checksum fields junked, frames as the reference sent them)."""
+    return _load("stack_tx_cases.bin", STACK_TX), _load("stack_tx_in.bin"), _load("stack_tx_out.bin")
 
 
 def ipv4_rx_cases():

@@ -73,11 +73,13 @@ def test_host_ipv4_sums_golden(tc, where, shift):
     np.testing.assert_array_equal(flags, cases["flags"])
 
 
+@pytest.mark.parametrize("src", ["ipv4_tx", "stack_tx"])
 @pytest.mark.parametrize("where,shift", WHERE)
-def test_host_tx_fill_golden(tc, where, shift):
+def test_host_tx_fill_golden(tc, where, shift, src):
     """In place in host memory == the reference's tx path, byte for byte;
-    bytes past the packets are left alone."""
-    cases, pin, pout = G.ipv4_tx_cases()
+    bytes past the packets are left alone.  stack_tx: frames the reference
+    stack itself transmitted (oracle/stack_gen.c)."""
+    cases, pin, pout = G.ipv4_tx_cases() if src == "ipv4_tx" else G.stack_tx_cases()
     arg, view, keep = host_copy(tc, pin, where, shift)
     view[pin.size:] = 0xA5
     flags = tc.host_batch_ipv4_tx_fill(arg, G.pkt_descs(cases, tc.PKT_DTYPE))

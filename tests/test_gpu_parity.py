@@ -290,6 +290,27 @@ def test_batch_ipv4_tx_fill_golden(tc, torch, geometry, g, u):
     np.testing.assert_array_equal(arena.cpu().numpy()[: pout.size], pout)
 
 
+@pytest.mark.parametrize("g,u", [(16, 1), (16, 6), (32, 4), (32, 6), (64, 16)])
+def test_batch_ipv4_tx_fill_stack_golden(tc, torch, geometry, g, u):
+    """Frames the reference stack itself transmitted (udp_out, send_out,
+    icmpv4_out, ipv4_out, ip_frag_out; oracle/stack_gen.c) with their filled
+    fields junked: the in-place fill gives the reference's frames back, byte
+    for byte, and the offload form + host apply gives the same bytes."""
+    geometry(g, u)
+    cases, pin, pout = G.stack_tx_cases()
+    pk = G.pkt_descs(cases, tc.PKT_DTYPE)
+    arena = to_dev(torch, pin)
+    d = tc.descs_to_device(pk)
+    flags = tc.batch_ipv4_tx_fill(arena, d, cases.size, int(cases["frame_len"].sum()))
+    np.testing.assert_array_equal(arena.cpu().numpy()[: pout.size], pout)
+    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+    arena = to_dev(torch, pin)
+    out, flags = tc.batch_ipv4_tx_offload(arena, d, cases.size, int(cases["frame_len"].sum()))
+    host = pin.copy()
+    tc.tx_apply_batch(host, pk, out.cpu().numpy(), flags.cpu().numpy())
+    np.testing.assert_array_equal(host[: pout.size], pout)
+
+
 @pytest.mark.parametrize("g,u", [(16, 1), (32, 4), (64, 2), (64, 16)])
 def test_batch_ipv4_tx_offload_golden(tc, torch, geometry, g, u):
     """tx offload: the packets stay untouched on the device, and the host

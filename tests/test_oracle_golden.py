@@ -89,15 +89,62 @@ def test_ipv4_tx_fill(oracle):
     assert (pin != pout).any()
 
 
+def test_stack_tx_fill(oracle):
+    """The reference stack's own transmitted frames (udp_out, send_out,
+    icmpv4_out, ipv4_out, ip_frag_out): the fill restores every byte."""
+    cases, pin, pout = G.stack_tx_cases()
+    assert cases.size > 1000
+    arena = pin.copy()
+    flags = oracle.batch_ipv4_tx_fill(arena, G.pkt_descs(cases, oracle.PKT_DTYPE), nthreads=4)
+    np.testing.assert_array_equal(flags, cases["flags"])
+    np.testing.assert_array_equal(arena, pout)
+    kinds = cases["kind"]
+    for proto in (1, 6, 17):
+        assert ((kinds >> 8) == proto).sum() >= 100, proto
+    assert (kinds & 1).sum() >= 100  # fragments: header checksum only
+    assert ((kinds >> 8) > 17).sum() >= 20  # other protocols (raw)
+
+
 def test_ipv4_rx_verify(oracle):
+    """Verdicts of the reference stack's receive path (oracle/stack_gen.c)."""
     cases, pool = G.ipv4_rx_cases()
-    assert cases.size == 600
+    assert cases.size > 4000
     verdict, flags = oracle.batch_ipv4_rx_verify(pool, G.pkt_descs(cases, oracle.PKT_DTYPE), nthreads=4)
     np.testing.assert_array_equal(verdict, cases["verdict"])
     np.testing.assert_array_equal(flags, cases["flags"])
-    # the fixture exercises every gate
-    for v in (0, -5, -11, -13):
-        assert (cases["verdict"] == v).sum() >= 5, v
+    # the fixture reaches every gate of every receive function
+    gate, proto, v = cases["gate"] & 0xFF, cases["gate"] >> 8, cases["verdict"]
+    for g, p, code, at_least in [(1, None, -5, 20), (1, None, -11, 20), (1, None, -13, 20),
+                                 (2, None, 0, 100), (3, 6, 0, 100), (3, 6, -1, 10), (3, 6, -13, 50),
+                                 (3, 6, -5, 5), (3, 17, 0, 100), (3, 17, -5, 10), (3, 17, -13, 50),
+                                 (3, 17, -14, 20), (3, 1, 0, 50), (3, 1, -5, 10)]:
+        sel = (gate == g) & (v == code) & ((proto == p) if p is not None else True)
+        assert sel.sum() >= at_least, (g, p, code, int(sel.sum()))
+    assert ((gate == 3) & (proto != 1) & (proto != 6) & (proto != 17)).sum() >= 20  # raw_in
+
+
+def test_ipv4_rx_tcp_gates_behind_checksum(oracle):
+    """tcp_in.c:87-103: with a valid checksum, the data-offset, port and flag
+    gates decide -- each reached by the reference-stack fixture."""
+    cases, pool = G.ipv4_rx_cases()
+    pk = G.pkt_descs(cases, oracle.PKT_DTYPE)
+    out, _ = oracle.batch_ipv4(pool, pk, nthreads=4)
+    seen = {"doff": 0, "port": 0, "flag": 0}
+    for i in np.nonzero(((cases["gate"] & 0xFF) == 3) & ((cases["gate"] >> 8) == 6))[0]:
+        o = int(cases["pool_off"][i])
+        ihl = int(pool[o] & 15) * 4
+        t = pool[o + ihl: o + ihl + 20]
+        if (t[16] | t[17]) and (out[i] >> 16):
+            continue  # the checksum gate decided
+        v = int(cases["verdict"][i])
+        if v == -5:
+            seen["doff"] += 1
+        elif v == -13 and (not (t[0] | t[1]) or not (t[2] | t[3])):
+            seen["port"] += 1
+        elif v == -13:
+            assert not (t[12] | t[13])
+            seen["flag"] += 1
+    assert min(seen.values()) >= 5, seen
 
 
 def test_batch_forms_agree_with_scalar(oracle):

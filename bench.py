@@ -3,6 +3,10 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
+--gpus N > 1 without a launcher starts N rank processes itself (one per GPU,
+torchrun's environment); under torchrun WORLD_SIZE must equal N.  Either way
+rank r times its own slice and the line reports the max over ranks.
+
 One "step" = one batched checksum pass (one kernel launch) over the whole
 synthetic batch already resident in HBM.  Before the K timed steps: W untimed
 warm-up steps, continued (untimed) until --settle-ms have passed, so the GPU
@@ -58,7 +62,14 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-kind", choices=("reference", "port"), default="reference",
+                    help="CPU baseline: the reference's own checksum_peso (oracle/_ref) or the oracle's port")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--trace-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-trace", action="store_true", help="skip the rocprofv3 kernel-trace child")
+    ap.add_argument("--cpu-rehearsal", action="store_true",
+                    help="rehearse the N-rank launcher, rendezvous, barrier and max-over-ranks timing on CPU "
+                         "(gloo, a numpy stand-in for the kernel; no GPU, no GPU numbers)")
     return ap.parse_args()
 
 
@@ -125,19 +136,48 @@ def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None):
         dist.barrier()
     torch.cuda.synchronize()
     ms = t0.elapsed_time(t1)  # events on the launch stream: pure kernel time of K launches
-    # the achievable side: a plain streaming read of the same bytes, same loads
+    probes = probe_compare(torch, tc, batch, lambda: launch(tc, batch, arena, descs, out, flags), arena, steps)
+    return dict(batch=batch, arena=arena, descs=descs, out=out, ms=ms, wall_s=wall, probes=probes)
+
+
+def probe_compare(torch, tc, batch, product, arena, steps, rounds=5):
+    """The roofline's achievable side, measured beside the product kernel
+    (after the timed region, never inside it): rounds of [product x m, plain
+    read x m, tile-shaped read x m] launches, each with its own events, so the
+    three see the same clocks and the same HBM state; per-launch medians.
+    Plain read: k_probe_read<4>, contiguous 1 KiB per load instruction.  Tile
+    read: k_probe_tile in the product's own geometry (lanes x loads, XCD
+    order) over the same bytes -- the product minus descriptors and sums."""
+    g, u = tc.pick_geometry(batch.total_bytes // max(batch.n, 1))
     sink = torch.zeros(1, dtype=torch.uint32, device=arena.device)
-    for _ in range(2):
-        tc.probe_read(arena, batch.arena_bytes, sink)
-    p0 = torch.cuda.Event(enable_timing=True)
-    p1 = torch.cuda.Event(enable_timing=True)
-    p0.record(stream)
-    for _ in range(steps):
-        tc.probe_read(arena, batch.arena_bytes, sink)
-    p1.record(stream)
-    torch.cuda.synchronize()
-    probe_gbs = batch.arena_bytes / (p0.elapsed_time(p1) / steps * 1e-3) / 1e9
-    return dict(batch=batch, arena=arena, descs=descs, out=out, ms=ms, wall_s=wall, probe_gbs=probe_gbs)
+    nbytes = batch.arena_bytes
+    tile_ok = True
+    try:
+        tc.probe_tile(arena, nbytes, g, u, sink)
+    except RuntimeError:
+        tile_ok = False
+    kinds = {"product": product, "read": lambda: tc.probe_read(arena, nbytes, sink)}
+    if tile_ok:
+        kinds["tile"] = lambda: tc.probe_tile(arena, nbytes, g, u, sink)
+    m = max(2, steps // rounds)
+    stream = torch.cuda.current_stream()
+    per = {k: [] for k in kinds}
+    for _ in range(rounds):
+        for k, fn in kinds.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            fn()  # one untimed launch: the previous kind's tail is not charged here
+            e0.record(stream)
+            for _ in range(m):
+                fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            per[k].append(e0.elapsed_time(e1) / m)
+    med = {k: sorted(v)[len(v) // 2] for k, v in per.items()}
+    res = {"product_ms": med["product"], "read_gbs": nbytes / (med["read"] * 1e-3) / 1e9,
+           "geometry": [g, u], "rounds": rounds, "launches_per_round": m}
+    if tile_ok:
+        res["tile_gbs"] = nbytes / (med["tile"] * 1e-3) / 1e9
+    return res
 
 
 def result_entry(r, steps):
@@ -145,6 +185,9 @@ def result_entry(r, steps):
     ms_step = r["ms"] / steps
     alg = algorithmic_bytes(b)
     ach = alg / (ms_step * 1e-3) / 1e9
+    p = r["probes"]
+    best = max(p["read_gbs"], p.get("tile_gbs", 0.0))
+    side = alg / (p["product_ms"] * 1e-3) / 1e9  # the product in the interleaved rounds
     return {
         "workload": b.config,
         "packets": b.n,
@@ -153,8 +196,12 @@ def result_entry(r, steps):
         "ms_per_step": ms_step,
         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4),
-                     "achievable_read": round(r["probe_gbs"], 1),
-                     "frac_of_achievable": round(ach / r["probe_gbs"], 4)},
+                     "achievable_read": round(best, 1),
+                     "frac_of_achievable": round(side / best, 4),
+                     "probes": {"plain_read_gbs": round(p["read_gbs"], 1),
+                                "tile_read_gbs": round(p["tile_gbs"], 1) if "tile_gbs" in p else None,
+                                "tile_geometry": p["geometry"], "product_gbs_same_rounds": round(side, 1),
+                                "rounds": p["rounds"], "launches_per_round": p["launches_per_round"]}},
     }
 
 
@@ -201,6 +248,51 @@ def pmc_traffic(config: str):
     return traffic, None
 
 
+def rocprof_trace(config: str, steps: int, warmup: int, settle_ms: float):
+    """The dominant kernel's launch durations from `rocprofv3 --kernel-trace
+    --stats` of this same bench (one config, same K/W/settle), run as a child
+    before this process touches the GPU: (median_ns, mean_ns, launches,
+    kernel name).  Only the full-size launches count (the largest grid of the
+    checksum kernel), i.e. the warm-up, settle and timed launches."""
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, "rocprofv3 not found"
+    d = tempfile.mkdtemp(prefix="tcsum_trace_")
+    cmd = [prof, "--kernel-trace", "--stats", "--output-format", "csv", "-d", d, "-o", "trace", "--",
+           sys.executable, os.path.abspath(__file__), "--pmc-child", "--trace-child", "--config", config,
+           "--steps", str(steps), "--warmup", str(warmup), "--settle-ms", str(settle_ms)]
+    try:
+        subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                       env=dict(os.environ, TMPDIR=d))
+    except (subprocess.SubprocessError, OSError) as e:
+        shutil.rmtree(d, ignore_errors=True)
+        return None, f"rocprofv3 kernel-trace pass failed: {type(e).__name__}"
+    files = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    keep = os.environ.get("TCSUM_PMC_KEEP")
+    if keep:
+        os.makedirs(keep, exist_ok=True)
+        for f in files + glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
+            shutil.copy(f, os.path.join(keep, f"trace_{config}_{os.path.basename(f)}"))
+    rows = []
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                name = row.get("Kernel_Name", "")
+                if "k_segments" in name or "k_ipv4" in name:
+                    rows.append((name, int(row["Grid_Size_X"]),
+                                 int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
+    shutil.rmtree(d, ignore_errors=True)
+    if not rows:
+        return None, "no checksum-kernel rows in the trace"
+    total = {}
+    for name, grid, dur in rows:
+        total[name] = total.get(name, 0) + dur
+    name = max(total, key=total.get)
+    grid = max(g for n, g, _ in rows if n == name)
+    durs = sorted(dur for n, g, dur in rows if n == name and g == grid)
+    return (durs[len(durs) // 2], sum(durs) / len(durs), len(durs), name), None
+
+
 # ------------------------------------------------------------ CPU baseline
 
 def cpu_model():
@@ -213,47 +305,68 @@ def cpu_model():
         return None
 
 
-def cpu_baseline(torch, r, seconds):
+def cpu_baseline(torch, r, seconds, kind="reference"):
     """The reference's checksum_peso (oracle/_ref/libtcpref.so, compiled from
-    /root/reference; else the oracle port) on a bounded sample of the same
-    segments, on this host's cores."""
+    /root/reference; kind "port" = the oracle's restatement) on the same
+    segments in host memory, timed on this host's cores:
+
+      value      1 thread -- the reference checksums on its single work_thread
+                 (exmsg.c:123) -- over a DRAM-resident sample (>= 1 GiB of the
+                 batch, larger than any L3; re-summed for >= `seconds`);
+      value_all  every logical CPU of the host (os.cpu_count()), same sample;
+      cache_resident  both, over a ~100 MB sample that fits the host's L3.
+
+    A requested "reference" that is not built fails (no silent fallback)."""
     from oracle import pyoracle
     import numpy as np
     pyoracle.build()
     b = r["batch"]
-    n = min(b.n, 65536 if b.config == "mtu" else 2048 if b.kind == "peso" else 16384)
-    end = int(b.descs["offset"][n - 1] + b.descs["len"][n - 1])
-    host = r["arena"][: end + 16].cpu().numpy()
-    what = "segments"
-    if b.kind == "peso":
-        segs = b.descs[:n].copy()
-        want = int(r["out"][:n].to(torch.int64).sum().item())
-    else:
-        # IPv4 packets: the reference's per-packet cost is checksum_peso over
-        # the L4 bytes (tcp_in.c:80 / udp.c:410) plus checksum16 over the
-        # 20-byte header (ipv4.c:243, ~0.5 % of the bytes, not timed); the
-        # synthetic packets are IHL 5 with total_len == frame length
-        off = b.descs["offset"][:n].astype(np.int64)
-        hdr = host[off[:, None] + np.arange(20)[None, :]]
-        segs = np.zeros(n, pyoracle.PESO_DTYPE)
-        segs["offset"] = off + 20
-        segs["len"] = b.descs["len"][:n] - 20
-        segs["src"] = hdr[:, 12:16]
-        segs["dst"] = hdr[:, 16:20]
-        segs["protocol"] = hdr[:, 9]
-        want = int((r["out"][:n].to(torch.int64) >> 16).sum().item())
-        what = "packets' L4 ranges"
-    rate1, kind, cs1 = pyoracle.time_peso(host, segs, 1, seconds, use_reference=True)
-    threads = min(16, os.cpu_count() or 1)
-    rateN, _, csN = pyoracle.time_peso(host, segs, threads, seconds / 2, use_reference=True)
-    return {
-        "value": round(rate1 / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
-        "sample": f"first {n} {what} of the {b.config} batch ({int(segs['len'].sum()) / 1e6:.0f} MB), "
-                  f"re-summed for >= {seconds:.0f} s",
-        "multi": {"value": round(rateN / GIB, 3), "cores": threads},
-        "host_cpu": cpu_model(),
-        "parity": bool(cs1 == want and csN == want),
-    }
+
+    def sample(max_bytes):
+        lens = b.descs["len"].astype(np.int64)
+        n = int(np.searchsorted(np.cumsum(lens), max_bytes)) + 1
+        n = max(1, min(b.n, n))
+        end = int(b.descs["offset"][n - 1] + b.descs["len"][n - 1])
+        host = r["arena"][: end + 16].cpu().numpy()
+        if b.kind == "peso":
+            segs = b.descs[:n].copy()
+            want = int(r["out"][:n].to(torch.int64).sum().item())
+        else:
+            # IPv4 packets: the reference's per-packet cost is checksum_peso over
+            # the L4 bytes (tcp_in.c:80 / udp.c:410) plus checksum16 over the
+            # 20-byte header (ipv4.c:243, ~0.5 % of the bytes, not timed); the
+            # synthetic packets are IHL 5 with total_len == frame length
+            off = b.descs["offset"][:n].astype(np.int64)
+            hdr = host[off[:, None] + np.arange(20)[None, :]]
+            segs = np.zeros(n, pyoracle.PESO_DTYPE)
+            segs["offset"] = off + 20
+            segs["len"] = b.descs["len"][:n] - 20
+            segs["src"] = hdr[:, 12:16]
+            segs["dst"] = hdr[:, 16:20]
+            segs["protocol"] = hdr[:, 9]
+            want = int((r["out"][:n].to(torch.int64) >> 16).sum().item())
+        return host, segs, want, n
+
+    threads_all = min(256, os.cpu_count() or 1)  # orc_time_peso runs at most 256 threads
+    res = {"unit": "GiB/s", "kind": kind, "cores": 1, "cores_all": threads_all, "host_cpu": cpu_model()}
+    what = "segments" if b.kind == "peso" else "packets' L4 ranges"
+    big = min(b.total_bytes, 1 << 30)
+    for label, nbytes, secs in (("dram", big, seconds), ("cache", 96 << 20, seconds / 2)):
+        host, segs, want, n = sample(nbytes)
+        rate1, got_kind, cs1 = pyoracle.time_peso(host, segs, 1, secs, kind=kind)
+        rate_all, _, cs_all = pyoracle.time_peso(host, segs, threads_all, max(2.0, secs / 2), kind=kind)
+        part = {"value": round(rate1 / GIB, 3), "value_all": round(rate_all / GIB, 3),
+                "sample_bytes": int(segs["len"].sum()),
+                "sample": f"first {n} {what} of the {b.config} batch ({int(segs['len'].sum()) / 1e6:.0f} MB), "
+                          f"re-summed for >= {secs:.0f} s (1 thread) / {max(2.0, secs / 2):.0f} s "
+                          f"({threads_all} threads)",
+                "parity": bool(cs1 == want and cs_all == want)}
+        del host
+        if label == "dram":
+            res.update(part)
+        else:
+            res["cache_resident"] = part
+    return res
 
 
 # ------------------------------------------------------------ end to end
@@ -343,15 +456,77 @@ def legacy_latency(tc):
     return res
 
 
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes of this
+    script (one per GPU, torchrun's environment, rendezvous on 127.0.0.1)
+    before anything touches a GPU, and exit with their status.  N larger than
+    the node's GPU count is refused (TCSUM_DIST_BACKEND=gloo rehearses more
+    ranks than GPUs, ranks then sharing devices)."""
+    from tcp_amd import dist as D
+    backend = os.environ.get("TCSUM_DIST_BACKEND", "nccl")
+    if not args.cpu_rehearsal:
+        import torch
+        ndev = torch.cuda.device_count()  # counts without initialising the GPU
+        if args.gpus > ndev and backend == "nccl":
+            print(f"bench.py: --gpus {args.gpus} but this node has {ndev} GPU(s); "
+                  "refusing to time fewer GPUs than asked", file=sys.stderr)
+            return 2
+        from tcp_amd import build
+        build.build()  # once, before the ranks start
+    return D.spawn_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:])
+
+
+def rehearsal(args, rank, world) -> None:
+    """The N>1 path on CPU: the same rank slices, barrier and max-over-ranks
+    time as the GPU run, with a numpy byte sum over stand-in bytes in place of
+    the kernel.  Prints a line marked "rehearsal"; never a measurement."""
+    import numpy as np
+    from tcp_amd import dist as D
+    from tcp_amd import workload
+    dist = D.init("gloo")
+    b = workload.make_batch(args.config, rank=rank, n=4096)
+    data = np.random.default_rng(b.byte_base).integers(0, 256, b.alloc_bytes, dtype=np.uint8)
+    for _ in range(args.warmup):
+        data.sum(dtype=np.uint64)
+    D.barrier(dist)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        s = int(data.sum(dtype=np.uint64))
+    dt = time.perf_counter() - t0
+    D.barrier(dist)
+    t = D.max_over_ranks(dist, dt)
+    ranks = D.gather_objects(dist, {"rank": rank, "byte_base": int(b.byte_base), "packets": int(b.n),
+                                    "payload_bytes": int(b.total_bytes), "stand_in_sum": s})
+    if rank == 0:
+        print(json.dumps({"rehearsal": "cpu-gloo (numpy stand-in for the kernel; not a measurement)",
+                          "n_gpus": world, "steps": args.steps, "scaling": "weak",
+                          "value": round(world * b.total_bytes * args.steps / t / GIB, 3),
+                          "max_rank_s": t, "ranks": ranks}), flush=True)
+    D.barrier(dist)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
     from tcp_amd import dist as D
+    if args.gpus > 1 and not D.launched() and not args.pmc_child:
+        sys.exit(launch_ranks(args))
     rank, local, world = D.env()
+    if world != max(args.gpus, 1):
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+              "(torchrun --nproc-per-node N ... --gpus N, or bench.py --gpus N alone)", file=sys.stderr)
+        sys.exit(2)
+    if args.cpu_rehearsal:
+        rehearsal(args, rank, world)
+        return
     n_gpus = max(world, 1)
 
     traffic, pmc_note = None, "skipped"
+    trace, trace_note = None, "skipped"
     if not args.pmc_child and world == 1 and not args.no_pmc:
         traffic, pmc_note = pmc_traffic(args.config)  # before this process touches the GPU
+    if not args.pmc_child and world == 1 and not args.no_trace:
+        trace, trace_note = rocprof_trace(args.config, args.steps, args.warmup, args.settle_ms)
 
     import torch
     from tcp_amd import build
@@ -362,12 +537,17 @@ def main():
     # one process per GPU; TCSUM_DIST_BACKEND=gloo rehearses N ranks on fewer
     # GPUs (ranks share devices round-robin; RCCL refuses two ranks per GPU)
     backend = os.environ.get("TCSUM_DIST_BACKEND", "nccl")
-    dev = local % max(1, torch.cuda.device_count())
+    ndev = torch.cuda.device_count()
+    if ndev == 0 or (backend == "nccl" and local >= ndev):
+        print(f"bench.py: rank {rank} (local {local}) has no GPU of its own ({ndev} on this node)",
+              file=sys.stderr)
+        sys.exit(2)
+    dev = local % ndev
     torch.cuda.set_device(dev)
     dist = D.init(backend, dev)  # barrier + max-time only; no data-path collective
 
     global SETTLE_MS
-    SETTLE_MS = 0.0 if args.pmc_child else max(0.0, args.settle_ms)
+    SETTLE_MS = 0.0 if args.pmc_child and not args.trace_child else max(0.0, args.settle_ms)
     if args.pmc_child:
         time_config(torch, tc, workload, args.config, 0, args.steps, args.warmup)
         return
@@ -384,6 +564,16 @@ def main():
         roof["traffic_note"] = pmc_note
     else:
         roof["traffic_vs_algorithmic"] = round(traffic / algorithmic_bytes(b), 4)
+    if trace is None:
+        roof["rocprof_frac"] = None
+        roof["rocprof_note"] = trace_note
+    else:  # the same algorithmic bytes over the profiled child's median launch
+        med_ns, mean_ns, nl, kname = trace
+        roof["rocprof_frac"] = round(algorithmic_bytes(b) / (med_ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
+        roof["rocprof"] = {"kernel": kname, "launches": nl, "median_us": round(med_ns / 1e3, 1),
+                           "mean_us": round(mean_ns / 1e3, 1),
+                           "source": "rocprofv3 --kernel-trace --stats of bench.py --config "
+                                     f"{args.config} (same K/W/settle), run as a child of this bench"}
 
     line = {
         "metric": METRIC,
@@ -409,7 +599,7 @@ def main():
     if world == 1:
         if not args.no_cpu:
             try:
-                line["cpu_baseline"] = cpu_baseline(torch, head, args.cpu_seconds)
+                line["cpu_baseline"] = cpu_baseline(torch, head, args.cpu_seconds, args.cpu_kind)
             except Exception as e:  # reported, never fatal to the GPU numbers
                 line["cpu_baseline"] = {"value": None, "error": repr(e)}
         if not args.no_e2e:

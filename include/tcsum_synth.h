@@ -38,6 +38,15 @@ int tcsum_synth_ipv4(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, u
  * roofline.  sink: one device u32 (written only on a 2^-32 fluke). */
 int tcsum_probe_read(const void *p /*[dev]*/, uint64_t nbytes, uint32_t *sink /*[dev]*/, void *stream);
 
+/* The same plain read in the product kernels' own tile shape: `lanes` lanes
+ * share a unit of lanes*loads consecutive 16-B chunks (lane l loads chunks
+ * u*lanes + l), 256/lanes units per workgroup, workgroups in the product's
+ * XCD-grouped order (k_segments / k_ipv4 / k_segments_wg minus descriptors,
+ * masking and sums).  lanes x loads in {16,32} x {4,6,8}, 64 x {4,8},
+ * 256 x {4,8,16}; otherwise TCSUM_ERR_PARAM. */
+int tcsum_probe_tile(const void *p /*[dev]*/, uint64_t nbytes, int lanes, int loads, uint32_t *sink /*[dev]*/,
+                     void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -189,21 +189,25 @@ def synth_fill(byte_offset: int, nbytes: int, seed: int) -> np.ndarray:
 
 
 def time_peso(arena: np.ndarray, segs: np.ndarray, nthreads: int, min_seconds: float,
-              use_reference: bool):
+              kind: str = "reference"):
     """Bytes/s of a checksum_peso-shaped CPU routine over the batch.
 
-    use_reference=True times the reference's own checksum_peso
-    (oracle/_ref/libtcpref.so, built from /root/reference) -- "kind":
-    "reference"; otherwise this restatement ("kind": "port").
-    Returns (bytes_per_second, kind, checksum_of_checksums).
+    kind "reference" times the reference's own checksum_peso
+    (oracle/_ref/libtcpref.so, built from /root/reference) and raises
+    FileNotFoundError when it was not built; kind "port" times this
+    restatement.  Returns (bytes_per_second, kind, checksum_of_checksums).
     """
     L = lib()
-    kind = "port"
-    fn = ctypes.cast(L.orc_checksum_peso, ctypes.c_void_p).value
-    if use_reference and os.path.exists(REF_LIB_PATH):
+    if kind == "reference":
+        if not os.path.exists(REF_LIB_PATH):
+            raise FileNotFoundError(f"{REF_LIB_PATH} (the reference's checksum_peso) is not built: "
+                                    "make -C oracle ref in the build container")
         ref = ctypes.CDLL(REF_LIB_PATH)
         fn = ctypes.cast(ref.tcpref_peso, ctypes.c_void_p).value
-        kind = "reference"
+    elif kind == "port":
+        fn = ctypes.cast(L.orc_checksum_peso, ctypes.c_void_p).value
+    else:
+        raise ValueError(kind)
     cs = ctypes.c_uint64()
     rate = L.orc_time_peso(fn, _ptr(arena), _ptr(segs), segs.size, nthreads, min_seconds,
                            ctypes.byref(cs))

@@ -5,7 +5,7 @@
 # Usage: scripts/gpu.sh TIMEOUT_S 'command'
 limit=$1; shift
 for attempt in 1 2 3 4 5 6; do
-    rm -rf gpurun_out
+    rm -f gpurun_out/steps.log  # results of earlier calls stay (copy what counts to profiles/)
     out=$(timeout $((limit + 900)) /usr/local/graft/bin/gpurun --timeout "$limit" -- "$@" 2>&1)
     rc=$?
     echo "$out" | tail -4

@@ -1,5 +1,8 @@
 """Where does tx fill time go?  Interleaved rounds in one process: ipv4 sums,
-tx fill with stores, tx offload (the same kernel without the stores), rx verify."""
+tx fill with stores, tx fill re-reading the field lines with the default
+cache policy right before its stores (TCSUM_TX_RELOAD=1, IP_OPT_RELOAD), tx
+offload (the same kernel without the stores), rx verify.  The reload variant
+must leave the same bytes as the plain fill."""
 import os
 import sys
 
@@ -24,6 +27,14 @@ def tx():
     tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
 
 
+def tx_reload():
+    os.environ["TCSUM_TX_RELOAD"] = "1"
+    try:
+        tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
+    finally:
+        del os.environ["TCSUM_TX_RELOAD"]
+
+
 outo = torch.empty(b.n, dtype=torch.uint32, device="cuda")
 flo = torch.empty(b.n, dtype=torch.uint8, device="cuda")
 
@@ -36,7 +47,11 @@ def rx():
     tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes, verdict=verdict, want_flags=False)
 
 
-variants = {"sums": sums, "tx": tx, "tx_offload": tx_offload, "rx": rx}
+tx()
+ref = arena.clone()
+tx_reload()
+assert torch.equal(arena, ref), "the reload variant changed the filled bytes"
+variants = {"sums": sums, "tx": tx, "tx_reload": tx_reload, "tx_offload": tx_offload, "rx": rx}
 times = {k: [] for k in variants}
 for r in range(5):
     for k, fn in variants.items():

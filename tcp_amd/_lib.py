@@ -61,6 +61,7 @@ SIGNATURES = {
     "tcsum_synth_fill": (_I, [_V, _U64, _U64, _U64, _V]),
     "tcsum_synth_ipv4": (_I, [_V, _V, _U32, _U64, _V]),
     "tcsum_probe_read": (_I, [_V, _U64, _V, _V]),
+    "tcsum_probe_tile": (_I, [_V, _U64, _I, _I, _V, _V]),
 }
 
 _lib = None

@@ -42,6 +42,15 @@ def stale() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not stale():
         return LIB
+    import fcntl
+    with open(LIB + ".lock", "w") as lk:  # ranks of one node build once, not N times at once
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not force and not stale():
+            return LIB
+        return _build_locked(verbose)
+
+
+def _build_locked(verbose: bool) -> str:
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}",

@@ -519,6 +519,14 @@ int tcsum_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, void *strea
                : TCSUM_ERR_SYS;
 }
 
+int tcsum_probe_tile(const void *p, uint64_t nbytes, int lanes, int loads, uint32_t *sink, void *stream)
+{
+    if (!p || !sink || (reinterpret_cast<uintptr_t>(p) & 15u))
+        return TCSUM_ERR_PARAM;
+    const hipError_t e = tcsum::launch_probe_tile(p, nbytes, lanes, loads, sink, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TCSUM_OK : e == hipErrorInvalidValue ? TCSUM_ERR_PARAM : TCSUM_ERR_SYS;
+}
+
 // ------------------------------------------------------------ host batches
 
 namespace { // defined with the host-queue batches below

@@ -505,19 +505,33 @@ __global__ __launch_bounds__(256) void k_segments_pp(const uint8_t *__restrict__
 enum IpMode : int { IP_SUMS = 0, IP_TX = 1, IP_RX = 2 };
 // k_ipv4 `opts` bits (runtime, uniform over the grid)
 constexpr uint32_t IP_OPT_NO_STORE = 1u; // IP_TX: compute the fill's values, leave the packets alone
+// IP_TX experiment (TCSUM_TX_RELOAD=1): re-read the header chunk(s) holding the
+// fields with the default cache policy right before the stores, so the lines
+// the stores land in are L2-resident (tx fill).
+constexpr uint32_t IP_OPT_RELOAD = 2u;
 // launch_ipv4 mode 3: IP_TX kernels with IP_OPT_NO_STORE
 constexpr int IP_TX_OFFLOAD = 3;
 
-// x[k] = w[q + k] for k < 6, q in 0..3: two stages of selects, no branches.
-__device__ __forceinline__ void pick6(uint32_t q, const uint32_t w[12], uint32_t x[6])
+// The 20 fixed header bytes at byte s0 (0..15) of the three aligned chunks
+// h0, h1, h2, as five dwords: hd[k] = bytes [s0 + 4k, s0 + 4k + 4).  Two
+// stages of selects on named scalars pick dwords q = s0 >> 2 .. q + 5, then
+// v_alignbyte shifts by s0 & 3.  (Written over an array, w[q + k], clang
+// turned the selects back into a dynamically indexed alloca and promoted it
+// to 20 KiB of LDS per workgroup: ds_write/ds_read on every packet.)
+struct Hdr5 {
+    uint32_t d0, d1, d2, d3, d4;
+};
+__device__ __forceinline__ Hdr5 header_dwords(u32x4 h0, u32x4 h1, u32x4 h2, uint32_t s0)
 {
-    uint32_t y[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-        y[i] = (q & 1u) ? w[i + 1] : w[i];
-#pragma unroll
-    for (int k = 0; k < 6; ++k)
-        x[k] = (q & 2u) ? y[k + 2] : y[k];
+    const bool b1 = s0 & 4u, b2 = s0 & 8u;
+    const uint32_t y0 = b1 ? h0.y : h0.x, y1 = b1 ? h0.z : h0.y, y2 = b1 ? h0.w : h0.z, y3 = b1 ? h1.x : h0.w;
+    const uint32_t y4 = b1 ? h1.y : h1.x, y5 = b1 ? h1.z : h1.y, y6 = b1 ? h1.w : h1.z, y7 = b1 ? h2.x : h1.w;
+    const uint32_t x0 = b2 ? y2 : y0, x1 = b2 ? y3 : y1, x2 = b2 ? y4 : y2;
+    const uint32_t x3 = b2 ? y5 : y3, x4 = b2 ? y6 : y4, x5 = b2 ? y7 : y5;
+    const uint32_t r = s0 & 3u;
+    return Hdr5{__builtin_amdgcn_alignbyte(x1, x0, r), __builtin_amdgcn_alignbyte(x2, x1, r),
+                __builtin_amdgcn_alignbyte(x3, x2, r), __builtin_amdgcn_alignbyte(x4, x3, r),
+                __builtin_amdgcn_alignbyte(x5, x4, r)};
 }
 
 // Sum of the chunk's bytes that fall in [r0, r1) (offsets from the chunk base c;
@@ -586,24 +600,15 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     }
     issue_fence();
 
-    uint32_t hd[5];
-    {
-        const uint32_t w[12] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w, h2.x, h2.y, h2.z, h2.w};
-        uint32_t x[6];
-        pick6(s0 >> 2, w, x);
-        const uint32_t r = s0 & 3u;
-#pragma unroll
-        for (int k = 0; k < 5; ++k)
-            hd[k] = __builtin_amdgcn_alignbyte(x[k + 1], x[k], r);
-    }
-    const uint32_t b0h = hd[0] & 0xFFu;
+    const Hdr5 hd = header_dwords(h0, h1, h2, s0);
+    const uint32_t b0h = hd.d0 & 0xFFu;
     const uint32_t version = b0h >> 4;
     const uint32_t ihl4 = (b0h & 0xFu) << 2;
-    const uint32_t tl = (((hd[0] >> 16) & 0xFFu) << 8) | (hd[0] >> 24);
-    const uint32_t b6 = (hd[1] >> 16) & 0xFFu, b7 = hd[1] >> 24;
+    const uint32_t tl = (((hd.d0 >> 16) & 0xFFu) << 8) | (hd.d0 >> 24);
+    const uint32_t b6 = (hd.d1 >> 16) & 0xFFu, b7 = hd.d1 >> 24;
     const bool frag = (b6 & 0x20u) || (((b6 & 0x1Fu) << 8) | b7);
-    const uint32_t proto = (hd[2] >> 8) & 0xFFu;
-    const uint32_t stored_ip = hd[2] >> 16;
+    const uint32_t proto = (hd.d2 >> 8) & 0xFFu;
+    const uint32_t stored_ip = hd.d2 >> 16;
     uint32_t fl = 0;
     if (version != 4)
         fl |= TCSUM_PKT_BAD_VERSION;
@@ -711,8 +716,8 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
             }
             ip = ~fh & 0xFFFFu;
             if (proto == 6 || proto == 17) {
-                uint32_t q = add_halves(0u, hd[3]); // src, packet bytes 12..15
-                q = add_halves(q, hd[4]);           // dst, packet bytes 16..19
+                uint32_t q = add_halves(0u, hd.d3); // src, packet bytes 12..15
+                q = add_halves(q, hd.d4);           // dst, packet bytes 16..19
                 q += proto << 8;
                 q += bswap16((end - hl) & 0xFFFFu);
                 l4 = ~fold_step(f4 + fold16(q)) & 0xFFFFu;
@@ -724,6 +729,16 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
         }
         if constexpr (IPM == IP_TX) {
             if (!bad && !(opts & IP_OPT_NO_STORE)) { // stored in host order, like the struct fields
+                if (opts & IP_OPT_RELOAD) {
+                    const u32x4 *c0 = reinterpret_cast<const u32x4 *>((start + 10u) & ~(uintptr_t)15u);
+                    const u32x4 *c1 = reinterpret_cast<const u32x4 *>(
+                        (start + (field_on ? hl + fld + 1u : 11u)) & ~(uintptr_t)15u);
+                    const u32x4 t0 = load16<false>(c0), t1 = load16<false>(c1);
+                    uint32_t dep;
+                    asm volatile("v_and_b32 %0, 0, %1" : "=v"(dep) : "v"(t0.x ^ t1.w)); // 0, opaque: stores wait
+                    ip += dep;
+                    l4 += dep;
+                }
                 pp[10] = (uint8_t)ip;
                 pp[11] = (uint8_t)(ip >> 8);
                 if (field_on) {
@@ -1132,6 +1147,52 @@ __global__ __launch_bounds__(256) void k_probe_read(const u32x4 *__restrict__ p,
         sink[0] = acc;
 }
 
+// The same plain read in the product's own tile shape: G lanes share a
+// "unit" of G*U consecutive chunks (lane gl loads chunks u*G + gl, u < U),
+// 256/G units per workgroup, workgroups in the product's XCD-grouped order --
+// k_segments / k_ipv4 minus descriptors, edge masking and sums (G = 256: one
+// unit per workgroup, k_segments_wg's shape).  The ceiling the product kernel
+// is compared with, on the same bytes.
+template <int G, int U>
+__global__ __launch_bounds__(256) void k_probe_tile(const u32x4 *__restrict__ p, uint64_t nchunks,
+                                                    uint32_t *__restrict__ sink, uint32_t xg)
+{
+    const uint64_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    const uint32_t gl = threadIdx.x & (G - 1);
+    const uint64_t base = (blk * (256u / G) + threadIdx.x / G) * (uint64_t)(G * U);
+    uint32_t acc = 0;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t idx = base + (uint64_t)(u * G) + gl;
+        v[u] = idx < nchunks ? load16<true>(p + idx) : u32x4(0u);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    if (acc == 0x9E3779B9u)
+        sink[0] = acc;
+}
+
+hipError_t launch_probe_tile(const void *p, uint64_t nbytes, int G, int U, uint32_t *sink, hipStream_t stream)
+{
+    const uint64_t nchunks = nbytes / 16;
+    if (nchunks == 0)
+        return hipSuccess;
+    const uint32_t xg = (uint32_t)pick_geometry(1500).xcd; // the product's order (TCSUM_XCD applies too)
+    const dim3 grid((uint32_t)((nchunks + 256ull * U - 1) / (256ull * U)));
+    const u32x4 *q = static_cast<const u32x4 *>(p);
+#define TCSUM_PT(GG, UU)                                                                         \
+    if (G == GG && U == UU) {                                                                  \
+        hipLaunchKernelGGL((k_probe_tile<GG, UU>), grid, dim3(256), 0, stream, q, nchunks, sink, xg); \
+        return hipGetLastError();                                                              \
+    }
+    TCSUM_PT(16, 4) TCSUM_PT(16, 6) TCSUM_PT(16, 8) TCSUM_PT(32, 4) TCSUM_PT(32, 6) TCSUM_PT(32, 8)
+    TCSUM_PT(64, 4) TCSUM_PT(64, 8) TCSUM_PT(256, 4) TCSUM_PT(256, 8) TCSUM_PT(256, 16)
+#undef TCSUM_PT
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, hipStream_t stream)
 {
     const uint64_t nchunks = nbytes / 16;
@@ -1361,8 +1422,11 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
     const dim3 grid((uint32_t)((n + per_block - 1) / per_block));
     const uint32_t xg = (uint32_t)g.xcd;
     switch (ip_mode) {
-    case IP_TX:
-        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, 0u, xg, stream);
+    case IP_TX: {
+        const char *rl = getenv("TCSUM_TX_RELOAD"); // measurement only (IP_OPT_RELOAD)
+        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict,
+                             rl && atoi(rl) ? IP_OPT_RELOAD : 0u, xg, stream);
+    }
     case IP_TX_OFFLOAD: // the tx values into `out` only; the packets are not written
         return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, IP_OPT_NO_STORE, xg,
                              stream);

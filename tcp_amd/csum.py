@@ -314,6 +314,17 @@ def probe_read(buf, nbytes: int | None = None, sink=None, stream=None):
     return sink
 
 
+def probe_tile(buf, nbytes: int, lanes: int, loads: int, sink=None, stream=None):
+    """Plain streaming read of `buf` in the product kernels' tile shape
+    (tcsum_probe_tile): the ceiling the checksum kernel is compared with."""
+    torch = _torch()
+    if sink is None:
+        sink = torch.zeros(1, dtype=torch.uint32, device=buf.device)
+    _lib.check(_lib.lib().tcsum_probe_tile(buf.data_ptr(), nbytes, lanes, loads, sink.data_ptr(),
+                                           _stream_ptr(stream)), "tcsum_probe_tile")
+    return sink
+
+
 def pick_geometry(mean_len: int):
     g, u = ctypes.c_int(), ctypes.c_int()
     _lib.lib().tcsum_pick_geometry(mean_len, ctypes.byref(g), ctypes.byref(u))

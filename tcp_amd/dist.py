@@ -8,6 +8,9 @@ barrier around the timed region and the max-over-ranks time.
 from __future__ import annotations
 
 import os
+import socket
+import subprocess
+import sys
 
 
 def env():
@@ -52,3 +55,49 @@ def gather_objects(dist, obj):
     out = [None] * dist.get_world_size()
     dist.all_gather_object(out, obj)
     return out
+
+
+def launched() -> bool:
+    """True when a launcher (torchrun, or spawn_ranks below) set up the ranks."""
+    return "WORLD_SIZE" in os.environ
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv: list[str], extra_env: dict | None = None, timeout: float | None = None) -> int:
+    """Start n rank processes of ``python argv...`` (one per GPU) with the
+    torchrun environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1,
+    MASTER_PORT) and wait for all of them.  Children are started before the
+    caller touches any GPU, as separate processes (never exec).  Returns 0 when
+    every rank exits 0, else the first nonzero exit status (a rank killed by a
+    signal counts as 128 + signal)."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        e = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        e.update(extra_env or {})
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=e))
+    rc = 0
+    for p in procs:
+        try:
+            code = p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                if q.poll() is None:
+                    q.kill()
+            p.wait()
+            code = 124
+        code = 128 - code if code < 0 else code
+        if code and not rc:
+            rc = code
+            for q in procs:  # one rank failed: the others would hang in the next barrier
+                if q.poll() is None:
+                    q.terminate()
+    return rc

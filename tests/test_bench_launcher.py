@@ -1,0 +1,52 @@
+"""bench.py's N-rank launcher on CPU (gloo): `bench.py --gpus N` with no
+launcher starts N ranks itself; a GPU count the node cannot provide, or a
+WORLD_SIZE that differs from --gpus, fails loudly."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def run(args, env=None, timeout=240):
+    e = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, timeout=timeout,
+                          env=e, cwd=ROOT)
+
+
+@pytest.mark.timeout(300)
+def test_launcher_world2_rehearsal():
+    r = run(["--gpus", "2", "--cpu-rehearsal", "--steps", "3", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0 alone prints
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["value"] > 0
+    ranks = sorted(line["ranks"], key=lambda x: x["rank"])
+    assert [x["rank"] for x in ranks] == [0, 1]
+    # weak scaling: consecutive, disjoint slices of one global stream
+    assert ranks[0]["byte_base"] == 0 and ranks[1]["byte_base"] >= ranks[0]["payload_bytes"]
+    assert ranks[0]["stand_in_sum"] != ranks[1]["stand_in_sum"]
+
+
+@pytest.mark.timeout(300)
+def test_launcher_refuses_missing_gpus():
+    """No GPU here: --gpus 2 must exit nonzero, not time fewer GPUs."""
+    r = run(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+    assert r.returncode != 0
+    assert "GPU" in r.stderr
+
+
+@pytest.mark.timeout(120)
+def test_world_size_must_match_gpus():
+    r = run(["--gpus", "2", "--steps", "1"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
+    r = run(["--steps", "1", "--cpu-rehearsal"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2

@@ -20,9 +20,11 @@
  * (pktbuf.c:203 -> :44) and deadlocks on a default pthread mutex.
  */
 #include <pthread.h>
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "net.h"
 #include "net_api.h"
@@ -131,6 +133,8 @@ static int udp_echo(void)
         ssize_t got = recvfrom(s, in, sizeof in, 0, (struct sockaddr *)&from, &len);
         if (got != n || memcmp(in, out, (size_t)n) != 0)
             return fprintf(stderr, "udp round %d: sent %d bytes, echo %ld\n", r, n, (long)got), 1;
+        if (r % 50 == 0)
+            printf("udp round %d ok\n", r);
     }
     close(s);
     printf("udp: %d datagrams (1-1400 B) echoed intact\n", UDP_ROUNDS);
@@ -172,23 +176,8 @@ static int tcp_echo(void)
     return 0;
 }
 
-int main(int argc, char **argv)
+static void print_engine(void)
 {
-    int do_tcp = !(argc > 1 && strcmp(argv[1], "--udp-only") == 0);
-#ifdef NET_CHECKSUM_GPU
-    if (tcsum_device_count() < 1) /* net_init ignores net_plat_init's result (net.c:22) */
-        return fprintf(stderr, "no gfx950 device: the GPU build cannot run here\n"), 2;
-#endif
-    if (net_init() != NET_ERR_OK) /* net_plat_init -> net_csum_gpu_init (HIP device, pinned staging) */
-        return fprintf(stderr, "net_init failed (no gfx950 device?)\n"), 2;
-    net_start();
-    sys_thread_create(udp_server, (void *)0);
-    if (do_tcp)
-        sys_thread_create(tcp_server, (void *)0);
-    sys_sleep(100);
-    int rc = udp_echo();
-    if (!rc && do_tcp)
-        rc = tcp_echo();
 #ifdef NET_CHECKSUM_GPU
     net_csum_gpu_stats_t st;
     net_csum_gpu_stats(&st);
@@ -197,14 +186,54 @@ int main(int argc, char **argv)
            (unsigned long long)st.tx_frames, (unsigned long long)st.tx_batches,
            (unsigned long long)st.rx_frames, (unsigned long long)st.rx_batches,
            (unsigned long long)st.rx_ip_filled, (unsigned long long)st.rx_used);
+#else
+    printf("engine: none (the reference's own CPU checksum, configs[0])\n");
+#endif
+}
+
+static const char *volatile stage = "start";
+static void watchdog(int sig)
+{
+    printf("watchdog: no progress for 60 s at stage '%s'\n", stage);
+    print_engine();
+    _exit(3);
+}
+
+int main(int argc, char **argv)
+{
+    setvbuf(stdout, NULL, _IONBF, 0);
+    signal(SIGALRM, watchdog);
+    alarm(60);
+    int do_tcp = !(argc > 1 && strcmp(argv[1], "--udp-only") == 0);
+#ifdef NET_CHECKSUM_GPU
+    if (tcsum_device_count() < 1) /* net_init ignores net_plat_init's result (net.c:22) */
+        return fprintf(stderr, "no gfx950 device: the GPU build cannot run here\n"), 2;
+#endif
+    stage = "net_init";
+    if (net_init() != NET_ERR_OK) /* net_plat_init -> net_csum_gpu_init (HIP device, pinned staging) */
+        return fprintf(stderr, "net_init failed\n"), 2;
+    stage = "net_start";
+    net_start();
+    sys_thread_create(udp_server, (void *)0);
+    if (do_tcp)
+        sys_thread_create(tcp_server, (void *)0);
+    sys_sleep(100);
+    stage = "udp";
+    int rc = udp_echo();
+    stage = "tcp";
+    if (!rc && do_tcp)
+        rc = tcp_echo();
+    alarm(0);
+    print_engine();
+#ifdef NET_CHECKSUM_GPU
+    net_csum_gpu_stats_t st;
+    net_csum_gpu_stats(&st);
     if (!rc && (st.tx_frames < 2 * UDP_ROUNDS || st.rx_frames < 2 * UDP_ROUNDS ||
                 st.rx_ip_filled != st.rx_frames || st.rx_used < 4 * UDP_ROUNDS)) {
         fprintf(stderr, "the frames did not all go through the GPU fill and sums\n");
         rc = 1;
     }
-#else
-    printf("engine: none (the reference's own CPU checksum, configs[0])\n");
 #endif
     fflush(stdout);
-    exit(rc); /* the stack's threads never return */
+    _exit(rc); /* the stack's threads never return; skip exit-time teardown under them */
 }

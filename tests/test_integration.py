@@ -42,7 +42,7 @@ def test_loop_echo_gpu():
     fill in loop_xmit, rx checksums from the batched sums in do_netif_in."""
     exe = os.path.join(BUILD, "loop_echo")
     assert os.path.exists(exe), "built in the build container by make -C integration (__graft_entry__.build)"
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=150)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=90)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "udp: 200 datagrams" in r.stdout and "tcp: 65536 bytes echoed intact" in r.stdout
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("engine:")][0]

@@ -574,19 +574,27 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     const uint32_t s0 = (uint32_t)(start & 15u);
     const u32x4 *base = reinterpret_cast<const u32x4 *>(pp - s0);
 
-    // fixed header: bytes [s0, s0 + 20) of base[0..2]
-    const u32x4 *hb = big_enough ? base : &g_zero_chunk;
-    const uint32_t h1i = big_enough ? 1u : 0u;
-    const uint32_t h2i = big_enough ? (s0 > 12 ? 2u : 1u) : 0u;
-    const u32x4 h0 = load16<false>(hb);
-    const u32x4 h1 = load16<false>(hb + h1i);
-    const u32x4 h2v = load16<false>(hb + h2i);
-    const u32x4 h2 = s0 > 12 ? h2v : u32x4(0u);
-
     // IPv4 bytes past 65,535 (the largest total_len) never count: bound the
     // loads there, so every position below fits comfortably in 32 bits
     const uint32_t frame_ld = frame < 65600u ? frame : 65600u;
     const uint32_t nch = big_enough ? (frame_ld + s0 + 15) >> 4 : 0u;
+
+    // fixed header: bytes [s0, s0 + 20) of base[0..2]
+    const u32x4 *hb = big_enough ? base : &g_zero_chunk;
+    const uint32_t h1i = big_enough ? 1u : 0u;
+    const u32x4 h0 = load16<false>(hb);
+    const u32x4 h1 = load16<false>(hb + h1i);
+    u32x4 h2, c2 = u32x4(0u), c3 = u32x4(0u);
+    if constexpr (IPM == IP_RX) {
+        // chunks 2 and 3 as well: an IHL-5 packet's TCP/UDP ports, data offset
+        // and flags (L4 bytes 0-3, 12-13) lie in chunks 1..3
+        c2 = load16<false>(nch > 2 ? base + 2 : &g_zero_chunk);
+        c3 = load16<false>(nch > 3 && s0 >= 12 ? base + 3 : &g_zero_chunk);
+        h2 = s0 > 12 ? c2 : u32x4(0u);
+    } else {
+        const u32x4 h2v = load16<false>(hb + (big_enough ? (s0 > 12 ? 2u : 1u) : 0u));
+        h2 = s0 > 12 ? h2v : u32x4(0u);
+    }
     const u32x4 *dbase = nch ? base : &g_zero_chunk;
     const uint32_t dlast = nch ? nch - 1u : 0u;
 
@@ -609,6 +617,15 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     const bool frag = (b6 & 0x20u) || (((b6 & 0x1Fu) << 8) | b7);
     const uint32_t proto = (hd.d2 >> 8) & 0xFFu;
     const uint32_t stored_ip = hd.d2 >> 16;
+    // rx: TCP/UDP header words of an IHL-5 packet (L4 bytes 0-3: ports;
+    // 12-15: data offset, flags), taken now from chunks 1..3 so those die here
+    uint32_t l4w0 = 0, l4w3 = 0;
+    if constexpr (IPM == IP_RX) {
+        const bool cw1 = s0 + 20u < 32u;
+        const Hdr5 l4h = header_dwords(cw1 ? h1 : c2, cw1 ? c2 : c3, u32x4(0u), (s0 + 4u) & 15u);
+        l4w0 = l4h.d0;
+        l4w3 = l4h.d3;
+    }
     uint32_t fl = 0;
     if (version != 4)
         fl |= TCSUM_PKT_BAD_VERSION;
@@ -640,7 +657,7 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     const int f0 = field_on ? (int)(hl + fld) + (int)s0 : -64;
     const int i0 = (int)s0 + 10; // IPv4 header checksum field
 
-    uint32_t acc_h = 0, acc_l = 0, acc_f = 0, acc_pt = 0, acc_tw = 0;
+    uint32_t acc_h = 0, acc_l = 0, acc_f = 0;
     // one pass of U chunks per lane starting at chunk b0 (pass 0: the loads
     // already in flight; later passes load and sum inside one iteration, so
     // no vector registers are carried around the loop -- see frame_consume)
@@ -651,9 +668,7 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
             const uint32_t idx = b0 + u * G + gl;
             const bool valid = idx < nch;
             const int c = (int)(16u * idx);
-            // rx reads the first 14 L4 bytes too (ports, data offset, flags)
-            const bool inner = valid && c >= h_end && c + 16 <= l_end && (f0 + 2 <= c || f0 >= c + 16) &&
-                               (IPM != IP_RX || c >= h_end + 14);
+            const bool inner = valid && c >= h_end && c + 16 <= l_end && (f0 + 2 <= c || f0 >= c + 16);
             if (valid && !inner) { // header chunks, the field chunk(s), the last chunk: rare
                 uint32_t th = region_sum(vv[u], c, (int)s0, h_end);
                 uint32_t tl4 = region_sum(vv[u], c, h_end, l_end);
@@ -666,15 +681,6 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
                 }
                 if (IPM == IP_TX)
                     th -= region_sum(vv[u], c, i0, i0 + 2); // ipv4.c:643
-                if (IPM == IP_RX) {
-                    // L4 header words as byte sums (zero iff every byte is zero;
-                    // a 2-byte region sums to <= 0xFFFF): TCP/UDP ports at
-                    // +0/+2, the TCP data-offset byte and flag word at +12
-                    acc_pt += region_sum(vv[u], c, h_end, h_end + 2) +
-                              (region_sum(vv[u], c, h_end + 2, h_end + 4) << 16);
-                    acc_tw += region_sum(vv[u], c, h_end + 12, h_end + 14) +
-                              (region_sum(vv[u], c, h_end + 12, h_end + 13) << 16);
-                }
                 ph += th;
                 pl += tl4;
             }
@@ -696,11 +702,8 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     }
     acc_h = group_sum<G>(acc_h);
     acc_l = group_sum<G>(acc_l);
-    if (IPM == IP_RX) {
+    if (IPM == IP_RX)
         acc_f = group_sum<G>(acc_f);
-        acc_pt = group_sum<G>(acc_pt);
-        acc_tw = group_sum<G>(acc_tw);
-    }
 
     if (live && gl == 0) {
         uint32_t ip = 0, l4 = 0;
@@ -752,9 +755,22 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
             // is_pkt_ok, then the L4 input ip_normal_in dispatches to
             // (ipv4.c:420-470), up to socket lookup.  Pinned by the reference
             // stack's own verdicts (tests/golden/ipv4_rx_*, oracle/stack_gen.c).
-            const uint32_t sport = acc_pt & 0xFFFFu, dport = acc_pt >> 16, fword = acc_tw & 0xFFFFu;
-            const uint32_t dob = (h_end + 12) & 1 ? (acc_tw >> 24) : ((acc_tw >> 16) & 0xFFu);
-            const uint32_t doff4 = (dob >> 4) << 2;
+            // TCP/UDP header words (L4 bytes 0-3: ports; 12-15: data offset,
+            // flags) from the 32 bytes at chunk (s0 + ihl4) / 16: chunks 1..3
+            // already in registers for IHL 5, two loads of this lane otherwise
+            uint32_t ports = l4w0, oflags = l4w3;
+            const bool l4_gates = version == 4 && ihl4 >= 20 && tl <= frame && tl >= ihl4 + 8u && !frag &&
+                                  (proto == 6 || proto == 17);
+            if (l4_gates && ihl4 != 20) { // IPv4 options: two loads of this lane
+                const uint32_t o = s0 + ihl4, cw = o >> 4;
+                const u32x4 wa = load16<false>(base + cw);
+                const u32x4 wb = load16<false>(cw + 1 < nch ? base + cw + 1 : &g_zero_chunk);
+                const Hdr5 l4h = header_dwords(wa, wb, u32x4(0u), o & 15u);
+                ports = l4h.d0;
+                oflags = l4h.d3;
+            }
+            const uint32_t sport = ports & 0xFFFFu, dport = ports >> 16, fword = oflags & 0xFFFFu;
+            const uint32_t doff4 = ((oflags & 0xFFu) >> 4) << 2;
             int v8;
             if (!big_enough)
                 v8 = TCSUM_ERR_SIZE; // pktbuf_set_cont(buf, 20), ipv4.c:475

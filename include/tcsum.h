@@ -316,6 +316,15 @@ void tcsum_host_free(void *p);
 int tcsum_host_register(void *p, size_t bytes);
 int tcsum_host_unregister(void *p);
 
+/* Free every buffer the batch calls cache on `device` between calls: the
+ * HBM copy of host spans (tcsum_host_batch_peso, the copy-engine path of the
+ * host-queue batches), descriptors, and the pinned host-queue staging; a
+ * running queue / call server is stopped first.  The next call allocates
+ * again.  (The copy-engine path keeps at most $TCSUM_HOSTQ_DMA_KEEP_MB, default
+ * 256, between calls by itself.)  Returns TCSUM_OK, TCSUM_ERR_PARAM, or
+ * TCSUM_ERR_SYS. */
+int tcsum_release(int device);
+
 /* Number of usable gfx950 devices (0 when none); never aborts. */
 int tcsum_device_count(void);
 

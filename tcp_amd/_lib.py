@@ -62,6 +62,7 @@ SIGNATURES = {
     "tcsum_synth_ipv4": (_I, [_V, _V, _U32, _U64, _V]),
     "tcsum_probe_read": (_I, [_V, _U64, _V, _V]),
     "tcsum_probe_tile": (_I, [_V, _U64, _I, _I, _V, _V]),
+    "tcsum_release": (_I, [_I]),
 }
 
 _lib = None

@@ -350,7 +350,8 @@ int tcsum_host_register(void *p, size_t bytes)
 {
     if (!p || bytes == 0)
         return TCSUM_ERR_PARAM;
-    if (hipHostRegister(p, bytes, hipHostRegisterMapped) != hipSuccess) {
+    // portable + mapped, like tcsum_host_alloc: every GPU of a *_multi batch maps it
+    if (hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) {
         (void)hipGetLastError();
         return TCSUM_ERR_SYS;
     }
@@ -1120,6 +1121,37 @@ struct SrvReaper {
 std::once_flag g_reap_once;
 void reap_at_exit() { std::call_once(g_reap_once, [] { atexit(reap_servers); }); }
 
+// Give back every cached batch buffer of a device (tcsum_release): the HBM
+// copy of host spans and descriptors, and the pinned host-queue staging.  The
+// servers go first: their next job would name the freed buffers.
+int release_ctx(Ctx &c)
+{
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (!c.ready)
+        return TCSUM_OK;
+    if (hipSetDevice(c.device) != hipSuccess)
+        return TCSUM_ERR_SYS;
+    if ((c.srv_running && srv_stop(c) != TCSUM_OK) || (c.cs_running && cs_stop(c) != TCSUM_OK))
+        return TCSUM_ERR_SYS;
+    for (hipStream_t st : c.hs)
+        (void)hipStreamSynchronize(st);
+    (void)hipStreamSynchronize(c.stream);
+    for (void *p : {(void *)c.d_arena, (void *)c.d_descs, (void *)c.d_out})
+        if (p)
+            (void)hipFree(p);
+    c.d_arena = nullptr;
+    c.d_descs = nullptr;
+    c.d_out = nullptr;
+    c.d_arena_cap = c.d_descs_cap = c.d_out_cap = 0;
+    for (Pinned *q : {&c.q_desc, &c.q_res, &c.q_arena}) {
+        if (q->h)
+            (void)hipHostFree(q->h);
+        q->h = q->d = nullptr;
+        q->cap = 0;
+    }
+    return TCSUM_OK;
+}
+
 // IPv4 batch over packets in host memory (the stack's netif queues): pinned
 // arenas are read -- and for tx written -- in place by the kernel over PCIe;
 // a pageable arena is first copied into pinned staging (and copied back after
@@ -1194,10 +1226,14 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     // one copy stream into HBM, each piece's kernel behind its copy's event
     // (tcsum_host_batch_peso's pipeline): 50.7 against 49.3 GiB/s for 1M
     // mixed frames (profiles/r01/hostq_dma.txt).  TCSUM_HOSTQ_DMA_KB: the
-    // span from which it is used (0 = never).
+    // span from which it is used (0 = never).  Only for DENSE batches -- the
+    // packets cover at least 3/4 of their span: a few frames spread over a big
+    // pinned pool would otherwise move gigabytes to sum kilobytes, where the
+    // in-place path reads only the packets' own bytes.
     const uint64_t dma_min = (uint64_t)env_int("TCSUM_HOSTQ_DMA_KB", 256 << 10) << 10;
     const uint64_t alo = lo & ~uint64_t(15), ahi = std::min<uint64_t>(arena_bytes, (hi + 15) & ~uint64_t(15));
-    bool dma = !staged && ip_mode != 1 && in_order && dma_min && hi > lo && hi - lo >= dma_min;
+    bool dma = !staged && ip_mode != 1 && in_order && dma_min && hi > lo && hi - lo >= dma_min &&
+               total * 4 >= (hi - lo) * 3;
     if (dma && (size_t)(ahi - alo) + 32 > c.d_arena_cap) {
         // no room in HBM for the span: the in-place path below needs none
         if (c.d_arena)
@@ -1217,18 +1253,21 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
         size_t k = 0;
         for (uint32_t i0 = 0; i0 < n && e == hipSuccess; ++k) {
             uint32_t i1 = i0;
-            uint64_t bytes = 0, end = copied_hi;
+            uint64_t bytes = 0, end = copied_hi, first = UINT64_MAX;
             while (i1 < n && (i1 == i0 || bytes < kPiece)) {
                 if (pkts[i1].len) {
                     bytes += pkts[i1].len;
+                    first = std::min<uint64_t>(first, pkts[i1].offset);
                     end = std::max<uint64_t>(end, pkts[i1].offset + pkts[i1].len);
                 }
                 ++i1;
             }
             end = std::min<uint64_t>(arena_bytes, (end + 15) & ~uint64_t(15));
-            if (end > copied_hi) {
-                e = hipMemcpyAsync(dbase + copied_hi, host_arena + copied_hi, end - copied_hi, hipMemcpyHostToDevice,
-                                   cs);
+            // this piece's own span (the 16-byte chunks its packets touch), not
+            // the gap before it
+            const uint64_t from = std::max<uint64_t>(copied_hi, first == UINT64_MAX ? end : first & ~uint64_t(15));
+            if (end > from) {
+                e = hipMemcpyAsync(dbase + from, host_arena + from, end - from, hipMemcpyHostToDevice, cs);
                 copied_hi = end;
             }
             hipEvent_t ev = c.hev[k % kHostEvents];
@@ -1243,6 +1282,14 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
             i0 = i1;
         }
         const hipError_t s1 = hipStreamSynchronize(ks), s2 = hipStreamSynchronize(cs);
+        // the HBM copy of the span is cached for the next batch only up to
+        // TCSUM_HOSTQ_DMA_KEEP_MB (default 256): a one-off multi-GiB verify
+        // does not keep its span allocated for the life of the process
+        if (c.d_arena_cap > ((size_t)env_int("TCSUM_HOSTQ_DMA_KEEP_MB", 256) << 20)) {
+            (void)hipFree(c.d_arena);
+            c.d_arena = nullptr;
+            c.d_arena_cap = 0;
+        }
         if (e != hipSuccess || s1 != hipSuccess || s2 != hipSuccess)
             return TCSUM_ERR_SYS;
         goto results;
@@ -1531,6 +1578,13 @@ uint16_t checksum_peso(tcsum_pktbuf_t *buf, const tcsum_ipaddr_t *dest, const tc
                                                 c.d_stage, c.d_desc, 1, c.d_result, 0u, c.stream);
     run_sync(c, e);
     return *c.result;
+}
+
+int tcsum_release(int device)
+{
+    if (device < 0 || device >= kMaxDev)
+        return TCSUM_ERR_PARAM;
+    return release_ctx(g_ctx[device]);
 }
 
 } // extern "C"

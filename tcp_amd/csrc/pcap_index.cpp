@@ -416,7 +416,8 @@ int pcapng_index(const uint8_t *f, uint64_t file_bytes, tcsum_pkt_t *pkts, int8_
         if (file_bytes - body < 12)
             return pcapng_index_seq(f, file_bytes, pkts, l2_verdict, max_frames, n_frames);
         const uint32_t type = rd32(f + body, swap), len = rd32(f + body + 4, swap);
-        if (len < 12 || (len & 3u) || len > file_bytes - body || (body > 0 && type == kShb))
+        if (len < 12 || (len & 3u) || len > file_bytes - body || (body > 0 && type == kShb) ||
+            rd32(f + body + len - 4, swap) != len) // the walk's own checks decide (ERR_PARAM, SIZE)
             return pcapng_index_seq(f, file_bytes, pkts, l2_verdict, max_frames, n_frames);
         if (type == kEpb || type == kPb || type == kSpb)
             break;
@@ -455,10 +456,9 @@ int pcapng_index(const uint8_t *f, uint64_t file_bytes, tcsum_pkt_t *pkts, int8_
             return S_SEQ;
         fr.next = q + len;
         if (type == kSpb) {
-            if (len < 16)
-                return S_BAD;
             fr.data = q + 12;
-            fr.caplen = std::min<uint32_t>(rd32(f + q + 8, swap), len - 16);
+            // as the one-piece walk: an SPB too short for its length word is an empty frame
+            fr.caplen = len < 16 ? 0u : std::min<uint32_t>(rd32(f + q + 8, swap), len - 16);
             if (!ifs.empty() && ifs[0].snaplen)
                 fr.caplen = std::min(fr.caplen, ifs[0].snaplen);
             fr.iface = 0;

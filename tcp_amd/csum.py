@@ -335,6 +335,11 @@ def device_count() -> int:
     return _lib.lib().tcsum_device_count()
 
 
+def release(device: int = 0) -> None:
+    """Free the buffers the batch calls cache on `device` (tcsum_release)."""
+    _lib.check(_lib.lib().tcsum_release(device), "tcsum_release")
+
+
 def plat_init(device: int = 0) -> None:
     _lib.check(_lib.lib().tcsum_plat_init(device), "tcsum_plat_init")
 

@@ -237,3 +237,36 @@ def test_host_pinned_copy_engine_path(tc, oracle, monkeypatch, mode):
     finally:
         del keep
         ha.free()
+
+
+@pytest.mark.parametrize("mode", ["sums", "rx"])
+def test_host_sparse_batch_and_release(tc, oracle, mode, monkeypatch):
+    """A few frames spread over a large pinned pool (the packets cover far
+    less than 3/4 of their span): the copy-engine path is not taken (it would
+    move the whole span), results equal the oracle; tcsum_release frees the
+    cached buffers and the next call allocates them again."""
+    monkeypatch.setenv("TCSUM_HOSTQ_DMA_KB", "1")
+    cases, pool = G.ipv4_rx_cases()
+    take = cases[:64]
+    stride = 1 << 20  # one frame per MiB: 64 frames over a 64 MiB pool
+    ha = tc.HostArena(64 * stride + 4096)
+    try:
+        ha.array[:] = 0
+        pk = np.zeros(take.size, tc.PKT_DTYPE)
+        for i, c in enumerate(take):
+            off, n = int(c["pool_off"]), int(c["frame_len"])
+            ha.array[i * stride + 7: i * stride + 7 + n] = pool[off: off + n]
+            pk["offset"][i] = i * stride + 7
+            pk["len"][i] = n
+        for rep in range(2):
+            if mode == "rx":
+                v, out, fl = tc.host_batch_ipv4_rx_verify(ha, pk)
+                np.testing.assert_array_equal(v, take["verdict"])
+            else:
+                out, fl = tc.host_batch_ipv4(ha, pk)
+            eo, ef = oracle.batch_ipv4(ha.array, pk, nthreads=4)
+            np.testing.assert_array_equal(out, eo)
+            np.testing.assert_array_equal(fl, ef)
+            tc.release(0)
+    finally:
+        ha.free()

@@ -347,3 +347,40 @@ def test_cli_verify_and_fill(tmp_path):
     assert r.stdout.startswith(f"{len(before)} frames: ")
     want, _, _ = PB.build(after, PB.RAW)
     assert dst.read_bytes() == want
+
+
+def test_pcapng_parallel_walk_same_acceptance(pcap, monkeypatch):
+    """The parallel pcapng walk accepts exactly what the one-piece walk
+    accepts: a header-region block whose trailing length disagrees is refused
+    by both; a Simple Packet Block too short for its length word is an empty
+    frame for both."""
+    import struct
+    rng = np.random.default_rng(7)
+    frames = [rng.integers(0, 256, int(rng.integers(20, 300)), dtype=np.uint8).tobytes() for _ in range(3000)]
+    buf, offs, lens = PB.build_ng(frames, (PB.RAW,), block="spb", extra_blocks=False)
+    # (a) corrupt the IDB's trailing length (the IDB follows the 28-byte SHB)
+    idb_len = struct.unpack_from("<I", buf, 28 + 4)[0]
+    bad = bytearray(buf)
+    struct.pack_into("<I", bad, 28 + idb_len - 4, idb_len + 4)
+    results = []
+    for kb in (None, "1"):
+        if kb is None:
+            monkeypatch.delenv("TCSUM_PCAP_PIECE_KB", raising=False)
+        else:
+            monkeypatch.setenv("TCSUM_PCAP_PIECE_KB", kb)
+        with pytest.raises(Exception):
+            pcap.index(bytes(bad))
+    # (b) a 12-byte SPB (no length word) in the middle of the packet blocks
+    k = int(offs[1500]) - 12  # the SPB of frame 1500 starts 12 bytes before its data
+    short = struct.pack("<III", 3, 12, 12)
+    good = bytes(buf[:k]) + short + bytes(buf[k:])
+    for kb in (None, "1", "4"):
+        if kb is None:
+            monkeypatch.delenv("TCSUM_PCAP_PIECE_KB", raising=False)
+        else:
+            monkeypatch.setenv("TCSUM_PCAP_PIECE_KB", kb)
+        results.append(pcap.index(good))
+    for r in results[1:]:
+        np.testing.assert_array_equal(r[0], results[0][0])
+        np.testing.assert_array_equal(r[1], results[0][1])
+    assert results[0][0].size == 3001 and results[0][0]["len"][1500] == 0

@@ -1,0 +1,80 @@
+"""A/B of launch-time switches (environment variables read per launch by
+libtcsum.so) in ONE process: interleaved rounds, median us per launch, and
+every variant's results must equal the default's.
+
+  python scripts/env_ab.py CONFIG VAR=VALUE[,VAR=VALUE...] ...
+  e.g. python scripts/env_ab.py mixed_rx TCSUM_IP_HDR_NT=1
+CONFIG: mtu | tso | mixed | mixed_tx | mixed_rx | mixed_txo
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import tcp_amd as tc  # noqa: E402
+from tcp_amd import workload  # noqa: E402
+
+cfg = sys.argv[1]
+variants = [{}] + [dict(kv.split("=", 1) for kv in a.split(",")) for a in sys.argv[2:]]
+b = workload.make_batch(cfg)
+arena, descs = workload.materialize(b)
+n = b.n
+peso = b.kind == "peso"
+out = torch.empty(n, dtype=torch.uint16 if peso else torch.uint32, device="cuda")
+verdict = torch.empty(n, dtype=torch.int8, device="cuda")
+flags = torch.empty(n, dtype=torch.uint8, device="cuda")
+
+
+def run():
+    if peso:
+        tc.batch_peso(arena, descs, n, b.total_bytes, out=out)
+    elif b.op == "tx":
+        tc.batch_ipv4_tx_fill(arena, descs, n, b.total_bytes, out=out, want_flags=False)
+    elif b.op == "txo":
+        tc.batch_ipv4_tx_offload(arena, descs, n, b.total_bytes, out=out, flags=flags)
+    elif b.op == "rx":
+        tc.batch_ipv4_rx_verify(arena, descs, n, b.total_bytes, verdict=verdict, out=out, want_flags=False)
+    else:
+        tc.batch_ipv4(arena, descs, n, b.total_bytes, out=out, want_flags=False)
+
+
+def with_env(env, fn):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+run()
+torch.cuda.synchronize()
+ref = (out.clone(), verdict.clone())
+for v in variants[1:]:
+    with_env(v, run)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref[0]) and torch.equal(verdict, ref[1]), f"{v} changed the results"
+times = [[] for _ in variants]
+for r in range(7):
+    for i, v in enumerate(variants):
+        def timed():
+            run()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / 10
+        times[i].append(with_env(v, timed))
+base = np.median(times[0])
+print(f"# {cfg}: {n} packets, {b.total_bytes} B; median of 7 rounds x 10 launches, interleaved")
+for v, t in zip(variants, times):
+    m = np.median(t)
+    print(f"{(','.join(f'{k}={x}' for k, x in v.items()) or 'default'):40s} {m*1e3:9.1f} us  {m/base:6.3f}x")

@@ -509,6 +509,8 @@ constexpr uint32_t IP_OPT_NO_STORE = 1u; // IP_TX: compute the fill's values, le
 // fields with the default cache policy right before the stores, so the lines
 // the stores land in are L2-resident (tx fill).
 constexpr uint32_t IP_OPT_RELOAD = 2u;
+// measurement (TCSUM_IP_HDR_NT=1): the header chunks load nontemporal too
+constexpr uint32_t IP_OPT_HDR_NT = 4u;
 // launch_ipv4 mode 3: IP_TX kernels with IP_OPT_NO_STORE
 constexpr int IP_TX_OFFLOAD = 3;
 
@@ -582,17 +584,21 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     // fixed header: bytes [s0, s0 + 20) of base[0..2]
     const u32x4 *hb = big_enough ? base : &g_zero_chunk;
     const uint32_t h1i = big_enough ? 1u : 0u;
-    const u32x4 h0 = load16<false>(hb);
-    const u32x4 h1 = load16<false>(hb + h1i);
+    // header loads: default cache policy (IP_OPT_HDR_NT, measurement: nontemporal
+    // like the data pass that loads the same chunks)
+    const bool hnt = opts & IP_OPT_HDR_NT;
+    auto hload = [hnt](const u32x4 *q) { return hnt ? load16<true>(q) : load16<false>(q); };
+    const u32x4 h0 = hload(hb);
+    const u32x4 h1 = hload(hb + h1i);
     u32x4 h2, c2 = u32x4(0u), c3 = u32x4(0u);
     if constexpr (IPM == IP_RX) {
         // chunks 2 and 3 as well: an IHL-5 packet's TCP/UDP ports, data offset
         // and flags (L4 bytes 0-3, 12-13) lie in chunks 1..3
-        c2 = load16<false>(nch > 2 ? base + 2 : &g_zero_chunk);
-        c3 = load16<false>(nch > 3 && s0 >= 12 ? base + 3 : &g_zero_chunk);
+        c2 = hload(nch > 2 ? base + 2 : &g_zero_chunk);
+        c3 = hload(nch > 3 && s0 >= 12 ? base + 3 : &g_zero_chunk);
         h2 = s0 > 12 ? c2 : u32x4(0u);
     } else {
-        const u32x4 h2v = load16<false>(hb + (big_enough ? (s0 > 12 ? 2u : 1u) : 0u));
+        const u32x4 h2v = hload(hb + (big_enough ? (s0 > 12 ? 2u : 1u) : 0u));
         h2 = s0 > 12 ? h2v : u32x4(0u);
     }
     const u32x4 *dbase = nch ? base : &g_zero_chunk;
@@ -1151,10 +1157,13 @@ __global__ __launch_bounds__(256) void k_probe_read(const u32x4 *__restrict__ p,
     const uint64_t base = wave * 64ull * U;
     uint32_t acc = 0;
     u32x4 v[U];
+    // unconditional loads, index clamped to the last chunk (as the checksum
+    // kernels do): a bounds test per load would put each one behind its own
+    // exec-mask branch
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t idx = base + u * 64ull + lane;
-        v[u] = idx < nchunks ? load16<NT>(p + idx) : u32x4(0u);
+        v[u] = load16<NT>(p + (idx < nchunks ? idx : nchunks - 1));
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -1179,9 +1188,9 @@ __global__ __launch_bounds__(256) void k_probe_tile(const u32x4 *__restrict__ p,
     uint32_t acc = 0;
     u32x4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < U; ++u) { // unconditional, clamped (see k_probe_read)
         const uint64_t idx = base + (uint64_t)(u * G) + gl;
-        v[u] = idx < nchunks ? load16<true>(p + idx) : u32x4(0u);
+        v[u] = load16<true>(p + (idx < nchunks ? idx : nchunks - 1));
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -1437,19 +1446,21 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
     const uint64_t per_block = 256u / (uint32_t)g.lanes;
     const dim3 grid((uint32_t)((n + per_block - 1) / per_block));
     const uint32_t xg = (uint32_t)g.xcd;
+    const char *hn = getenv("TCSUM_IP_HDR_NT"); // measurement only (IP_OPT_HDR_NT)
+    const uint32_t o = hn && atoi(hn) ? IP_OPT_HDR_NT : 0u;
     switch (ip_mode) {
     case IP_TX: {
         const char *rl = getenv("TCSUM_TX_RELOAD"); // measurement only (IP_OPT_RELOAD)
         return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict,
-                             rl && atoi(rl) ? IP_OPT_RELOAD : 0u, xg, stream);
+                             o | (rl && atoi(rl) ? IP_OPT_RELOAD : 0u), xg, stream);
     }
     case IP_TX_OFFLOAD: // the tx values into `out` only; the packets are not written
-        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, IP_OPT_NO_STORE, xg,
+        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, o | IP_OPT_NO_STORE, xg,
                              stream);
     case IP_RX:
-        return ipv4_u<IP_RX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, 0u, xg, stream);
+        return ipv4_u<IP_RX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, o, xg, stream);
     default:
-        return ipv4_u<IP_SUMS>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, 0u, xg, stream);
+        return ipv4_u<IP_SUMS>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, o, xg, stream);
     }
 }
 

@@ -143,11 +143,13 @@ def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None):
 def probe_compare(torch, tc, batch, product, arena, steps, rounds=5):
     """The roofline's achievable side, measured beside the product kernel
     (after the timed region, never inside it): rounds of [product x m, plain
-    read x m, tile-shaped read x m] launches, each with its own events, so the
-    three see the same clocks and the same HBM state; per-launch medians.
+    read x m, tile-shaped reads x m] launches, each with its own events, so
+    they see the same clocks and the same HBM state; per-launch medians.
     Plain read: k_probe_read<4>, contiguous 1 KiB per load instruction.  Tile
     read: k_probe_tile in the product's own geometry (lanes x loads, XCD
-    order) over the same bytes -- the product minus descriptors and sums."""
+    order) over the same bytes -- the product minus descriptors and sums;
+    tile_dep: the same with each unit's loads behind one dependent 16-B read,
+    as the product's loads wait for its descriptor.  achievable = the fastest."""
     g, u = tc.pick_geometry(batch.total_bytes // max(batch.n, 1))
     sink = torch.zeros(1, dtype=torch.uint32, device=arena.device)
     nbytes = batch.arena_bytes
@@ -159,6 +161,14 @@ def probe_compare(torch, tc, batch, product, arena, steps, rounds=5):
     kinds = {"product": product, "read": lambda: tc.probe_read(arena, nbytes, sink)}
     if tile_ok:
         kinds["tile"] = lambda: tc.probe_tile(arena, nbytes, g, u, sink)
+
+        def tile_dep():  # each unit's loads behind one dependent 16-B read, like the product's descriptor
+            os.environ["TCSUM_PROBE_DEP"] = "1"
+            try:
+                tc.probe_tile(arena, nbytes, g, u, sink)
+            finally:
+                del os.environ["TCSUM_PROBE_DEP"]
+        kinds["tile_dep"] = tile_dep
     m = max(2, steps // rounds)
     stream = torch.cuda.current_stream()
     per = {k: [] for k in kinds}
@@ -177,6 +187,7 @@ def probe_compare(torch, tc, batch, product, arena, steps, rounds=5):
            "geometry": [g, u], "rounds": rounds, "launches_per_round": m}
     if tile_ok:
         res["tile_gbs"] = nbytes / (med["tile"] * 1e-3) / 1e9
+        res["tile_dep_gbs"] = nbytes / (med["tile_dep"] * 1e-3) / 1e9
     return res
 
 
@@ -186,7 +197,7 @@ def result_entry(r, steps):
     alg = algorithmic_bytes(b)
     ach = alg / (ms_step * 1e-3) / 1e9
     p = r["probes"]
-    best = max(p["read_gbs"], p.get("tile_gbs", 0.0))
+    best = max(p["read_gbs"], p.get("tile_gbs", 0.0), p.get("tile_dep_gbs", 0.0))
     side = alg / (p["product_ms"] * 1e-3) / 1e9  # the product in the interleaved rounds
     return {
         "workload": b.config,
@@ -200,6 +211,7 @@ def result_entry(r, steps):
                      "frac_of_achievable": round(side / best, 4),
                      "probes": {"plain_read_gbs": round(p["read_gbs"], 1),
                                 "tile_read_gbs": round(p["tile_gbs"], 1) if "tile_gbs" in p else None,
+                                "tile_dep_read_gbs": round(p["tile_dep_gbs"], 1) if "tile_dep_gbs" in p else None,
                                 "tile_geometry": p["geometry"], "product_gbs_same_rounds": round(side, 1),
                                 "rounds": p["rounds"], "launches_per_round": p["launches_per_round"]}},
     }

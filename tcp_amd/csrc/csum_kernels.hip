@@ -601,8 +601,17 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
         const u32x4 h2v = hload(hb + (big_enough ? (s0 > 12 ? 2u : 1u) : 0u));
         h2 = s0 > 12 ? h2v : u32x4(0u);
     }
-    const u32x4 *dbase = nch ? base : &g_zero_chunk;
-    const uint32_t dlast = nch ? nch - 1u : 0u;
+    // The data pass counts chunks from the packet's 128-B line, not from its
+    // 16-B chunk: the G*U-chunk span of each pass then ends on a line
+    // boundary, so no line is split between two passes (a split line is
+    // fetched once per pass: the nontemporal first fetch is gone from L2 by
+    // the time the next pass, a memory latency later, wants the other half).
+    // Chunks of that line before the packet are loaded (same line, same page)
+    // but fall outside every byte range below.
+    const uint32_t sl = (uint32_t)(start & 127u);
+    const uint32_t dch = big_enough ? (frame_ld + sl + 15) >> 4 : 0u;
+    const u32x4 *dbase = dch ? reinterpret_cast<const u32x4 *>(pp - sl) : &g_zero_chunk;
+    const uint32_t dlast = dch ? dch - 1u : 0u;
 
     // first pass of data loads before the header is consumed: its latency
     // overlaps them (vmcnt counts in issue order)
@@ -610,7 +619,7 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t idx = u * G + gl;
-        v[u] = load16<true>(dbase + (idx < nch ? idx : dlast));
+        v[u] = load16<true>(dbase + (idx < dch ? idx : dlast));
     }
     issue_fence();
 
@@ -623,15 +632,6 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     const bool frag = (b6 & 0x20u) || (((b6 & 0x1Fu) << 8) | b7);
     const uint32_t proto = (hd.d2 >> 8) & 0xFFu;
     const uint32_t stored_ip = hd.d2 >> 16;
-    // rx: TCP/UDP header words of an IHL-5 packet (L4 bytes 0-3: ports;
-    // 12-15: data offset, flags), taken now from chunks 1..3 so those die here
-    uint32_t l4w0 = 0, l4w3 = 0;
-    if constexpr (IPM == IP_RX) {
-        const bool cw1 = s0 + 20u < 32u;
-        const Hdr5 l4h = header_dwords(cw1 ? h1 : c2, cw1 ? c2 : c3, u32x4(0u), (s0 + 4u) & 15u);
-        l4w0 = l4h.d0;
-        l4w3 = l4h.d3;
-    }
     uint32_t fl = 0;
     if (version != 4)
         fl |= TCSUM_PKT_BAD_VERSION;
@@ -655,13 +655,80 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     // rx: is it zero?) -- none for fragments, short L4, or ICMP on rx
     const bool field_on = IPM != IP_SUMS && !bad && !frag && fld && !(fl & TCSUM_PKT_L4_SHORT) &&
                           !(IPM == IP_RX && proto == 1);
+    // The L4 pseudo-header (tools.c:58-70), folded now: src, dst (packet bytes
+    // 12..19), {0, proto}, the L4 length; kept as one register past the data pass
+    uint32_t pseudo = 0;
+    if (proto == 6 || proto == 17)
+        pseudo = fold16(add_halves(add_halves(0u, hd.d3), hd.d4) + (proto << 8) + bswap16((end - hl) & 0xFFFFu));
+    if (big_enough && proto != 6 && proto != 17 && proto != 1)
+        fl |= TCSUM_PKT_PROTO_OTHER;
 
-    // byte ranges, from base (end <= tl <= 65535 whenever it matters; clamp so
-    // a huge bogus frame cannot overflow)
-    const int h_end = (int)(hl < 65600u ? hl : 65600u) + (int)s0;
-    const int l_end = (int)(end < 65600u ? end : 65600u) + (int)s0;
-    const int f0 = field_on ? (int)(hl + fld) + (int)s0 : -64;
-    const int i0 = (int)s0 + 10; // IPv4 header checksum field
+    // rx: every gate that needs no sum, decided now, in the reference's order
+    // (the verdict at the end only places the two checksum tests between them):
+    //   pre  -- ipv4_in before the header checksum test (ipv4.c:475, 222-240)
+    //   mid  -- the L4 input before its checksum test (tcp_in.c:70-74 and
+    //           pktbuf_remove_header, udp.c:386-403, icmpv4.c:68)
+    //   post -- the L4 input after it (tcp_in.c:87-103)
+    // packed as three int8 in one register.
+    uint32_t vcodes = 0;
+    if constexpr (IPM == IP_RX) {
+        int vpre = 0, vmid = 0, vpost = 0;
+        if (!big_enough)
+            vpre = TCSUM_ERR_SIZE; // pktbuf_set_cont(buf, 20), ipv4.c:475
+        else if (version != 4)
+            vpre = TCSUM_ERR_NOT_SUPPORT; // ipv4.c:222-226
+        else if (ihl4 < 20 || tl < 20 || frame < tl)
+            vpre = TCSUM_ERR_SIZE; // ipv4.c:228-240
+        else if (frag)
+            vmid = 0; // ipv4.c:506-509: queued for reassembly, OK past the header test
+        else if (proto == 6 || proto == 17) { // TCP: pktbuf_remove_header + tcp_in (ipv4.c:450-452); UDP: udp_in
+            // the header words (L4 bytes 0-3: ports; 12-15: data offset,
+            // flags) from the 32 bytes at chunk (s0 + ihl4) / 16: chunks 1..3
+            // already in registers for IHL 5, two more loads otherwise
+            uint32_t ports = 0, oflags = 0;
+            if (tl >= ihl4 + 8u) {
+                const uint32_t o = s0 + ihl4, cw = o >> 4;
+                u32x4 wa, wb;
+                if (ihl4 == 20) {
+                    wa = cw == 1 ? h1 : c2;
+                    wb = cw == 1 ? c2 : c3;
+                } else {
+                    wa = load16<false>(base + cw);
+                    wb = load16<false>(cw + 1 < nch ? base + cw + 1 : &g_zero_chunk);
+                }
+                const Hdr5 l4h = header_dwords(wa, wb, u32x4(0u), o & 15u);
+                ports = l4h.d0;
+                oflags = l4h.d3;
+            }
+            const uint32_t sport = ports & 0xFFFFu, dport = ports >> 16, fword = oflags & 0xFFFFu;
+            if (proto == 6) {
+                if (ihl4 > tl)
+                    vmid = TCSUM_ERR_SIZE; // the reference runs off its block list (pktbuf.c:264-281)
+                else if (tl - ihl4 < 20)
+                    vmid = TCSUM_ERR_SYS; // pktbuf_set_cont fails: tcp_in returns -1, tcp_in.c:70-74
+                else if (tl - ihl4 < (((oflags & 0xFFu) >> 4) << 2))
+                    vpost = TCSUM_ERR_SIZE; // tcp_in.c:87-91
+                else if (sport == 0 || dport == 0 || fword == 0)
+                    vpost = TCSUM_ERR_BROKEN; // tcp_in.c:93-103
+            } else {
+                if (tl < ihl4 + 8)
+                    vmid = TCSUM_ERR_SIZE; // pktbuf_set_cont(buf, 8 + ihl), udp.c:386-391
+                else if (dport == 0)
+                    vmid = TCSUM_ERR_UNREACHABLE; // no socket has port 0: udp.c:337-340, :399-403
+            }
+        } else if (proto == 1) { // icmpv4_in, ipv4.c:427; its checksum test cannot fail (A10)
+            vmid = tl < ihl4 + 4 ? TCSUM_ERR_SIZE : 0; // pktbuf_set_cont(buf, ihl + 4), icmpv4.c:68
+        } // other protocols: raw_in, no checksum (ipv4.c:460-469)
+        vcodes = (uint32_t)(uint8_t)vpre | ((uint32_t)(uint8_t)vmid << 8) | ((uint32_t)(uint8_t)vpost << 16) |
+                 (stored_ip != 0 ? 1u << 24 : 0u);
+    }
+
+    // byte ranges, from the data pass's line base (end <= tl <= 65535 whenever
+    // it matters; clamp so a huge bogus frame cannot overflow)
+    const int h_end = (int)(hl < 65600u ? hl : 65600u) + (int)sl;
+    const int l_end = (int)(end < 65600u ? end : 65600u) + (int)sl;
+    const int f0 = field_on ? (int)(hl + fld) + (int)sl : -64;
+    const int i0 = (int)sl + 10; // IPv4 header checksum field
 
     uint32_t acc_h = 0, acc_l = 0, acc_f = 0;
     // one pass of U chunks per lane starting at chunk b0 (pass 0: the loads
@@ -672,11 +739,11 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t idx = b0 + u * G + gl;
-            const bool valid = idx < nch;
+            const bool valid = idx < dch;
             const int c = (int)(16u * idx);
             const bool inner = valid && c >= h_end && c + 16 <= l_end && (f0 + 2 <= c || f0 >= c + 16);
             if (valid && !inner) { // header chunks, the field chunk(s), the last chunk: rare
-                uint32_t th = region_sum(vv[u], c, (int)s0, h_end);
+                uint32_t th = region_sum(vv[u], c, (int)sl, h_end);
                 uint32_t tl4 = region_sum(vv[u], c, h_end, l_end);
                 if (field_on) {
                     const uint32_t tf = region_sum(vv[u], c, f0, f0 + 2);
@@ -695,14 +762,14 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
         acc_h += ph; // header <= 60 bytes: no overflow
         acc_l = fold_step(acc_l + pl);
     };
-    if (nch)
+    if (dch)
         pass(v, 0u);
-    for (uint32_t b0 = G * U; b0 < nch; b0 += G * U) {
+    for (uint32_t b0 = G * U; b0 < dch; b0 += G * U) {
         u32x4 w[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t idx = b0 + u * G + gl;
-            w[u] = load16<true>(dbase + (idx < nch ? idx : dlast));
+            w[u] = load16<true>(dbase + (idx < dch ? idx : dlast));
         }
         pass(w, b0);
     }
@@ -724,17 +791,10 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
                 f4 = rot8(f4);
             }
             ip = ~fh & 0xFFFFu;
-            if (proto == 6 || proto == 17) {
-                uint32_t q = add_halves(0u, hd.d3); // src, packet bytes 12..15
-                q = add_halves(q, hd.d4);           // dst, packet bytes 16..19
-                q += proto << 8;
-                q += bswap16((end - hl) & 0xFFFFu);
-                l4 = ~fold_step(f4 + fold16(q)) & 0xFFFFu;
-            } else if (proto == 1) {
+            if (proto == 6 || proto == 17)
+                l4 = ~fold_step(f4 + pseudo) & 0xFFFFu;
+            else if (proto == 1)
                 l4 = ~f4 & 0xFFFFu;
-            } else {
-                fl |= TCSUM_PKT_PROTO_OTHER;
-            }
         }
         if constexpr (IPM == IP_TX) {
             if (!bad && !(opts & IP_OPT_NO_STORE)) { // stored in host order, like the struct fields
@@ -761,61 +821,19 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
             // is_pkt_ok, then the L4 input ip_normal_in dispatches to
             // (ipv4.c:420-470), up to socket lookup.  Pinned by the reference
             // stack's own verdicts (tests/golden/ipv4_rx_*, oracle/stack_gen.c).
-            // TCP/UDP header words (L4 bytes 0-3: ports; 12-15: data offset,
-            // flags) from the 32 bytes at chunk (s0 + ihl4) / 16: chunks 1..3
-            // already in registers for IHL 5, two loads of this lane otherwise
-            uint32_t ports = l4w0, oflags = l4w3;
-            const bool l4_gates = version == 4 && ihl4 >= 20 && tl <= frame && tl >= ihl4 + 8u && !frag &&
-                                  (proto == 6 || proto == 17);
-            if (l4_gates && ihl4 != 20) { // IPv4 options: two loads of this lane
-                const uint32_t o = s0 + ihl4, cw = o >> 4;
-                const u32x4 wa = load16<false>(base + cw);
-                const u32x4 wb = load16<false>(cw + 1 < nch ? base + cw + 1 : &g_zero_chunk);
-                const Hdr5 l4h = header_dwords(wa, wb, u32x4(0u), o & 15u);
-                ports = l4h.d0;
-                oflags = l4h.d3;
-            }
-            const uint32_t sport = ports & 0xFFFFu, dport = ports >> 16, fword = oflags & 0xFFFFu;
-            const uint32_t doff4 = ((oflags & 0xFFu) >> 4) << 2;
+            const int vpre = (int8_t)(vcodes & 0xFFu), vmid = (int8_t)((vcodes >> 8) & 0xFFu);
+            const int vpost = (int8_t)((vcodes >> 16) & 0xFFu);
             int v8;
-            if (!big_enough)
-                v8 = TCSUM_ERR_SIZE; // pktbuf_set_cont(buf, 20), ipv4.c:475
-            else if (version != 4)
-                v8 = TCSUM_ERR_NOT_SUPPORT; // ipv4.c:222-226
-            else if (ihl4 < 20 || tl < 20 || frame < tl)
-                v8 = TCSUM_ERR_SIZE; // ipv4.c:228-240
-            else if (stored_ip != 0 && ip != 0)
+            if (vpre)
+                v8 = vpre;
+            else if ((vcodes >> 24) && ip != 0)
                 v8 = TCSUM_ERR_BROKEN; // ipv4.c:241-249
-            else if (frag)
-                v8 = TCSUM_OK; // ipv4.c:506-509: queued for reassembly
-            else if (proto == 6) { // pktbuf_remove_header + tcp_in, ipv4.c:450-452
-                if (ihl4 > tl)
-                    v8 = TCSUM_ERR_SIZE; // the reference runs off its block list (pktbuf.c:264-281)
-                else if (tl - ihl4 < 20)
-                    v8 = TCSUM_ERR_SYS; // pktbuf_set_cont fails: tcp_in returns -1, tcp_in.c:70-74
-                else if (acc_f != 0 && l4 != 0)
-                    v8 = TCSUM_ERR_BROKEN; // tcp_in.c:77-85
-                else if (tl - ihl4 < doff4)
-                    v8 = TCSUM_ERR_SIZE; // tcp_in.c:87-91
-                else if (sport == 0 || dport == 0 || fword == 0)
-                    v8 = TCSUM_ERR_BROKEN; // tcp_in.c:93-103
-                else
-                    v8 = TCSUM_OK;
-            } else if (proto == 17) { // udp_in, ipv4.c:436
-                if (tl < ihl4 + 8)
-                    v8 = TCSUM_ERR_SIZE; // pktbuf_set_cont(buf, 8 + ihl), udp.c:386-391
-                else if (dport == 0)
-                    v8 = TCSUM_ERR_UNREACHABLE; // no socket has port 0: udp.c:337-340, :399-403
-                else if (acc_f != 0 && l4 != 0)
-                    v8 = TCSUM_ERR_BROKEN; // udp.c:407-415
-                else
-                    v8 = TCSUM_OK;
-            } else if (proto == 1) { // icmpv4_in, ipv4.c:427
-                // pktbuf_set_cont(buf, ihl + 4), icmpv4.c:68; its checksum test cannot fail (A10)
-                v8 = tl < ihl4 + 4 ? TCSUM_ERR_SIZE : TCSUM_OK;
-            } else {
-                v8 = TCSUM_OK; // raw_in: no checksum, ipv4.c:460-469
-            }
+            else if (vmid)
+                v8 = vmid;
+            else if (acc_f != 0 && l4 != 0)
+                v8 = TCSUM_ERR_BROKEN; // tcp_in.c:77-85, udp.c:407-415 (field_on: TCP/UDP only)
+            else
+                v8 = vpost;
             verdict_out[pk] = (int8_t)v8;
         }
         if (out)
@@ -1178,13 +1196,22 @@ __global__ __launch_bounds__(256) void k_probe_read(const u32x4 *__restrict__ p,
 // k_segments / k_ipv4 minus descriptors, edge masking and sums (G = 256: one
 // unit per workgroup, k_segments_wg's shape).  The ceiling the product kernel
 // is compared with, on the same bytes.
-template <int G, int U>
+// DEP: each unit first reads a 16-B "descriptor" (its own first chunk, so no
+// extra bytes) and issues the tile's loads only behind it, as the product
+// kernels wait for their descriptor before the data loads.
+template <int G, int U, bool DEP>
 __global__ __launch_bounds__(256) void k_probe_tile(const u32x4 *__restrict__ p, uint64_t nchunks,
                                                     uint32_t *__restrict__ sink, uint32_t xg)
 {
     const uint64_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
     const uint32_t gl = threadIdx.x & (G - 1);
-    const uint64_t base = (blk * (256u / G) + threadIdx.x / G) * (uint64_t)(G * U);
+    uint64_t base = (blk * (256u / G) + threadIdx.x / G) * (uint64_t)(G * U);
+    if constexpr (DEP) {
+        const u32x4 d = p[base < nchunks ? base : nchunks - 1];
+        uint32_t zero;
+        asm volatile("v_and_b32 %0, 0, %1" : "=v"(zero) : "v"(d.x)); // 0, but only once d is here
+        base += zero;
+    }
     uint32_t acc = 0;
     u32x4 v[U];
 #pragma unroll
@@ -1207,9 +1234,14 @@ hipError_t launch_probe_tile(const void *p, uint64_t nbytes, int G, int U, uint3
     const uint32_t xg = (uint32_t)pick_geometry(1500).xcd; // the product's order (TCSUM_XCD applies too)
     const dim3 grid((uint32_t)((nchunks + 256ull * U - 1) / (256ull * U)));
     const u32x4 *q = static_cast<const u32x4 *>(p);
+    const char *dep_s = getenv("TCSUM_PROBE_DEP");
+    const bool dep = dep_s && atoi(dep_s);
 #define TCSUM_PT(GG, UU)                                                                         \
     if (G == GG && U == UU) {                                                                  \
-        hipLaunchKernelGGL((k_probe_tile<GG, UU>), grid, dim3(256), 0, stream, q, nchunks, sink, xg); \
+        if (dep)                                                                               \
+            hipLaunchKernelGGL((k_probe_tile<GG, UU, true>), grid, dim3(256), 0, stream, q, nchunks, sink, xg); \
+        else                                                                                   \
+            hipLaunchKernelGGL((k_probe_tile<GG, UU, false>), grid, dim3(256), 0, stream, q, nchunks, sink, xg); \
         return hipGetLastError();                                                              \
     }
     TCSUM_PT(16, 4) TCSUM_PT(16, 6) TCSUM_PT(16, 8) TCSUM_PT(32, 4) TCSUM_PT(32, 6) TCSUM_PT(32, 8)

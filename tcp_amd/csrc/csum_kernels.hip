@@ -1464,6 +1464,11 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
         g.lanes = 16;
     if (g.lanes > 64) // k_ipv4 keeps a packet inside one wave (no workgroup-per-packet form)
         g.lanes = 64;
+    // rx keeps more registers live through the data pass (the gate codes, the
+    // field sum): with 16 lanes per packet instead of 32 it measured 3.8 %
+    // faster on configs[3] (profiles/r02/geom_rx.txt); the other modes keep 32
+    if (ip_mode == IP_RX && g.lanes == 32 && !getenv("TCSUM_G"))
+        g.lanes = 16;
     const uint64_t per_launch = kMaxBlocks * (256u / (uint32_t)g.lanes);
     if (n > per_launch) { // see kMaxBlocks
         for (uint64_t i0 = 0; i0 < n; i0 += per_launch) {

@@ -66,6 +66,7 @@ def parse():
                     help="CPU baseline: the reference's own checksum_peso (oracle/_ref) or the oracle's port")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--trace-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--e2e-multi-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-trace", action="store_true", help="skip the rocprofv3 kernel-trace child")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="rehearse the N-rank launcher, rendezvous, barrier and max-over-ranks timing on CPU "
@@ -423,16 +424,59 @@ def e2e(torch, tc, r):
                "h2d_copy_gib_s": round(link, 2),
                "matches_device_resident": same}
         ndev = torch.cuda.device_count()
-        if ndev > 1:  # the same host batch sharded over every GPU of the node
-            devs = list(range(ndev))
-            out = tc.host_batch_peso_multi(host, b.descs, devs)
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                out = tc.host_batch_peso_multi(host, b.descs, devs)
-            dt = (time.perf_counter() - t0) / reps
-            res["multi_device"] = {"gpus": ndev, "gib_s": round(b.total_bytes / dt / GIB, 2),
-                                   "matches_device_resident": bool((out == r["out"].cpu().numpy()).all())}
+        if ndev > 1:  # the same host batch sharded over every GPU of the node, in a child with a time limit
+            res["multi_device"] = e2e_multi_child(b.config, ndev)
         return res
+    finally:
+        L.tcsum_host_free(p)
+
+
+def e2e_multi_child(config: str, ndev: int, timeout_s: float = 240.0):
+    """tcsum_host_batch_peso_multi over every GPU of the node, measured in a
+    child process (`bench.py --e2e-multi-child`) so that a first run of the
+    cross-device path on a new node can only cost this field, never the bench
+    line: the child is killed after timeout_s."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--e2e-multi-child", "--config", config]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"gpus": ndev, "error": f"timed out after {timeout_s:.0f} s"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"gpus": ndev, "error": f"rc {r.returncode}: {r.stderr[-300:]}"}
+    return json.loads(lines[-1])
+
+
+def e2e_multi_main(config: str) -> None:
+    """The child: the batch generated on GPU 0, copied to pinned host memory,
+    then checksummed from there by every GPU (one shard each) and checked
+    against the device-resident results."""
+    import ctypes
+    import numpy as np
+    import torch
+    import tcp_amd as tc
+    from tcp_amd import _lib, workload
+    b = workload.make_batch(config)
+    arena, descs = workload.materialize(b)
+    want = tc.batch_peso(arena, descs, b.n, b.total_bytes).cpu().numpy()
+    L = _lib.lib()
+    p = L.tcsum_host_alloc(b.alloc_bytes)
+    if not p:
+        raise MemoryError("tcsum_host_alloc")
+    try:
+        host = np.ctypeslib.as_array((ctypes.c_uint8 * b.alloc_bytes).from_address(p))
+        host[:] = arena[: b.alloc_bytes].cpu().numpy()
+        del arena
+        torch.cuda.empty_cache()
+        devs = list(range(torch.cuda.device_count()))
+        out = tc.host_batch_peso_multi(host, b.descs, devs)
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            out = tc.host_batch_peso_multi(host, b.descs, devs)
+        dt = (time.perf_counter() - t0) / reps
+        print(json.dumps({"gpus": len(devs), "gib_s": round(b.total_bytes / dt / GIB, 2),
+                          "matches_device_resident": bool((out == want).all())}), flush=True)
     finally:
         L.tcsum_host_free(p)
 
@@ -520,6 +564,9 @@ def rehearsal(args, rank, world) -> None:
 
 def main():
     args = parse()
+    if args.e2e_multi_child:
+        e2e_multi_main(args.config)
+        return
     from tcp_amd import dist as D
     if args.gpus > 1 and not D.launched() and not args.pmc_child:
         sys.exit(launch_ranks(args))

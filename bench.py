@@ -137,11 +137,12 @@ def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None):
         dist.barrier()
     torch.cuda.synchronize()
     ms = t0.elapsed_time(t1)  # events on the launch stream: pure kernel time of K launches
-    probes = probe_compare(torch, tc, batch, lambda: launch(tc, batch, arena, descs, out, flags), arena, steps)
+    probes = probe_compare(torch, tc, batch, lambda: launch(tc, batch, arena, descs, out, flags), arena, steps,
+                           descs=descs)
     return dict(batch=batch, arena=arena, descs=descs, out=out, ms=ms, wall_s=wall, probes=probes)
 
 
-def probe_compare(torch, tc, batch, product, arena, steps, rounds=5):
+def probe_compare(torch, tc, batch, product, arena, steps, rounds=5, descs=None):
     """The roofline's achievable side, measured beside the product kernel
     (after the timed region, never inside it): rounds of [product x m, plain
     read x m, tile-shaped reads x m] launches, each with its own events, so
@@ -150,7 +151,11 @@ def probe_compare(torch, tc, batch, product, arena, steps, rounds=5):
     read: k_probe_tile in the product's own geometry (lanes x loads, XCD
     order) over the same bytes -- the product minus descriptors and sums;
     tile_dep: the same with each unit's loads behind one dependent 16-B read,
-    as the product's loads wait for its descriptor.  achievable = the fastest."""
+    as the product's loads wait for its descriptor.  segments (checksum_peso
+    batches): tcsum_probe_segments -- the product's own descriptors, lanes,
+    loads, edge policy and block order with the arithmetic and the store
+    removed, priced on the same algorithmic bytes as the product.
+    achievable = the fastest."""
     g, u = tc.pick_geometry(batch.total_bytes // max(batch.n, 1))
     sink = torch.zeros(1, dtype=torch.uint32, device=arena.device)
     nbytes = batch.arena_bytes
@@ -170,6 +175,11 @@ def probe_compare(torch, tc, batch, product, arena, steps, rounds=5):
             finally:
                 del os.environ["TCSUM_PROBE_DEP"]
         kinds["tile_dep"] = tile_dep
+    if batch.kind == "peso" and descs is not None:
+        kinds["segments"] = lambda: tc.probe_segments(arena, descs, batch.n, batch.total_bytes, sink)
+    elif descs is not None:
+        kinds["segments"] = lambda: tc.probe_ipv4(arena, descs, batch.n, batch.total_bytes, rx=batch.op == "rx",
+                                                  sink=sink)
     m = max(2, steps // rounds)
     stream = torch.cuda.current_stream()
     per = {k: [] for k in kinds}
@@ -189,6 +199,8 @@ def probe_compare(torch, tc, batch, product, arena, steps, rounds=5):
     if tile_ok:
         res["tile_gbs"] = nbytes / (med["tile"] * 1e-3) / 1e9
         res["tile_dep_gbs"] = nbytes / (med["tile_dep"] * 1e-3) / 1e9
+    if "segments" in med:
+        res["segments_gbs"] = algorithmic_bytes(batch) / (med["segments"] * 1e-3) / 1e9
     return res
 
 
@@ -198,7 +210,7 @@ def result_entry(r, steps):
     alg = algorithmic_bytes(b)
     ach = alg / (ms_step * 1e-3) / 1e9
     p = r["probes"]
-    best = max(p["read_gbs"], p.get("tile_gbs", 0.0), p.get("tile_dep_gbs", 0.0))
+    best = max(p["read_gbs"], p.get("tile_gbs", 0.0), p.get("tile_dep_gbs", 0.0), p.get("segments_gbs", 0.0))
     side = alg / (p["product_ms"] * 1e-3) / 1e9  # the product in the interleaved rounds
     return {
         "workload": b.config,
@@ -213,6 +225,7 @@ def result_entry(r, steps):
                      "probes": {"plain_read_gbs": round(p["read_gbs"], 1),
                                 "tile_read_gbs": round(p["tile_gbs"], 1) if "tile_gbs" in p else None,
                                 "tile_dep_read_gbs": round(p["tile_dep_gbs"], 1) if "tile_dep_gbs" in p else None,
+                                "segments_read_gbs": round(p["segments_gbs"], 1) if "segments_gbs" in p else None,
                                 "tile_geometry": p["geometry"], "product_gbs_same_rounds": round(side, 1),
                                 "rounds": p["rounds"], "launches_per_round": p["launches_per_round"]}},
     }

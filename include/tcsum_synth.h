@@ -47,6 +47,22 @@ int tcsum_probe_read(const void *p /*[dev]*/, uint64_t nbytes, uint32_t *sink /*
 int tcsum_probe_tile(const void *p /*[dev]*/, uint64_t nbytes, int lanes, int loads, uint32_t *sink /*[dev]*/,
                      void *stream);
 
+/* tcsum_batch_peso's loads and nothing else: the same descriptors, lanes,
+ * edge / interior cache policies and workgroup order, with the sums, the
+ * reduction and the result store replaced by an XOR fold -- the rate the
+ * checksum kernel would run at if its arithmetic were free.  Geometries the
+ * batch call picks for the configs (16 x 3..8, 32 x 4/6, 8 x 4, 256 x 16);
+ * otherwise TCSUM_ERR_PARAM. */
+int tcsum_probe_segments(const void *arena /*[dev]*/, const tcsum_peso_t *segs /*[dev]*/, uint32_t n,
+                         uint64_t total_bytes_hint, uint32_t *sink /*[dev]*/, void *stream);
+
+/* The same for the IPv4 batch calls: tcsum_batch_ipv4's descriptor, header
+ * and line-aligned data loads (rx != 0: tcsum_batch_ipv4_rx_verify's, two
+ * more header chunks and its lane count), XOR-folded, nothing stored but the
+ * fluke sink.  Geometries 16 x 3..8, 32 x 4/6, 64 x 16; else TCSUM_ERR_PARAM. */
+int tcsum_probe_ipv4(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,
+                     uint64_t total_bytes_hint, int rx, uint32_t *sink /*[dev]*/, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,7 +7,7 @@ from .csum import (PESO_DTYPE, PKT_DTYPE, SEG_DTYPE, batch_ipv4, batch_ipv4_rx_v
                    batch_ipv4_tx_offload, tx_apply_batch, batch_peso, batch_segments,
                    checksum16, checksum_peso, descs_to_device, device_count, host_batch_peso, host_batch_peso_multi,
                    HostArena, host_register, host_unregister, host_batch_ipv4, host_batch_ipv4_rx_verify, host_batch_ipv4_tx_fill,
-                   pick_geometry, pktbuf_checksum16, plat_init, probe_read, probe_tile, queue_server, release, call_server, synth_fill,
+                   pick_geometry, pktbuf_checksum16, plat_init, probe_ipv4, probe_read, probe_segments, probe_tile, queue_server, release, call_server, synth_fill,
                    synth_ipv4)
 from .pktbuf import IpAddr, PktBuf
 from . import pcap, workload
@@ -17,5 +17,5 @@ __all__ = [
     "batch_ipv4_tx_fill", "batch_ipv4_tx_offload", "tx_apply_batch", "batch_ipv4_rx_verify",
     "host_batch_peso", "host_batch_peso_multi", "HostArena", "host_register", "host_unregister", "host_batch_ipv4", "host_batch_ipv4_tx_fill", "host_batch_ipv4_rx_verify",
     "synth_fill", "synth_ipv4", "descs_to_device", "device_count", "pick_geometry",
-    "plat_init", "probe_read", "probe_tile", "queue_server", "release", "call_server", "PktBuf", "IpAddr", "SEG_DTYPE", "PESO_DTYPE", "PKT_DTYPE", "pcap", "workload",
+    "plat_init", "probe_ipv4", "probe_read", "probe_segments", "probe_tile", "queue_server", "release", "call_server", "PktBuf", "IpAddr", "SEG_DTYPE", "PESO_DTYPE", "PKT_DTYPE", "pcap", "workload",
 ]

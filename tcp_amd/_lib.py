@@ -63,6 +63,8 @@ SIGNATURES = {
     "tcsum_probe_read": (_I, [_V, _U64, _V, _V]),
     "tcsum_probe_tile": (_I, [_V, _U64, _I, _I, _V, _V]),
     "tcsum_release": (_I, [_I]),
+    "tcsum_probe_segments": (_I, [_V, _V, _U32, _U64, _V, _V]),
+    "tcsum_probe_ipv4": (_I, [_V, _V, _U32, _U64, _I, _V, _V]),
 }
 
 _lib = None

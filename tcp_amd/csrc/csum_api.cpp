@@ -520,6 +520,26 @@ int tcsum_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, void *strea
                : TCSUM_ERR_SYS;
 }
 
+int tcsum_probe_segments(const void *arena, const tcsum_peso_t *segs, uint32_t n, uint64_t total_bytes_hint,
+                         uint32_t *sink, void *stream)
+{
+    if (!arena || !segs || !sink)
+        return TCSUM_ERR_PARAM;
+    const hipError_t e = tcsum::launch_probe_desc(arena, segs, n, mean_of(total_bytes_hint, n), sink,
+                                                  static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TCSUM_OK : e == hipErrorInvalidValue ? TCSUM_ERR_PARAM : TCSUM_ERR_SYS;
+}
+
+int tcsum_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t total_bytes_hint, int rx,
+                     uint32_t *sink, void *stream)
+{
+    if (!arena || !pkts || !sink)
+        return TCSUM_ERR_PARAM;
+    const hipError_t e = tcsum::launch_probe_ipv4(arena, pkts, n, mean_of(total_bytes_hint, n), rx,
+                                                  sink, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TCSUM_OK : e == hipErrorInvalidValue ? TCSUM_ERR_PARAM : TCSUM_ERR_SYS;
+}
+
 int tcsum_probe_tile(const void *p, uint64_t nbytes, int lanes, int loads, uint32_t *sink, void *stream)
 {
     if (!p || !sink || (reinterpret_cast<uintptr_t>(p) & 15u))

@@ -88,6 +88,10 @@ hipError_t launch_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, u
                              hipStream_t stream);
 
 hipError_t launch_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, hipStream_t stream);
+hipError_t launch_probe_desc(const void *arena, const void *descs, uint32_t n, uint64_t mean_len, uint32_t *sink,
+                             hipStream_t stream);
+hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t mean_len, int rx,
+                             uint32_t *sink, hipStream_t stream);
 hipError_t launch_probe_tile(const void *p, uint64_t nbytes, int lanes, int loads, uint32_t *sink, hipStream_t stream);
 
 hipError_t launch_synth_ipv4(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t seed,

@@ -325,6 +325,26 @@ def probe_tile(buf, nbytes: int, lanes: int, loads: int, sink=None, stream=None)
     return sink
 
 
+def probe_segments(arena, segs, n: int, total_bytes: int, sink=None, stream=None):
+    """tcsum_probe_segments: batch_peso's loads with free arithmetic."""
+    torch = _torch()
+    if sink is None:
+        sink = torch.zeros(1, dtype=torch.uint32, device=arena.device)
+    _lib.check(_lib.lib().tcsum_probe_segments(arena.data_ptr(), segs.data_ptr(), n, total_bytes, sink.data_ptr(),
+                                               _stream_ptr(stream)), "tcsum_probe_segments")
+    return sink
+
+
+def probe_ipv4(arena, pkts, n: int, total_bytes: int, rx: bool = False, sink=None, stream=None):
+    """tcsum_probe_ipv4: the IPv4 batch calls' loads with free arithmetic."""
+    torch = _torch()
+    if sink is None:
+        sink = torch.zeros(1, dtype=torch.uint32, device=arena.device)
+    _lib.check(_lib.lib().tcsum_probe_ipv4(arena.data_ptr(), pkts.data_ptr(), n, total_bytes, int(bool(rx)),
+                                           sink.data_ptr(), _stream_ptr(stream)), "tcsum_probe_ipv4")
+    return sink
+
+
 def pick_geometry(mean_len: int):
     g, u = ctypes.c_int(), ctypes.c_int()
     _lib.lib().tcsum_pick_geometry(mean_len, ctypes.byref(g), ctypes.byref(u))

@@ -753,3 +753,27 @@ def test_fuzz_vs_oracle(tc, torch, oracle, geometry, seed):
     ev, _ = oracle.batch_ipv4_rx_verify(ip, pk, nthreads=8)
     np.testing.assert_array_equal(verdict.cpu().numpy(), ev)
     assert (ev == 0).sum() > m // 4
+
+
+@pytest.mark.parametrize("config", ["mtu", "tso", "mixed", "mixed_rx"])
+def test_measurement_probes_leave_arena_and_sink_alone(torch, tc, config):
+    """bench.py's achievable-side probes (tcsum_probe_read / _tile /
+    _segments / _ipv4) read the batch and write nothing but a 2^-32 sink: the arena is
+    unchanged, the sink still 0, and every geometry pick_geometry returns for
+    a batch has a probe_segments / probe_ipv4 instance."""
+    from tcp_amd import workload
+    n = {"mtu": 20000, "tso": 64, "mixed": 4000, "mixed_rx": 4000}[config]
+    b = workload.make_batch(config, n=n)
+    arena, descs = workload.materialize(b)
+    before = arena.clone()
+    sink = torch.zeros(1, dtype=torch.uint32, device=arena.device)
+    tc.probe_read(arena, b.arena_bytes, sink)
+    g, u = tc.pick_geometry(b.total_bytes // b.n)
+    tc.probe_tile(arena, b.arena_bytes, g, u, sink)
+    if b.kind == "peso":
+        tc.probe_segments(arena, descs, b.n, b.total_bytes, sink)
+    else:
+        tc.probe_ipv4(arena, descs, b.n, b.total_bytes, rx=b.op == "rx", sink=sink)
+    torch.cuda.synchronize()
+    assert int(sink.item()) == 0
+    assert torch.equal(arena, before)

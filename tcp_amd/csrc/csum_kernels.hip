@@ -1286,11 +1286,20 @@ __global__ __launch_bounds__(256) void k_probe_tile(const u32x4 *__restrict__ p,
 template <int G, int U>
 __global__ __launch_bounds__(256) void k_probe_desc(const uint8_t *__restrict__ arena,
                                                     const void *__restrict__ descs, uint32_t n,
-                                                    uint32_t *__restrict__ sink, uint32_t xg)
+                                                    uint32_t *__restrict__ sink, uint32_t xg, uint32_t pace)
 {
     const uint32_t gl = threadIdx.x & (G - 1);
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
     const uint32_t seg = G == 256 ? blk : blk * (256u / G) + threadIdx.x / G;
+    if (pace) { // measurement (TCSUM_PROBE_PACE): hold the wave back before its first load
+        uint32_t k = pace & 0xFFu;
+        if (pace & 0x100u)
+            k *= (threadIdx.x >> 6) + 1u; // staggered by wave in the workgroup
+        if (pace & 0x200u)
+            k *= (blockIdx.x & 3u); // staggered by workgroup
+        for (uint32_t i = 0; i < k; ++i)
+            __builtin_amdgcn_s_sleep(1);
+    }
     const SegDesc d = load_desc<MODE_PESO>(descs, seg, seg < n);
     Frame<U> f;
     frame_issue<G, U>(f, arena, d.off, d.len, gl);
@@ -1319,13 +1328,15 @@ hipError_t launch_probe_desc(const void *arena, const void *descs, uint32_t n, u
     const Geometry g = pick_geometry(mean_len);
     const uint32_t xg = (uint32_t)g.xcd;
     const uint8_t *a = static_cast<const uint8_t *>(arena);
+    const char *pe = getenv("TCSUM_PROBE_PACE");
+    const uint32_t pace = pe ? (uint32_t)strtoul(pe, nullptr, 0) : 0u;
 #define TCSUM_PD(GG, UU)                                                                                     \
     if (g.lanes == GG && g.loads == UU) {                                                                    \
         const uint32_t per_block = GG == 256 ? 1u : 256u / GG;                                               \
         if ((n + per_block - 1) / per_block >= (1u << 24))                                                   \
             return hipErrorInvalidValue;                                                                     \
         hipLaunchKernelGGL((k_probe_desc<GG, UU>), dim3((n + per_block - 1) / per_block), dim3(256), 0, stream, a, \
-                           descs, n, sink, xg);                                                              \
+                           descs, n, sink, xg, pace);                                                        \
         return hipGetLastError();                                                                            \
     }
     TCSUM_PD(16, 3) TCSUM_PD(16, 4) TCSUM_PD(16, 6) TCSUM_PD(16, 8) TCSUM_PD(32, 4) TCSUM_PD(32, 6)

@@ -163,13 +163,21 @@ def test_c_netif_queue_demo(tc):
     assert "queue server: 200 queues" in r.stdout
 
 
-@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0, 0, 0]])
-@pytest.mark.parametrize("where,shift", [("pinned", 0), ("pinned", 7), ("pageable", 3)])
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0, 0, 0], "distinct"])
+@pytest.mark.parametrize("where,shift", [("pinned", 0), ("pinned", 7), ("pageable", 3), ("registered", 5)])
 def test_host_multi_device_golden(tc, oracle, devices, where, shift):
     """tcsum_host_batch_ipv4{,_tx_fill,_rx_verify}_multi: byte-balanced shards
-    over a device list (one GPU here, listed repeatedly, so every shard
-    boundary is crossed) give the reference's sums, tx bytes and rx verdicts
-    in packet order; also fewer packets than devices."""
+    over a device list give the reference's sums, tx bytes and rx verdicts in
+    packet order; also fewer packets than devices.  One GPU listed repeatedly
+    crosses every shard boundary; "distinct" (every GPU of the box, skipped on
+    a one-GPU box) is what maps a pinned / registered arena on a second
+    device and runs the shards concurrently."""
+    if devices == "distinct":
+        import torch
+        nd = torch.cuda.device_count()
+        if nd < 2:
+            pytest.skip("one GPU: cross-device mapping unmeasured here")
+        devices = list(range(nd))
     cases, pool = G.ipv4_cases()
     arg, view, keep = host_copy(tc, pool, where, shift)
     out, flags = tc.host_batch_ipv4(arg, G.pkt_descs(cases, tc.PKT_DTYPE), devices=devices)

@@ -1,8 +1,11 @@
-"""A/B two builds of libtcsum.so in ONE process (box-to-box spread is larger
-than the effects measured): interleaved rounds, median ms per launch, and the
-outputs of every build must be identical.
+"""A/B two or more builds of libtcsum.so in ONE process (box-to-box spread is
+larger than the effects measured): interleaved rounds whose starting build
+rotates (the first build timed in a round measured ~1 % slow on the headline,
+whichever it was), median ms per launch, and the outputs of every build must
+be identical (AB_ALLOW_DIFF=1 for measurement builds that store nothing).
 
-  python scripts/ab_lib.py LIB_A LIB_B [configs]   (configs: mtu,tso,mixed,mixed_tx,mixed_rx)
+  python scripts/ab_lib.py LIB_A LIB_B [LIB_C ...] [configs]
+  (configs: mtu,tso,mixed,mixed_tx,mixed_rx)
 """
 import ctypes
 import os
@@ -25,9 +28,11 @@ def load(path):
     return L
 
 
-libs = [load(p) for p in sys.argv[1:3]]
-configs = sys.argv[3].split(",") if len(sys.argv) > 3 else ["mtu", "tso", "mixed", "mixed_tx", "mixed_rx"]
-rounds, reps = 5, 10
+paths = [a for a in sys.argv[1:] if a.endswith(".so")]
+rest = [a for a in sys.argv[1:] if not a.endswith(".so")]
+libs = [load(p) for p in paths]
+configs = rest[0].split(",") if rest else ["mtu", "tso", "mixed", "mixed_tx", "mixed_rx"]
+rounds, reps = 8, 10
 for cfg in configs:
     base = cfg.split("_")[0] if cfg in ("mixed_tx", "mixed_rx") else cfg
     b = workload.make_batch(base)
@@ -52,7 +57,8 @@ for cfg in configs:
 
     times = [[] for _ in libs]
     for r in range(rounds):
-        for i in range(len(libs)):
+        for k in range(len(libs)):
+            i = (r + k) % len(libs)
             run(i)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -63,7 +69,7 @@ for cfg in configs:
             times[i].append(e0.elapsed_time(e1) / reps)
     same = all(torch.equal(outs[0], o) for o in outs[1:])
     print(f"== {cfg} n={b.n} bytes={b.total_bytes} identical={same}", flush=True)
-    for i, p in enumerate(sys.argv[1:3]):
+    for i, p in enumerate(paths):
         med = float(np.median(times[i]))
         print(f"  {os.path.basename(p):24s} {med * 1e3:8.1f} us  {b.total_bytes / med / 1e6:8.1f} GB/s payload"
               f"  (min {min(times[i]) * 1e3:.1f})", flush=True)

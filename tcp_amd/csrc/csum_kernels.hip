@@ -66,6 +66,22 @@ __device__ __forceinline__ uint32_t chunk_sum_w(uint32_t acc, u32x4 v, uint32_t 
     return dot_halves(acc, v.w, w);
 }
 
+// Four independent accumulators, one per dword of the chunk: the dot2 ops of
+// one chunk do not wait on each other (a single chain put an s_nop between
+// every two of them), and the last chunk to arrive costs one dot2 latency,
+// not four, in the wave's tail.
+struct Acc4 {
+    uint32_t x, y, z, w;
+};
+__device__ __forceinline__ void acc4_add(Acc4 &a, u32x4 v, uint32_t w)
+{
+    a.x = dot_halves(a.x, v.x, w);
+    a.y = dot_halves(a.y, v.y, w);
+    a.z = dot_halves(a.z, v.z, w);
+    a.w = dot_halves(a.w, v.w, w);
+}
+__device__ __forceinline__ uint32_t acc4_total(const Acc4 &a) { return (a.x + a.y) + (a.z + a.w); }
+
 // Keep only bytes [lo, hi) of a chunk (positions 0..16).
 __device__ __forceinline__ u32x4 mask_chunk(u32x4 v, int lo, int hi);
 
@@ -283,10 +299,11 @@ __device__ __forceinline__ uint32_t frame_consume(Frame<U> &f, uint32_t gl)
     }
     // pass 0: the loads frame_issue put in flight
     {
-        uint32_t part = 0;
+        Acc4 p{0u, 0u, 0u, 0u};
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            part = chunk_sum_w(part, f.v[u], (uint32_t)(u * G) + gl < f.ni ? 0x00010001u : 0u);
+            acc4_add(p, f.v[u], (uint32_t)(u * G) + gl < f.ni ? 0x00010001u : 0u);
+        const uint32_t part = acc4_total(p); // <= 4 * 16 * 131070 < 2^23
         acc = EXACT ? acc + part : fold_step(acc + part);
     }
     // later passes load and sum inside one iteration: nothing vector-sized is
@@ -299,12 +316,13 @@ __device__ __forceinline__ uint32_t frame_consume(Frame<U> &f, uint32_t gl)
             const uint32_t j = b0 + u * G + gl;
             w[u] = load16<true>(f.ibase + (j < f.ni ? j : f.ilast));
         }
-        uint32_t part = 0;
+        Acc4 p{0u, 0u, 0u, 0u};
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t j = b0 + u * G + gl;
-            part = chunk_sum_w(part, w[u], j < f.ni ? 0x00010001u : 0u);
+            acc4_add(p, w[u], j < f.ni ? 0x00010001u : 0u);
         }
+        const uint32_t part = acc4_total(p);
         acc = EXACT ? acc + part : fold_step(acc + part);
     }
     return acc;
@@ -323,9 +341,31 @@ __device__ __forceinline__ uint32_t sum_range(const uint8_t *__restrict__ arena,
     return frame_consume<G, U, EXACT>(f, gl);
 }
 
+// checksum_peso's pseudo-header words, folded (tools.c:58-70): src, dst,
+// {0, proto}, htons((uint16_t)len).  Depends on the descriptor only, so the
+// kernels compute it while the range's bytes are in flight.
+__device__ __forceinline__ uint32_t peso_pseudo16(const SegDesc &d)
+{
+    uint32_t q = add_halves(0u, d.src);
+    q = add_halves(q, d.dst);
+    q += d.proto << 8;
+    q += bswap16(d.len & 0xFFFFu);
+    return fold16(q);
+}
+
+// Computed now, inside the load shadow: the empty asm pins the value here,
+// so the compiler cannot sink the arithmetic into the tail behind the last load.
+__device__ __forceinline__ uint32_t pinned(uint32_t x)
+{
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 // The packet's first lane turns the group's sum into the reference's u16.
+// MODE_PESO: q16 = peso_pseudo16(d) (ignored by the other modes).
 template <int MODE>
-__device__ __forceinline__ uint16_t finalize(uint32_t acc, uintptr_t start, const SegDesc &d, uint32_t aux)
+__device__ __forceinline__ uint16_t finalize(uint32_t acc, uintptr_t start, const SegDesc &d, uint32_t aux,
+                                             uint32_t q16)
 {
     uint32_t r;
     if constexpr (MODE == MODE_EXACT) {
@@ -349,33 +389,56 @@ __device__ __forceinline__ uint16_t finalize(uint32_t acc, uintptr_t start, cons
             const uint32_t t = fold_step(f + (d.pre & 0xFFFFu)); // pktbuf.c:657
             r = (aux & 1u) ? (~t & 0xFFFFu) : t;
         } else {
-            // tools.c:58-70: src, dst, {0, proto}, htons((uint16_t)len)
-            uint32_t q = add_halves(0u, d.src);
-            q = add_halves(q, d.dst);
-            q += d.proto << 8;
-            q += bswap16(d.len & 0xFFFFu);
-            r = ~fold_step(f + fold16(q)) & 0xFFFFu; // pktbuf_checksum16(..., 1), tools.c:73
+            r = ~fold_step(f + q16) & 0xFFFFu; // pktbuf_checksum16(..., 1), tools.c:73
         }
     }
     return (uint16_t)r;
 }
 
 // One wave-slice of packets per wave, one launch-wide pass.
+//
+// Results leave through the workgroup's LAST wave: each wave puts its packets'
+// u16 into LDS and bumps an LDS counter; the wave that brings it to 4 stores
+// all 256/G results with one coalesced store and the other three end at once.
+// With every wave storing its own 4 results (an 8-byte partial store each) the
+// headline ran 1.1 % slower -- as slow as its loads plus the stores' tail in
+// every wave; with the gathered store it matches the same kernel with no
+// store at all (profiles/r02/ab_store.txt).  A nontemporal store cost 4 %.
 template <int G, int U, int MODE>
 __global__ __launch_bounds__(256) void k_segments(const uint8_t *__restrict__ arena,
                                                   const void *__restrict__ descs, uint32_t n,
                                                   uint16_t *__restrict__ out, uint32_t aux, uint32_t xg)
 {
     static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G");
+    constexpr uint32_t PER = 256u / G; // ranges per workgroup
+    __shared__ uint16_t res[PER];
+    __shared__ uint32_t arrived;
+    if (threadIdx.x == 0)
+        arrived = 0;
+    __syncthreads();
     const uint32_t gl = threadIdx.x & (G - 1);
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
-    const uint32_t seg = blk * (256u / G) + threadIdx.x / G; // no 32-bit wrap for any n
+    const uint32_t seg = blk * PER + threadIdx.x / G; // no 32-bit wrap for any n
     const bool live = seg < n;
     const SegDesc d = load_desc<MODE>(descs, seg, live);
-    uint32_t acc = sum_range<G, U, MODE == MODE_EXACT>(arena, d.off, d.len, gl, [] {});
+    uint32_t q16 = 0;
+    uint32_t acc = sum_range<G, U, MODE == MODE_EXACT>(arena, d.off, d.len, gl, [&] {
+        if constexpr (MODE == MODE_PESO)
+            q16 = pinned(peso_pseudo16(d));
+    });
     acc = group_sum<G>(acc);
-    if (live && gl == 0)
-        out[seg] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + d.off), d, aux);
+    if (gl == 0)
+        res[threadIdx.x / G] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + d.off), d, aux, q16);
+    uint32_t order = 0;
+    if ((threadIdx.x & 63u) == 0) // release: this wave's res[] entries before the count
+        order = __hip_atomic_fetch_add(&arrived, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    order = __builtin_amdgcn_readfirstlane(order);
+    if (order == 3u) { // the last wave: every entry is in LDS
+        const uint32_t l = threadIdx.x & 63u;
+        const uint32_t sl = blk * PER + l;
+        if (l < PER && sl < n)
+            out[sl] = res[l];
+    }
 }
 
 // One range per workgroup: all four waves on one range (G = 256), for ranges
@@ -392,14 +455,18 @@ __global__ __launch_bounds__(256) void k_segments_wg(const uint8_t *__restrict__
     const uint32_t seg = xcd_block(blockIdx.x, gridDim.x, xg); // grid == n: one range per workgroup
     const bool live = seg < n;
     const SegDesc d = load_desc<MODE>(descs, seg, live);
-    uint32_t acc = sum_range<256, U, MODE == MODE_EXACT>(arena, d.off, d.len, gl, [] {});
+    uint32_t q16 = 0;
+    uint32_t acc = sum_range<256, U, MODE == MODE_EXACT>(arena, d.off, d.len, gl, [&] {
+        if constexpr (MODE == MODE_PESO)
+            q16 = pinned(peso_pseudo16(d));
+    });
     acc = group_sum<64>(acc); // < 2^23 (folded lanes) or exact
     if ((gl & 63u) == 0)
         part[gl >> 6] = acc;
     __syncthreads();
     if (gl == 0 && live)
         out[seg] = finalize<MODE>(part[0] + part[1] + part[2] + part[3], reinterpret_cast<uintptr_t>(arena + d.off),
-                                  d, aux);
+                                  d, aux, q16);
 }
 
 // Persistent form: a resident grid walks the batch; each wave prefetches its
@@ -423,7 +490,8 @@ __global__ __launch_bounds__(256) void k_segments_p(const uint8_t *__restrict__ 
                                                            [&] { nd = load_desc<MODE>(descs, nseg, nseg < n); });
         acc = group_sum<G>(acc);
         if (seg < n && gl == 0)
-            out[seg] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + d.off), d, aux);
+            out[seg] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + d.off), d, aux,
+                                      MODE == MODE_PESO ? peso_pseudo16(d) : 0u);
         seg = nseg;
         d = nd;
     }
@@ -444,7 +512,8 @@ __device__ __forceinline__ void finish_range(Frame<U> &f, const SegDesc &d, uint
     uint32_t acc = frame_consume<G, U, MODE == MODE_EXACT>(f, gl);
     acc = group_sum<G>(acc);
     if (seg < n && gl == 0)
-        out[seg] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + d.off), d, aux);
+        out[seg] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + d.off), d, aux,
+                                  MODE == MODE_PESO ? peso_pseudo16(d) : 0u);
 }
 
 template <int G, int U, int MODE>
@@ -1122,11 +1191,11 @@ __global__ __launch_bounds__(64) void k_call(CallBox *__restrict__ box, const ui
             const uint32_t comp = (ctl & CALL_COMPLEMENT) ? 1u : 0u;
             uint16_t r;
             if (mode == MODE_EXACT)
-                r = finalize<MODE_EXACT>(acc, start, d, comp | ((uint32_t)d.off << 1));
+                r = finalize<MODE_EXACT>(acc, start, d, comp | ((uint32_t)d.off << 1), 0u);
             else if (mode == MODE_PESO)
-                r = finalize<MODE_PESO>(acc, start, d, 0u);
+                r = finalize<MODE_PESO>(acc, start, d, 0u, peso_pseudo16(d));
             else
-                r = finalize<MODE_SEG>(acc, start, d, comp);
+                r = finalize<MODE_SEG>(acc, start, d, comp, 0u);
             __hip_atomic_store(&box->res, ((uint64_t)r << 32) | last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         t_last = __builtin_amdgcn_s_memrealtime();

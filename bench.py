@@ -331,7 +331,7 @@ def cpu_model():
         return None
 
 
-def cpu_baseline(torch, r, seconds, kind="reference"):
+def cpu_baseline(torch, r, seconds, kind="reference", cache_sample=True):
     """The reference's checksum_peso (oracle/_ref/libtcpref.so, compiled from
     /root/reference; kind "port" = the oracle's restatement) on the same
     segments in host memory, timed on this host's cores:
@@ -342,6 +342,7 @@ def cpu_baseline(torch, r, seconds, kind="reference"):
       value_all  every logical CPU of the host (os.cpu_count()), same sample;
       cache_resident  both, over a ~100 MB sample that fits the host's L3.
 
+    cache_sample=False (the secondary configs): the DRAM sample only.
     A requested "reference" that is not built fails (no silent fallback)."""
     from oracle import pyoracle
     import numpy as np
@@ -377,7 +378,8 @@ def cpu_baseline(torch, r, seconds, kind="reference"):
     res = {"unit": "GiB/s", "kind": kind, "cores": 1, "cores_all": threads_all, "host_cpu": cpu_model()}
     what = "segments" if b.kind == "peso" else "packets' L4 ranges"
     big = min(b.total_bytes, 1 << 30)
-    for label, nbytes, secs in (("dram", big, seconds), ("cache", 96 << 20, seconds / 2)):
+    legs = [("dram", big, seconds)] + ([("cache", 96 << 20, seconds / 2)] if cache_sample else [])
+    for label, nbytes, secs in legs:
         host, segs, want, n = sample(nbytes)
         rate1, got_kind, cs1 = pyoracle.time_peso(host, segs, 1, secs, kind=kind)
         rate_all, _, cs_all = pyoracle.time_peso(host, segs, threads_all, max(2.0, secs / 2), kind=kind)
@@ -689,6 +691,12 @@ def main():
         for cfg in [c for c in args.secondary.split(",") if c and c != args.config]:
             r = time_config(torch, tc, workload, cfg, 0, max(5, args.steps // 2), args.warmup)
             extra[cfg] = result_entry(r, max(5, args.steps // 2))
+            if cfg in ("tso", "mixed") and not args.no_cpu:  # CPU numbers for configs 2-4
+                try:
+                    extra[cfg]["cpu_baseline"] = cpu_baseline(torch, r, args.cpu_seconds / 2, args.cpu_kind,
+                                                              cache_sample=False)
+                except Exception as e:
+                    extra[cfg]["cpu_baseline"] = {"value": None, "error": repr(e)}
             del r
             torch.cuda.empty_cache()
         line["configs"] = extra

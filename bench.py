@@ -389,6 +389,12 @@ def cpu_baseline(torch, r, seconds, kind="reference", cache_sample=True):
                           f"re-summed for >= {secs:.0f} s (1 thread) / {max(2.0, secs / 2):.0f} s "
                           f"({threads_all} threads)",
                 "parity": bool(cs1 == want and cs_all == want)}
+        if label == "dram" and cache_sample and kind == "reference":
+            # BASELINE.md's optional strong-CPU line: the reference at -O3 with AVX2
+            s1, _, c1 = pyoracle.time_peso(host, segs, 1, secs / 2, kind="reference_o3")
+            s_all, _, c_all = pyoracle.time_peso(host, segs, threads_all, 2.0, kind="reference_o3")
+            part["strong_cpu"] = {"flags": "-O3 -march=x86-64-v3", "value": round(s1 / GIB, 3),
+                                  "value_all": round(s_all / GIB, 3), "parity": bool(c1 == want and c_all == want)}
         del host
         if label == "dram":
             res.update(part)

@@ -18,6 +18,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 REF_LIB_PATH = os.path.join(HERE, "_ref", "libtcpref.so")
+REF_O3_LIB_PATH = os.path.join(HERE, "_ref", "libtcpref_o3.so")  # -O3 -march=x86-64-v3
 
 # numpy views of the batch descriptors (identical to include/tcsum.h)
 SEG_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("pre_sum", "<u4")])
@@ -193,16 +194,18 @@ def time_peso(arena: np.ndarray, segs: np.ndarray, nthreads: int, min_seconds: f
     """Bytes/s of a checksum_peso-shaped CPU routine over the batch.
 
     kind "reference" times the reference's own checksum_peso
-    (oracle/_ref/libtcpref.so, built from /root/reference) and raises
+    (oracle/_ref/libtcpref.so, built from /root/reference at the reference's
+    -O2; "reference_o3": the same sources at -O3 -march=x86-64-v3) and raises
     FileNotFoundError when it was not built; kind "port" times this
     restatement.  Returns (bytes_per_second, kind, checksum_of_checksums).
     """
     L = lib()
-    if kind == "reference":
-        if not os.path.exists(REF_LIB_PATH):
-            raise FileNotFoundError(f"{REF_LIB_PATH} (the reference's checksum_peso) is not built: "
+    if kind in ("reference", "reference_o3"):
+        path = REF_LIB_PATH if kind == "reference" else REF_O3_LIB_PATH
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} (the reference's checksum_peso) is not built: "
                                     "make -C oracle ref in the build container")
-        ref = ctypes.CDLL(REF_LIB_PATH)
+        ref = ctypes.CDLL(path)
         fn = ctypes.cast(ref.tcpref_peso, ctypes.c_void_p).value
     elif kind == "port":
         fn = ctypes.cast(L.orc_checksum_peso, ctypes.c_void_p).value

@@ -777,3 +777,27 @@ def test_measurement_probes_leave_arena_and_sink_alone(torch, tc, config):
     torch.cuda.synchronize()
     assert int(sink.item()) == 0
     assert torch.equal(arena, before)
+
+
+@pytest.mark.parametrize("g,u", [(4, 1), (8, 4), (16, 6), (32, 6), (64, 16), (256, 16)])
+def test_ragged_batch_sizes_write_only_their_results(tc, torch, oracle, geometry, g, u):
+    """Batch sizes that leave the last workgroup partly empty (k_segments
+    stores a workgroup's results from its last wave, k_ipv4 per packet): every
+    result equals the oracle's and nothing past out[n) is written."""
+    rng = np.random.default_rng(77)
+    host = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    arena = torch.from_numpy(host).cuda()
+    geometry(g, u)
+    for n in (1, 2, 3, 15, 17, 63, 65, 1001):
+        p = np.zeros(n, tc.PESO_DTYPE)
+        p["len"] = rng.integers(1, 3000, n)
+        p["offset"] = rng.integers(0, host.size - 3000, n)
+        p["src"] = rng.integers(0, 256, (n, 4))
+        p["dst"] = rng.integers(0, 256, (n, 4))
+        p["protocol"] = rng.choice([6, 17], n)
+        out = torch.full((n + 300,), 0xABCD, dtype=torch.int32, device="cuda").view(torch.uint16)
+        tc.batch_peso(arena, tc.descs_to_device(p), n, int(p["len"].sum()), out=out)
+        got = out.cpu().numpy()
+        np.testing.assert_array_equal(got[:n], oracle.batch_peso(host, p, nthreads=8))
+        sentinel = np.full(n + 300, 0xABCD, np.int32).view(np.uint16)  # int32 fill seen as u16 pairs
+        np.testing.assert_array_equal(got[n:], sentinel[n:])

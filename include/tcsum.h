@@ -116,7 +116,12 @@ int tcsum_batch_ipv4(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev
  *   UDP checksum (L4 + 6; 0 is stored as 0) udp.c:320-321
  *   ICMP checksum (L4 + 2)                  icmpv4.c:45-58
  * L4 fields are left alone for fragments and short L4s; nothing is written
- * for SHORT / BAD_* packets.  out (ip | l4 << 16) and flags may be NULL. */
+ * for SHORT / BAD_* packets.  out (ip | l4 << 16) and flags may be NULL.
+ * From 131,072 packets on (TCSUM_TX_SPLIT=0/1 forces either form) the stores
+ * are deferred: one launch computes every packet's values and field
+ * positions into stream-ordered scratch (hipMallocAsync, 4-8 B per packet,
+ * freed on the stream), a second short launch writes all the fields.  Same
+ * bytes either way; the batch is complete when the stream reaches the end. */
 int tcsum_batch_ipv4_tx_fill(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,
                              uint32_t *out /*[dev] or NULL*/, uint8_t *flags /*[dev] or NULL*/,
                              uint64_t total_bytes_hint, void *stream);

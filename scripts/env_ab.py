@@ -53,13 +53,21 @@ def with_env(env, fn):
                 os.environ[k] = v
 
 
+# a tx fill writes the packets: every variant, run on the unfilled arena, must
+# leave the same bytes as the default
+arena_in = arena.clone() if b.op == "tx" else None
 run()
 torch.cuda.synchronize()
 ref = (out.clone(), verdict.clone())
+arena_ref = arena.clone() if b.op == "tx" else None
 for v in variants[1:]:
+    if arena_ref is not None:
+        arena.copy_(arena_in)
     with_env(v, run)
     torch.cuda.synchronize()
     assert torch.equal(out, ref[0]) and torch.equal(verdict, ref[1]), f"{v} changed the results"
+    if arena_ref is not None:
+        assert torch.equal(arena, arena_ref), f"{v} changed the filled packets"
 times = [[] for _ in variants]
 for r in range(7):
     for i, v in enumerate(variants):

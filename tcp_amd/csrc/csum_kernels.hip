@@ -580,8 +580,15 @@ constexpr uint32_t IP_OPT_NO_STORE = 1u; // IP_TX: compute the fill's values, le
 constexpr uint32_t IP_OPT_RELOAD = 2u;
 // measurement (TCSUM_IP_HDR_NT=1): the header chunks load nontemporal too
 constexpr uint32_t IP_OPT_HDR_NT = 4u;
+// IP_TX, deferred stores (launch_ipv4 mode 4): the values go to `out` and each
+// packet's store positions to a side array (through the verdict pointer, which
+// tx never uses); k_tx_scatter then writes them into the packets in a second,
+// short launch (tx fill)
+constexpr uint32_t IP_OPT_DEFER = 8u;
 // launch_ipv4 mode 3: IP_TX kernels with IP_OPT_NO_STORE
 constexpr int IP_TX_OFFLOAD = 3;
+// launch_ipv4 mode 4: the tx fill as k_ipv4<IP_TX> with IP_OPT_DEFER + k_tx_scatter
+constexpr int IP_TX_SPLIT = 4;
 
 // The 20 fixed header bytes at byte s0 (0..15) of the three aligned chunks
 // h0, h1, h2, as five dwords: hd[k] = bytes [s0 + 4k, s0 + 4k + 4).  Two
@@ -866,7 +873,9 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
                 l4 = ~f4 & 0xFFFFu;
         }
         if constexpr (IPM == IP_TX) {
-            if (!bad && !(opts & IP_OPT_NO_STORE)) { // stored in host order, like the struct fields
+            if (opts & IP_OPT_DEFER) // bit 16: the IPv4 field; low 16: the L4 field's offset (0: none)
+                reinterpret_cast<uint32_t *>(verdict_out)[pk] = bad ? 0u : (1u << 16) | (field_on ? hl + fld : 0u);
+            else if (!bad && !(opts & IP_OPT_NO_STORE)) { // stored in host order, like the struct fields
                 if (opts & IP_OPT_RELOAD) {
                     const u32x4 *c0 = reinterpret_cast<const u32x4 *>((start + 10u) & ~(uintptr_t)15u);
                     const u32x4 *c1 = reinterpret_cast<const u32x4 *>(
@@ -921,6 +930,35 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
     ipv4_packet<G, U, IPM>(arena, pkts, blk * (256u / G) + threadIdx.x / G, n, out, flags_out, verdict_out,
                            opts); // no 32-bit wrap for any n
+}
+
+// The deferred tx stores (IP_OPT_DEFER): one lane per packet writes the values
+// k_ipv4 left in `csums` at the positions it left in `pos`.
+// The deferred tx stores (IP_OPT_DEFER): one lane per packet writes the values
+// k_ipv4 left in `csums` at the positions it left in `pos` (bit 16: the IPv4
+// header field; low 16 bits: the L4 field's offset, 0 for none).  All the
+// packets' field writes then reach memory in one short burst instead of one at
+// a time through the read stream (u16 or nontemporal stores: no different;
+// system-scope write-through stores: slower; profiles/r02/ab_tx_split*.txt).
+__global__ __launch_bounds__(256) void k_tx_scatter(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
+                                                    uint32_t n, const uint32_t *__restrict__ csums,
+                                                    const uint32_t *__restrict__ pos)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t q = pos[i];
+    if (!q)
+        return;
+    const uint32_t v = csums[i];
+    uint8_t *pp = arena + pkts[i].offset;
+    pp[10] = (uint8_t)v; // ipv4.c:643,656, host order like the struct field
+    pp[11] = (uint8_t)(v >> 8);
+    const uint32_t f = q & 0xFFFFu;
+    if (f) { // tcp_out.c:19-20 / udp.c:320-321 / icmpv4.c:45-58
+        pp[f] = (uint8_t)(v >> 16);
+        pp[f + 1] = (uint8_t)(v >> 24);
+    }
 }
 
 // k_ipv4's loads and nothing else (measurement: tcsum_probe_ipv4): the 16-B
@@ -1678,6 +1716,21 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
         const char *rl = getenv("TCSUM_TX_RELOAD"); // measurement only (IP_OPT_RELOAD)
         return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict,
                              o | (rl && atoi(rl) ? IP_OPT_RELOAD : 0u), xg, stream);
+    }
+    case IP_TX_SPLIT: { // the fill with its stores deferred to k_tx_scatter
+        uint32_t *side = nullptr; // positions [n], then the values [n] when the caller wants no `out`
+        hipError_t e = hipMallocAsync(reinterpret_cast<void **>(&side), (size_t)n * (out ? 4u : 8u), stream);
+        if (e != hipSuccess)
+            return e;
+        uint32_t *vals = out ? out : side + n;
+        e = ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, vals, flags, reinterpret_cast<int8_t *>(side),
+                          o | IP_OPT_DEFER, xg, stream);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, arena, pkts, n, vals, side);
+            e = hipGetLastError();
+        }
+        const hipError_t f = hipFreeAsync(side, stream);
+        return e != hipSuccess ? e : f;
     }
     case IP_TX_OFFLOAD: // the tx values into `out` only; the packets are not written
         return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, o | IP_OPT_NO_STORE, xg,

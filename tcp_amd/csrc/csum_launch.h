@@ -31,7 +31,8 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
                            uint32_t n, uint16_t *out, uint32_t aux, hipStream_t stream);
 
 // ip_mode: 0 sums, 1 tx fill (writes into arena), 2 rx verify (verdict required),
-//          3 tx offload (the tx fill's values into out only; out required)
+//          3 tx offload (the tx fill's values into out only; out required),
+//          4 tx fill with its stores deferred to a second launch (k_tx_scatter)
 hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
                        uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream);
 

@@ -276,10 +276,13 @@ def test_ipv4_odd_arena_base(tc, torch):
     np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
 
 
+@pytest.mark.parametrize("split", ["0", "1"])
 @pytest.mark.parametrize("g,u", [(16, 1), (16, 4), (32, 3), (32, 4), (64, 2), (64, 16)])
-def test_batch_ipv4_tx_fill_golden(tc, torch, geometry, g, u):
-    """In-place fill == the reference's tx path on the same packets, byte for byte."""
+def test_batch_ipv4_tx_fill_golden(tc, torch, geometry, monkeypatch, g, u, split):
+    """In-place fill == the reference's tx path on the same packets, byte for
+    byte; stores in the kernel (split 0) and deferred to k_tx_scatter (1)."""
     geometry(g, u)
+    monkeypatch.setenv("TCSUM_TX_SPLIT", split)
     cases, pin, pout = G.ipv4_tx_cases()
     arena = to_dev(torch, pin)
     d = tc.descs_to_device(G.pkt_descs(cases, tc.PKT_DTYPE))
@@ -290,13 +293,16 @@ def test_batch_ipv4_tx_fill_golden(tc, torch, geometry, g, u):
     np.testing.assert_array_equal(arena.cpu().numpy()[: pout.size], pout)
 
 
+@pytest.mark.parametrize("split", ["0", "1"])
 @pytest.mark.parametrize("g,u", [(16, 1), (16, 6), (32, 4), (32, 6), (64, 16)])
-def test_batch_ipv4_tx_fill_stack_golden(tc, torch, geometry, g, u):
+def test_batch_ipv4_tx_fill_stack_golden(tc, torch, geometry, monkeypatch, g, u, split):
     """Frames the reference stack itself transmitted (udp_out, send_out,
     icmpv4_out, ipv4_out, ip_frag_out; oracle/stack_gen.c) with their filled
-    fields junked: the in-place fill gives the reference's frames back, byte
-    for byte, and the offload form + host apply gives the same bytes."""
+    fields junked: the in-place fill (stores in the kernel or deferred) gives
+    the reference's frames back, byte for byte, and the offload form + host
+    apply gives the same bytes."""
     geometry(g, u)
+    monkeypatch.setenv("TCSUM_TX_SPLIT", split)
     cases, pin, pout = G.stack_tx_cases()
     pk = G.pkt_descs(cases, tc.PKT_DTYPE)
     arena = to_dev(torch, pin)
@@ -331,17 +337,28 @@ def test_batch_ipv4_tx_offload_golden(tc, torch, geometry, g, u):
     np.testing.assert_array_equal(out.cpu().numpy(), fill_out.cpu().numpy())
 
 
-def test_tx_offload_full_mixed(tc, torch):
-    """configs[3] at full size: offload + host apply == in-place fill, every byte."""
+def test_tx_offload_full_mixed(tc, torch, monkeypatch):
+    """configs[3] at full size: offload + host apply == in-place fill, every
+    byte, with the fill's stores deferred (the default at this size) and in
+    the kernel; the fill's `out` equals the offload's."""
     from tcp_amd import workload
     b = workload.make_batch("mixed")
     arena, descs = workload.materialize(b)
+    unfilled = arena.clone()
     out, flags = tc.batch_ipv4_tx_offload(arena, descs, b.n, b.total_bytes)
-    host = arena.cpu().numpy()
-    tc.tx_apply_batch(host, b.descs, out.cpu().numpy(), flags.cpu().numpy())
+    host = torch.from_numpy(arena.cpu().numpy())
+    tc.tx_apply_batch(host.numpy(), b.descs, out.cpu().numpy(), flags.cpu().numpy())
+    want = host.to(arena.device)
+    del host
+    fill_out = torch.empty_like(out)
+    tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, out=fill_out, want_flags=False)
+    torch.cuda.synchronize()
+    assert torch.equal(arena, want) and torch.equal(fill_out, out)
+    arena.copy_(unfilled)
+    monkeypatch.setenv("TCSUM_TX_SPLIT", "0")
     tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
     torch.cuda.synchronize()
-    assert torch.equal(arena, torch.from_numpy(host).to(arena.device))
+    assert torch.equal(arena, want)
 
 
 @pytest.mark.parametrize("g,u", [(16, 1), (16, 4), (32, 3), (32, 4), (64, 2), (64, 16)])

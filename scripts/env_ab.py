@@ -3,7 +3,7 @@ libtcsum.so) in ONE process: interleaved rounds, median us per launch, and
 every variant's results must equal the default's.
 
   python scripts/env_ab.py CONFIG VAR=VALUE[,VAR=VALUE...] ...
-  e.g. python scripts/env_ab.py mixed_rx TCSUM_IP_HDR_NT=1
+  e.g. python scripts/env_ab.py mixed_tx TCSUM_TX_SPLIT=0
 CONFIG: mtu | tso | mixed | mixed_tx | mixed_rx | mixed_txo
 """
 import os

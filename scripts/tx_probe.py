@@ -1,8 +1,9 @@
 """Where does tx fill time go?  Interleaved rounds in one process: ipv4 sums,
-tx fill with stores, tx fill re-reading the field lines with the default
-cache policy right before its stores (TCSUM_TX_RELOAD=1, IP_OPT_RELOAD), tx
-offload (the same kernel without the stores), rx verify.  The reload variant
-must leave the same bytes as the plain fill."""
+tx fill (stores deferred to k_tx_scatter: the default for this size), tx fill
+with the stores in the kernel (TCSUM_TX_SPLIT=0), tx offload (the same kernel
+without the stores), rx verify.  Both fill forms must leave the same bytes.
+(Round 2 also had a variant re-reading the field lines with the default cache
+policy before the stores: no gain, profiles/r02/tx_probe_rx_fast.txt.)"""
 import os
 import sys
 
@@ -27,12 +28,12 @@ def tx():
     tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
 
 
-def tx_reload():
-    os.environ["TCSUM_TX_RELOAD"] = "1"
+def tx_fused():
+    os.environ["TCSUM_TX_SPLIT"] = "0"
     try:
         tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
     finally:
-        del os.environ["TCSUM_TX_RELOAD"]
+        del os.environ["TCSUM_TX_SPLIT"]
 
 
 outo = torch.empty(b.n, dtype=torch.uint32, device="cuda")
@@ -49,9 +50,9 @@ def rx():
 
 tx()
 ref = arena.clone()
-tx_reload()
-assert torch.equal(arena, ref), "the reload variant changed the filled bytes"
-variants = {"sums": sums, "tx": tx, "tx_reload": tx_reload, "tx_offload": tx_offload, "rx": rx}
+tx_fused()
+assert torch.equal(arena, ref), "the two fill forms left different bytes"
+variants = {"sums": sums, "tx": tx, "tx_fused": tx_fused, "tx_offload": tx_offload, "rx": rx}
 times = {k: [] for k in variants}
 for r in range(5):
     for k, fn in variants.items():

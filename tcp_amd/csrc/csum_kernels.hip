@@ -574,17 +574,11 @@ __global__ __launch_bounds__(256) void k_segments_pp(const uint8_t *__restrict__
 enum IpMode : int { IP_SUMS = 0, IP_TX = 1, IP_RX = 2 };
 // k_ipv4 `opts` bits (runtime, uniform over the grid)
 constexpr uint32_t IP_OPT_NO_STORE = 1u; // IP_TX: compute the fill's values, leave the packets alone
-// IP_TX experiment (TCSUM_TX_RELOAD=1): re-read the header chunk(s) holding the
-// fields with the default cache policy right before the stores, so the lines
-// the stores land in are L2-resident (tx fill).
-constexpr uint32_t IP_OPT_RELOAD = 2u;
-// measurement (TCSUM_IP_HDR_NT=1): the header chunks load nontemporal too
-constexpr uint32_t IP_OPT_HDR_NT = 4u;
 // IP_TX, deferred stores (launch_ipv4 mode 4): the values go to `out` and each
 // packet's store positions to a side array (through the verdict pointer, which
 // tx never uses); k_tx_scatter then writes them into the packets in a second,
 // short launch (tx fill)
-constexpr uint32_t IP_OPT_DEFER = 8u;
+constexpr uint32_t IP_OPT_DEFER = 2u;
 // launch_ipv4 mode 3: IP_TX kernels with IP_OPT_NO_STORE
 constexpr int IP_TX_OFFLOAD = 3;
 // launch_ipv4 mode 4: the tx fill as k_ipv4<IP_TX> with IP_OPT_DEFER + k_tx_scatter
@@ -660,10 +654,10 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     // fixed header: bytes [s0, s0 + 20) of base[0..2]
     const u32x4 *hb = big_enough ? base : &g_zero_chunk;
     const uint32_t h1i = big_enough ? 1u : 0u;
-    // header loads: default cache policy (IP_OPT_HDR_NT, measurement: nontemporal
-    // like the data pass that loads the same chunks)
-    const bool hnt = opts & IP_OPT_HDR_NT;
-    auto hload = [hnt](const u32x4 *q) { return hnt ? load16<true>(q) : load16<false>(q); };
+    // header loads: default cache policy (nontemporal like the data pass that
+    // loads the same chunks: no different in time or traffic,
+    // profiles/r02/ab_hdr_nt_*.txt)
+    auto hload = [](const u32x4 *q) { return load16<false>(q); };
     const u32x4 h0 = hload(hb);
     const u32x4 h1 = hload(hb + h1i);
     u32x4 h2, c2 = u32x4(0u), c3 = u32x4(0u);
@@ -876,16 +870,6 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
             if (opts & IP_OPT_DEFER) // bit 16: the IPv4 field; low 16: the L4 field's offset (0: none)
                 reinterpret_cast<uint32_t *>(verdict_out)[pk] = bad ? 0u : (1u << 16) | (field_on ? hl + fld : 0u);
             else if (!bad && !(opts & IP_OPT_NO_STORE)) { // stored in host order, like the struct fields
-                if (opts & IP_OPT_RELOAD) {
-                    const u32x4 *c0 = reinterpret_cast<const u32x4 *>((start + 10u) & ~(uintptr_t)15u);
-                    const u32x4 *c1 = reinterpret_cast<const u32x4 *>(
-                        (start + (field_on ? hl + fld + 1u : 11u)) & ~(uintptr_t)15u);
-                    const u32x4 t0 = load16<false>(c0), t1 = load16<false>(c1);
-                    uint32_t dep;
-                    asm volatile("v_and_b32 %0, 0, %1" : "=v"(dep) : "v"(t0.x ^ t1.w)); // 0, opaque: stores wait
-                    ip += dep;
-                    l4 += dep;
-                }
                 pp[10] = (uint8_t)ip;
                 pp[11] = (uint8_t)(ip >> 8);
                 if (field_on) {
@@ -932,8 +916,6 @@ __global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const
                            opts); // no 32-bit wrap for any n
 }
 
-// The deferred tx stores (IP_OPT_DEFER): one lane per packet writes the values
-// k_ipv4 left in `csums` at the positions it left in `pos`.
 // The deferred tx stores (IP_OPT_DEFER): one lane per packet writes the values
 // k_ipv4 left in `csums` at the positions it left in `pos` (bit 16: the IPv4
 // header field; low 16 bits: the L4 field's offset, 0 for none).  All the
@@ -1709,14 +1691,9 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
     const uint64_t per_block = 256u / (uint32_t)g.lanes;
     const dim3 grid((uint32_t)((n + per_block - 1) / per_block));
     const uint32_t xg = (uint32_t)g.xcd;
-    const char *hn = getenv("TCSUM_IP_HDR_NT"); // measurement only (IP_OPT_HDR_NT)
-    const uint32_t o = hn && atoi(hn) ? IP_OPT_HDR_NT : 0u;
     switch (ip_mode) {
-    case IP_TX: {
-        const char *rl = getenv("TCSUM_TX_RELOAD"); // measurement only (IP_OPT_RELOAD)
-        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict,
-                             o | (rl && atoi(rl) ? IP_OPT_RELOAD : 0u), xg, stream);
-    }
+    case IP_TX:
+        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, 0u, xg, stream);
     case IP_TX_SPLIT: { // the fill with its stores deferred to k_tx_scatter
         uint32_t *side = nullptr; // positions [n], then the values [n] when the caller wants no `out`
         hipError_t e = hipMallocAsync(reinterpret_cast<void **>(&side), (size_t)n * (out ? 4u : 8u), stream);
@@ -1724,7 +1701,7 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
             return e;
         uint32_t *vals = out ? out : side + n;
         e = ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, vals, flags, reinterpret_cast<int8_t *>(side),
-                          o | IP_OPT_DEFER, xg, stream);
+                          IP_OPT_DEFER, xg, stream);
         if (e == hipSuccess) {
             hipLaunchKernelGGL(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, arena, pkts, n, vals, side);
             e = hipGetLastError();
@@ -1733,12 +1710,12 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
         return e != hipSuccess ? e : f;
     }
     case IP_TX_OFFLOAD: // the tx values into `out` only; the packets are not written
-        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, o | IP_OPT_NO_STORE, xg,
+        return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, IP_OPT_NO_STORE, xg,
                              stream);
     case IP_RX:
-        return ipv4_u<IP_RX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, o, xg, stream);
+        return ipv4_u<IP_RX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, 0u, xg, stream);
     default:
-        return ipv4_u<IP_SUMS>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, o, xg, stream);
+        return ipv4_u<IP_SUMS>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, 0u, xg, stream);
     }
 }
 

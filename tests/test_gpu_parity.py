@@ -554,6 +554,51 @@ def test_huge_batch_index_math(tc, torch, oracle, geometry):
     np.testing.assert_array_equal(out.cpu().numpy(), exp)
 
 
+def test_huge_ipv4_batch_index_math(tc, torch, oracle, geometry):
+    """67M IPv4 packets at 64 lanes each (4 per workgroup): more than 2^24
+    workgroups, so launch_ipv4 cuts the batch into two launches.  Sums, the tx
+    fill (stores deferred: one scratch per launch) and rx verify give the
+    oracle's values on a sample around the seam and spread over the batch."""
+    geometry(64, 1)
+    n, L = (1 << 26) + 1000, 28
+    seam = ((1 << 24) - 1) * 4  # packets per launch at 64 lanes (kMaxBlocks)
+    rng = np.random.default_rng(23)
+    host = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    host[:, 0], host[:, 1], host[:, 2], host[:, 3] = 0x45, 0, 0, L  # IHL 5, total_len 28
+    host[:, 6] &= 0x40  # DF at most: no fragments
+    host[:, 7] = 0
+    host[:, 9] = np.where(rng.integers(0, 2, n) == 0, 17, 1)  # UDP or ICMP
+    pk = np.zeros(n, tc.PKT_DTYPE)
+    pk["offset"] = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    pk["len"] = L
+    idx = np.unique(np.concatenate([np.arange(2000), np.arange(seam - 3000, n), rng.choice(n, 50000)]))
+    sample = np.ascontiguousarray(host[idx]).reshape(-1)
+    spk = np.zeros(idx.size, tc.PKT_DTYPE)
+    spk["offset"] = np.arange(idx.size, dtype=np.uint64) * np.uint64(L)
+    spk["len"] = L
+    arena = torch.from_numpy(host.reshape(-1)).cuda()
+    del host
+    d = tc.descs_to_device(pk)
+    tidx = torch.from_numpy(idx).cuda()
+
+    out, flags = tc.batch_ipv4(arena, d, n, n * L)
+    eo, ef = oracle.batch_ipv4(sample, spk)
+    np.testing.assert_array_equal(out.view(torch.int32)[tidx].cpu().numpy().view(np.uint32), eo)
+    np.testing.assert_array_equal(flags[tidx].cpu().numpy(), ef)
+    del out, flags
+
+    tflags = tc.batch_ipv4_tx_fill(arena, d, n, n * L)  # >= 131,072 packets: deferred stores
+    efl = oracle.batch_ipv4_tx_fill(sample, spk)  # sample is filled in place
+    np.testing.assert_array_equal(tflags[tidx].cpu().numpy(), efl)
+    got = arena.view(n, L)[tidx].cpu().numpy().reshape(-1)
+    np.testing.assert_array_equal(got, sample)
+
+    verdict, vflags = tc.batch_ipv4_rx_verify(arena, d, n, n * L)
+    ev, evf = oracle.batch_ipv4_rx_verify(sample, spk)
+    np.testing.assert_array_equal(verdict[tidx].cpu().numpy(), ev)
+    np.testing.assert_array_equal(vflags[tidx].cpu().numpy(), evf)
+
+
 @pytest.mark.parametrize("order,chunk_mb", [("permuted", None), ("offset", None), ("offset", "1")])
 def test_host_batch_end_to_end(tc, oracle, monkeypatch, order, chunk_mb):
     """Pinned host arena -> H2D -> kernel -> D2H matches the device-resident

@@ -8,6 +8,8 @@
 //   line     one 128-B line per header written whole (8 lanes x 16 B)
 //   rmw      one lane per header reads its 16-B chunk (default policy) and
 //            writes it back with the field changed
+//   sec32/64 the aligned 32-/64-B sector holding the field, written whole
+//            (rmw: read first, the sector's own bytes written back)
 //   dense    2 bytes per header into a dense array (the write bytes alone)
 // Build: hipcc --offload-arch=gfx950 -O3 -o build/write_probe scripts/write_probe.hip
 #include <hip/hip_runtime.h>
@@ -64,6 +66,27 @@ __global__ __launch_bounds__(256) void k_rmw(uint8_t *a, uint64_t stride, uint32
     *c = x;
 }
 
+// one aligned S-byte sector per header (S/16 lanes x 16 B), written whole;
+// RMW: read first (the sector's own bytes back, one field changed)
+template <int S, bool RMW>
+__global__ __launch_bounds__(256) void k_sector(uint8_t *a, uint64_t stride, uint32_t n, const uint32_t *perm,
+                                                uint16_t v)
+{
+    constexpr uint32_t L = S / 16;
+    const uint32_t i = blockIdx.x * (256u / L) + threadIdx.x / L;
+    if (i >= n)
+        return;
+    const uint32_t p = perm ? perm[i] : i;
+    u32x4 *c = (u32x4 *)((uintptr_t)(a + (uint64_t)p * stride + 10) & ~(uintptr_t)(S - 1)) + (threadIdx.x % L);
+    if constexpr (RMW) {
+        u32x4 x = *c;
+        x.x ^= v;
+        *c = x;
+    } else {
+        *c = u32x4(v + p);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_dense(uint8_t *a, uint64_t stride, uint32_t n, const uint32_t *perm,
                                                uint16_t v)
 {
@@ -92,6 +115,8 @@ int main(int argc, char **argv)
 {
     const uint64_t total = 4752ull << 20;
     std::vector<uint64_t> strides = {64, 128, 256, 512, 1024, 2048, 4096, 4532, 8192, 16384};
+    if (argc > 2)
+        strides = {strtoull(argv[2], 0, 0)};
     uint8_t *a;
     CHECK(hipMalloc(&a, total + 4096));
     CHECK(hipMemset(a, 0x11, total + 4096));
@@ -120,6 +145,8 @@ int main(int argc, char **argv)
             uint32_t per_block;
         } vs[] = {{"u16", k_u16, false, 256}, {"u16 perm", k_u16, true, 256}, {"line", k_line, false, 32},
                   {"line perm", k_line, true, 32}, {"rmw", k_rmw, false, 256}, {"rmw perm", k_rmw, true, 256},
+                  {"sec32", k_sector<32, false>, false, 128}, {"sec32 rmw", k_sector<32, true>, false, 128},
+                  {"sec64", k_sector<64, false>, false, 64}, {"sec64 rmw", k_sector<64, true>, false, 64},
                   {"dense", k_dense, false, 256}};
         constexpr int NV = sizeof(vs) / sizeof(vs[0]);
         std::vector<float> t[NV];

@@ -337,6 +337,40 @@ def test_batch_ipv4_tx_offload_golden(tc, torch, geometry, g, u):
     np.testing.assert_array_equal(out.cpu().numpy(), fill_out.cpu().numpy())
 
 
+@pytest.mark.parametrize("layout", ["packed", "gaps", "shuffled"])
+def test_tx_fill_deferred_neighbours(tc, torch, oracle, monkeypatch, layout):
+    """The deferred fill (k_tx_scatter) on tiny packets (28-160 B: neighbours'
+    fields share 64-B sectors and 128-B lines), back to back at an odd base,
+    with gaps between some (bytes of no packet: must stay untouched), or with
+    the descriptors shuffled: every byte of the arena equals the oracle's fill."""
+    monkeypatch.setenv("TCSUM_TX_SPLIT", "1")
+    rng = np.random.default_rng({"packed": 1, "gaps": 2, "shuffled": 3}[layout])
+    n = 20000
+    proto = rng.choice([6, 17, 1], n)
+    lo = np.where(proto == 6, 40, np.where(proto == 17, 28, 24))
+    lens = rng.integers(lo, 161)
+    gap = rng.integers(0, 40, n) * (rng.random(n) < 0.3) if layout == "gaps" else np.zeros(n, np.int64)
+    offs = 7 + np.concatenate([[0], np.cumsum(lens + gap)[:-1]])
+    arena = rng.integers(0, 256, int(offs[-1] + lens[-1] + 200), dtype=np.uint8)
+    for i in range(n):
+        o, L = int(offs[i]), int(lens[i])
+        arena[o] = 0x45
+        arena[o + 2: o + 4] = (L >> 8, L & 0xFF)
+        arena[o + 6] &= 0x40  # DF at most: not a fragment
+        arena[o + 7] = 0
+        arena[o + 9] = proto[i]
+    pk = np.zeros(n, tc.PKT_DTYPE)
+    pk["offset"], pk["len"] = offs, lens
+    if layout == "shuffled":
+        pk = pk[rng.permutation(n)]
+    want = arena.copy()
+    wfl = oracle.batch_ipv4_tx_fill(want, pk)
+    d_arena = to_dev(torch, arena)
+    fl = tc.batch_ipv4_tx_fill(d_arena, tc.descs_to_device(pk), n, int(lens.sum()))
+    np.testing.assert_array_equal(fl.cpu().numpy(), wfl)
+    np.testing.assert_array_equal(d_arena.cpu().numpy()[: arena.size], want)
+
+
 def test_tx_offload_full_mixed(tc, torch, monkeypatch):
     """configs[3] at full size: offload + host apply == in-place fill, every
     byte, with the fill's stores deferred (the default at this size) and in

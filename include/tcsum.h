@@ -119,7 +119,8 @@ int tcsum_batch_ipv4(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev
  * for SHORT / BAD_* packets.  out (ip | l4 << 16) and flags may be NULL.
  * From 131,072 packets on (TCSUM_TX_SPLIT=0/1 forces either form) the stores
  * are deferred: one launch computes every packet's values and field
- * positions into stream-ordered scratch (hipMallocAsync, 4-8 B per packet,
+ * positions into stream-ordered scratch (4-8 B per packet, from a memory
+ * pool the library keeps per device, up to 1 GiB retained between calls;
  * freed on the stream), a second short launch writes all the fields.  Same
  * bytes either way; the batch is complete when the stream reaches the end. */
 int tcsum_batch_ipv4_tx_fill(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,

@@ -27,6 +27,8 @@
 
 #include <stdlib.h>
 
+#include <mutex>
+
 namespace tcsum {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -1663,6 +1665,38 @@ static hipError_t ipv4_u(int G, int U, dim3 grid, uint8_t *arena, const tcsum_pk
     return hipErrorInvalidValue;
 }
 
+// Stream-ordered scratch for the deferred tx fill, from a pool of the
+// library's own per device that keeps up to 1 GiB between calls: the default
+// pool hands its memory back at every synchronization, and mapping it again
+// cost a synchronized 1M-packet fill ~190 us (profiles/r02/tx_sync_probe.txt).
+static hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t stream)
+{
+    static std::mutex mu;
+    static hipMemPool_t pools[64] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess)
+        return e;
+    hipMemPool_t pool = nullptr;
+    if (dev >= 0 && dev < 64) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!pools[dev]) {
+            hipMemPoolProps props = {};
+            props.allocType = hipMemAllocationTypePinned;
+            props.location.type = hipMemLocationTypeDevice;
+            props.location.id = dev;
+            if (hipMemPoolCreate(&pools[dev], &props) == hipSuccess) {
+                uint64_t keep = 1ull << 30;
+                (void)hipMemPoolSetAttribute(pools[dev], hipMemPoolAttrReleaseThreshold, &keep);
+            } else {
+                pools[dev] = nullptr;
+            }
+        }
+        pool = pools[dev];
+    }
+    return pool ? hipMallocFromPoolAsync(p, bytes, pool, stream) : hipMallocAsync(p, bytes, stream);
+}
+
 hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
                        uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream)
 {
@@ -1696,7 +1730,7 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
         return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, 0u, xg, stream);
     case IP_TX_SPLIT: { // the fill with its stores deferred to k_tx_scatter
         uint32_t *side = nullptr; // positions [n], then the values [n] when the caller wants no `out`
-        hipError_t e = hipMallocAsync(reinterpret_cast<void **>(&side), (size_t)n * (out ? 4u : 8u), stream);
+        hipError_t e = scratch_alloc(reinterpret_cast<void **>(&side), (size_t)n * (out ? 4u : 8u), stream);
         if (e != hipSuccess)
             return e;
         uint32_t *vals = out ? out : side + n;

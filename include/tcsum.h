@@ -15,7 +15,9 @@
  *   - All pointers marked [dev] are device (HBM) pointers; [host] are host.
  *   - `stream` is a hipStream_t passed as void* (NULL = the null stream).
  *     Batch calls are asynchronous on that stream; nothing is allocated or
- *     freed inside them (they are safe to capture in a hipGraph).
+ *     freed inside them (they are safe to capture in a hipGraph) -- except
+ *     the stream-ordered scratch of a large tcsum_batch_ipv4_tx_fill outside
+ *     capture (see there).
  *   - Results are the u16 exactly as the reference returns it: the value as it
  *     sits in little-endian host memory, so storing it into the header field
  *     yields network-order bytes (net/src/tools.c:24-54).
@@ -122,7 +124,9 @@ int tcsum_batch_ipv4(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev
  * positions into stream-ordered scratch (4-8 B per packet, from a memory
  * pool the library keeps per device, up to 1 GiB retained between calls;
  * freed on the stream), a second short launch writes all the fields.  Same
- * bytes either way; the batch is complete when the stream reaches the end. */
+ * bytes either way; the batch is complete when the stream reaches the end.
+ * On a stream under hipGraph capture the fill is one launch that allocates
+ * nothing, like every other batch call. */
 int tcsum_batch_ipv4_tx_fill(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,
                              uint32_t *out /*[dev] or NULL*/, uint8_t *flags /*[dev] or NULL*/,
                              uint64_t total_bytes_hint, void *stream);

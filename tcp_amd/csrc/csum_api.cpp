@@ -424,8 +424,14 @@ int tcsum_batch_ipv4_tx_fill(void *arena, const tcsum_pkt_t *pkts, uint32_t n, u
     // configs[3] than storing each packet's fields as its sums finish, which
     // trickles a million isolated writes through the read stream (DESIGN.md
     // §6, tx fill).  Small batches keep one launch.  TCSUM_TX_SPLIT=0/1 forces.
+    // Under hipGraph capture the single-launch form is taken: it allocates
+    // nothing (this header's convention).
     const char *sp = getenv("TCSUM_TX_SPLIT");
-    const bool split = sp ? atoi(sp) != 0 : n >= kTxSplitMin;
+    bool split = sp ? atoi(sp) != 0 : n >= kTxSplitMin;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (split && hipStreamIsCapturing(static_cast<hipStream_t>(stream), &cap) == hipSuccess &&
+        cap != hipStreamCaptureStatusNone)
+        split = false;
     const hipError_t e = tcsum::launch_ipv4(split ? 4 : 1, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
                                             static_cast<uint8_t *>(arena), pkts, n, out, flags, nullptr,
                                             static_cast<hipStream_t>(stream));

@@ -547,6 +547,28 @@ def test_hip_graph_capture_and_replay(tc, torch, oracle):
     assert (exp2 != exp).mean() > 0.99
 
 
+def test_hip_graph_capture_tx_fill(tc, torch, oracle):
+    """A tx fill large enough for the deferred form (>= 131,072 packets) takes
+    the single-launch form under capture (no allocation inside a graph): the
+    replayed graph fills the packets like the oracle, twice."""
+    from tcp_amd import workload
+    b = workload.make_batch("mixed_tx", n=140000)
+    arena, descs = workload.materialize(b)
+    unfilled = arena.clone()
+    want = arena.cpu().numpy()
+    oracle.batch_ipv4_tx_fill(want, b.descs, nthreads=8)
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
+    for _ in range(2):
+        arena.copy_(unfilled)
+        g.replay()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(arena.cpu().numpy(), want)
+
+
 def test_concurrent_streams(tc, torch, oracle):
     """Independent batches on independent streams do not interfere.  Outputs
     are allocated once up front: a tensor freed on one stream and reused by

@@ -276,13 +276,22 @@ def test_ipv4_odd_arena_base(tc, torch):
     np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
+TX_FORMS = ["fused", "deferred"]
+
+
+def set_tx_form(monkeypatch, form):
+    """The two forms of the in-place tx fill: stores in the kernel
+    (k_ipv4<IP_TX>) or deferred to k_tx_scatter."""
+    monkeypatch.setenv("TCSUM_TX_SPLIT", "1" if form == "deferred" else "0")
+
+
+@pytest.mark.parametrize("form", TX_FORMS)
 @pytest.mark.parametrize("g,u", [(16, 1), (16, 4), (32, 3), (32, 4), (64, 2), (64, 16)])
-def test_batch_ipv4_tx_fill_golden(tc, torch, geometry, monkeypatch, g, u, split):
+def test_batch_ipv4_tx_fill_golden(tc, torch, geometry, monkeypatch, g, u, form):
     """In-place fill == the reference's tx path on the same packets, byte for
-    byte; stores in the kernel (split 0) and deferred to k_tx_scatter (1)."""
+    byte, in every form of the fill."""
     geometry(g, u)
-    monkeypatch.setenv("TCSUM_TX_SPLIT", split)
+    set_tx_form(monkeypatch, form)
     cases, pin, pout = G.ipv4_tx_cases()
     arena = to_dev(torch, pin)
     d = tc.descs_to_device(G.pkt_descs(cases, tc.PKT_DTYPE))
@@ -293,16 +302,16 @@ def test_batch_ipv4_tx_fill_golden(tc, torch, geometry, monkeypatch, g, u, split
     np.testing.assert_array_equal(arena.cpu().numpy()[: pout.size], pout)
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
+@pytest.mark.parametrize("form", TX_FORMS)
 @pytest.mark.parametrize("g,u", [(16, 1), (16, 6), (32, 4), (32, 6), (64, 16)])
-def test_batch_ipv4_tx_fill_stack_golden(tc, torch, geometry, monkeypatch, g, u, split):
+def test_batch_ipv4_tx_fill_stack_golden(tc, torch, geometry, monkeypatch, g, u, form):
     """Frames the reference stack itself transmitted (udp_out, send_out,
     icmpv4_out, ipv4_out, ip_frag_out; oracle/stack_gen.c) with their filled
-    fields junked: the in-place fill (stores in the kernel or deferred) gives
-    the reference's frames back, byte for byte, and the offload form + host
-    apply gives the same bytes."""
+    fields junked: the in-place fill (every form) gives the reference's frames
+    back, byte for byte, and the offload form + host apply gives the same
+    bytes."""
     geometry(g, u)
-    monkeypatch.setenv("TCSUM_TX_SPLIT", split)
+    set_tx_form(monkeypatch, form)
     cases, pin, pout = G.stack_tx_cases()
     pk = G.pkt_descs(cases, tc.PKT_DTYPE)
     arena = to_dev(torch, pin)
@@ -337,18 +346,21 @@ def test_batch_ipv4_tx_offload_golden(tc, torch, geometry, g, u):
     np.testing.assert_array_equal(out.cpu().numpy(), fill_out.cpu().numpy())
 
 
+@pytest.mark.parametrize("form", TX_FORMS)
+@pytest.mark.parametrize("top", [160, 700])
 @pytest.mark.parametrize("layout", ["packed", "gaps", "shuffled"])
-def test_tx_fill_deferred_neighbours(tc, torch, oracle, monkeypatch, layout):
-    """The deferred fill (k_tx_scatter) on tiny packets (28-160 B: neighbours'
-    fields share 64-B sectors and 128-B lines), back to back at an odd base,
-    with gaps between some (bytes of no packet: must stay untouched), or with
-    the descriptors shuffled: every byte of the arena equals the oracle's fill."""
-    monkeypatch.setenv("TCSUM_TX_SPLIT", "1")
-    rng = np.random.default_rng({"packed": 1, "gaps": 2, "shuffled": 3}[layout])
+def test_tx_fill_neighbours(tc, torch, oracle, monkeypatch, layout, top, form):
+    """Both fill forms on small packets (28-160 B: neighbours' fields share
+    64-B sectors and 128-B lines; 28-700 B: a mix), back to back at an odd
+    base, with gaps between some (bytes of no packet: must stay untouched), or
+    with the descriptors shuffled: every byte of the arena equals the
+    oracle's fill."""
+    set_tx_form(monkeypatch, form)
+    rng = np.random.default_rng({"packed": 1, "gaps": 2, "shuffled": 3}[layout] + top)
     n = 20000
     proto = rng.choice([6, 17, 1], n)
     lo = np.where(proto == 6, 40, np.where(proto == 17, 28, 24))
-    lens = rng.integers(lo, 161)
+    lens = rng.integers(lo, top + 1)
     gap = rng.integers(0, 40, n) * (rng.random(n) < 0.3) if layout == "gaps" else np.zeros(n, np.int64)
     offs = 7 + np.concatenate([[0], np.cumsum(lens + gap)[:-1]])
     arena = rng.integers(0, 256, int(offs[-1] + lens[-1] + 200), dtype=np.uint8)
@@ -373,8 +385,8 @@ def test_tx_fill_deferred_neighbours(tc, torch, oracle, monkeypatch, layout):
 
 def test_tx_offload_full_mixed(tc, torch, monkeypatch):
     """configs[3] at full size: offload + host apply == in-place fill, every
-    byte, with the fill's stores deferred (the default at this size) and in
-    the kernel; the fill's `out` equals the offload's."""
+    byte, in the default form at this size and in the other two; the fill's
+    `out` equals the offload's."""
     from tcp_amd import workload
     b = workload.make_batch("mixed")
     arena, descs = workload.materialize(b)
@@ -388,11 +400,12 @@ def test_tx_offload_full_mixed(tc, torch, monkeypatch):
     tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, out=fill_out, want_flags=False)
     torch.cuda.synchronize()
     assert torch.equal(arena, want) and torch.equal(fill_out, out)
-    arena.copy_(unfilled)
-    monkeypatch.setenv("TCSUM_TX_SPLIT", "0")
-    tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
-    torch.cuda.synchronize()
-    assert torch.equal(arena, want)
+    for form in TX_FORMS:
+        arena.copy_(unfilled)
+        set_tx_form(monkeypatch, form)
+        tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
+        torch.cuda.synchronize()
+        assert torch.equal(arena, want), form
 
 
 @pytest.mark.parametrize("g,u", [(16, 1), (16, 4), (32, 3), (32, 4), (64, 2), (64, 16)])

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <mutex>
 #include <stddef.h>
@@ -69,7 +70,8 @@ struct Pinned {
 
 struct Ctx {
     std::mutex mu;
-    bool ready = false;
+    // set last by ctx_init under mu; legacy_ctx reads it before taking mu
+    std::atomic<bool> ready{false};
     int device = -1;
     hipStream_t stream = nullptr; // legacy (synchronous) calls
     // pinned, fine-grained staging the kernel reads/writes directly

@@ -11,6 +11,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 
 def env():
@@ -84,20 +85,30 @@ def spawn_ranks(n: int, argv: list[str], extra_env: dict | None = None, timeout:
                  MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         e.update(extra_env or {})
         procs.append(subprocess.Popen([sys.executable] + list(argv), env=e))
+    # poll every rank (not one after another): a rank that fails while rank 0
+    # waits in a barrier must end the others at once, not after a rendezvous
+    # time-out
+    t0 = time.monotonic()
     rc = 0
-    for p in procs:
+    while True:
+        codes = [p.poll() for p in procs]
+        for code in codes:
+            if code:
+                code = 128 - code if code < 0 else code
+                rc = rc or code
+        if rc or all(c is not None for c in codes):
+            break
+        if timeout is not None and time.monotonic() - t0 > timeout:
+            rc = 124
+            break
+        time.sleep(0.05)
+    for q in procs:  # one rank failed or timed out: the others would hang in the next barrier
+        if q.poll() is None:
+            q.terminate() if rc != 124 else q.kill()
+    for q in procs:
         try:
-            code = p.wait(timeout=timeout)
+            q.wait(timeout=10)
         except subprocess.TimeoutExpired:
-            for q in procs:
-                if q.poll() is None:
-                    q.kill()
-            p.wait()
-            code = 124
-        code = 128 - code if code < 0 else code
-        if code and not rc:
-            rc = code
-            for q in procs:  # one rank failed: the others would hang in the next barrier
-                if q.poll() is None:
-                    q.terminate()
+            q.kill()
+            q.wait()
     return rc

@@ -50,3 +50,21 @@ def test_world_size_must_match_gpus():
     assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
     r = run(["--steps", "1", "--cpu-rehearsal"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2
+
+
+@pytest.mark.timeout(120)
+def test_spawn_ranks_failing_rank_ends_the_others(tmp_path):
+    """A rank that fails while rank 0 is still running (e.g. waiting in a
+    barrier) ends the whole launch at once with its exit status."""
+    import time
+    sys.path.insert(0, ROOT)
+    from tcp_amd import dist as D
+    prog = tmp_path / "rank.py"
+    prog.write_text("import os, sys, time\n"
+                    "if os.environ['RANK'] == '1':\n"
+                    "    sys.exit(3)\n"
+                    "time.sleep(60)\n")
+    t0 = time.monotonic()
+    assert D.spawn_ranks(2, [str(prog)]) == 3
+    assert time.monotonic() - t0 < 30
+    assert D.spawn_ranks(2, [str(prog)], extra_env={"RANK": "0"}, timeout=1.0) == 124  # both sleep: time-out

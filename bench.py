@@ -233,6 +233,11 @@ def result_entry(r, steps):
 
 # ------------------------------------------------------------ PMC traffic
 
+def is_step_kernel(name: str) -> bool:
+    """The kernels one bench step launches (the probes are not among them)."""
+    return "k_segments" in name or "k_ipv4<" in name or "k_tx_scatter" in name
+
+
 def pmc_traffic(config: str):
     """HBM bytes per launch from rocprofv3 counters, in separate passes
     (FETCH_SIZE, then WRITE_SIZE), run as a child before this process touches
@@ -258,18 +263,17 @@ def pmc_traffic(config: str):
             os.makedirs(keep, exist_ok=True)
             for i, f in enumerate(files):
                 shutil.copy(f, os.path.join(keep, f"pmc_{counter.lower()}_{config}{'_%d' % i if i else ''}.csv"))
-        per = []
+        per = {}  # kernel name -> values; a step is one launch of each (tx fill: k_ipv4 + k_tx_scatter)
         for f in files:
             with open(f) as fh:
                 for row in csv.DictReader(fh):
                     name = row.get("Kernel_Name", "")
-                    if "k_segments" in name or "k_ipv4" in name:  # the checksum kernels only
-                        if row.get("Counter_Name", counter) == counter:
-                            per.append(float(row["Counter_Value"]))
+                    if is_step_kernel(name) and row.get("Counter_Name", counter) == counter:
+                        per.setdefault(name.split("(")[0], []).append(float(row["Counter_Value"]))
         shutil.rmtree(d, ignore_errors=True)
         if not per:
             return None, f"no {counter} rows for the checksum kernel"
-        vals[counter] = sorted(per)[len(per) // 2]
+        vals[counter] = sum(sorted(v)[len(v) // 2] for v in per.values())
     traffic = vals["FETCH_SIZE"] * 1024 * 2 + vals["WRITE_SIZE"] * 1024
     return traffic, None
 
@@ -304,7 +308,7 @@ def rocprof_trace(config: str, steps: int, warmup: int, settle_ms: float):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 name = row.get("Kernel_Name", "")
-                if "k_segments" in name or "k_ipv4" in name:
+                if is_step_kernel(name):
                     rows.append((name, int(row["Grid_Size_X"]),
                                  int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
     shutil.rmtree(d, ignore_errors=True)
@@ -313,10 +317,16 @@ def rocprof_trace(config: str, steps: int, warmup: int, settle_ms: float):
     total = {}
     for name, grid, dur in rows:
         total[name] = total.get(name, 0) + dur
+
+    def median_at_full_grid(name):
+        grid = max(g for n, g, _ in rows if n == name)
+        return sorted(dur for n, g, dur in rows if n == name and g == grid)
+
     name = max(total, key=total.get)
-    grid = max(g for n, g, _ in rows if n == name)
-    durs = sorted(dur for n, g, dur in rows if n == name and g == grid)
-    return (durs[len(durs) // 2], sum(durs) / len(durs), len(durs), name), None
+    durs = median_at_full_grid(name)
+    # every kernel of a step (tx fill: the fill + k_tx_scatter), median each
+    step_ns = sum(median_at_full_grid(k)[len(median_at_full_grid(k)) // 2] for k in total)
+    return (durs[len(durs) // 2], sum(durs) / len(durs), len(durs), name, step_ns, len(total)), None
 
 
 # ------------------------------------------------------------ CPU baseline
@@ -648,10 +658,13 @@ def main():
         roof["rocprof_frac"] = None
         roof["rocprof_note"] = trace_note
     else:  # the same algorithmic bytes over the profiled child's median launch
-        med_ns, mean_ns, nl, kname = trace
+        med_ns, mean_ns, nl, kname, step_ns, nk = trace
         roof["rocprof_frac"] = round(algorithmic_bytes(b) / (med_ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
+        if nk > 1:  # the same bytes over every kernel of a step (their medians summed)
+            roof["rocprof_step_frac"] = round(algorithmic_bytes(b) / (step_ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
         roof["rocprof"] = {"kernel": kname, "launches": nl, "median_us": round(med_ns / 1e3, 1),
-                           "mean_us": round(mean_ns / 1e3, 1),
+                           "mean_us": round(mean_ns / 1e3, 1), "step_kernels": nk,
+                           "step_median_us": round(step_ns / 1e3, 1),
                            "source": "rocprofv3 --kernel-trace --stats of bench.py --config "
                                      f"{args.config} (same K/W/settle), run as a child of this bench"}
 

@@ -6,6 +6,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <chrono>
 #include <mutex>
 #include <stddef.h>
@@ -595,6 +598,15 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
 {
     if (n == 0)
         return TCSUM_OK;
+    // TCSUM_E2E_TRACE=1: host-side phase times of this call on stderr (measurement)
+    const char *tr = getenv("TCSUM_E2E_TRACE");
+    const bool trace = tr && atoi(tr);
+    const auto t_start = std::chrono::steady_clock::now();
+    auto stamp = [&](const char *what) {
+        if (trace)
+            fprintf(stderr, "e2e %-16s %9.1f us\n", what,
+                    std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_start).count());
+    };
     if (!host_arena || !segs || !out || device < 0 || device >= kMaxDev)
         return TCSUM_ERR_PARAM;
     // One parallel pass over the descriptors: per block of kSpanBlock
@@ -623,6 +635,7 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         all.merge(sp);
     if (all.bad)
         return TCSUM_ERR_PARAM;
+    stamp("span pass");
     const uint64_t glo = all.hi ? all.lo & ~uint64_t(15) : 0, ghi = all.hi;
     Ctx &c = g_ctx[device];
     std::lock_guard<std::mutex> lk(c.mu);
@@ -711,12 +724,15 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     };
     // the first chunk's bytes start crossing the link while the host stages
     // the descriptors
+    stamp("buffers");
     if (copy_bytes(ch[0]) != hipSuccess)
         return fail(TCSUM_ERR_SYS);
+    stamp("first copy");
     if (stage_descs)
         par_memcpy(c.q_desc.h, reinterpret_cast<const uint8_t *>(segs), sizeof(tcsum_peso_t) * n);
     if (hipMemcpyAsync(c.d_descs, hsegs, sizeof(tcsum_peso_t) * n, hipMemcpyHostToDevice, cs) != hipSuccess)
         return fail(TCSUM_ERR_SYS);
+    stamp("descs staged");
     for (size_t k = 0; k < ch.size(); ++k) {
         if (k && copy_bytes(ch[k]) != hipSuccess)
             return fail(TCSUM_ERR_SYS);
@@ -733,10 +749,13 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     }
     if (hipMemcpyAsync(hout, c.d_out, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, ks) != hipSuccess)
         return fail(TCSUM_ERR_SYS);
+    stamp("all issued");
     if (hipStreamSynchronize(ks) != hipSuccess || hipStreamSynchronize(cs) != hipSuccess)
         return TCSUM_ERR_SYS;
+    stamp("synced");
     if (hout != out)
         memcpy(out, hout, sizeof(uint16_t) * n);
+    stamp("done");
     return TCSUM_OK;
 }
 
@@ -818,6 +837,89 @@ uint8_t *mapped_host(const void *p)
     return static_cast<uint8_t *>(d);
 }
 
+// Host worker threads, started on first use and kept for the life of the
+// process (never joined: nothing waits on them at exit).  parallel_for on
+// freshly created std::threads paid ~35 us per thread: the span pass of a
+// 1M-segment host batch took 635 us, most of it thread creation, before its
+// first byte could be copied (profiles/r02/e2e_phase.txt).  Callers from
+// several threads at once (the *_multi batches) share the pool; a caller
+// runs its own job's tasks too until none is left unclaimed, so a job always
+// completes even when every worker is busy (or absent, after a fork).
+struct PoolJob {
+    std::function<void(size_t)> fn;
+    size_t k = 0;
+    std::atomic<size_t> next{0}; // next task index to claim
+    size_t left = 0;             // tasks not finished (under mu)
+    std::mutex mu;
+    std::condition_variable cv;
+    // run claimed task i and count it done
+    void finish(size_t i)
+    {
+        fn(i);
+        std::lock_guard<std::mutex> l(mu); // the owner can only see 0 once this is released
+        if (--left == 0)
+            cv.notify_all();
+    }
+    // claim and run one task; false when every task is claimed
+    bool run_one()
+    {
+        const size_t i = next.fetch_add(1);
+        if (i >= k)
+            return false;
+        finish(i);
+        return true;
+    }
+};
+
+class HostPool {
+  public:
+    explicit HostPool(unsigned workers)
+    {
+        for (unsigned i = 0; i < workers; ++i)
+            std::thread([this] { loop(); }).detach();
+    }
+    void submit(PoolJob *j)
+    {
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            q_.push_back(j);
+        }
+        cv_.notify_all();
+    }
+    void retire(PoolJob *j) // the owner's job is done: drop it if still queued
+    {
+        std::lock_guard<std::mutex> l(mu_);
+        q_.erase(std::remove(q_.begin(), q_.end(), j), q_.end());
+    }
+
+  private:
+    void loop()
+    {
+        for (;;) {
+            PoolJob *j = nullptr;
+            size_t i = 0;
+            {
+                std::unique_lock<std::mutex> l(mu_);
+                for (;;) {
+                    cv_.wait(l, [&] { return !q_.empty(); });
+                    j = q_.front();
+                    // claim under the queue lock: the task is then counted in
+                    // the job's `left`, so its owner (which retires the job
+                    // under this lock, after `left` reaches 0) keeps it alive
+                    i = j->next.fetch_add(1);
+                    if (i < j->k)
+                        break;
+                    q_.pop_front();
+                }
+            }
+            j->finish(i);
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<PoolJob *> q_;
+};
+
 // f(begin, end) over [0, n) split across host threads, at least `min_per`
 // items each (one core moves ~10-20 GB/s through memcpy; the PCIe link takes
 // ~55).  TCSUM_COPY_THREADS caps the count (default 16, the box's CPU share).
@@ -836,16 +938,24 @@ void parallel_for(size_t n, size_t min_per, F &&f)
         f(size_t(0), n);
         return;
     }
-    std::vector<std::thread> th;
-    th.reserve(k - 1);
+    static HostPool *pool = new HostPool(cap - 1); // kept: see HostPool
     const size_t per = (n + k - 1) / k;
-    for (size_t i = 1; i < k; ++i) {
+    PoolJob job;
+    job.fn = [&f, n, per](size_t i) {
         const size_t b = std::min(n, i * per), e = std::min(n, b + per);
-        th.emplace_back([&f, b, e] { f(b, e); });
+        if (e > b)
+            f(b, e);
+    };
+    job.k = k;
+    job.left = k;
+    pool->submit(&job);
+    while (job.run_one()) {
     }
-    f(size_t(0), std::min(n, per));
-    for (auto &t : th)
-        t.join();
+    {
+        std::unique_lock<std::mutex> l(job.mu);
+        job.cv.wait(l, [&] { return job.left == 0; });
+    }
+    pool->retire(&job);
 }
 }
 

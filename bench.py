@@ -451,7 +451,7 @@ def e2e(torch, tc, r):
         link = nbytes / ((time.perf_counter() - t0) / reps) / GIB
         del dst
         res = {"gib_s": round(b.total_bytes / dt / GIB, 2), "ms_per_batch": round(dt * 1e3, 3),
-               "path": "pinned host -> hipMemcpyAsync H2D (>= 64 MiB chunks in order on one copy stream, kernels on a second stream behind per-chunk events) -> kernel -> D2H",
+               "path": "pinned host -> hipMemcpyAsync H2D (the first 64 MiB before the rest of the descriptors are read, then chunks of a quarter of the batch, in order on one copy stream; 16-B descriptors; kernels on a second stream behind per-chunk events) -> kernel -> D2H",
                "h2d_copy_gib_s": round(link, 2),
                "matches_device_resident": same}
         ndev = torch.cuda.device_count()

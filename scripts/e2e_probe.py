@@ -35,13 +35,17 @@ torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / 5
 print(f"plain H2D copy (one shot)        {b.alloc_bytes / dt / GIB:7.2f} GiB/s", flush=True)
 
-for mb in (8, 16, 32, 64, 128, 256, 512):
-    os.environ["TCSUM_E2E_CHUNK_MB"] = str(mb)
+for mb in (None, 32, 64, 128, 256, 384, 512):
+    if mb is None:  # the library's own choice (a quarter of the batch, >= 64 MiB)
+        os.environ.pop("TCSUM_E2E_CHUNK_MB", None)
+    else:
+        os.environ["TCSUM_E2E_CHUNK_MB"] = str(mb)
     out = tc.host_batch_peso(host, b.descs)
     t0 = time.perf_counter()
     for _ in range(5):
         out = tc.host_batch_peso(host, b.descs)
     dt = (time.perf_counter() - t0) / 5
     ok = bool((out == want).all())
-    print(f"host_batch_peso chunk {mb:4d} MiB     {b.total_bytes / dt / GIB:7.2f} GiB/s  match={ok}", flush=True)
+    label = "default" if mb is None else f"{mb:4d} MiB"
+    print(f"host_batch_peso chunk {label:>8}     {b.total_bytes / dt / GIB:7.2f} GiB/s  match={ok}", flush=True)
 L.tcsum_host_free(p)

@@ -90,7 +90,9 @@ struct Ctx {
     hipEvent_t hev[kHostEvents] = {};
     uint8_t *d_arena = nullptr;
     size_t d_arena_cap = 0;
-    tcsum_peso_t *d_descs = nullptr;
+    uint8_t *d_lead = nullptr; // the first chunk's bytes, copied before the rest is known
+    size_t d_lead_cap = 0;
+    tcsum_seg_t *d_descs = nullptr;
     size_t d_descs_cap = 0;
     uint16_t *d_out = nullptr;
     size_t d_out_cap = 0;
@@ -609,34 +611,58 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     };
     if (!host_arena || !segs || !out || device < 0 || device >= kMaxDev)
         return TCSUM_ERR_PARAM;
-    // One parallel pass over the descriptors: per block of kSpanBlock
-    // segments, validity and the byte span [lo, hi) its segments touch.
+    // Per block of kSpanBlock segments: validity and the byte span [lo, hi)
+    // its segments touch.
     constexpr uint32_t kSpanBlock = 4096;
     const uint32_t nblk = (n + kSpanBlock - 1) / kSpanBlock;
     std::vector<HostSpan> blk(nblk);
-    parallel_for(nblk, 16, [&](size_t b, size_t e) {
-        for (size_t k = b; k < e; ++k) {
-            HostSpan sp;
-            const uint32_t i1 = (uint32_t)std::min<uint64_t>(n, (k + 1) * (uint64_t)kSpanBlock);
-            for (uint32_t i = (uint32_t)k * kSpanBlock; i < i1; ++i) {
-                const uint64_t o = segs[i].offset, l = segs[i].len;
-                sp.bad |= o > arena_bytes || l > arena_bytes - o;
-                if (l) {
-                    sp.lo = o < sp.lo ? o : sp.lo;
-                    sp.hi = o + l > sp.hi ? o + l : sp.hi;
-                    sp.bytes += l;
-                }
+    auto span_of = [&](size_t k) {
+        HostSpan sp;
+        const uint32_t i1 = (uint32_t)std::min<uint64_t>(n, (k + 1) * (uint64_t)kSpanBlock);
+        for (uint32_t i = (uint32_t)k * kSpanBlock; i < i1; ++i) {
+            const uint64_t o = segs[i].offset, l = segs[i].len;
+            sp.bad |= o > arena_bytes || l > arena_bytes - o;
+            if (l) {
+                sp.lo = o < sp.lo ? o : sp.lo;
+                sp.hi = o + l > sp.hi ? o + l : sp.hi;
+                sp.bytes += l;
             }
-            blk[k] = sp;
         }
-    });
-    HostSpan all;
-    for (const HostSpan &sp : blk)
-        all.merge(sp);
-    if (all.bad)
+        return sp;
+    };
+    // Chunks of >= `target` packet bytes (whole span blocks).  All copies go
+    // in order on ONE copy stream, so the host link never idles between
+    // chunks and no two copies compete for it; each chunk's kernel waits on
+    // its copy's event on the kernel stream and runs under the next copy.
+    // Every copy costs ~18 us of link idle before it (rocprofv3
+    // --memory-copy-trace, profiles/r02/e2e_phase.txt), so chunks are large:
+    // a quarter of the batch, at least 64 MiB (TCSUM_E2E_CHUNK_MB: fixed size).
+    uint64_t total_hint = 0;
+    for (uint32_t i = 0; i < n; i += std::max<uint32_t>(1, n / 64)) // the batch's bytes, from a sample
+        total_hint += segs[i].len;
+    total_hint = total_hint * (uint64_t)n / ((n + std::max<uint32_t>(1, n / 64) - 1) / std::max<uint32_t>(1, n / 64));
+    uint64_t target = std::max<uint64_t>(64ull << 20, total_hint / 4);
+    if (const char *v = getenv("TCSUM_E2E_CHUNK_MB"))
+        target = (uint64_t)std::max(1, atoi(v)) << 20;
+    // The lead: the first blocks, up to 64 MiB of packet bytes, looked at on
+    // this thread before anything else.  When they are dense (their span at
+    // most 1.25x their bytes) their copy starts at once, into a buffer of
+    // their own, and the rest of the descriptors are looked at while it runs
+    // (the whole pass first kept the link idle for 420-635 us of a 29-ms
+    // batch).
+    const uint64_t lead_target = std::min<uint64_t>(target, 64ull << 20);
+    uint32_t m = 0;
+    HostSpan lead;
+    while (m < nblk && lead.bytes < lead_target) {
+        blk[m] = span_of(m);
+        lead.merge(blk[m]);
+        ++m;
+    }
+    if (lead.bad)
         return TCSUM_ERR_PARAM;
-    stamp("span pass");
-    const uint64_t glo = all.hi ? all.lo & ~uint64_t(15) : 0, ghi = all.hi;
+    const bool early = m < nblk && lead.hi > lead.lo && lead.hi - lead.lo <= lead.bytes + lead.bytes / 4;
+    stamp("lead");
+
     Ctx &c = g_ctx[device];
     std::lock_guard<std::mutex> lk(c.mu);
     int rc = ctx_init(c, device);
@@ -644,77 +670,33 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         return rc;
     if (hipSetDevice(device) != hipSuccess)
         return TCSUM_ERR_SYS;
-
-    // device buffers (grow-only).  Only the span [glo, ghi) the segments touch
-    // lives in HBM (a shard of a multi-device batch holds its own part only),
-    // plus a 16-byte tail so the last aligned chunk is in bounds; `dbase` is
-    // the device address arena offset 0 would have.
-    const size_t need_arena = ((ghi - glo + 15) & ~size_t(15)) + 16;
-    if (need_arena > c.d_arena_cap) {
-        if (c.d_arena)
-            (void)hipFree(c.d_arena);
-        c.d_arena_cap = 0;
-        if (hipMalloc(reinterpret_cast<void **>(&c.d_arena), need_arena) != hipSuccess)
-            return TCSUM_ERR_MEM;
-        c.d_arena_cap = need_arena;
-    }
-    if (n > c.d_descs_cap) {
-        if (c.d_descs)
-            (void)hipFree(c.d_descs);
-        if (c.d_out)
-            (void)hipFree(c.d_out);
-        c.d_descs_cap = c.d_out_cap = 0;
-        if (hipMalloc(reinterpret_cast<void **>(&c.d_descs), sizeof(tcsum_peso_t) * n) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&c.d_out), sizeof(uint16_t) * n) != hipSuccess)
-            return TCSUM_ERR_MEM;
-        c.d_descs_cap = c.d_out_cap = n;
-    }
-
-    // Chunks of >= ~64 MiB of packet bytes (whole span blocks).  All copies go
-    // in order on ONE copy stream, so the host link never idles between
-    // chunks and no two copies compete for it; each chunk's kernel waits on
-    // its copy's event on the kernel stream and runs under the next copy.
-    uint64_t target = 64ull << 20; // TCSUM_E2E_CHUNK_MB overrides (measurement)
-    if (const char *v = getenv("TCSUM_E2E_CHUNK_MB"))
-        target = (uint64_t)std::max(1, atoi(v)) << 20;
-    std::vector<uint32_t> cut{0}; // chunk k = span blocks [cut[k], cut[k+1])
-    std::vector<HostSpan> ch;
-    for (uint32_t k = 0; k < nblk; ++k) {
-        if (ch.empty() || ch.back().bytes >= target) {
-            ch.emplace_back();
-            if (k)
-                cut.push_back(k);
-        }
-        ch.back().merge(blk[k]);
-    }
-    cut.push_back(nblk);
-    // segments in no particular order: every chunk's span covers most of the
-    // batch's, so copy the batch's span once and run one kernel on it
-    uint64_t spans = 0;
-    for (const HostSpan &sp : ch)
-        spans += sp.hi > sp.lo ? sp.hi - sp.lo : 0;
-    if (ch.size() > 1 && spans > (ghi - glo) + (ghi - glo) / 4) {
-        ch.assign(1, all);
-        cut.assign({0u, nblk});
-    }
     const uint8_t *h = static_cast<const uint8_t *>(host_arena);
-    uint8_t *const dbase = c.d_arena - glo;
     hipStream_t cs = c.hs[0], ks = c.hs[1];
-    auto copy_bytes = [&](const HostSpan &sp) {
+    // device buffers (grow-only) hold only the spans the segments touch (a
+    // shard of a multi-device batch holds its own part only), plus a 16-byte
+    // tail so the last aligned chunk is in bounds
+    auto grow = [](uint8_t *&buf, size_t &cap, size_t need) {
+        if (need <= cap)
+            return true;
+        if (buf)
+            (void)hipFree(buf);
+        buf = nullptr;
+        cap = 0;
+        if (hipMalloc(reinterpret_cast<void **>(&buf), need) != hipSuccess)
+            return false;
+        cap = need;
+        return true;
+    };
+    auto span_bytes = [](const HostSpan &sp) {
+        return sp.hi > sp.lo ? (((sp.hi - (sp.lo & ~uint64_t(15))) + 15) & ~uint64_t(15)) + 16 : 16;
+    };
+    // copy a span to `dbase` (the device address arena offset 0 has there)
+    auto copy_bytes = [&](uint8_t *dbase, const HostSpan &sp) {
         if (sp.hi <= sp.lo)
             return hipSuccess;
         const uint64_t lo = sp.lo & ~uint64_t(15), hi = std::min(arena_bytes, (sp.hi + 15) & ~uint64_t(15));
         return hipMemcpyAsync(dbase + lo, h + lo, hi - lo, hipMemcpyHostToDevice, cs);
     };
-    // a hipMemcpyAsync from pageable memory is staged by the runtime per call
-    // (~100 us per chunk), so descriptors and results go through pinned
-    // staging unless the caller's arrays are pinned already
-    const bool stage_descs = !mapped_host(segs), stage_out = !mapped_host(out);
-    if ((stage_descs && !c.q_desc.reserve(sizeof(tcsum_peso_t) * n)) ||
-        (stage_out && !c.q_res.reserve(sizeof(uint16_t) * n + 64)))
-        return TCSUM_ERR_MEM;
-    const tcsum_peso_t *hsegs = stage_descs ? reinterpret_cast<const tcsum_peso_t *>(c.q_desc.h) : segs;
-    uint16_t *hout = stage_out ? reinterpret_cast<uint16_t *>(c.q_res.h) : out;
     // once a copy is queued, an error return first drains both streams: no
     // copy may still read the caller's memory after the call returns
     auto fail = [&](int code) {
@@ -722,28 +704,115 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         (void)hipStreamSynchronize(cs);
         return code;
     };
-    // the first chunk's bytes start crossing the link while the host stages
-    // the descriptors
-    stamp("buffers");
-    if (copy_bytes(ch[0]) != hipSuccess)
+    uint8_t *lead_base = nullptr;
+    if (early) {
+        if (!grow(c.d_lead, c.d_lead_cap, span_bytes(lead)))
+            return TCSUM_ERR_MEM;
+        lead_base = c.d_lead - (lead.lo & ~uint64_t(15));
+        if (copy_bytes(lead_base, lead) != hipSuccess)
+            return fail(TCSUM_ERR_SYS);
+        stamp("lead copy");
+    }
+    // the rest of the descriptors, in parallel
+    const uint32_t r0 = early ? m : 0u; // first block after the lead's copy
+    parallel_for(nblk - m, 16, [&](size_t b, size_t e) {
+        for (size_t k = m + b; k < m + e; ++k)
+            blk[k] = span_of(k);
+    });
+    HostSpan rest;
+    for (uint32_t k = r0; k < nblk; ++k)
+        rest.merge(blk[k]);
+    if (rest.bad)
+        return fail(TCSUM_ERR_PARAM);
+    stamp("span pass");
+    const uint64_t glo = rest.hi ? rest.lo & ~uint64_t(15) : 0;
+    if (!grow(c.d_arena, c.d_arena_cap, span_bytes(rest)))
+        return fail(TCSUM_ERR_MEM);
+    uint8_t *const dbase = c.d_arena - glo;
+    if (n > c.d_descs_cap) {
+        if (c.d_descs)
+            (void)hipFree(c.d_descs);
+        if (c.d_out)
+            (void)hipFree(c.d_out);
+        c.d_descs = nullptr;
+        c.d_out = nullptr;
+        c.d_descs_cap = c.d_out_cap = 0;
+        if (hipMalloc(reinterpret_cast<void **>(&c.d_descs), sizeof(tcsum_seg_t) * n) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&c.d_out), sizeof(uint16_t) * n) != hipSuccess)
+            return fail(TCSUM_ERR_MEM);
+        c.d_descs_cap = c.d_out_cap = n;
+    }
+    // chunks: [the lead], then the rest in `target`-byte chunks
+    struct Chunk {
+        uint32_t b0, b1; // span blocks [b0, b1)
+        HostSpan sp;
+        uint8_t *base;
+    };
+    std::vector<Chunk> ch;
+    if (early)
+        ch.push_back({0u, m, lead, lead_base});
+    const size_t first_rest = ch.size();
+    for (uint32_t k = r0; k < nblk; ++k) {
+        if (ch.size() == first_rest || ch.back().sp.bytes >= target)
+            ch.push_back({k, k, HostSpan(), dbase});
+        ch.back().sp.merge(blk[k]);
+        ch.back().b1 = k + 1;
+    }
+    // segments in no particular order: every chunk's span covers most of the
+    // batch's, so copy the batch's span once and run one kernel on it
+    uint64_t spans = 0;
+    for (size_t k = first_rest; k < ch.size(); ++k)
+        spans += ch[k].sp.hi > ch[k].sp.lo ? ch[k].sp.hi - ch[k].sp.lo : 0;
+    const uint64_t rest_span = rest.hi > rest.lo ? rest.hi - rest.lo : 0;
+    if (ch.size() > first_rest + 1 && spans > rest_span + rest_span / 4) {
+        ch.resize(first_rest);
+        ch.push_back({r0, nblk, rest, dbase});
+    }
+    // a hipMemcpyAsync from pageable memory is staged by the runtime per call
+    // (~100 us per chunk), so descriptors and results go through pinned
+    // staging.  The descriptors cross the link as tcsum_seg_t (16 B, not 24):
+    // checksum_peso is pktbuf_checksum16 over the segment with the folded
+    // pseudo-header as pre_sum (tools.c:58-73), so the pseudo-header is folded
+    // here, in the staging pass, and the kernels run as pktbuf_checksum16
+    const bool stage_out = !mapped_host(out);
+    if (!c.q_desc.reserve(sizeof(tcsum_seg_t) * n) || (stage_out && !c.q_res.reserve(sizeof(uint16_t) * n + 64)))
+        return fail(TCSUM_ERR_MEM);
+    uint16_t *hout = stage_out ? reinterpret_cast<uint16_t *>(c.q_res.h) : out;
+    if (!early && copy_bytes(ch[0].base, ch[0].sp) != hipSuccess) // its bytes cross while the host stages
         return fail(TCSUM_ERR_SYS);
-    stamp("first copy");
-    if (stage_descs)
-        par_memcpy(c.q_desc.h, reinterpret_cast<const uint8_t *>(segs), sizeof(tcsum_peso_t) * n);
-    if (hipMemcpyAsync(c.d_descs, hsegs, sizeof(tcsum_peso_t) * n, hipMemcpyHostToDevice, cs) != hipSuccess)
+    tcsum_seg_t *hseg = reinterpret_cast<tcsum_seg_t *>(c.q_desc.h);
+    parallel_for(n, size_t(1) << 16, [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; ++i) {
+            const tcsum_peso_t &d = segs[i];
+            uint32_t src, dst;
+            memcpy(&src, d.src, 4);
+            memcpy(&dst, d.dst, 4);
+            // memory-order words of src, dst, {0, proto}, htons((u16)len)
+            uint64_t q = (src & 0xFFFFu) + (src >> 16) + (dst & 0xFFFFu) + (dst >> 16) + ((uint32_t)d.protocol << 8) +
+                         (((d.len & 0xFFu) << 8) | ((d.len >> 8) & 0xFFu));
+            while (q >> 16)
+                q = (q & 0xFFFFu) + (q >> 16);
+            hseg[i].offset = d.offset;
+            hseg[i].len = d.len;
+            hseg[i].pre_sum = (uint32_t)q;
+        }
+    });
+    if (hipMemcpyAsync(c.d_descs, hseg, sizeof(tcsum_seg_t) * n, hipMemcpyHostToDevice, cs) != hipSuccess)
         return fail(TCSUM_ERR_SYS);
     stamp("descs staged");
     for (size_t k = 0; k < ch.size(); ++k) {
-        if (k && copy_bytes(ch[k]) != hipSuccess)
+        if (k && copy_bytes(ch[k].base, ch[k].sp) != hipSuccess)
             return fail(TCSUM_ERR_SYS);
         hipEvent_t ev = c.hev[k % kHostEvents];
         if (hipEventRecord(ev, cs) != hipSuccess || hipStreamWaitEvent(ks, ev, 0) != hipSuccess)
             return fail(TCSUM_ERR_SYS);
-        const uint32_t i0 = cut[k] * kSpanBlock;
-        const uint32_t i1 = (uint32_t)std::min<uint64_t>(n, (uint64_t)cut[k + 1] * kSpanBlock);
-        const hipError_t e = tcsum::launch_segments(tcsum::MODE_PESO,
-                                                    tcsum::pick_geometry(mean_of(ch[k].bytes, i1 - i0)), dbase,
-                                                    c.d_descs + i0, i1 - i0, c.d_out + i0, 0u, ks);
+        const uint32_t i0 = ch[k].b0 * kSpanBlock;
+        const uint32_t i1 = (uint32_t)std::min<uint64_t>(n, (uint64_t)ch[k].b1 * kSpanBlock);
+        if (i1 <= i0)
+            continue;
+        const hipError_t e = tcsum::launch_segments(tcsum::MODE_SEG,
+                                                    tcsum::pick_geometry(mean_of(ch[k].sp.bytes, i1 - i0)),
+                                                    ch[k].base, c.d_descs + i0, i1 - i0, c.d_out + i0, 1u, ks);
         if (e != hipSuccess)
             return fail(TCSUM_ERR_SYS);
     }
@@ -1284,10 +1353,12 @@ int release_ctx(Ctx &c)
     for (hipStream_t st : c.hs)
         (void)hipStreamSynchronize(st);
     (void)hipStreamSynchronize(c.stream);
-    for (void *p : {(void *)c.d_arena, (void *)c.d_descs, (void *)c.d_out})
+    for (void *p : {(void *)c.d_arena, (void *)c.d_lead, (void *)c.d_descs, (void *)c.d_out})
         if (p)
             (void)hipFree(p);
     c.d_arena = nullptr;
+    c.d_lead = nullptr;
+    c.d_lead_cap = 0;
     c.d_descs = nullptr;
     c.d_out = nullptr;
     c.d_arena_cap = c.d_descs_cap = c.d_out_cap = 0;

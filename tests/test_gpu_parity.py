@@ -684,6 +684,29 @@ def test_host_batch_end_to_end(tc, oracle, monkeypatch, order, chunk_mb):
     np.testing.assert_array_equal(out, oracle.batch_peso(host, d, nthreads=8))
 
 
+@pytest.mark.parametrize("case", ["late_low", "rest_empty", "lead_sparse", "chunks"])
+def test_host_batch_lead_and_rest(tc, oracle, monkeypatch, case):
+    """The host batch's lead (its first 64 MiB of segments, copied before the
+    rest of the descriptors are read, into a buffer of its own when dense)
+    and the rest: a later segment back inside / below the lead's span, a rest
+    of empty segments, a sparse lead (no early copy), several rest chunks."""
+    from tcp_amd import workload
+    b = workload.make_batch("mtu", n=60000)  # 90 MB: a 64-MiB lead + a rest
+    host = oracle.synth_fill(b.byte_base, b.alloc_bytes, b.seed)
+    d = b.descs.copy()
+    if case == "late_low":
+        d[-100:]["offset"] = d[:100]["offset"][::-1] + 3  # back inside the lead's bytes
+        d[-100:]["len"] = 1400
+    elif case == "rest_empty":
+        d[50000:]["len"] = 0
+    elif case == "lead_sparse":
+        d = d[::2].copy()  # every other 1500-B slot: the lead's span is 2x its bytes
+    else:
+        monkeypatch.setenv("TCSUM_E2E_CHUNK_MB", "8")
+    out = tc.host_batch_peso(host, d)
+    np.testing.assert_array_equal(out, oracle.batch_peso(host, d, nthreads=8))
+
+
 @pytest.mark.parametrize("shift", [0, 7])
 def test_host_batch_pinned(tc, oracle, shift):
     """A pinned arena (tcsum_host_alloc), ragged segments in any order, at an

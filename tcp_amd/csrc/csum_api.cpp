@@ -1477,10 +1477,13 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     // packets cover at least 3/4 of their span: a few frames spread over a big
     // pinned pool would otherwise move gigabytes to sum kilobytes, where the
     // in-place path reads only the packets' own bytes.
+    // A pageable read-only batch takes the same path, each piece staged into
+    // pinned memory by the host threads just before its copy (the staging of
+    // piece k+1 overlaps the copy of piece k) instead of being read in place
+    // from the staging by the kernel.
     const uint64_t dma_min = (uint64_t)env_int("TCSUM_HOSTQ_DMA_KB", 256 << 10) << 10;
     const uint64_t alo = lo & ~uint64_t(15), ahi = std::min<uint64_t>(arena_bytes, (hi + 15) & ~uint64_t(15));
-    bool dma = !staged && ip_mode != 1 && in_order && dma_min && hi > lo && hi - lo >= dma_min &&
-               total * 4 >= (hi - lo) * 3;
+    bool dma = ip_mode != 1 && in_order && dma_min && hi > lo && hi - lo >= dma_min && total * 4 >= (hi - lo) * 3;
     if (dma && (size_t)(ahi - alo) + 32 > c.d_arena_cap) {
         // no room in HBM for the span: the in-place path below needs none
         if (c.d_arena)
@@ -1495,15 +1498,20 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     if (dma) {
         uint8_t *const dbase = c.d_arena + 16 - alo;
         hipStream_t cs = c.hs[0], ks = c.hs[1];
-        // pieces of a quarter of the span, at least 64 MiB: every copy costs
+        // pieces growing from 64 MiB (a short first piece: little to stage
+        // before the link starts) to a quarter of the span: every copy costs
         // ~18 us of idle link before it (tcsum_host_batch_peso)
-        const uint64_t kPiece = std::max<uint64_t>(64ull << 20, (hi - lo) / 4);
+        const uint64_t kPieceMax = std::max<uint64_t>(64ull << 20, (hi - lo) / 4);
+        uint64_t piece = 64ull << 20;
+        // host address of arena offset x: `src + x` (the staging when pageable;
+        // it covers [lo - kPad, hi + kPad), which holds every aligned piece)
+        const uintptr_t src = staged ? reinterpret_cast<uintptr_t>(st) - lo : reinterpret_cast<uintptr_t>(host_arena);
         uint64_t copied_hi = alo;
         size_t k = 0;
-        for (uint32_t i0 = 0; i0 < n && e == hipSuccess; ++k) {
+        for (uint32_t i0 = 0; i0 < n && e == hipSuccess; ++k, piece = std::min(kPieceMax, piece * 2)) {
             uint32_t i1 = i0;
             uint64_t bytes = 0, end = copied_hi, first = UINT64_MAX;
-            while (i1 < n && (i1 == i0 || bytes < kPiece)) {
+            while (i1 < n && (i1 == i0 || bytes < piece)) {
                 if (pkts[i1].len) {
                     bytes += pkts[i1].len;
                     first = std::min<uint64_t>(first, pkts[i1].offset);
@@ -1516,7 +1524,10 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
             // the gap before it
             const uint64_t from = std::max<uint64_t>(copied_hi, first == UINT64_MAX ? end : first & ~uint64_t(15));
             if (end > from) {
-                e = hipMemcpyAsync(dbase + from, host_arena + from, end - from, hipMemcpyHostToDevice, cs);
+                if (staged)
+                    par_memcpy(reinterpret_cast<uint8_t *>(src + from), host_arena + from, end - from);
+                e = hipMemcpyAsync(dbase + from, reinterpret_cast<const void *>(src + from), end - from,
+                                   hipMemcpyHostToDevice, cs);
                 copied_hi = end;
             }
             hipEvent_t ev = c.hev[k % kHostEvents];

@@ -202,16 +202,18 @@ def test_host_multi_device_golden(tc, oracle, devices, where, shift):
     np.testing.assert_array_equal(v2, cases["verdict"][:2])
 
 
+@pytest.mark.parametrize("where", ["pinned", "pageable"])
 @pytest.mark.parametrize("mode", ["sums", "rx"])
-def test_host_pinned_copy_engine_path(tc, oracle, monkeypatch, mode):
-    """Large pinned read-only batches go through the copy engine into HBM in
-    64-MiB pieces (TCSUM_HOSTQ_DMA_KB lowered so a test-sized batch takes
-    that path): same results as the in-place path and as the oracle; the
-    reference's fixtures too."""
+def test_host_pinned_copy_engine_path(tc, oracle, monkeypatch, mode, where):
+    """Large read-only batches in offset order go through the copy engine into
+    HBM in pieces growing from 64 MiB (pageable ones staged piece by piece into
+    pinned memory first; TCSUM_HOSTQ_DMA_KB lowered so a test-sized batch
+    takes that path): same results as the in-place path and as the oracle;
+    the reference's fixtures too."""
     from tcp_amd import workload
     monkeypatch.setenv("TCSUM_HOSTQ_DMA_KB", "1")
     cases, pool = G.ipv4_rx_cases() if mode == "rx" else G.ipv4_cases()
-    arg, view, keep = host_copy(tc, pool, "pinned", 5)
+    arg, view, keep = host_copy(tc, pool, where, 5)
     pk = G.pkt_descs(cases, tc.PKT_DTYPE)
     if mode == "rx":
         verdict, out, flags = tc.host_batch_ipv4_rx_verify(arg, pk)
@@ -224,27 +226,33 @@ def test_host_pinned_copy_engine_path(tc, oracle, monkeypatch, mode):
     # a batch of several pieces (~140 MB), against the in-place path and the oracle
     b = workload.make_batch("mixed_rx", n=30000)
     dev, _ = workload.materialize(b)
-    ha = tc.HostArena(b.alloc_bytes)
+    ha = tc.HostArena(b.alloc_bytes) if where == "pinned" else None
     try:
-        ha.array[:] = dev.cpu().numpy()
+        if ha is not None:
+            ha.array[:] = dev.cpu().numpy()
+            arg, host = ha, ha.array
+        else:
+            host = dev.cpu().numpy().copy()
+            arg = host
         if mode == "rx":
-            v_dma, o_dma, f_dma = tc.host_batch_ipv4_rx_verify(ha, b.descs)
+            v_dma, o_dma, f_dma = tc.host_batch_ipv4_rx_verify(arg, b.descs)
             monkeypatch.setenv("TCSUM_HOSTQ_DMA_KB", "0")
-            v_in, o_in, f_in = tc.host_batch_ipv4_rx_verify(ha, b.descs)
-            ev, ef = oracle.batch_ipv4_rx_verify(ha.array, b.descs, nthreads=8)
+            v_in, o_in, f_in = tc.host_batch_ipv4_rx_verify(arg, b.descs)
+            ev, ef = oracle.batch_ipv4_rx_verify(host, b.descs, nthreads=8)
             np.testing.assert_array_equal(v_dma, ev)
             np.testing.assert_array_equal(v_dma, v_in)
         else:
-            o_dma, f_dma = tc.host_batch_ipv4(ha, b.descs)
+            o_dma, f_dma = tc.host_batch_ipv4(arg, b.descs)
             monkeypatch.setenv("TCSUM_HOSTQ_DMA_KB", "0")
-            o_in, f_in = tc.host_batch_ipv4(ha, b.descs)
-            eo, ef = oracle.batch_ipv4(ha.array, b.descs, nthreads=8)
+            o_in, f_in = tc.host_batch_ipv4(arg, b.descs)
+            eo, ef = oracle.batch_ipv4(host, b.descs, nthreads=8)
             np.testing.assert_array_equal(o_dma, eo)
         np.testing.assert_array_equal(o_dma, o_in)
         np.testing.assert_array_equal(f_dma, f_in)
     finally:
         del keep
-        ha.free()
+        if ha is not None:
+            ha.free()
 
 
 @pytest.mark.parametrize("mode", ["sums", "rx"])

@@ -831,20 +831,48 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
 extern "C++" {
 // Contiguous shards of a descriptor array balanced by bytes:
 // shard d is [cut[d], cut[d+1]).
+// Shard k starts after the first segment whose inclusive byte prefix reaches
+// quantile k.  Block sums in parallel first (a serial pass over 8M
+// descriptors would hold every device's copies back by milliseconds), then
+// each cut is found inside the one block where the prefix crosses it.
 template <class D>
 std::vector<uint32_t> byte_shards(const D *descs, uint32_t n, int ndev)
 {
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < n; ++i)
-        total += descs[i].len;
+    constexpr uint32_t kB = 1u << 16;
+    const uint32_t nb = (n + kB - 1) / kB;
+    std::vector<uint64_t> pre((size_t)nb + 1, 0); // pre[b]: bytes of blocks < b
+    parallel_for(nb, 1, [&](size_t b, size_t e) {
+        for (size_t k = b; k < e; ++k) {
+            uint64_t t = 0;
+            const uint32_t i1 = (uint32_t)std::min<uint64_t>(n, (k + 1) * (uint64_t)kB);
+            for (uint32_t i = (uint32_t)k * kB; i < i1; ++i)
+                t += descs[i].len;
+            pre[k + 1] = t;
+        }
+    });
+    for (uint32_t b = 0; b < nb; ++b)
+        pre[b + 1] += pre[b];
+    const uint64_t total = pre[nb];
     std::vector<uint32_t> cut((size_t)ndev + 1, n);
     cut[0] = 0;
-    uint64_t acc = 0;
-    int k = 1;
-    for (uint32_t i = 0; i < n && k < ndev; ++i) {
-        acc += descs[i].len;
-        while (k < ndev && acc * (uint64_t)ndev >= total * (uint64_t)k) // shard k starts after byte quantile k
-            cut[k++] = i + 1;
+    uint32_t b = 0;
+    for (int k = 1; k < ndev; ++k) {
+        auto reached = [&](uint64_t acc) { return acc * (uint64_t)ndev >= total * (uint64_t)k; };
+        while (b < nb && !reached(pre[b + 1])) // the first block whose end reaches quantile k
+            ++b;
+        if (b == nb)
+            break; // never reached: this and every later shard start at n
+        uint64_t acc = pre[b];
+        const uint32_t i0 = std::max<uint32_t>(b * kB, k > 1 ? cut[k - 1] - 1 : 0u);
+        for (uint32_t i = b * kB; i < i0; ++i)
+            acc += descs[i].len;
+        for (uint32_t i = i0;; ++i) {
+            acc += descs[i].len;
+            if (reached(acc)) {
+                cut[k] = i + 1;
+                break;
+            }
+        }
     }
     return cut;
 }

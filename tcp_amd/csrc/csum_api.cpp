@@ -1496,8 +1496,8 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
         goto results;
     }
     {
-    // Large pinned batches that are only read (sums, rx) go through the copy
-    // engine instead of the kernel's own PCIe reads: pieces copied in order on
+    // Large pinned batches go through the copy engine instead of the kernel's
+    // own PCIe reads: pieces copied in order on
     // one copy stream into HBM, each piece's kernel behind its copy's event
     // (tcsum_host_batch_peso's pipeline): 50.7 against 49.3 GiB/s for 1M
     // mixed frames (profiles/r01/hostq_dma.txt).  TCSUM_HOSTQ_DMA_KB: the
@@ -1505,13 +1505,16 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     // packets cover at least 3/4 of their span: a few frames spread over a big
     // pinned pool would otherwise move gigabytes to sum kilobytes, where the
     // in-place path reads only the packets' own bytes.
-    // A pageable read-only batch takes the same path, each piece staged into
+    // A pageable batch takes the same path, each piece staged into
     // pinned memory by the host threads just before its copy (the staging of
     // piece k+1 overlaps the copy of piece k) instead of being read in place
     // from the staging by the kernel.
     const uint64_t dma_min = (uint64_t)env_int("TCSUM_HOSTQ_DMA_KB", 256 << 10) << 10;
     const uint64_t alo = lo & ~uint64_t(15), ahi = std::min<uint64_t>(arena_bytes, (hi + 15) & ~uint64_t(15));
-    bool dma = ip_mode != 1 && in_order && dma_min && hi > lo && hi - lo >= dma_min && total * 4 >= (hi - lo) * 3;
+    // A tx fill takes it too: the packets are read from the HBM copy and the
+    // fields stored straight into the frames in host memory (or the staging)
+    // by k_tx_scatter, over PCIe as posted writes.
+    bool dma = in_order && dma_min && hi > lo && hi - lo >= dma_min && total * 4 >= (hi - lo) * 3;
     if (dma && (size_t)(ahi - alo) + 32 > c.d_arena_cap) {
         // no room in HBM for the span: the in-place path below needs none
         if (c.d_arena)
@@ -1563,10 +1566,13 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
                 e = hipEventRecord(ev, cs);
             if (e == hipSuccess)
                 e = hipStreamWaitEvent(ks, ev, 0);
-            if (e == hipSuccess)
-                e = tcsum::launch_ipv4(ip_mode, tcsum::pick_geometry(mean_of(bytes, i1 - i0)), dbase, d_pkts + i0,
-                                       i1 - i0, d_out ? d_out + i0 : nullptr, d_flags ? d_flags + i0 : nullptr,
-                                       d_verdict ? d_verdict + i0 : nullptr, ks);
+            const Geometry g = tcsum::pick_geometry(mean_of(bytes, i1 - i0));
+            if (e == hipSuccess && ip_mode == 1) // values from HBM, fields into the frames where they live
+                e = tcsum::launch_ipv4_tx_to(g, dbase, d_arena, d_pkts + i0, i1 - i0, d_out ? d_out + i0 : nullptr,
+                                             d_flags ? d_flags + i0 : nullptr, ks);
+            else if (e == hipSuccess)
+                e = tcsum::launch_ipv4(ip_mode, g, dbase, d_pkts + i0, i1 - i0, d_out ? d_out + i0 : nullptr,
+                                       d_flags ? d_flags + i0 : nullptr, d_verdict ? d_verdict + i0 : nullptr, ks);
             i0 = i1;
         }
         const hipError_t s1 = hipStreamSynchronize(ks), s2 = hipStreamSynchronize(cs);

@@ -1697,6 +1697,50 @@ static hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t stream)
     return pool ? hipMallocFromPoolAsync(p, bytes, pool, stream) : hipMallocAsync(p, bytes, stream);
 }
 
+// The tx fill with its stores deferred (IP_OPT_DEFER + k_tx_scatter): the
+// values are computed from `arena` and stored into `store`, the same packets
+// at another address (the same arena, or the host memory an HBM copy was
+// made from: the scatter's stores then cross PCIe as posted writes).
+static hipError_t tx_split(Geometry g, dim3 grid, uint32_t xg, uint8_t *arena, uint8_t *store,
+                           const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out, uint8_t *flags, hipStream_t stream)
+{
+    uint32_t *side = nullptr; // positions [n], then the values [n] when the caller wants no `out`
+    hipError_t e = scratch_alloc(reinterpret_cast<void **>(&side), (size_t)n * (out ? 4u : 8u), stream);
+    if (e != hipSuccess)
+        return e;
+    uint32_t *vals = out ? out : side + n;
+    e = ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, vals, flags, reinterpret_cast<int8_t *>(side),
+                      IP_OPT_DEFER, xg, stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, store, pkts, n, vals, side);
+        e = hipGetLastError();
+    }
+    const hipError_t f = hipFreeAsync(side, stream);
+    return e != hipSuccess ? e : f;
+}
+
+hipError_t launch_ipv4_tx_to(Geometry g, uint8_t *arena, uint8_t *store, const tcsum_pkt_t *pkts, uint32_t n,
+                             uint32_t *out, uint8_t *flags, hipStream_t stream)
+{
+    if (n == 0)
+        return hipSuccess;
+    g.lanes = g.lanes < 16 ? 16 : g.lanes > 64 ? 64 : g.lanes; // launch_ipv4's rules
+    const uint64_t per_launch = kMaxBlocks * (256u / (uint32_t)g.lanes);
+    if (n > per_launch) {
+        for (uint64_t i0 = 0; i0 < n; i0 += per_launch) {
+            const uint32_t m = (uint32_t)(n - i0 < per_launch ? n - i0 : per_launch);
+            const hipError_t e = launch_ipv4_tx_to(g, arena, store, pkts + i0, m, out ? out + i0 : nullptr,
+                                                   flags ? flags + i0 : nullptr, stream);
+            if (e != hipSuccess)
+                return e;
+        }
+        return hipSuccess;
+    }
+    const uint64_t per_block = 256u / (uint32_t)g.lanes;
+    return tx_split(g, dim3((uint32_t)((n + per_block - 1) / per_block)), (uint32_t)g.xcd, arena, store, pkts, n,
+                    out, flags, stream);
+}
+
 hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
                        uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream)
 {
@@ -1728,21 +1772,8 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
     switch (ip_mode) {
     case IP_TX:
         return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, 0u, xg, stream);
-    case IP_TX_SPLIT: { // the fill with its stores deferred to k_tx_scatter
-        uint32_t *side = nullptr; // positions [n], then the values [n] when the caller wants no `out`
-        hipError_t e = scratch_alloc(reinterpret_cast<void **>(&side), (size_t)n * (out ? 4u : 8u), stream);
-        if (e != hipSuccess)
-            return e;
-        uint32_t *vals = out ? out : side + n;
-        e = ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, vals, flags, reinterpret_cast<int8_t *>(side),
-                          IP_OPT_DEFER, xg, stream);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, arena, pkts, n, vals, side);
-            e = hipGetLastError();
-        }
-        const hipError_t f = hipFreeAsync(side, stream);
-        return e != hipSuccess ? e : f;
-    }
+    case IP_TX_SPLIT: // the fill with its stores deferred to k_tx_scatter
+        return tx_split(g, grid, xg, arena, arena, pkts, n, out, flags, stream);
     case IP_TX_OFFLOAD: // the tx values into `out` only; the packets are not written
         return ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, out, flags, verdict, IP_OPT_NO_STORE, xg,
                              stream);

@@ -36,6 +36,11 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
 hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
                        uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream);
 
+// The tx fill (deferred stores) reading `arena` and storing the fields into
+// `store` (the same packets at another device-visible address).
+hipError_t launch_ipv4_tx_to(Geometry g, uint8_t *arena, uint8_t *store, const tcsum_pkt_t *pkts, uint32_t n,
+                             uint32_t *out, uint8_t *flags, hipStream_t stream);
+
 // Queue server (k_server): one job at a time.  SrvHost lives in pinned,
 // coherent host memory (the host writes the job, then `req`, and reads `done`);
 // SrvCtl in device memory (zeroed before every launch).

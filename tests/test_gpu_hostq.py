@@ -203,6 +203,36 @@ def test_host_multi_device_golden(tc, oracle, devices, where, shift):
 
 
 @pytest.mark.parametrize("where", ["pinned", "pageable"])
+def test_host_tx_fill_copy_engine_path(tc, oracle, monkeypatch, where):
+    """A large tx fill in offset order through the copy engine: packets read
+    from their HBM copy, the fields stored into the frames in host memory (or
+    the pageable batch's staging) by k_tx_scatter -- every byte equals the
+    in-place fill's and the oracle's."""
+    from tcp_amd import workload
+    b = workload.make_batch("mixed_tx", n=30000)  # ~140 MB: pieces of 64 and 128 MiB
+    dev, _ = workload.materialize(b)
+    unfilled = dev.cpu().numpy()
+    want = unfilled.copy()
+    wfl = oracle.batch_ipv4_tx_fill(want, b.descs, nthreads=8)
+    ha = tc.HostArena(unfilled.size) if where == "pinned" else None
+    try:
+        for dma_kb in ("1", "0"):  # copy-engine path, then the in-place one
+            monkeypatch.setenv("TCSUM_HOSTQ_DMA_KB", dma_kb)
+            if ha is not None:
+                ha.array[:] = unfilled
+                arg, host = ha, ha.array
+            else:
+                host = unfilled.copy()
+                arg = host
+            fl = tc.host_batch_ipv4_tx_fill(arg, b.descs)
+            np.testing.assert_array_equal(fl, wfl)
+            np.testing.assert_array_equal(host, want)
+    finally:
+        if ha is not None:
+            ha.free()
+
+
+@pytest.mark.parametrize("where", ["pinned", "pageable"])
 @pytest.mark.parametrize("mode", ["sums", "rx"])
 def test_host_pinned_copy_engine_path(tc, oracle, monkeypatch, mode, where):
     """Large read-only batches in offset order go through the copy engine into

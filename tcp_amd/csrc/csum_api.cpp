@@ -1017,12 +1017,10 @@ class HostPool {
     std::deque<PoolJob *> q_;
 };
 
-// f(begin, end) over [0, n) split across host threads, at least `min_per`
-// items each (one core moves ~10-20 GB/s through memcpy; the PCIe link takes
-// ~55).  TCSUM_COPY_THREADS caps the count (default 16, the box's CPU share).
 extern "C++" {
-template <class F>
-void parallel_for(size_t n, size_t min_per, F &&f)
+// Host threads a parallel pass may use: TCSUM_COPY_THREADS (default 16, the
+// box's CPU share), at most the machine's.
+unsigned host_threads()
 {
     static const unsigned cap = [] {
         const char *s = getenv("TCSUM_COPY_THREADS");
@@ -1030,12 +1028,31 @@ void parallel_for(size_t n, size_t min_per, F &&f)
         const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
         return std::max(1u, std::min(hw, (unsigned)(v > 0 ? v : 1)));
     }();
+    return cap;
+}
+
+// The one pool of the process (every parallel_for instantiation shares it).
+HostPool &host_pool()
+{
+    static HostPool *pool = new HostPool(host_threads() - 1); // kept: see HostPool
+    return *pool;
+}
+}
+
+// f(begin, end) over [0, n) split across host threads, at least `min_per`
+// items each (one core moves ~10-20 GB/s through memcpy; the PCIe link takes
+// ~55).
+extern "C++" {
+template <class F>
+void parallel_for(size_t n, size_t min_per, F &&f)
+{
+    const unsigned cap = host_threads();
     size_t k = std::min<size_t>(cap, min_per ? n / min_per : cap);
     if (k <= 1) {
         f(size_t(0), n);
         return;
     }
-    static HostPool *pool = new HostPool(cap - 1); // kept: see HostPool
+    HostPool *pool = &host_pool();
     const size_t per = (n + k - 1) / k;
     PoolJob job;
     job.fn = [&f, n, per](size_t i) {

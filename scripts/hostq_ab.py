@@ -49,6 +49,7 @@ cases = {
     "rx pinned": (lambda: tc.host_batch_ipv4_rx_verify(ha, b.descs), b.total_bytes),
     "rx pageable": (lambda: tc.host_batch_ipv4_rx_verify(page, b.descs), b.total_bytes),
     "tx pinned": (lambda: tc.host_batch_ipv4_tx_fill(ha, b.descs), b.total_bytes),
+    "tx pageable": (lambda: tc.host_batch_ipv4_tx_fill(page, b.descs), b.total_bytes),
     "peso e2e": (lambda: tc.host_batch_peso(mhost.array, m.descs), m.total_bytes),
 }
 res = {k: [[] for _ in libs] for k in cases}

@@ -1531,7 +1531,11 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     // A tx fill takes it too: the packets are read from the HBM copy and the
     // fields stored straight into the frames in host memory (or the staging)
     // by k_tx_scatter, over PCIe as posted writes.
-    bool dma = in_order && dma_min && hi > lo && hi - lo >= dma_min && total * 4 >= (hi - lo) * 3;
+    // A pinned tx fill only from 4x that span: its last piece's field stores
+    // trail the copies, and at 298 MB the in-place fill was 3.6 % faster
+    // (4.7 GB: 3.3 % slower; profiles/r02/hostq_ab_pieces.txt).
+    bool dma = in_order && dma_min && hi > lo && hi - lo >= dma_min && total * 4 >= (hi - lo) * 3 &&
+               (ip_mode != 1 || staged || hi - lo >= 4 * dma_min);
     if (dma && (size_t)(ahi - alo) + 32 > c.d_arena_cap) {
         // no room in HBM for the span: the in-place path below needs none
         if (c.d_arena)
@@ -1546,11 +1550,17 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     if (dma) {
         uint8_t *const dbase = c.d_arena + 16 - alo;
         hipStream_t cs = c.hs[0], ks = c.hs[1];
-        // pieces growing from 64 MiB (a short first piece: little to stage
-        // before the link starts) to a quarter of the span: every copy costs
-        // ~18 us of idle link before it (tcsum_host_batch_peso)
-        const uint64_t kPieceMax = std::max<uint64_t>(64ull << 20, (hi - lo) / 4);
-        uint64_t piece = 64ull << 20;
+        // Pinned: pieces growing from 64 MiB to a quarter of the span (an
+        // eighth for tx, whose last piece's field stores trail the copies):
+        // every copy costs ~18 us of idle link before it
+        // (tcsum_host_batch_peso).  Pageable: the host's staging copy is the
+        // slower side, so pieces stay small (1/16 of the span, 32..128 MiB)
+        // and the link waits for little more than the first one.
+        const uint64_t span = hi - lo;
+        const uint64_t kPieceMax =
+            staged ? std::min<uint64_t>(128ull << 20, std::max<uint64_t>(32ull << 20, span / 16))
+                   : std::max<uint64_t>(64ull << 20, span / (ip_mode == 1 ? 8 : 4));
+        uint64_t piece = std::min<uint64_t>(64ull << 20, kPieceMax);
         // host address of arena offset x: `src + x` (the staging when pageable;
         // it covers [lo - kPad, hi + kPad), which holds every aligned piece)
         const uintptr_t src = staged ? reinterpret_cast<uintptr_t>(st) - lo : reinterpret_cast<uintptr_t>(host_arena);

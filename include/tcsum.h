@@ -191,7 +191,11 @@ int tcsum_batch_ipv4_rx_verify(const void *arena /*[dev]*/, const tcsum_pkt_t *p
  * tcsum_batch_peso -> D2H of the results; returns after the results are in
  * host_out.  host_arena should come from tcsum_host_alloc (pinned) for full
  * PCIe rate.  Segments may be in any order (in offset order the copies and
- * kernels pipeline; otherwise the batch's byte span is copied once). */
+ * kernels pipeline; otherwise the batch's byte span is copied once).  The
+ * first ~64 MiB of segments are checked before anything else; a bad segment
+ * after them is found while their copy runs (the call drains it and returns
+ * NET_ERR_PARAM), so on a host without a usable device such a batch reports
+ * the device error first. */
 int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_bytes,
                           const tcsum_peso_t *segs /*[host]*/, uint32_t n,
                           uint16_t *out /*[host]*/);

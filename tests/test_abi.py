@@ -213,25 +213,26 @@ def test_tx_apply_reproduces_the_reference_fill(libpath):
 
 def test_host_pool_concurrent_span_passes(libpath):
     """The host worker pool behind the host batches' parallel passes: eight
-    callers at once (the *_multi shape), each a 1M-segment span pass that finds
-    the bad last descriptor -- every call returns NET_ERR_PARAM, before any
-    device is touched, with no hang or lost task."""
+    callers at once (the *_multi shape), each a host-queue batch of 1M
+    descriptors whose parallel pass finds the bad last one -- every call
+    returns NET_ERR_PARAM, before any device is touched, with no hang or
+    lost task."""
     import threading
     from tcp_amd import _lib
     L = _lib.lib()
     n = 1 << 20
-    segs = np.zeros(n, dtype=np.dtype([("offset", "<u8"), ("len", "<u4"), ("b", "u1", 12)]))
-    segs["offset"] = np.arange(n, dtype=np.uint64) * 16
-    segs["len"] = 16
-    segs["offset"][-1] = n * 16  # one segment past the arena
+    pk = np.zeros(n, dtype=np.dtype([("offset", "<u8"), ("len", "<u4"), ("rsv", "<u4")]))
+    pk["offset"] = np.arange(n, dtype=np.uint64) * 16
+    pk["len"] = 16
+    pk["offset"][-1] = n * 16  # one packet past the arena
     arena = np.zeros(n * 16, np.uint8)
-    out = np.zeros(n, np.uint16)
+    out = np.zeros(n, np.uint32)
     rcs = []
 
     def caller():
         for _ in range(20):
-            rcs.append(L.tcsum_host_batch_peso(0, arena.ctypes.data, arena.size, segs.ctypes.data, n,
-                                               out.ctypes.data))
+            rcs.append(L.tcsum_host_batch_ipv4(0, arena.ctypes.data, arena.size, pk.ctypes.data, n,
+                                               out.ctypes.data, None))
 
     th = [threading.Thread(target=caller) for _ in range(8)]
     for t in th:

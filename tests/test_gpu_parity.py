@@ -759,6 +759,26 @@ def test_host_batch_multi_device(tc, oracle, devices):
                                   oracle.batch_peso(host, few, nthreads=1))
 
 
+@pytest.mark.parametrize("devices", [[0, 0, 0], [0] * 7])
+def test_host_batch_multi_device_many_blocks(tc, oracle, devices):
+    """The multi-device shard cuts over many 64K-descriptor blocks (the cut
+    search runs per block, in parallel): 400,000 ragged segments in offset
+    order, some empty runs, results in segment order."""
+    rng = np.random.default_rng(77)
+    n = 400000
+    lens = rng.integers(0, 1501, n)
+    lens[100000:130000] = 0  # an empty run: quantiles fall around it
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]) + 3
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1] + 64), dtype=np.uint8)
+    p = np.zeros(n, tc.PESO_DTYPE)
+    p["offset"], p["len"] = offs, lens
+    p["src"] = rng.integers(0, 256, (n, 4))
+    p["dst"] = rng.integers(0, 256, (n, 4))
+    p["protocol"] = rng.choice([6, 17], n)
+    out = tc.host_batch_peso_multi(host, p, devices)
+    np.testing.assert_array_equal(out, oracle.batch_peso(host, p, nthreads=8))
+
+
 # --------------------------------------------------- full BASELINE sizes
 
 def test_full_mtu_batch_exact(tc, torch, oracle):

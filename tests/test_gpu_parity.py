@@ -707,6 +707,24 @@ def test_host_batch_lead_and_rest(tc, oracle, monkeypatch, case):
     np.testing.assert_array_equal(out, oracle.batch_peso(host, d, nthreads=8))
 
 
+def test_host_batch_long_segments(tc, oracle):
+    """The host batch's 16-byte descriptors carry the pseudo-header folded on
+    the host: segments of 64 KiB and longer (the length word is (u16)len,
+    tools.c:69 -- 65,536 B gives 0), odd offsets, empty ones, every protocol
+    byte value."""
+    rng = np.random.default_rng(91)
+    lens = np.array([65535, 65536, 65537, 70000, 131072, 0, 1, 2, 9000, 65534] * 8)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]) + rng.integers(0, 2, lens.size).cumsum()
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1] + 64), dtype=np.uint8)
+    p = np.zeros(lens.size, tc.PESO_DTYPE)
+    p["offset"], p["len"] = offs, lens
+    p["src"] = rng.integers(0, 256, (lens.size, 4))
+    p["dst"] = rng.integers(0, 256, (lens.size, 4))
+    p["protocol"] = rng.integers(0, 256, lens.size)
+    out = tc.host_batch_peso(host, p)
+    np.testing.assert_array_equal(out, oracle.batch_peso(host, p, nthreads=4))
+
+
 @pytest.mark.parametrize("shift", [0, 7])
 def test_host_batch_pinned(tc, oracle, shift):
     """A pinned arena (tcsum_host_alloc), ragged segments in any order, at an

@@ -637,10 +637,11 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     // Every copy costs ~18 us of link idle before it (rocprofv3
     // --memory-copy-trace, profiles/r02/e2e_phase.txt), so chunks are large:
     // a quarter of the batch, at least 64 MiB (TCSUM_E2E_CHUNK_MB: fixed size).
-    uint64_t total_hint = 0;
-    for (uint32_t i = 0; i < n; i += std::max<uint32_t>(1, n / 64)) // the batch's bytes, from a sample
-        total_hint += segs[i].len;
-    total_hint = total_hint * (uint64_t)n / ((n + std::max<uint32_t>(1, n / 64) - 1) / std::max<uint32_t>(1, n / 64));
+    const uint32_t step = std::max<uint32_t>(1, n / 64); // the batch's bytes, estimated from 64 segments
+    uint64_t sampled = 0, taken = 0;
+    for (uint32_t i = 0; i < n; i += step, ++taken)
+        sampled += segs[i].len;
+    const uint64_t total_hint = sampled / taken * (uint64_t)n;
     uint64_t target = std::max<uint64_t>(64ull << 20, total_hint / 4);
     if (const char *v = getenv("TCSUM_E2E_CHUNK_MB"))
         target = (uint64_t)std::max(1, atoi(v)) << 20;

@@ -316,3 +316,65 @@ def test_host_sparse_batch_and_release(tc, oracle, mode, monkeypatch):
             tc.release(0)
     finally:
         ha.free()
+
+
+def _semi_valid_ipv4(rng, arena, offs, lens):
+    """IPv4 headers at each packet start (IHL 5, total_len = frame length,
+    TCP / UDP / ICMP / other, some fragments): enough for every rx gate and
+    tx branch to be taken; the rest of the bytes stay random."""
+    for o, L in zip(offs.tolist(), lens.tolist()):
+        if L < 20:
+            continue
+        arena[o] = 0x45
+        arena[o + 2: o + 4] = (L >> 8, L & 0xFF)
+        arena[o + 6] = 0x20 if rng.random() < 0.05 else 0x40
+        arena[o + 7] = 0
+        arena[o + 9] = rng.choice([6, 17, 1, 50])
+
+
+@pytest.mark.parametrize("seed", range(32))
+def test_host_paths_fuzz(tc, oracle, monkeypatch, seed):
+    """Seeded fuzz over the host-memory batch paths: sizes from one frame to
+    tens of thousands, packed / gapped / shuffled / sparse layouts, pinned /
+    registered / pageable memory, the copy-engine threshold off, forced or
+    default -- sums, rx verdicts, the tx fill's bytes, and the bulk
+    checksum_peso batch, each against the oracle."""
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.choice([1, 7, 50, 1000, 20000, 60000]))
+    layout = rng.choice(["packed", "gaps", "shuffled", "sparse"])
+    where = str(rng.choice(["pinned", "registered", "pageable"]))
+    monkeypatch.setenv("TCSUM_HOSTQ_DMA_KB", str(rng.choice(["0", "1", "262144"])))
+    monkeypatch.setenv("TCSUM_E2E_CHUNK_MB", str(rng.choice(["1", "8", "64"])))
+    lens = rng.integers(0, 3000, n) if rng.random() < 0.5 else rng.integers(20, 9001, n)
+    gap = {"gaps": rng.integers(0, 64, n),
+           "sparse": rng.integers(0, (1 << 16) if n <= 1000 else 4096, n)}.get(layout, np.zeros(n, np.int64))
+    offs = 5 + np.concatenate([[0], np.cumsum(lens + gap)[:-1]]).astype(np.int64)
+    data = rng.integers(0, 256, int(offs[-1] + lens[-1] + 32), dtype=np.uint8)
+    _semi_valid_ipv4(rng, data, offs, lens)
+    pk = np.zeros(n, tc.PKT_DTYPE)
+    pk["offset"], pk["len"] = offs, lens
+    if layout == "shuffled":
+        pk = pk[rng.permutation(n)]
+    arg, view, keep = host_copy(tc, data, where, int(rng.integers(0, 9)))
+    try:
+        out, flags = tc.host_batch_ipv4(arg, pk)
+        eo, ef = oracle.batch_ipv4(np.array(view[: data.size]), pk, nthreads=8)
+        np.testing.assert_array_equal(out, eo)
+        np.testing.assert_array_equal(flags, ef)
+        v, _, _ = tc.host_batch_ipv4_rx_verify(arg, pk)
+        ev, _ = oracle.batch_ipv4_rx_verify(np.array(view[: data.size]), pk, nthreads=8)
+        np.testing.assert_array_equal(v, ev)
+        segs = np.zeros(n, tc.PESO_DTYPE)
+        segs["offset"], segs["len"] = pk["offset"], pk["len"]
+        segs["src"] = rng.integers(0, 256, (n, 4))
+        segs["dst"] = rng.integers(0, 256, (n, 4))
+        segs["protocol"] = rng.integers(0, 256, n)
+        np.testing.assert_array_equal(tc.host_batch_peso(np.array(view[: data.size]), segs),
+                                      oracle.batch_peso(np.array(view[: data.size]), segs, nthreads=8))
+        want = np.array(view[: data.size])
+        wfl = oracle.batch_ipv4_tx_fill(want, pk, nthreads=8)
+        fl = tc.host_batch_ipv4_tx_fill(arg, pk)
+        np.testing.assert_array_equal(fl, wfl)
+        np.testing.assert_array_equal(np.array(view[: data.size]), want)
+    finally:
+        del keep

@@ -131,6 +131,18 @@ int tcsum_batch_ipv4_tx_fill(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[d
                              uint32_t *out /*[dev] or NULL*/, uint8_t *flags /*[dev] or NULL*/,
                              uint64_t total_bytes_hint, void *stream);
 
+/* tcsum_batch_ipv4_tx_fill in its deferred-store form (the faster one for
+ * large batches) with scratch the caller owns: scratch_bytes >= 8 * n,
+ * 4-byte aligned, device memory, not touched by anything else until the
+ * stream passes the call.  Nothing is allocated, so unlike the plain call's
+ * deferred form it can be captured in a hipGraph (replays of one graph must
+ * not run concurrently: they share the scratch).  Same bytes as
+ * tcsum_batch_ipv4_tx_fill. */
+int tcsum_batch_ipv4_tx_fill_scratch(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,
+                                     uint32_t *out /*[dev] or NULL*/, uint8_t *flags /*[dev] or NULL*/,
+                                     void *scratch /*[dev]*/, uint64_t scratch_bytes, uint64_t total_bytes_hint,
+                                     void *stream);
+
 /* Batched tx offload (NIC checksum-offload style): the
  * values tcsum_batch_ipv4_tx_fill would store -- out[i] = ip | l4 << 16, with
  * the checksum fields read as zero -- and flags[i], WITHOUT writing the

@@ -30,6 +30,7 @@ SIGNATURES = {
     "tcsum_batch_peso": (_I, [_V, _V, _U32, _V, _U64, _V]),
     "tcsum_batch_ipv4": (_I, [_V, _V, _U32, _V, _V, _U64, _V]),
     "tcsum_batch_ipv4_tx_fill": (_I, [_V, _V, _U32, _V, _V, _U64, _V]),
+    "tcsum_batch_ipv4_tx_fill_scratch": (_I, [_V, _V, _U32, _V, _V, _V, _U64, _U64, _V]),
     "tcsum_batch_ipv4_rx_verify": (_I, [_V, _V, _U32, _V, _V, _V, _U64, _V]),
     "tcsum_batch_ipv4_tx_offload": (_I, [_V, _V, _U32, _V, _V, _U64, _V]),
     "tcsum_tx_apply": (_I, [_V, _U32, _U32, ctypes.c_uint8]),

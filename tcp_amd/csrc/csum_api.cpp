@@ -445,6 +445,21 @@ int tcsum_batch_ipv4_tx_fill(void *arena, const tcsum_pkt_t *pkts, uint32_t n, u
     return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
 }
 
+int tcsum_batch_ipv4_tx_fill_scratch(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
+                                     uint8_t *flags, void *scratch, uint64_t scratch_bytes, uint64_t total_bytes_hint,
+                                     void *stream)
+{
+    if (n == 0)
+        return TCSUM_OK;
+    if (!arena || !pkts || !scratch || (reinterpret_cast<uintptr_t>(scratch) & 3u) || scratch_bytes < 8ull * n)
+        return TCSUM_ERR_PARAM;
+    const hipError_t e = tcsum::launch_ipv4_tx_scratch(tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
+                                                       static_cast<uint8_t *>(arena), pkts, n, out, flags,
+                                                       static_cast<uint32_t *>(scratch),
+                                                       static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
+}
+
 int tcsum_batch_ipv4_tx_offload(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
                                 uint8_t *flags, uint64_t total_bytes_hint, void *stream)
 {

@@ -1701,22 +1701,54 @@ static hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t stream)
 // values are computed from `arena` and stored into `store`, the same packets
 // at another address (the same arena, or the host memory an HBM copy was
 // made from: the scatter's stores then cross PCIe as posted writes).
-static hipError_t tx_split(Geometry g, dim3 grid, uint32_t xg, uint8_t *arena, uint8_t *store,
-                           const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out, uint8_t *flags, hipStream_t stream)
+// `side`: 8 * n bytes of scratch (positions [n], then the values [n] when the
+// caller wants no `out`).
+static hipError_t tx_split_in(Geometry g, dim3 grid, uint32_t xg, uint8_t *arena, uint8_t *store,
+                              const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out, uint8_t *flags, uint32_t *side,
+                              hipStream_t stream)
 {
-    uint32_t *side = nullptr; // positions [n], then the values [n] when the caller wants no `out`
-    hipError_t e = scratch_alloc(reinterpret_cast<void **>(&side), (size_t)n * (out ? 4u : 8u), stream);
-    if (e != hipSuccess)
-        return e;
     uint32_t *vals = out ? out : side + n;
-    e = ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, vals, flags, reinterpret_cast<int8_t *>(side),
-                      IP_OPT_DEFER, xg, stream);
+    hipError_t e = ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, vals, flags,
+                                 reinterpret_cast<int8_t *>(side), IP_OPT_DEFER, xg, stream);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, store, pkts, n, vals, side);
         e = hipGetLastError();
     }
+    return e;
+}
+
+static hipError_t tx_split(Geometry g, dim3 grid, uint32_t xg, uint8_t *arena, uint8_t *store,
+                           const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out, uint8_t *flags, hipStream_t stream)
+{
+    uint32_t *side = nullptr;
+    hipError_t e = scratch_alloc(reinterpret_cast<void **>(&side), (size_t)n * (out ? 4u : 8u), stream);
+    if (e != hipSuccess)
+        return e;
+    e = tx_split_in(g, grid, xg, arena, store, pkts, n, out, flags, side, stream);
     const hipError_t f = hipFreeAsync(side, stream);
     return e != hipSuccess ? e : f;
+}
+
+hipError_t launch_ipv4_tx_scratch(Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
+                                  uint8_t *flags, uint32_t *scratch, hipStream_t stream)
+{
+    if (n == 0)
+        return hipSuccess;
+    g.lanes = g.lanes < 16 ? 16 : g.lanes > 64 ? 64 : g.lanes; // launch_ipv4's rules
+    const uint64_t per_launch = kMaxBlocks * (256u / (uint32_t)g.lanes);
+    if (n > per_launch) { // each part uses the scratch of its own packets
+        for (uint64_t i0 = 0; i0 < n; i0 += per_launch) {
+            const uint32_t m = (uint32_t)(n - i0 < per_launch ? n - i0 : per_launch);
+            const hipError_t e = launch_ipv4_tx_scratch(g, arena, pkts + i0, m, out ? out + i0 : nullptr,
+                                                        flags ? flags + i0 : nullptr, scratch + 2 * i0, stream);
+            if (e != hipSuccess)
+                return e;
+        }
+        return hipSuccess;
+    }
+    const uint64_t per_block = 256u / (uint32_t)g.lanes;
+    return tx_split_in(g, dim3((uint32_t)((n + per_block - 1) / per_block)), (uint32_t)g.xcd, arena, arena, pkts,
+                       n, out, flags, scratch, stream);
 }
 
 hipError_t launch_ipv4_tx_to(Geometry g, uint8_t *arena, uint8_t *store, const tcsum_pkt_t *pkts, uint32_t n,

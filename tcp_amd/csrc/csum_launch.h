@@ -41,6 +41,11 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
 hipError_t launch_ipv4_tx_to(Geometry g, uint8_t *arena, uint8_t *store, const tcsum_pkt_t *pkts, uint32_t n,
                              uint32_t *out, uint8_t *flags, hipStream_t stream);
 
+// The tx fill with its stores deferred, in scratch the caller owns (8 * n
+// bytes): no allocation, so it can be captured in a hipGraph.
+hipError_t launch_ipv4_tx_scratch(Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
+                                  uint8_t *flags, uint32_t *scratch, hipStream_t stream);
+
 // Queue server (k_server): one job at a time.  SrvHost lives in pinned,
 // coherent host memory (the host writes the job, then `req`, and reads `done`);
 // SrvCtl in device memory (zeroed before every launch).

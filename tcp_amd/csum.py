@@ -110,15 +110,24 @@ def batch_ipv4(arena, pkts, n: int, total_bytes: int = 0, out=None, flags=None, 
 
 
 def batch_ipv4_tx_fill(arena, pkts, n: int, total_bytes: int = 0, out=None, flags=None, want_flags=True,
-                       stream=None):
-    """Write the IPv4 / TCP / UDP / ICMP checksums into the packets in place."""
+                       stream=None, scratch=None):
+    """Write the IPv4 / TCP / UDP / ICMP checksums into the packets in place.
+    scratch: a device tensor of >= 8*n bytes the caller owns
+    (tcsum_batch_ipv4_tx_fill_scratch: the deferred-store form with no
+    allocation, capturable in a hipGraph)."""
     torch = _torch()
     if flags is None and want_flags:
         flags = torch.empty(n, dtype=torch.uint8, device=arena.device)
-    rc = _lib.lib().tcsum_batch_ipv4_tx_fill(arena.data_ptr(), pkts.data_ptr(), n,
-                                             out.data_ptr() if out is not None else None,
-                                             flags.data_ptr() if flags is not None else None, total_bytes,
-                                             _stream_ptr(stream))
+    o = out.data_ptr() if out is not None else None
+    f = flags.data_ptr() if flags is not None else None
+    if scratch is None:
+        rc = _lib.lib().tcsum_batch_ipv4_tx_fill(arena.data_ptr(), pkts.data_ptr(), n, o, f, total_bytes,
+                                                 _stream_ptr(stream))
+    else:
+        rc = _lib.lib().tcsum_batch_ipv4_tx_fill_scratch(arena.data_ptr(), pkts.data_ptr(), n, o, f,
+                                                         scratch.data_ptr(),
+                                                         scratch.numel() * scratch.element_size(), total_bytes,
+                                                         _stream_ptr(stream))
     _lib.check(rc, "tcsum_batch_ipv4_tx_fill")
     return flags
 

@@ -124,6 +124,10 @@ def test_batch_argument_errors_without_device(libpath):
     assert L.tcsum_batch_segments(None, None, 4, None, 1, 0, None) == _lib.ERR_PARAM
     assert L.tcsum_batch_ipv4(None, None, 4, None, None, 0, None) == _lib.ERR_PARAM
     assert L.tcsum_batch_ipv4_tx_fill(None, None, 4, None, None, 0, None) == _lib.ERR_PARAM
+    assert L.tcsum_batch_ipv4_tx_fill_scratch(ctypes.c_void_p(64), ctypes.c_void_p(64), 4, None, None,
+                                              ctypes.c_void_p(64), 31, 0, None) == _lib.ERR_PARAM  # < 8 * n
+    assert L.tcsum_batch_ipv4_tx_fill_scratch(ctypes.c_void_p(64), ctypes.c_void_p(64), 4, None, None,
+                                              ctypes.c_void_p(66), 64, 0, None) == _lib.ERR_PARAM  # misaligned
     assert L.tcsum_batch_ipv4_rx_verify(None, None, 4, None, None, None, 0, None) == _lib.ERR_PARAM
     assert L.tcsum_batch_peso(None, None, 0, None, 0, None) == _lib.OK  # empty batch
     assert L.tcsum_synth_fill(ctypes.c_void_p(8), 16, 0, 1, None) == _lib.ERR_PARAM  # misaligned

@@ -582,6 +582,41 @@ def test_hip_graph_capture_tx_fill(tc, torch, oracle):
         np.testing.assert_array_equal(arena.cpu().numpy(), want)
 
 
+def test_hip_graph_capture_tx_fill_scratch(tc, torch, oracle):
+    """The deferred-store tx fill with caller scratch
+    (tcsum_batch_ipv4_tx_fill_scratch) captured in a hipGraph: the replays
+    fill the packets like the oracle and report the same values as the plain
+    call; outside a graph it leaves the same bytes too."""
+    from tcp_amd import workload
+    b = workload.make_batch("mixed_tx", n=140000)
+    arena, descs = workload.materialize(b)
+    unfilled = arena.clone()
+    want = arena.cpu().numpy()
+    oracle.batch_ipv4_tx_fill(want, b.descs, nthreads=8)
+    scratch = torch.empty(8 * b.n, dtype=torch.uint8, device="cuda")
+    out = torch.empty(b.n, dtype=torch.uint32, device="cuda")
+    ref_out = torch.empty_like(out)
+    tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, out=ref_out, want_flags=False)
+    torch.cuda.synchronize()
+    assert np.array_equal(arena.cpu().numpy(), want)
+    arena.copy_(unfilled)
+    tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False, scratch=scratch)  # no graph
+    torch.cuda.synchronize()
+    assert np.array_equal(arena.cpu().numpy(), want)
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, out=out, want_flags=False, scratch=scratch)
+    for _ in range(2):
+        arena.copy_(unfilled)
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(arena.cpu().numpy(), want)
+        assert torch.equal(out, ref_out)
+
+
 def test_concurrent_streams(tc, torch, oracle):
     """Independent batches on independent streams do not interfere.  Outputs
     are allocated once up front: a tensor freed on one stream and reused by

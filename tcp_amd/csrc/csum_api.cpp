@@ -85,6 +85,7 @@ struct Ctx {
     uint8_t *d_stage = nullptr; // device-side addresses of the three above
     void *d_desc = nullptr;
     uint16_t *d_result = nullptr;
+    uint32_t sync_seq = 0; // run_sync's completion word
     // host-resident batches
     hipStream_t hs[kHostStreams] = {};
     hipEvent_t hev[kHostEvents] = {};
@@ -234,6 +235,31 @@ void run_sync(Ctx &c, hipError_t launched)
 {
     if (launched != hipSuccess)
         die("kernel launch", launched);
+    // The stream writes a sequence number into pinned memory behind the
+    // kernel and the host spins on that word: 13.5-15.5 us per drop-in call
+    // against 16.9-17.6 us blocking in hipStreamSynchronize
+    // (profiles/r02/legacy_latency_poll.txt).  TCSUM_SYNC=block: the latter.
+    static const bool block = getenv("TCSUM_SYNC") && strcmp(getenv("TCSUM_SYNC"), "block") == 0;
+    if (!block) {
+        uint32_t *flag = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(c.result) + 32);
+        void *dflag = reinterpret_cast<uint8_t *>(c.d_result) + 32;
+        const uint32_t seq = ++c.sync_seq ? c.sync_seq : ++c.sync_seq;
+        hipError_t e = hipStreamWriteValue32(c.stream, dflag, seq, 0);
+        if (e != hipSuccess)
+            die("hipStreamWriteValue32", e);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned spins = 1; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq; ++spins) {
+            if ((spins & 4095u) == 0) {
+                e = hipStreamQuery(c.stream);
+                if (e != hipSuccess && e != hipErrorNotReady)
+                    die("kernel", e);
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+                    die("kernel (no completion in 10 s)", hipErrorLaunchTimeOut);
+            }
+            __builtin_ia32_pause();
+        }
+        return;
+    }
     hipError_t e = hipStreamSynchronize(c.stream);
     if (e != hipSuccess)
         die("hipStreamSynchronize", e);

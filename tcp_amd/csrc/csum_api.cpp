@@ -231,38 +231,43 @@ void ensure_stage(Ctx &c, size_t bytes)
     c.stage_cap = cap;
 }
 
+// Wait for everything queued on c.stream.  The stream writes a sequence
+// number into pinned memory behind the last kernel and the host spins on that
+// word: 13.5-15.5 us per drop-in call against 16.9-17.6 us blocking in
+// hipStreamSynchronize (profiles/r02/legacy_latency_poll.txt).
+// TCSUM_SYNC=block: the latter.
+hipError_t stream_wait(Ctx &c)
+{
+    static const bool block = getenv("TCSUM_SYNC") && strcmp(getenv("TCSUM_SYNC"), "block") == 0;
+    if (block)
+        return hipStreamSynchronize(c.stream);
+    uint32_t *flag = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(c.result) + 32);
+    void *dflag = reinterpret_cast<uint8_t *>(c.d_result) + 32;
+    const uint32_t seq = ++c.sync_seq ? c.sync_seq : ++c.sync_seq;
+    hipError_t e = hipStreamWriteValue32(c.stream, dflag, seq, 0);
+    if (e != hipSuccess)
+        return e;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spins = 1; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq; ++spins) {
+        if ((spins & 4095u) == 0) {
+            e = hipStreamQuery(c.stream);
+            if (e != hipSuccess && e != hipErrorNotReady)
+                return e;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+                return hipErrorLaunchTimeOut;
+        }
+        __builtin_ia32_pause();
+    }
+    return hipSuccess;
+}
+
 void run_sync(Ctx &c, hipError_t launched)
 {
     if (launched != hipSuccess)
         die("kernel launch", launched);
-    // The stream writes a sequence number into pinned memory behind the
-    // kernel and the host spins on that word: 13.5-15.5 us per drop-in call
-    // against 16.9-17.6 us blocking in hipStreamSynchronize
-    // (profiles/r02/legacy_latency_poll.txt).  TCSUM_SYNC=block: the latter.
-    static const bool block = getenv("TCSUM_SYNC") && strcmp(getenv("TCSUM_SYNC"), "block") == 0;
-    if (!block) {
-        uint32_t *flag = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(c.result) + 32);
-        void *dflag = reinterpret_cast<uint8_t *>(c.d_result) + 32;
-        const uint32_t seq = ++c.sync_seq ? c.sync_seq : ++c.sync_seq;
-        hipError_t e = hipStreamWriteValue32(c.stream, dflag, seq, 0);
-        if (e != hipSuccess)
-            die("hipStreamWriteValue32", e);
-        const auto t0 = std::chrono::steady_clock::now();
-        for (unsigned spins = 1; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq; ++spins) {
-            if ((spins & 4095u) == 0) {
-                e = hipStreamQuery(c.stream);
-                if (e != hipSuccess && e != hipErrorNotReady)
-                    die("kernel", e);
-                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
-                    die("kernel (no completion in 10 s)", hipErrorLaunchTimeOut);
-            }
-            __builtin_ia32_pause();
-        }
-        return;
-    }
-    hipError_t e = hipStreamSynchronize(c.stream);
+    const hipError_t e = stream_wait(c);
     if (e != hipSuccess)
-        die("hipStreamSynchronize", e);
+        die("waiting for the kernel", e);
 }
 
 // ---- pktbuf cursor, restated from net/src/pktbuf.c:153-170, 446-483 ----
@@ -1690,7 +1695,7 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     }
     // on a failed launch the pieces already launched still read the arena
     // (and the staging the next call reuses): drain them before returning
-    const hipError_t se = hipStreamSynchronize(c.stream);
+    const hipError_t se = e == hipSuccess ? stream_wait(c) : hipStreamSynchronize(c.stream);
     if (e != hipSuccess || se != hipSuccess)
         return TCSUM_ERR_SYS;
     }

@@ -538,8 +538,9 @@ def legacy_latency(tc):
         finally:
             if served:
                 tc.call_server(False)
-    res["note"] = ("plain: one launch + one sync per call; served_: tcsum_call_server (one resident wave "
-                   "polling pinned memory). Use the batch API for throughput")
+    res["note"] = ("plain: one launch per call, the host spinning on a completion word the stream writes behind "
+                   "it; served_: tcsum_call_server (one resident wave polling pinned memory). Use the batch API "
+                   "for throughput")
     return res
 
 

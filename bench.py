@@ -522,7 +522,7 @@ def legacy_latency(tc):
     buf = tc.PktBuf([seg[i: i + 127] for i in range(0, 1500, 127)])
     d, s_ = tc.IpAddr.v4([192, 168, 74, 3]), tc.IpAddr.v4([192, 168, 74, 2])
     res = {}
-    for served in (False, True):  # one launch + sync per call / the call server's resident wave
+    for served in (False, True):  # one launch + its wait per call / the call server's resident wave
         if served:
             tc.call_server(True)
         try:

@@ -101,7 +101,7 @@ struct Ctx {
     // of a pageable arena, all read and written by the kernel over PCIe
     Pinned q_desc, q_res, q_arena;
     // queue server (tcsum_queue_server): a resident grid serving host-queue
-    // jobs posted through pinned memory, instead of a launch + sync per job
+    // jobs posted through pinned memory, instead of a launch + wait per job
     bool srv_on = false;      // enabled for this device
     bool srv_running = false; // a grid was launched and not yet seen to finish
     hipStream_t srv_stream = nullptr;
@@ -111,7 +111,7 @@ struct Ctx {
     uint32_t srv_seq = 0; // last job posted (0 = none)
     uint64_t *srv_trace = nullptr; // TCSUM_SERVER_TRACE stamps (host address)
     // call server (tcsum_call_server): one resident wave serving the three
-    // synchronous drop-in symbols, instead of a launch + sync per call
+    // synchronous drop-in symbols, instead of a launch + wait per call
     bool cs_on = false;      // enabled for this device
     bool cs_running = false; // the wave was launched and not yet seen to finish
     hipStream_t cs_stream = nullptr;

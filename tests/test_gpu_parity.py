@@ -137,7 +137,9 @@ def test_reference_stack_objects_link_against_libtcsum(tc):
 
 def test_c_host_batch_demo(tc):
     """tests/c/batch_demo.c: a plain C host (HIP C API + libtcsum.so) runs the
-    batch and end-to-end paths; the CPU oracle checks every result."""
+    batch and end-to-end paths, and a tx fill captured in a hipGraph through
+    the C API (tcsum_batch_ipv4_tx_fill_scratch); the CPU oracle checks every
+    result."""
     import subprocess
     exe = os.path.join(os.path.dirname(G.GOLDEN), "c", "build", "batch_demo")
     if not os.path.exists(exe):

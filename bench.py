@@ -457,9 +457,41 @@ def e2e(torch, tc, r):
         ndev = torch.cuda.device_count()
         if ndev > 1:  # the same host batch sharded over every GPU of the node, in a child with a time limit
             res["multi_device"] = e2e_multi_child(b.config, ndev)
-        return res
     finally:
         L.tcsum_host_free(p)
+    try:
+        res["host_queue_rx"] = e2e_host_queue_rx(torch, tc)
+    except Exception as e:  # reported, never fatal
+        res["host_queue_rx"] = {"error": repr(e)}
+    return res
+
+
+def e2e_host_queue_rx(torch, tc):
+    """The receive path from host memory (the frames plat/netif_pcap.c hands
+    the stack): configs[3]'s 1M IPv4 frames in pinned host memory ->
+    tcsum_host_batch_ipv4_rx_verify (copy-engine pieces, k_ipv4 rx) ->
+    verdicts; checked against the device-resident verdicts."""
+    from tcp_amd import workload
+    b = workload.make_batch("mixed_rx")
+    arena, descs = workload.materialize(b)
+    want, _ = tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes, want_flags=False)
+    want = want.cpu().numpy()
+    ha = tc.HostArena(arena.numel())
+    try:
+        ha.array[:] = arena.cpu().numpy()
+        del arena, descs
+        torch.cuda.empty_cache()
+        v, _, _ = tc.host_batch_ipv4_rx_verify(ha, b.descs)  # warm (device buffers)
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            v, _, _ = tc.host_batch_ipv4_rx_verify(ha, b.descs)
+        dt = (time.perf_counter() - t0) / reps
+        return {"gib_s": round(b.total_bytes / dt / GIB, 2), "ms_per_batch": round(dt * 1e3, 2), "frames": b.n,
+                "path": "pinned host frames -> copy-engine pieces into HBM -> k_ipv4 rx verify -> verdicts to host",
+                "matches_device_resident": bool((v == want).all())}
+    finally:
+        ha.free()
 
 
 def e2e_multi_child(config: str, ndev: int, timeout_s: float = 240.0):

@@ -1868,6 +1868,13 @@ uint16_t checksum16(int offset, void *buf, uint16_t len, uint32_t pre_sum, int c
         memcpy(c.cs_stage + par, buf, len);
         return (uint16_t)cs_post(c, ctl, len, pre_sum, 0u, 0u, 0u);
     }
+    if (len + par <= tcsum::kCallInline) { // the bytes travel in the kernel arguments
+        static const bool inl = !(getenv("TCSUM_INLINE") && atoi(getenv("TCSUM_INLINE")) == 0); // measurement
+        if (inl) {
+            run_sync(c, tcsum::launch_inline16(buf, len, par, pre_sum, complement, c.d_result, c.stream));
+            return *c.result;
+        }
+    }
     ensure_stage(c, len);
     uint8_t *dst = c.stage + par;
     if (len)

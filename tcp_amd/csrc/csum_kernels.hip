@@ -26,6 +26,7 @@
 #include "csum_launch.h"
 
 #include <stdlib.h>
+#include <string.h>
 
 #include <mutex>
 
@@ -1859,6 +1860,44 @@ hipError_t launch_server(SrvHost *h, SrvCtl *d, uint32_t last, uint64_t idle_tic
     // PCIe round trip for its bytes (the server's frames live in host memory)
     hipLaunchKernelGGL((k_server<64, 16>), dim3((uint32_t)(wgs > 0 ? wgs : 1)), dim3(256), 0, stream, h, d, last,
                        idle_ticks);
+    return hipGetLastError();
+}
+
+// checksum16 on <= kCallInline bytes with the bytes in the kernel arguments
+// (the call server's inline job, as a one-shot launch): no PCIe read of a
+// descriptor or of staged bytes before the sum -- ipv4.c:243,656's 20-byte
+// header checks.  w: the bytes at offset `odd`, zero-padded to 24.
+__global__ __launch_bounds__(64) void k_inline16(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
+                                                 uint32_t w5, uint32_t odd, uint32_t len, uint32_t pre,
+                                                 uint32_t comp, uint16_t *__restrict__ out)
+{
+    if (threadIdx.x != 0)
+        return;
+    uint32_t acc = 0; // the exact word sum of the six dwords is the range's
+    acc = dot_halves(acc, w0, 0x00010001u);
+    acc = dot_halves(acc, w1, 0x00010001u);
+    acc = dot_halves(acc, w2, 0x00010001u);
+    acc = dot_halves(acc, w3, 0x00010001u);
+    acc = dot_halves(acc, w4, 0x00010001u);
+    acc = dot_halves(acc, w5, 0x00010001u);
+    SegDesc d;
+    d.off = odd;
+    d.len = len;
+    d.pre = pre;
+    d.src = d.dst = d.proto = 0u;
+    *out = finalize<MODE_EXACT>(acc, odd, d, comp | (odd << 1), 0u);
+}
+
+hipError_t launch_inline16(const void *bytes, uint32_t len, uint32_t odd, uint32_t pre, int complement,
+                           uint16_t *out, hipStream_t stream)
+{
+    if (len + odd > kCallInline)
+        return hipErrorInvalidValue;
+    uint32_t w[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+    if (len)
+        memcpy(reinterpret_cast<uint8_t *>(w) + odd, bytes, len);
+    hipLaunchKernelGGL(k_inline16, dim3(1), dim3(64), 0, stream, w[0], w[1], w[2], w[3], w[4], w[5], odd, len, pre,
+                       complement ? 1u : 0u, out);
     return hipGetLastError();
 }
 

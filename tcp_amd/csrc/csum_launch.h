@@ -92,6 +92,11 @@ struct CallBox {
 };
 static_assert(sizeof(CallBox) == 128, "CallBox: job line + result line");
 
+// checksum16 (MODE_EXACT) on len + odd <= kCallInline bytes passed in the
+// kernel arguments; the u16 result into *out.
+hipError_t launch_inline16(const void *bytes, uint32_t len, uint32_t odd, uint32_t pre, int complement,
+                           uint16_t *out, hipStream_t stream);
+
 hipError_t launch_call_server(CallBox *box /*device-visible address*/, const uint8_t *stage /*device-visible*/,
                               uint32_t last, uint64_t idle_ticks, hipStream_t stream);
 

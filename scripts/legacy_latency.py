@@ -11,8 +11,8 @@ import sys, json; sys.path.insert(0, %r)
 import bench, tcp_amd
 print(json.dumps(bench.legacy_latency(tcp_amd)))
 """ % ROOT
-runs = [("block", "1"), ("poll", "0"), ("poll", "1")] * 2  # (TCSUM_SYNC, TCSUM_INLINE)
-for mode, inl in runs:  # "poll": anything but "block"; TCSUM_INLINE=0: checksum16 bytes staged, not in the kernel arguments
-    env = dict(os.environ, TCSUM_SYNC=mode, TCSUM_INLINE=inl)
+runs = [("block", "1"), ("poll", "0"), ("poll", "1")] * 2  # (TCSUM_SYNC, TCSUM_ARGS_LAUNCH)
+for mode, inl in runs:  # "poll": anything but "block"; TCSUM_ARGS_LAUNCH=0: descriptor (and bytes) via pinned memory
+    env = dict(os.environ, TCSUM_SYNC=mode, TCSUM_ARGS_LAUNCH=inl)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True)
-    print(mode, "inline" if inl == "1" else "staged", r.stdout.strip() or r.stderr[-500:])
+    print(mode, "args" if inl == "1" else "pinned-desc", r.stdout.strip() or r.stderr[-500:])

@@ -126,6 +126,17 @@ struct Ctx {
 // ranges take the launch path).
 constexpr size_t kCallStageMax = 1u << 16;
 
+// Launch-path drop-in calls up to this many bytes pass their descriptor (and
+// up to kCallInline bytes) in the kernel arguments: one wave, one pass
+// (k_once / k_inline16).  TCSUM_ARGS_LAUNCH=0: the descriptor in pinned
+// memory, as before (measurement).
+constexpr size_t kOnceMax = 16u << 10;
+bool args_launch()
+{
+    static const bool on = !(getenv("TCSUM_ARGS_LAUNCH") && atoi(getenv("TCSUM_ARGS_LAUNCH")) == 0);
+    return on;
+}
+
 Ctx g_ctx[kMaxDev];
 std::mutex g_default_mu;
 int g_default_dev = -1;
@@ -1868,17 +1879,20 @@ uint16_t checksum16(int offset, void *buf, uint16_t len, uint32_t pre_sum, int c
         memcpy(c.cs_stage + par, buf, len);
         return (uint16_t)cs_post(c, ctl, len, pre_sum, 0u, 0u, 0u);
     }
-    if (len + par <= tcsum::kCallInline) { // the bytes travel in the kernel arguments
-        static const bool inl = !(getenv("TCSUM_INLINE") && atoi(getenv("TCSUM_INLINE")) == 0); // measurement
-        if (inl) {
-            run_sync(c, tcsum::launch_inline16(buf, len, par, pre_sum, complement, c.d_result, c.stream));
-            return *c.result;
-        }
+    if (len + par <= tcsum::kCallInline && args_launch()) { // the bytes travel in the kernel arguments
+        run_sync(c, tcsum::launch_inline16(tcsum::MODE_EXACT, buf, len, par, pre_sum, complement, c.d_result,
+                                           c.stream));
+        return *c.result;
     }
     ensure_stage(c, len);
     uint8_t *dst = c.stage + par;
     if (len)
         memcpy(dst, buf, len);
+    if (len <= kOnceMax && args_launch()) { // the descriptor travels in the kernel arguments
+        run_sync(c, tcsum::launch_once(tcsum::MODE_EXACT, c.d_stage, par, len, pre_sum, 0u, 0u, 0u, complement,
+                                       c.d_result, c.stream));
+        return *c.result;
+    }
     tcsum_seg_t *d = static_cast<tcsum_seg_t *>(c.desc);
     d->offset = par;
     d->len = len;
@@ -1910,8 +1924,20 @@ uint16_t pktbuf_checksum16(tcsum_pktbuf_t *buf, int len, int pre_sum, int comple
         gather(buf, len, c.cs_stage);
         return (uint16_t)cs_post(c, ctl, (uint32_t)len, (uint32_t)pre_sum, 0u, 0u, 0u);
     }
+    if ((uint32_t)len <= tcsum::kCallInline && args_launch()) { // the bytes travel in the kernel arguments
+        uint8_t small[tcsum::kCallInline];
+        gather(buf, len, small);
+        run_sync(c, tcsum::launch_inline16(tcsum::MODE_SEG, small, (uint32_t)len, 0u, (uint32_t)pre_sum, complement,
+                                           c.d_result, c.stream));
+        return *c.result;
+    }
     ensure_stage(c, (size_t)len);
     gather(buf, len, c.stage);
+    if ((size_t)len <= kOnceMax && args_launch()) { // the descriptor travels in the kernel arguments
+        run_sync(c, tcsum::launch_once(tcsum::MODE_SEG, c.d_stage, 0u, (uint32_t)len, (uint32_t)pre_sum, 0u, 0u, 0u,
+                                       complement, c.d_result, c.stream));
+        return *c.result;
+    }
     tcsum_seg_t *d = static_cast<tcsum_seg_t *>(c.desc);
     d->offset = 0;
     d->len = (uint32_t)len;
@@ -1942,6 +1968,14 @@ uint16_t checksum_peso(tcsum_pktbuf_t *buf, const tcsum_ipaddr_t *dest, const tc
     ensure_stage(c, total > 0 ? (size_t)total : 0);
     if (total > 0)
         gather(buf, total, c.stage); // leaves the cursor at the end, like tools.c:73
+    if ((total <= 0 || (size_t)total <= kOnceMax) && args_launch()) { // the descriptor in the kernel arguments
+        uint32_t s32, d32;
+        memcpy(&s32, src->addr, 4);
+        memcpy(&d32, dest->addr, 4);
+        run_sync(c, tcsum::launch_once(tcsum::MODE_PESO, c.d_stage, 0u, total > 0 ? (uint32_t)total : 0u, 0u, s32,
+                                       d32, protocol, 0, c.d_result, c.stream));
+        return *c.result;
+    }
     tcsum_peso_t *d = static_cast<tcsum_peso_t *>(c.desc);
     d->offset = 0;
     d->len = total > 0 ? (uint32_t)total : 0;

@@ -1867,6 +1867,7 @@ hipError_t launch_server(SrvHost *h, SrvCtl *d, uint32_t last, uint64_t idle_tic
 // (the call server's inline job, as a one-shot launch): no PCIe read of a
 // descriptor or of staged bytes before the sum -- ipv4.c:243,656's 20-byte
 // header checks.  w: the bytes at offset `odd`, zero-padded to 24.
+template <int MODE>
 __global__ __launch_bounds__(64) void k_inline16(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
                                                  uint32_t w5, uint32_t odd, uint32_t len, uint32_t pre,
                                                  uint32_t comp, uint16_t *__restrict__ out)
@@ -1885,19 +1886,72 @@ __global__ __launch_bounds__(64) void k_inline16(uint32_t w0, uint32_t w1, uint3
     d.len = len;
     d.pre = pre;
     d.src = d.dst = d.proto = 0u;
-    *out = finalize<MODE_EXACT>(acc, odd, d, comp | (odd << 1), 0u);
+    if constexpr (MODE == MODE_EXACT)
+        *out = finalize<MODE_EXACT>(acc, odd, d, comp | (odd << 1), 0u);
+    else
+        *out = finalize<MODE_SEG>(acc, odd, d, comp, 0u);
 }
 
-hipError_t launch_inline16(const void *bytes, uint32_t len, uint32_t odd, uint32_t pre, int complement,
+// One staged range (the drop-in symbols' launch path) with its descriptor in
+// the kernel arguments instead of pinned memory: one PCIe read less before
+// the bytes.  The call server's staged job as a one-shot launch.
+template <int MODE>
+__global__ __launch_bounds__(64) void k_once(const uint8_t *__restrict__ stage, uint32_t off, uint32_t len,
+                                             uint32_t pre, uint32_t src, uint32_t dst, uint32_t proto, uint32_t comp,
+                                             uint16_t *__restrict__ out)
+{
+    constexpr int G = 64, U = 16; // 16 KiB per pass
+    const uint32_t gl = threadIdx.x;
+    SegDesc d;
+    d.off = off;
+    d.len = len;
+    d.pre = pre;
+    d.src = src;
+    d.dst = dst;
+    d.proto = proto;
+    uint32_t acc = sum_range<G, U, MODE == MODE_EXACT>(stage, off, len, gl, [] {});
+    acc = group_sum<G>(acc);
+    if (gl == 0) {
+        const uintptr_t start = reinterpret_cast<uintptr_t>(stage + off);
+        if constexpr (MODE == MODE_EXACT)
+            *out = finalize<MODE_EXACT>(acc, start, d, comp | ((off & 1u) << 1), 0u);
+        else if constexpr (MODE == MODE_PESO)
+            *out = finalize<MODE_PESO>(acc, start, d, 0u, peso_pseudo16(d));
+        else
+            *out = finalize<MODE_SEG>(acc, start, d, comp, 0u);
+    }
+}
+
+hipError_t launch_once(Mode mode, const uint8_t *stage, uint32_t off, uint32_t len, uint32_t pre, uint32_t src,
+                       uint32_t dst, uint32_t proto, int complement, uint16_t *out, hipStream_t stream)
+{
+    const uint32_t comp = complement ? 1u : 0u;
+    if (mode == MODE_EXACT)
+        hipLaunchKernelGGL(k_once<MODE_EXACT>, dim3(1), dim3(64), 0, stream, stage, off, len, pre, src, dst, proto,
+                           comp, out);
+    else if (mode == MODE_PESO)
+        hipLaunchKernelGGL(k_once<MODE_PESO>, dim3(1), dim3(64), 0, stream, stage, off, len, pre, src, dst, proto,
+                           comp, out);
+    else
+        hipLaunchKernelGGL(k_once<MODE_SEG>, dim3(1), dim3(64), 0, stream, stage, off, len, pre, src, dst, proto,
+                           comp, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_inline16(Mode mode, const void *bytes, uint32_t len, uint32_t odd, uint32_t pre, int complement,
                            uint16_t *out, hipStream_t stream)
 {
-    if (len + odd > kCallInline)
+    if (len + odd > kCallInline || (mode != MODE_EXACT && mode != MODE_SEG))
         return hipErrorInvalidValue;
     uint32_t w[6] = {0u, 0u, 0u, 0u, 0u, 0u};
     if (len)
         memcpy(reinterpret_cast<uint8_t *>(w) + odd, bytes, len);
-    hipLaunchKernelGGL(k_inline16, dim3(1), dim3(64), 0, stream, w[0], w[1], w[2], w[3], w[4], w[5], odd, len, pre,
-                       complement ? 1u : 0u, out);
+    if (mode == MODE_EXACT)
+        hipLaunchKernelGGL(k_inline16<MODE_EXACT>, dim3(1), dim3(64), 0, stream, w[0], w[1], w[2], w[3], w[4], w[5],
+                           odd, len, pre, complement ? 1u : 0u, out);
+    else
+        hipLaunchKernelGGL(k_inline16<MODE_SEG>, dim3(1), dim3(64), 0, stream, w[0], w[1], w[2], w[3], w[4], w[5],
+                           odd, len, pre, complement ? 1u : 0u, out);
     return hipGetLastError();
 }
 

@@ -92,10 +92,15 @@ struct CallBox {
 };
 static_assert(sizeof(CallBox) == 128, "CallBox: job line + result line");
 
-// checksum16 (MODE_EXACT) on len + odd <= kCallInline bytes passed in the
-// kernel arguments; the u16 result into *out.
-hipError_t launch_inline16(const void *bytes, uint32_t len, uint32_t odd, uint32_t pre, int complement,
+// MODE_EXACT (checksum16) or MODE_SEG (pktbuf_checksum16) on len + odd <=
+// kCallInline bytes passed in the kernel arguments; the u16 result into *out.
+hipError_t launch_inline16(Mode mode, const void *bytes, uint32_t len, uint32_t odd, uint32_t pre, int complement,
                            uint16_t *out, hipStream_t stream);
+
+// One range of staged bytes at stage + off, its descriptor in the kernel
+// arguments (src/dst/proto: MODE_PESO only); the u16 result into *out.
+hipError_t launch_once(Mode mode, const uint8_t *stage, uint32_t off, uint32_t len, uint32_t pre, uint32_t src,
+                       uint32_t dst, uint32_t proto, int complement, uint16_t *out, hipStream_t stream);
 
 hipError_t launch_call_server(CallBox *box /*device-visible address*/, const uint8_t *stage /*device-visible*/,
                               uint32_t last, uint64_t idle_ticks, hipStream_t stream);

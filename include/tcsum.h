@@ -344,10 +344,12 @@ int tcsum_host_unregister(void *p);
 
 /* Free every buffer the batch calls cache on `device` between calls: the
  * HBM copy of host spans (tcsum_host_batch_peso, the copy-engine path of the
- * host-queue batches), descriptors, and the pinned host-queue staging; a
- * running queue / call server is stopped first.  The next call allocates
- * again.  (The copy-engine path keeps at most $TCSUM_HOSTQ_DMA_KEEP_MB, default
- * 256, between calls by itself.)  Returns TCSUM_OK, TCSUM_ERR_PARAM, or
+ * host-queue batches), descriptors, the pinned host-queue staging, and the
+ * memory the tx fill's scratch pool keeps (up to 1 GiB); a running queue /
+ * call server is stopped first and the device is synchronized, so no work of
+ * the caller's may still be queued on it.  The next call allocates again.
+ * (The copy-engine path keeps at most $TCSUM_HOSTQ_DMA_KEEP_MB, default 256,
+ * between calls by itself.)  Returns TCSUM_OK, TCSUM_ERR_PARAM, or
  * TCSUM_ERR_SYS. */
 int tcsum_release(int device);
 

@@ -246,7 +246,10 @@ void ensure_stage(Ctx &c, size_t bytes)
 // number into pinned memory behind the last kernel and the host spins on that
 // word: 13.5-15.5 us per drop-in call against 16.9-17.6 us blocking in
 // hipStreamSynchronize (profiles/r02/legacy_latency_poll.txt).
-// TCSUM_SYNC=block: the latter.
+// TCSUM_SYNC=block: the latter.  The spin is only the fast path: after 10 s
+// (a contended GPU, a profiler serialising kernels) the wait continues in
+// hipStreamSynchronize, so a caller never gets control back while its kernels
+// may still read or write its buffers; only a real device error is returned.
 hipError_t stream_wait(Ctx &c)
 {
     static const bool block = getenv("TCSUM_SYNC") && strcmp(getenv("TCSUM_SYNC"), "block") == 0;
@@ -265,7 +268,7 @@ hipError_t stream_wait(Ctx &c)
             if (e != hipSuccess && e != hipErrorNotReady)
                 return e;
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
-                return hipErrorLaunchTimeOut;
+                return hipStreamSynchronize(c.stream); // drains the stream, whatever it takes
         }
         __builtin_ia32_pause();
     }
@@ -1471,6 +1474,11 @@ int release_ctx(Ctx &c)
         q->h = q->d = nullptr;
         q->cap = 0;
     }
+    // the tx fill's pooled scratch (every stream of this context is idle;
+    // a caller's own stream on this device must be too, tcsum.h)
+    (void)hipDeviceSynchronize();
+    if (tcsum::scratch_trim(c.device) != hipSuccess)
+        return TCSUM_ERR_SYS;
     return TCSUM_OK;
 }
 

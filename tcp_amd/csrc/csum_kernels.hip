@@ -1670,32 +1670,45 @@ static hipError_t ipv4_u(int G, int U, dim3 grid, uint8_t *arena, const tcsum_pk
 // library's own per device that keeps up to 1 GiB between calls: the default
 // pool hands its memory back at every synchronization, and mapping it again
 // cost a synchronized 1M-packet fill ~190 us (profiles/r02/tx_sync_probe.txt).
+// The pool is the one of the device the caller's stream belongs to (the
+// calling thread's current device only for the null stream).
+static std::mutex g_scratch_mu;
+static hipMemPool_t g_scratch_pools[64] = {};
+
 static hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t stream)
 {
-    static std::mutex mu;
-    static hipMemPool_t pools[64] = {};
     int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
+    hipError_t e = stream ? hipStreamGetDevice(stream, &dev) : hipGetDevice(&dev);
     if (e != hipSuccess)
         return e;
     hipMemPool_t pool = nullptr;
     if (dev >= 0 && dev < 64) {
-        std::lock_guard<std::mutex> lk(mu);
-        if (!pools[dev]) {
+        std::lock_guard<std::mutex> lk(g_scratch_mu);
+        if (!g_scratch_pools[dev]) {
             hipMemPoolProps props = {};
             props.allocType = hipMemAllocationTypePinned;
             props.location.type = hipMemLocationTypeDevice;
             props.location.id = dev;
-            if (hipMemPoolCreate(&pools[dev], &props) == hipSuccess) {
+            if (hipMemPoolCreate(&g_scratch_pools[dev], &props) == hipSuccess) {
                 uint64_t keep = 1ull << 30;
-                (void)hipMemPoolSetAttribute(pools[dev], hipMemPoolAttrReleaseThreshold, &keep);
+                (void)hipMemPoolSetAttribute(g_scratch_pools[dev], hipMemPoolAttrReleaseThreshold, &keep);
             } else {
-                pools[dev] = nullptr;
+                g_scratch_pools[dev] = nullptr;
             }
         }
-        pool = pools[dev];
+        pool = g_scratch_pools[dev];
     }
     return pool ? hipMallocFromPoolAsync(p, bytes, pool, stream) : hipMallocAsync(p, bytes, stream);
+}
+
+// tcsum_release: hand the pool's kept memory back (the caller has synchronized
+// every stream that allocated from it).
+hipError_t scratch_trim(int dev)
+{
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    if (dev < 0 || dev >= 64 || !g_scratch_pools[dev])
+        return hipSuccess;
+    return hipMemPoolTrimTo(g_scratch_pools[dev], 0);
 }
 
 // The tx fill with its stores deferred (IP_OPT_DEFER + k_tx_scatter): the

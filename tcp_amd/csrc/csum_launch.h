@@ -43,6 +43,9 @@ hipError_t launch_ipv4_tx_to(Geometry g, uint8_t *arena, uint8_t *store, const t
 
 // The tx fill with its stores deferred, in scratch the caller owns (8 * n
 // bytes): no allocation, so it can be captured in a hipGraph.
+// give back the tx fill's pooled scratch of device dev (tcsum_release)
+hipError_t scratch_trim(int dev);
+
 hipError_t launch_ipv4_tx_scratch(Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
                                   uint8_t *flags, uint32_t *scratch, hipStream_t stream);
 

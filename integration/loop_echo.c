@@ -18,6 +18,13 @@
  * The one platform fix: sys_mutex_create is made recursive here (the Makefile
  * weakens the Linux definition), as pktbuf_free takes the pktbuf lock twice
  * (pktbuf.c:203 -> :44) and deadlocks on a default pthread mutex.
+ *
+ * Options: --udp-only; --rounds N (UDP datagrams, default 200); --tcp-bytes N
+ * (default 65536); --ref-udp-server: the UDP server is the reference's own
+ * app/echo/udp_echo_server.c, compiled unchanged (it binds INADDR_ANY,
+ * udp_echo_server.c:22, and echoes at most 125 bytes, :31-33, so datagrams
+ * are 1-125 B).  Both phases print their wall time: round trips per second
+ * for UDP, MB/s for TCP (configs[0]'s only numbers).
  */
 #include <pthread.h>
 #include <signal.h>
@@ -26,8 +33,11 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <time.h>
+
 #include "net.h"
 #include "net_api.h"
+#include "app/echo/udp_echo_server.h"
 #include "net_csum_gpu.h"
 #include "sys_plat.h"
 #ifdef NET_CHECKSUM_GPU
@@ -47,8 +57,14 @@ sys_mutex_t sys_mutex_create(void)
 
 #define UDP_PORT 7
 #define TCP_PORT 8
-#define UDP_ROUNDS 200
-#define TCP_BYTES (64 * 1024)
+static int UDP_ROUNDS = 200, UDP_MAX = 1400, TCP_BYTES = 64 * 1024;
+
+static double now_s(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
 
 static void udp_server(void *arg)
 {
@@ -123,8 +139,11 @@ static int udp_echo(void)
     to.sin_addr.s_addr = inet_addr("127.0.0.1");
     to.sin_port = htons(UDP_PORT);
     static uint8_t out[1500], in[2048];
+    const double t0 = now_s();
+    long bytes = 0;
     for (int r = 0; r < UDP_ROUNDS; r++) {
-        int n = 1 + (r * 37) % 1400; /* the loop netif has mtu 0: no fragmentation (ipv4.c:616) */
+        int n = 1 + (r * 37) % UDP_MAX; /* the loop netif has mtu 0: no fragmentation (ipv4.c:616) */
+        bytes += n;
         fill(out, n, r);
         if (sendto(s, out, (size_t)n, 0, (const struct sockaddr *)&to, sizeof to) != n)
             return fprintf(stderr, "udp round %d: sendto failed\n", r), 1;
@@ -136,8 +155,11 @@ static int udp_echo(void)
         if (r % 50 == 0)
             printf("udp round %d ok\n", r);
     }
+    const double dt = now_s() - t0;
     close(s);
-    printf("udp: %d datagrams (1-1400 B) echoed intact\n", UDP_ROUNDS);
+    printf("udp: %d datagrams (1-%d B) echoed intact\n", UDP_ROUNDS, UDP_MAX);
+    printf("timing udp: %d round trips, %ld bytes each way, %.3f s: %.0f round trips/s, %.3f MB/s\n", UDP_ROUNDS,
+           bytes, dt, UDP_ROUNDS / dt, bytes / dt / 1e6);
     return 0;
 }
 
@@ -153,9 +175,12 @@ static int tcp_echo(void)
     to.sin_port = htons(TCP_PORT);
     if (connect(s, (const struct sockaddr *)&to, sizeof to) < 0)
         return fprintf(stderr, "tcp client: connect failed\n"), 1;
-    static uint8_t out[TCP_BYTES], in[TCP_BYTES];
+    uint8_t *out = (uint8_t *)malloc((size_t)TCP_BYTES), *in = (uint8_t *)malloc((size_t)TCP_BYTES);
+    if (!out || !in)
+        return fprintf(stderr, "tcp client: out of memory\n"), 1;
     fill(out, TCP_BYTES, 99);
     int sent = 0, got = 0;
+    const double t0 = now_s();
     while (got < TCP_BYTES) {
         if (sent < TCP_BYTES) {
             int chunk = TCP_BYTES - sent < 700 ? TCP_BYTES - sent : 700;
@@ -169,10 +194,12 @@ static int tcp_echo(void)
             return fprintf(stderr, "tcp: recv failed at %d of %d\n", got, TCP_BYTES), 1;
         got += (int)k;
     }
-    if (memcmp(in, out, TCP_BYTES) != 0)
+    const double dt = now_s() - t0;
+    if (memcmp(in, out, (size_t)TCP_BYTES) != 0)
         return fprintf(stderr, "tcp: echoed bytes differ\n"), 1;
     close(s);
     printf("tcp: %d bytes echoed intact\n", TCP_BYTES);
+    printf("timing tcp: %d bytes each way, %.3f s: %.3f MB/s\n", TCP_BYTES, dt, TCP_BYTES / dt / 1e6);
     return 0;
 }
 
@@ -204,7 +231,17 @@ int main(int argc, char **argv)
     setvbuf(stdout, NULL, _IONBF, 0);
     signal(SIGALRM, watchdog);
     alarm(60);
-    int do_tcp = !(argc > 1 && strcmp(argv[1], "--udp-only") == 0);
+    int do_tcp = 1, ref_server = 0;
+    for (int i = 1; i < argc; i++) {
+        if (!strcmp(argv[i], "--udp-only"))
+            do_tcp = 0;
+        else if (!strcmp(argv[i], "--ref-udp-server"))
+            ref_server = 1, UDP_MAX = 125;
+        else if (!strcmp(argv[i], "--rounds") && i + 1 < argc)
+            UDP_ROUNDS = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--tcp-bytes") && i + 1 < argc)
+            TCP_BYTES = atoi(argv[++i]);
+    }
 #ifdef NET_CHECKSUM_GPU
     if (tcsum_device_count() < 1) /* net_init ignores net_plat_init's result (net.c:22) */
         return fprintf(stderr, "no gfx950 device: the GPU build cannot run here\n"), 2;
@@ -214,7 +251,10 @@ int main(int argc, char **argv)
         return fprintf(stderr, "net_init failed\n"), 2;
     stage = "net_start";
     net_start();
-    sys_thread_create(udp_server, (void *)0);
+    if (ref_server)
+        udp_echo_server_start(UDP_PORT); /* the reference's app/echo server, unchanged */
+    else
+        sys_thread_create(udp_server, (void *)0);
     if (do_tcp)
         sys_thread_create(tcp_server, (void *)0);
     sys_sleep(100);

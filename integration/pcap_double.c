@@ -164,6 +164,8 @@ static void answer_arp_locked(const uint8_t *f, uint32_t len)
 {
     if (len < 42 || f[12] != 0x08 || f[13] != 0x06 || f[20] != 0 || f[21] != 1)
         return;
+    if (memcmp(f + 28, f + 38, 4) == 0)
+        return; /* a gratuitous request (arp_make_gratuitous): nobody answers */
     uint8_t r[60];
     memset(r, 0, sizeof r);
     memcpy(r, f + 6, 6);          /* to the requester */
@@ -176,7 +178,7 @@ static void answer_arp_locked(const uint8_t *f, uint32_t len)
     memcpy(r + 32, f + 22, 6);    /* target: the requester */
     memcpy(r + 38, f + 28, 4);
     rx_push_locked(frame_new(r, sizeof r));
-    arp_replies++;
+    __atomic_fetch_add(&arp_replies, 1, __ATOMIC_RELAXED);
 }
 
 /* ------------------------------------------------------------ libpcap */
@@ -301,7 +303,7 @@ int pcap_next_ex(pcap_t *p, struct pcap_pkthdr **hdr, const u_char **data)
             rx_tail = NULL;
         rx_pending--;
         if (!passes(p, f)) {
-            filtered++;
+            __atomic_fetch_add(&filtered, 1, __ATOMIC_RELAXED);
             free(f);
             continue;
         }
@@ -323,7 +325,7 @@ int pcap_inject(pcap_t *p, const void *buf, size_t len)
     pthread_mutex_lock(&mu);
     if (inject_fail > 0) {
         inject_fail--;
-        inject_failures++;
+        __atomic_fetch_add(&inject_failures, 1, __ATOMIC_RELAXED);
         pthread_mutex_unlock(&mu);
         free(f);
         snprintf(p->err, sizeof p->err, "pcap_double: injected send failure");

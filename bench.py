@@ -103,7 +103,7 @@ def launch(tc, batch, arena, descs, out, flags=None):
 SETTLE_MS = 30.0  # set from --settle-ms in main()
 
 
-def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None):
+def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None, probes=True):
     batch = workload.make_batch(config, rank=rank)
     arena, descs = workload.materialize(batch)
     dt = torch.uint16 if batch.kind == "peso" else torch.int8 if batch.op == "rx" else torch.uint32
@@ -137,9 +137,18 @@ def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None):
         dist.barrier()
     torch.cuda.synchronize()
     ms = t0.elapsed_time(t1)  # events on the launch stream: pure kernel time of K launches
-    probes = probe_compare(torch, tc, batch, lambda: launch(tc, batch, arena, descs, out, flags), arena, steps,
-                           descs=descs)
-    return dict(batch=batch, arena=arena, descs=descs, out=out, ms=ms, wall_s=wall, probes=probes)
+    r = dict(batch=batch, arena=arena, descs=descs, out=out, flags=flags, ms=ms, wall_s=wall, steps=steps)
+    if probes:
+        run_probes(torch, tc, r)
+    return r
+
+
+def run_probes(torch, tc, r) -> None:
+    """The probes, after the timed region (and after self_check: the tx probe
+    leaves the batch's checksum fields junk)."""
+    batch, arena, descs, out, flags = r["batch"], r["arena"], r["descs"], r["out"], r["flags"]
+    r["probes"] = probe_compare(torch, tc, batch, lambda: launch(tc, batch, arena, descs, out, flags), arena,
+                                r["steps"], descs=descs)
 
 
 def probe_compare(torch, tc, batch, product, arena, steps, rounds=5, descs=None):
@@ -180,6 +189,9 @@ def probe_compare(torch, tc, batch, product, arena, steps, rounds=5, descs=None)
     elif descs is not None:
         kinds["segments"] = lambda: tc.probe_ipv4(arena, descs, batch.n, batch.total_bytes, rx=batch.op == "rx",
                                                   sink=sink)
+        if batch.op == "tx":  # the ceiling for a kernel that must write: the same loads + the fill's own writes
+            kinds["segments_tx"] = lambda: tc.probe_ipv4(arena, descs, batch.n, batch.total_bytes, tx=True,
+                                                         sink=sink)
     m = max(2, steps // rounds)
     stream = torch.cuda.current_stream()
     per = {k: [] for k in kinds}
@@ -201,6 +213,8 @@ def probe_compare(torch, tc, batch, product, arena, steps, rounds=5, descs=None)
         res["tile_dep_gbs"] = nbytes / (med["tile_dep"] * 1e-3) / 1e9
     if "segments" in med:
         res["segments_gbs"] = algorithmic_bytes(batch) / (med["segments"] * 1e-3) / 1e9
+    if "segments_tx" in med:
+        res["segments_tx_gbs"] = algorithmic_bytes(batch) / (med["segments_tx"] * 1e-3) / 1e9
     return res
 
 
@@ -212,7 +226,9 @@ def result_entry(r, steps):
     p = r["probes"]
     best = max(p["read_gbs"], p.get("tile_gbs", 0.0), p.get("tile_dep_gbs", 0.0), p.get("segments_gbs", 0.0))
     side = alg / (p["product_ms"] * 1e-3) / 1e9  # the product in the interleaved rounds
-    return {
+    # a kernel that writes is priced against the probe that makes the same writes
+    ceil = p.get("segments_tx_gbs", best)
+    entry = {
         "workload": b.config,
         "packets": b.n,
         "payload_bytes": b.total_bytes,
@@ -221,14 +237,19 @@ def result_entry(r, steps):
         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4),
                      "achievable_read": round(best, 1),
-                     "frac_of_achievable": round(side / best, 4),
+                     "achievable": round(ceil, 1),
+                     "achievable_kind": "segments_tx (the fill's loads + its own field writes)"
+                                        if "segments_tx_gbs" in p else "fastest read probe",
+                     "frac_of_achievable": round(side / ceil, 4),
                      "probes": {"plain_read_gbs": round(p["read_gbs"], 1),
                                 "tile_read_gbs": round(p["tile_gbs"], 1) if "tile_gbs" in p else None,
                                 "tile_dep_read_gbs": round(p["tile_dep_gbs"], 1) if "tile_dep_gbs" in p else None,
                                 "segments_read_gbs": round(p["segments_gbs"], 1) if "segments_gbs" in p else None,
+                                "segments_tx_gbs": round(p["segments_tx_gbs"], 1) if "segments_tx_gbs" in p else None,
                                 "tile_geometry": p["geometry"], "product_gbs_same_rounds": round(side, 1),
                                 "rounds": p["rounds"], "launches_per_round": p["launches_per_round"]}},
     }
+    return entry
 
 
 # ------------------------------------------------------------ PMC traffic
@@ -576,6 +597,64 @@ def legacy_latency(tc):
     return res
 
 
+SELF_CHECK_N = 4096  # segments per rank re-summed after the timed region
+
+
+def device_identity(torch, dev: int) -> dict:
+    """Which GPU this rank timed: its HIP ordinal and PCI address (RCCL runs
+    one rank per GPU; two ranks on one device would double-count it)."""
+    p = torch.cuda.get_device_properties(dev)
+    pci = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    return {"ordinal": dev, "pci": pci, "uuid": str(p.uuid), "name": p.name,
+            "visible": os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")}
+
+
+def self_check(torch, tc, workload, head, seed: int) -> dict:
+    """Re-sum a seeded sample of this rank's own segments in a separate,
+    smaller launch and compare with what the timed launches produced: a
+    self-consistency check that needs no oracle on the box (the oracle
+    parity lives in tests/).  The tx fill writes into the packets, so for it
+    the sample is filled again and must come out byte-identical
+    (idempotence)."""
+    import numpy as np
+    b, arena, out = head["batch"], head["arena"], head["out"]
+    n = min(SELF_CHECK_N, b.n)
+    idx = np.sort(np.random.default_rng(seed).choice(b.n, size=n, replace=False))
+    sub = tc.descs_to_device(b.descs[idx], arena.device)
+    want_idx = torch.from_numpy(idx).to(arena.device)
+    if b.kind == "peso":
+        got = tc.batch_peso(arena, sub, n, 0)
+        bad = int((got != out[want_idx]).sum().item())
+    elif b.op == "tx":
+        lens = np.minimum(b.descs["len"][idx].astype(np.int64), 78)  # the fill writes only there
+        offs = b.descs["offset"][idx].astype(np.int64)
+        pos = torch.from_numpy(np.concatenate([o + np.arange(k) for o, k in zip(offs, lens)])).to(arena.device)
+        before = arena[pos].clone()
+        tc.batch_ipv4_tx_fill(arena, sub, n, 0, want_flags=False)
+        bad = int((arena[pos] != before).sum().item())
+    elif b.op == "rx":
+        got, _ = tc.batch_ipv4_rx_verify(arena, sub, n, 0, want_flags=False)
+        bad = int((got != out[want_idx]).sum().item())
+    elif b.op == "txo":
+        got, _ = tc.batch_ipv4_tx_offload(arena, sub, n, 0)
+        bad = int((got != out[want_idx]).sum().item())
+    else:
+        got, _ = tc.batch_ipv4(arena, sub, n, 0, want_flags=False)
+        bad = int((got != out[want_idx]).sum().item())
+    torch.cuda.synchronize()
+    return {"segments": n, "mismatches": bad}
+
+
+def check_devices(devices: list, backend: str):
+    """None when every rank timed its own GPU, else the reason."""
+    if backend != "nccl" or len(devices) < 2:
+        return None
+    keys = [d["pci"] or d["uuid"] for d in devices]
+    if len(set(keys)) != len(keys):
+        return f"ranks share a GPU: {keys}"
+    return None
+
+
 def launch_ranks(args) -> int:
     """`bench.py --gpus N` without a launcher: start N rank processes of this
     script (one per GPU, torchrun's environment, rendezvous on 127.0.0.1)
@@ -615,13 +694,21 @@ def rehearsal(args, rank, world) -> None:
     dt = time.perf_counter() - t0
     D.barrier(dist)
     t = D.max_over_ranks(dist, dt)
+    # the same post-timing checks as the GPU run: which device each rank used
+    # (here: its CPU process) and the stand-in re-run against its timed result
+    bad = int(int(data.astype(np.uint64).sum()) != s)
+    dev = {"ordinal": None, "pci": None, "uuid": f"cpu-rank-{rank}-pid-{os.getpid()}", "name": "cpu (rehearsal)"}
     ranks = D.gather_objects(dist, {"rank": rank, "byte_base": int(b.byte_base), "packets": int(b.n),
-                                    "payload_bytes": int(b.total_bytes), "stand_in_sum": s})
+                                    "payload_bytes": int(b.total_bytes), "stand_in_sum": s, "device": dev,
+                                    "self_check": {"segments": 1, "mismatches": bad}})
     if rank == 0:
         print(json.dumps({"rehearsal": "cpu-gloo (numpy stand-in for the kernel; not a measurement)",
                           "n_gpus": world, "steps": args.steps, "scaling": "weak",
                           "value": round(world * b.total_bytes * args.steps / t / GIB, 3),
-                          "max_rank_s": t, "ranks": ranks}), flush=True)
+                          "max_rank_s": t, "ranks": ranks, "devices": [r["device"] for r in ranks],
+                          "self_check": {"segments_per_rank": 1,
+                                         "mismatches": sum(r["self_check"]["mismatches"] for r in ranks)}}),
+              flush=True)
     D.barrier(dist)
     dist.destroy_process_group()
 
@@ -671,12 +758,21 @@ def main():
 
     global SETTLE_MS
     SETTLE_MS = 0.0 if args.pmc_child and not args.trace_child else max(0.0, args.settle_ms)
-    if args.pmc_child:
-        time_config(torch, tc, workload, args.config, 0, args.steps, args.warmup)
+    if args.pmc_child:  # no probes: the tx probe launches k_tx_scatter, a step kernel by name
+        time_config(torch, tc, workload, args.config, 0, args.steps, args.warmup, probes=False)
         return
 
-    head = time_config(torch, tc, workload, args.config, rank, args.steps, args.warmup, dist)
+    head = time_config(torch, tc, workload, args.config, rank, args.steps, args.warmup, dist, probes=False)
     ms = D.max_over_ranks(dist, head["ms"], device="cuda" if backend == "nccl" else "cpu")
+    # after the timed region: every rank names its GPU and re-sums a sample of
+    # its own slice against its timed results
+    mine = {"rank": rank, "device": device_identity(torch, dev),
+            "self_check": self_check(torch, tc, workload, head, 20240807 + rank)}
+    ranks = D.gather_objects(dist, mine)
+    devices = [dict(r["device"], rank=r["rank"]) for r in ranks]
+    shared = check_devices(devices, backend)
+    mism = sum(r["self_check"]["mismatches"] for r in ranks)
+    run_probes(torch, tc, head)
     b = head["batch"]
     ms_step = ms / args.steps
     value = n_gpus * b.total_bytes * args.steps / (ms * 1e-3) / GIB
@@ -720,7 +816,19 @@ def main():
                    if b.kind == "peso" else "IPv4 header + L4 (ipv4.c:243, tcp_in.c:80, udp.c:410)",
                    "parallelism": f"{n_gpus} independent GPU shards, no collective"},
         "roofline": roof,
+        "devices": devices,
+        "self_check": {"segments_per_rank": mine["self_check"]["segments"], "mismatches": mism,
+                       "what": "a seeded sample of each rank's segments re-summed in a separate launch after the "
+                               "timed region, compared with the timed results (tx fill: filled again, must not "
+                               "change a byte)"},
     }
+    if shared or mism:
+        if rank == 0:
+            line["error"] = shared or f"{mism} sampled segments differ from the timed results"
+            print(json.dumps(line), flush=True)
+            print(f"bench.py: {line['error']}", file=sys.stderr)
+        D.barrier(dist)
+        sys.exit(2 if shared else 3)
 
     if world == 1:
         if not args.no_cpu:

@@ -57,11 +57,17 @@ int tcsum_probe_segments(const void *arena /*[dev]*/, const tcsum_peso_t *segs /
                          uint64_t total_bytes_hint, uint32_t *sink /*[dev]*/, void *stream);
 
 /* The same for the IPv4 batch calls: tcsum_batch_ipv4's descriptor, header
- * and line-aligned data loads (rx != 0: tcsum_batch_ipv4_rx_verify's, two
- * more header chunks and its lane count), XOR-folded, nothing stored but the
- * fluke sink.  Geometries 16 x 3..8, 32 x 4/6, 64 x 16; else TCSUM_ERR_PARAM. */
+ * and line-aligned data loads, XOR-folded, nothing stored but the fluke sink
+ * (mode 0).  mode 1: tcsum_batch_ipv4_rx_verify's (two more header chunks,
+ * its lane count).  mode 2, the ceiling for the tx fill, which must write:
+ * mode 0's loads plus exactly the deferred fill's writes -- 8 bytes of scratch
+ * per packet (a value and the field positions, derived from the header by the
+ * fill's own rules) and then the fill's k_tx_scatter storing the fields; the
+ * stored values are the XOR fold, so every IPv4 / L4 checksum field of the
+ * batch is left holding junk (the arena is written despite the const).
+ * Geometries 16 x 3..8, 32 x 4/6, 64 x 16; else TCSUM_ERR_PARAM. */
 int tcsum_probe_ipv4(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,
-                     uint64_t total_bytes_hint, int rx, uint32_t *sink /*[dev]*/, void *stream);
+                     uint64_t total_bytes_hint, int mode, uint32_t *sink /*[dev]*/, void *stream);
 
 #ifdef __cplusplus
 }

@@ -129,12 +129,13 @@ constexpr size_t kCallStageMax = 1u << 16;
 // Launch-path drop-in calls up to this many bytes pass their descriptor (and
 // up to kCallInline bytes) in the kernel arguments: one wave, one pass
 // (k_once / k_inline16).  TCSUM_ARGS_LAUNCH=0: the descriptor in pinned
-// memory, as before (measurement).
+// memory, as before (measurement; read per call so one process can run both,
+// tests/test_gpu_parity.py).
 constexpr size_t kOnceMax = 16u << 10;
 bool args_launch()
 {
-    static const bool on = !(getenv("TCSUM_ARGS_LAUNCH") && atoi(getenv("TCSUM_ARGS_LAUNCH")) == 0);
-    return on;
+    const char *s = getenv("TCSUM_ARGS_LAUNCH");
+    return !(s && atoi(s) == 0);
 }
 
 Ctx g_ctx[kMaxDev];
@@ -613,12 +614,12 @@ int tcsum_probe_segments(const void *arena, const tcsum_peso_t *segs, uint32_t n
     return e == hipSuccess ? TCSUM_OK : e == hipErrorInvalidValue ? TCSUM_ERR_PARAM : TCSUM_ERR_SYS;
 }
 
-int tcsum_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t total_bytes_hint, int rx,
+int tcsum_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t total_bytes_hint, int mode,
                      uint32_t *sink, void *stream)
 {
-    if (!arena || !pkts || !sink)
+    if (!arena || !pkts || !sink || mode < 0 || mode > 2)
         return TCSUM_ERR_PARAM;
-    const hipError_t e = tcsum::launch_probe_ipv4(arena, pkts, n, mean_of(total_bytes_hint, n), rx,
+    const hipError_t e = tcsum::launch_probe_ipv4(arena, pkts, n, mean_of(total_bytes_hint, n), mode,
                                                   sink, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? TCSUM_OK : e == hipErrorInvalidValue ? TCSUM_ERR_PARAM : TCSUM_ERR_SYS;
 }

@@ -472,6 +472,92 @@ __global__ __launch_bounds__(256) void k_segments_wg(const uint8_t *__restrict__
                                   d, aux, q16);
 }
 
+// One range per workgroup of W waves, with the lane -> chunk map as a
+// parameter (measured against k_segments_wg for configs[2],
+// scripts/wg_shape_ab.py): GL = 0 interleaves the whole workgroup (load u of
+// lane t is interior chunk u * 64W + t: each load instruction of the
+// workgroup covers 64W contiguous chunks, k_segments_wg's map); GL > 0 cuts
+// the range into sub-ranges of GL * U chunks, one per GL-lane group, each
+// walked like one headline packet (k_segments<16, 6>: load u of lane l is
+// chunk u * GL + l of its sub-range).  A pass covers 64W * U chunks; longer
+// ranges take more passes.  Edges as in frame_issue: lane 0 loads the first
+// chunk and lane 1 the last with the default policy, masked; every interior
+// chunk is nontemporal and whole.
+template <int W, int GL, int U, int MODE>
+__global__ __launch_bounds__(W * 64) void k_segments_wgx(const uint8_t *__restrict__ arena,
+                                                         const void *__restrict__ descs, uint32_t n,
+                                                         uint16_t *__restrict__ out, uint32_t aux, uint32_t xg)
+{
+    static_assert(MODE != MODE_EXACT, "the exact u32 sum stays on k_segments");
+    constexpr uint32_t T = W * 64u, CPP = T * U;
+    __shared__ uint32_t part[W];
+    const uint32_t t = threadIdx.x;
+    const uint32_t seg = xcd_block(blockIdx.x, gridDim.x, xg); // grid == n
+    const bool live = seg < n;
+    const SegDesc d = load_desc<MODE>(descs, seg, live);
+    const uint8_t *p = arena + d.off;
+    const uint32_t s0 = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
+    const u32x4 *base = reinterpret_cast<const u32x4 *>(p - s0);
+    const uint64_t e = (uint64_t)d.len + s0;
+    const uint32_t nch = d.len ? (uint32_t)((e + 15) >> 4) : 0u;
+    const uint32_t ni = nch > 2 ? nch - 2 : 0u;
+    const u32x4 *ib = ni ? base + 1 : &g_zero_chunk;
+    const uint32_t ilast = ni ? ni - 1u : 0u;
+    const uint32_t eidx = t == 0 ? 0u : (nch ? nch - 1u : 0u);
+    const bool has_edge = t < 2 && nch > 0 && (t == 0 || nch >= 2);
+    const u32x4 ev = load16<false>((nch ? base : &g_zero_chunk) + (nch ? eidx : 0u));
+    const uint32_t lane_off = GL ? (t / GL) * (GL * U) + (t % GL) : t;
+    constexpr uint32_t ustep = GL ? GL : T;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t j = lane_off + u * ustep;
+        v[u] = load16<true>(ib + (j < ni ? j : ilast));
+    }
+    uint32_t q16 = 0;
+    if constexpr (MODE == MODE_PESO)
+        q16 = pinned(peso_pseudo16(d));
+    issue_fence();
+    uint32_t acc;
+    {
+        const uint64_t c = 16ull * eidx;
+        const int lo = has_edge && eidx == 0 ? (int)s0 : 0;
+        const int hi = has_edge ? (int)(e - c < 16 ? e - c : 16) : 0;
+        acc = chunk_sum_masked(0u, ev, lo, hi);
+    }
+    {
+        Acc4 pa{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            acc4_add(pa, v[u], lane_off + u * ustep < ni ? 0x00010001u : 0u);
+        acc = fold_step(acc + acc4_total(pa));
+    }
+    for (uint32_t b0 = CPP; b0 < ni; b0 += CPP) {
+        u32x4 w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = b0 + lane_off + u * ustep;
+            w[u] = load16<true>(ib + (j < ni ? j : ilast));
+        }
+        Acc4 pa{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            acc4_add(pa, w[u], b0 + lane_off + u * ustep < ni ? 0x00010001u : 0u);
+        acc = fold_step(acc + acc4_total(pa));
+    }
+    acc = group_sum<64>(acc); // < 2^23
+    if ((t & 63u) == 0)
+        part[t >> 6] = acc;
+    __syncthreads();
+    if (t == 0 && live) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            s += part[w]; // < 16 * 2^23
+        out[seg] = finalize<MODE>(s, reinterpret_cast<uintptr_t>(p), d, aux, q16);
+    }
+}
+
 // Persistent form: a resident grid walks the batch; each wave prefetches its
 // next descriptor while the current packets' bytes are in flight, so the
 // descriptor -> data dependence costs one latency per wave, not per packet.
@@ -951,11 +1037,19 @@ __global__ __launch_bounds__(256) void k_tx_scatter(uint8_t *__restrict__ arena,
 // the line-aligned nontemporal data pass -- same lanes, same clamping, same
 // XCD order -- folded by XOR into a sink stored on a 2^-32 fluke.  The rate
 // the IPv4 kernels would run at if their arithmetic and stores were free.
-template <int G, int U, bool RX>
+// PM_TX adds exactly the deferred tx fill's writes (the ceiling for a kernel
+// that must write): every packet's 8 bytes of scratch -- a value word and the
+// field positions k_ipv4<IP_TX> derives from the header (same rules) -- and
+// then k_tx_scatter, the product's own scatter, writing the fields.  The
+// values are the XOR fold, so the packets' checksum fields end up junk.
+enum ProbeMode : int { PM_SUMS = 0, PM_RX = 1, PM_TX = 2 };
+template <int G, int U, int PM>
 __global__ __launch_bounds__(256) void k_probe_ipv4(const uint8_t *__restrict__ arena,
                                                     const tcsum_pkt_t *__restrict__ pkts, uint32_t n,
-                                                    uint32_t *__restrict__ sink, uint32_t xg)
+                                                    uint32_t *__restrict__ sink, uint32_t xg,
+                                                    uint32_t *__restrict__ vals, uint32_t *__restrict__ posv)
 {
+    constexpr bool RX = PM == PM_RX;
     const uint32_t gl = threadIdx.x & (G - 1);
     const uint32_t pk = xcd_block(blockIdx.x, gridDim.x, xg) * (256u / G) + threadIdx.x / G;
     const bool live = pk < n;
@@ -993,8 +1087,30 @@ __global__ __launch_bounds__(256) void k_probe_ipv4(const uint8_t *__restrict__ 
         }
     }
     const uint32_t acc = x.x ^ x.y ^ x.z ^ x.w;
-    if (acc == 0x9E3779B9u)
+    if constexpr (PM == PM_TX) {
+        // the positions k_ipv4<IP_TX> stores with IP_OPT_DEFER (ipv4_packet)
+        const Hdr5 hd = header_dwords(h0, h1, h2, s0);
+        const uint32_t b0h = hd.d0 & 0xFFu, ihl4 = (b0h & 0xFu) << 2;
+        const uint32_t tl = (((hd.d0 >> 16) & 0xFFu) << 8) | (hd.d0 >> 24);
+        const uint32_t b6 = (hd.d1 >> 16) & 0xFFu, b7 = hd.d1 >> 24;
+        const bool frag = (b6 & 0x20u) || (((b6 & 0x1Fu) << 8) | b7);
+        const uint32_t proto = (hd.d2 >> 8) & 0xFFu;
+        const bool bad = !big_enough || (b0h >> 4) != 4 || ihl4 < 20 || ihl4 > frame || tl < 20 || tl > frame ||
+                         tl < ihl4;
+        uint32_t hl = ihl4 < 20 ? 20u : ihl4;
+        hl = hl > frame ? frame : hl;
+        uint32_t end = tl < hl ? hl : tl;
+        end = end > frame ? frame : end;
+        uint32_t min_l4;
+        const uint32_t fld = l4_field(proto, min_l4);
+        const bool field_on = !bad && !frag && fld && end - hl >= min_l4;
+        if (live && gl == 0) {
+            vals[pk] = acc;
+            posv[pk] = bad ? 0u : (1u << 16) | (field_on ? hl + fld : 0u);
+        }
+    } else if (acc == 0x9E3779B9u) {
         sink[0] = acc;
+    }
 }
 
 // ---------------------------------------------------------------- queue server
@@ -1598,6 +1714,22 @@ static hipError_t seg_u(int G, int U, int persist, uint32_t xg, uint32_t n, cons
     if (G == 256) { // one range per workgroup
         const dim3 grid(n);
         const uint8_t *a = static_cast<const uint8_t *>(arena);
+        // TCSUM_WGX=W,GL,U: k_segments_wgx's shapes (checksum_peso batches)
+        if (const char *x = MODE == MODE_PESO ? getenv("TCSUM_WGX") : nullptr) {
+            int w = 0, gl = -1, u = 0;
+            if (sscanf(x, "%d,%d,%d", &w, &gl, &u) != 3)
+                return hipErrorInvalidValue;
+#define TCSUM_WGX(WW, GG, UU)                                                                                \
+    if (w == WW && gl == GG && u == UU) {                                                                    \
+        hipLaunchKernelGGL((k_segments_wgx<WW, GG, UU, MODE_PESO>), grid, dim3(WW * 64), 0, s, a, descs, n, out, aux, \
+                           xg);                                                                              \
+        return hipGetLastError();                                                                            \
+    }
+            TCSUM_WGX(4, 0, 16) TCSUM_WGX(8, 0, 8) TCSUM_WGX(16, 0, 4) TCSUM_WGX(4, 16, 16) TCSUM_WGX(8, 16, 8)
+            TCSUM_WGX(16, 16, 4) TCSUM_WGX(16, 16, 6) TCSUM_WGX(8, 64, 8) TCSUM_WGX(16, 64, 4)
+#undef TCSUM_WGX
+            return hipErrorInvalidValue;
+        }
         switch (U) {
         case 4: hipLaunchKernelGGL((k_segments_wg<4, MODE>), grid, dim3(256), 0, s, a, descs, n, out, aux, xg); break;
         case 8: hipLaunchKernelGGL((k_segments_wg<8, MODE>), grid, dim3(256), 0, s, a, descs, n, out, aux, xg); break;
@@ -1830,17 +1962,19 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
     }
 }
 
-hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t mean_len, int rx,
+hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t mean_len, int mode,
                              uint32_t *sink, hipStream_t stream)
 {
     if (n == 0)
         return hipSuccess;
+    if (mode < PM_SUMS || mode > PM_TX)
+        return hipErrorInvalidValue;
     Geometry g = pick_geometry(mean_len); // launch_ipv4's geometry rules
     if (g.lanes < 16)
         g.lanes = 16;
     if (g.lanes > 64)
         g.lanes = 64;
-    if (rx && g.lanes == 32 && !getenv("TCSUM_G"))
+    if (mode == PM_RX && g.lanes == 32 && !getenv("TCSUM_G"))
         g.lanes = 16;
     const uint32_t per_block = 256u / (uint32_t)g.lanes;
     const uint64_t blocks = ((uint64_t)n + per_block - 1) / per_block;
@@ -1848,20 +1982,41 @@ hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_
         return hipErrorInvalidValue;
     const uint8_t *a = static_cast<const uint8_t *>(arena);
     const uint32_t xg = (uint32_t)g.xcd;
+    // PM_TX: the deferred fill's scratch (values, positions), from its pool
+    uint32_t *side = nullptr;
+    if (mode == PM_TX) {
+        const hipError_t e = scratch_alloc(reinterpret_cast<void **>(&side), (size_t)n * 8u, stream);
+        if (e != hipSuccess)
+            return e;
+    }
+    uint32_t *vals = side, *posv = side ? side + n : nullptr;
+    hipError_t e = hipErrorInvalidValue;
 #define TCSUM_PI(GG, UU)                                                                                     \
-    if (g.lanes == GG && g.loads == UU) {                                                                    \
-        if (rx)                                                                                              \
-            hipLaunchKernelGGL((k_probe_ipv4<GG, UU, true>), dim3((uint32_t)blocks), dim3(256), 0, stream, a, pkts, \
-                               n, sink, xg);                                                                 \
+    if (e == hipErrorInvalidValue && g.lanes == GG && g.loads == UU) {                                       \
+        if (mode == PM_RX)                                                                                   \
+            hipLaunchKernelGGL((k_probe_ipv4<GG, UU, PM_RX>), dim3((uint32_t)blocks), dim3(256), 0, stream, a,   \
+                               pkts, n, sink, xg, vals, posv);                                              \
+        else if (mode == PM_TX)                                                                              \
+            hipLaunchKernelGGL((k_probe_ipv4<GG, UU, PM_TX>), dim3((uint32_t)blocks), dim3(256), 0, stream, a,   \
+                               pkts, n, sink, xg, vals, posv);                                              \
         else                                                                                                 \
-            hipLaunchKernelGGL((k_probe_ipv4<GG, UU, false>), dim3((uint32_t)blocks), dim3(256), 0, stream, a, pkts, \
-                               n, sink, xg);                                                                 \
-        return hipGetLastError();                                                                            \
+            hipLaunchKernelGGL((k_probe_ipv4<GG, UU, PM_SUMS>), dim3((uint32_t)blocks), dim3(256), 0, stream, a, \
+                               pkts, n, sink, xg, vals, posv);                                              \
+        e = hipGetLastError();                                                                               \
     }
     TCSUM_PI(16, 3) TCSUM_PI(16, 4) TCSUM_PI(16, 6) TCSUM_PI(16, 8) TCSUM_PI(32, 4) TCSUM_PI(32, 6)
     TCSUM_PI(64, 16)
 #undef TCSUM_PI
-    return hipErrorInvalidValue;
+    if (mode == PM_TX) {
+        if (e == hipSuccess) { // the product's scatter, on the probe's values and positions
+            hipLaunchKernelGGL(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, const_cast<uint8_t *>(a),
+                               pkts, n, vals, posv);
+            e = hipGetLastError();
+        }
+        const hipError_t f = hipFreeAsync(side, stream);
+        e = e != hipSuccess ? e : f;
+    }
+    return e;
 }
 
 hipError_t launch_server(SrvHost *h, SrvCtl *d, uint32_t last, uint64_t idle_ticks, int wgs, hipStream_t stream)

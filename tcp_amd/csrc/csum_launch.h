@@ -114,7 +114,9 @@ hipError_t launch_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, u
 hipError_t launch_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, hipStream_t stream);
 hipError_t launch_probe_desc(const void *arena, const void *descs, uint32_t n, uint64_t mean_len, uint32_t *sink,
                              hipStream_t stream);
-hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t mean_len, int rx,
+// mode 0: tcsum_batch_ipv4's loads; 1: rx verify's; 2: the deferred tx fill's
+// loads + its scratch writes + k_tx_scatter (writes junk into the fields)
+hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t mean_len, int mode,
                              uint32_t *sink, hipStream_t stream);
 hipError_t launch_probe_tile(const void *p, uint64_t nbytes, int lanes, int loads, uint32_t *sink, hipStream_t stream);
 

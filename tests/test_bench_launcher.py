@@ -34,6 +34,23 @@ def test_launcher_world2_rehearsal():
     # weak scaling: consecutive, disjoint slices of one global stream
     assert ranks[0]["byte_base"] == 0 and ranks[1]["byte_base"] >= ranks[0]["payload_bytes"]
     assert ranks[0]["stand_in_sum"] != ranks[1]["stand_in_sum"]
+    # each rank names the device it timed; rank 0's line lists them all
+    devs = line["devices"]
+    assert len(devs) == 2 and len({d["uuid"] for d in devs}) == 2
+    # each rank re-ran its stand-in after the timed region: no mismatch
+    assert line["self_check"]["mismatches"] == 0 and line["self_check"]["segments_per_rank"] >= 1
+
+
+def test_shared_gpu_is_refused():
+    """Under RCCL two ranks on one GPU make the aggregate meaningless: the
+    bench's device check names them (bench.py exits 2 on it)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    a = {"ordinal": 0, "pci": "0000:05:00", "uuid": "u0"}
+    b = {"ordinal": 1, "pci": "0000:15:00", "uuid": "u1"}
+    assert bench.check_devices([a, b], "nccl") is None
+    assert "share a GPU" in bench.check_devices([a, dict(a)], "nccl")
+    assert bench.check_devices([a, dict(a)], "gloo") is None  # a rehearsal may share on purpose
 
 
 @pytest.mark.timeout(300)

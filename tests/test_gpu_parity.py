@@ -121,6 +121,55 @@ def test_checksum_peso_golden(tc):
         assert pos == int(c["final_pos"]) == int(c["total"]) and blk is None
 
 
+def test_dropin_golden_with_descriptor_in_pinned_memory(tc, monkeypatch):
+    """TCSUM_ARGS_LAUNCH=0: every drop-in call takes the path with its
+    descriptor in pinned memory (the one calls above 16 KiB always take);
+    the same reference results and cursors as the kernel-argument path."""
+    monkeypatch.setenv("TCSUM_ARGS_LAUNCH", "0")
+    test_kats(tc)
+    test_checksum16_golden(tc)
+    test_pktbuf_checksum16_golden(tc)
+    test_checksum_peso_golden(tc)
+
+
+@pytest.mark.parametrize("args_launch", ["1", "0"])
+def test_pktbuf_checksum16_16k_to_64k(tc, oracle, monkeypatch, args_launch):
+    """pktbuf_checksum16 on chains of 16-64 KiB (the reference's pool stops
+    at 12,700 B, so its goldens do; parity here is against the oracle, which
+    those goldens pin): irregular 1..127-byte blocks, a seek, any length up to
+    what is left (and one past it: 0, pktbuf.c:650-655), any pre_sum and
+    complement; result and final cursor (pos, block)."""
+    monkeypatch.setenv("TCSUM_ARGS_LAUNCH", args_launch)
+    rng = np.random.default_rng(1616 + int(args_launch))
+    for case in range(60):
+        total = int(rng.integers(16 << 10, (64 << 10) + 1))
+        sizes = []
+        while sum(sizes) < total:
+            sizes.append(int(min(rng.integers(1, 128), total - sum(sizes))))
+        data = rng.integers(0, 256, total, dtype=np.uint8)
+        if case % 7 == 0:
+            data[:] = 0xFF
+        pieces, at = [], 0
+        for s in sizes:
+            pieces.append(data[at: at + s].tobytes())
+            at += s
+        buf = tc.PktBuf(pieces)
+        seek = int(rng.integers(0, min(total, 3000)))
+        if seek:
+            buf.seek(seek)
+        left = total - seek
+        length = left + 1 if case % 11 == 5 else int(rng.integers(0, left + 1))
+        pre, comp = int(rng.integers(0, 1 << 31)), int(rng.integers(0, 2))
+        # the oracle's pieces from the cursor: the rest of the cursor's block, then whole blocks
+        pos, blk, boff = buf.cursor()
+        rest = [pieces[blk][boff:]] + pieces[blk + 1:] if blk is not None else []
+        want = oracle.pieces_checksum16(rest, length, pre, comp)
+        got = tc.pktbuf_checksum16(buf, length, pre, comp)
+        assert got == want, (case, total, seek, length)
+        end = seek + (length if length <= left else 0)
+        assert buf.cursor()[0] == end, (case, buf.cursor(), end)
+
+
 def test_reference_stack_objects_link_against_libtcsum(tc):
     """oracle/_ref/dropin_stack: the reference's own pktbuf.o/tools.o (checksum
     definitions localized, as INTEGRATION.md patches them out) linked with

@@ -43,7 +43,6 @@ SIGNATURES = {
     "tcsum_host_batch_ipv4_multi": (_I, [_V, _I, _V, _U64, _V, _U32, _V, _V]),
     "tcsum_host_batch_ipv4_tx_fill_multi": (_I, [_V, _I, _V, _U64, _V, _U32, _V, _V]),
     "tcsum_host_batch_ipv4_rx_verify_multi": (_I, [_V, _I, _V, _U64, _V, _U32, _V, _V, _V]),
-    "tcsum_pcap_index": (_I, [_V, _U64, _V, _V, _U32, ctypes.POINTER(_U32)]),
     "tcsum_queue_server": (_I, [_I, _I]),
     "tcsum_call_server": (_I, [_I, _I]),
     "tcsum_plat_init": (_I, [_I]),
@@ -68,7 +67,14 @@ SIGNATURES = {
     "tcsum_probe_ipv4": (_I, [_V, _V, _U32, _U64, _I, _V, _V]),
 }
 
+# tcsum_pcap.h: the capture-file helper, libtcsum_pcap.so (host-only)
+PCAP_LIB_PATH = os.path.join(PKG, "libtcsum_pcap.so")
+PCAP_SIGNATURES = {
+    "tcsum_pcap_index": (_I, [_V, _U64, _V, _V, _U32, ctypes.POINTER(_U32)]),
+}
+
 _lib = None
+_pcap_lib = None
 
 
 def lib() -> ctypes.CDLL:
@@ -93,6 +99,21 @@ def lib() -> ctypes.CDLL:
             f.argtypes = args
         _lib = L
     return _lib
+
+
+def pcap_lib() -> ctypes.CDLL:
+    """The capture-file helper library (include/tcsum_pcap.h)."""
+    global _pcap_lib
+    if _pcap_lib is None:
+        if not os.path.exists(PCAP_LIB_PATH):
+            raise RuntimeError(f"{PCAP_LIB_PATH} is missing: build it with __graft_entry__.build()")
+        L = ctypes.CDLL(PCAP_LIB_PATH)
+        for name, (res, args) in PCAP_SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _pcap_lib = L
+    return _pcap_lib
 
 
 def check(rc: int, what: str) -> None:

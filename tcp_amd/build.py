@@ -19,10 +19,14 @@ INCLUDE = os.path.join(ROOT, "include")
 LIB = os.path.join(PKG, "libtcsum.so")
 ARCH = "gfx950"
 
-SOURCES = [os.path.join(CSRC, "csum_kernels.hip"), os.path.join(CSRC, "csum_api.cpp"),
-           os.path.join(CSRC, "pcap_index.cpp")]
+SOURCES = [os.path.join(CSRC, "csum_kernels.hip"), os.path.join(CSRC, "csum_api.cpp")]
 HEADERS = [os.path.join(CSRC, "csum_launch.h")] + [
     os.path.join(INCLUDE, h) for h in ("tcsum.h", "tcsum_legacy.h", "tcsum_synth.h")]
+# The capture-file helper (include/tcsum_pcap.h): host-only C++, a library of
+# its own -- not part of the checksum path, so not in libtcsum.so.
+PCAP_LIB = os.path.join(PKG, "libtcsum_pcap.so")
+PCAP_SOURCES = [os.path.join(CSRC, "pcap_index.cpp")]
+PCAP_HEADERS = [os.path.join(INCLUDE, h) for h in ("tcsum.h", "tcsum_pcap.h")]
 
 
 def hipcc() -> str:
@@ -32,11 +36,15 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found: the gfx950 library cannot be built")
 
 
-def stale() -> bool:
-    if not os.path.exists(LIB):
+def _stale(lib: str, deps) -> bool:
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS + [__file__])
+    t = os.path.getmtime(lib)
+    return any(os.path.getmtime(p) > t for p in list(deps) + [__file__])
+
+
+def stale() -> bool:
+    return _stale(LIB, SOURCES + HEADERS) or _stale(PCAP_LIB, PCAP_SOURCES + PCAP_HEADERS)
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -51,10 +59,20 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
 
 def _build_locked(verbose: bool) -> str:
+    if _stale(PCAP_LIB, PCAP_SOURCES + PCAP_HEADERS) or not os.path.exists(PCAP_LIB):
+        tmp = PCAP_LIB + ".tmp"
+        cmd = [os.environ.get("CXX", "g++"), "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall",
+               f"-I{INCLUDE}", PCAP_SOURCES[0], "-o", tmp]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        os.replace(tmp, PCAP_LIB)
+    if not _stale(LIB, SOURCES + HEADERS):
+        return LIB
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}",
-           "-x", "hip", SOURCES[0], "-x", "hip", SOURCES[1], "-x", "hip", SOURCES[2], "-o", tmp]
+           "-x", "hip", SOURCES[0], "-x", "hip", SOURCES[1], "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

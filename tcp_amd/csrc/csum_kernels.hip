@@ -1727,6 +1727,7 @@ static hipError_t seg_u(int G, int U, int persist, uint32_t xg, uint32_t n, cons
     }
             TCSUM_WGX(4, 0, 16) TCSUM_WGX(8, 0, 8) TCSUM_WGX(16, 0, 4) TCSUM_WGX(4, 16, 16) TCSUM_WGX(8, 16, 8)
             TCSUM_WGX(16, 16, 4) TCSUM_WGX(16, 16, 6) TCSUM_WGX(8, 64, 8) TCSUM_WGX(16, 64, 4)
+            TCSUM_WGX(4, 16, 6) TCSUM_WGX(4, 16, 8) TCSUM_WGX(4, 0, 8) TCSUM_WGX(4, 0, 4)
 #undef TCSUM_WGX
             return hipErrorInvalidValue;
         }

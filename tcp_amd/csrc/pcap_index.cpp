@@ -18,7 +18,7 @@
 #include <thread>
 #include <vector>
 
-#include "tcsum.h"
+#include "tcsum_pcap.h"
 
 namespace {
 

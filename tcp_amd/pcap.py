@@ -1,6 +1,6 @@
 """Capture files on the rx path: a libpcap savefile's bytes are the arena.
 
-`index` wraps tcsum_pcap_index (include/tcsum.h): one descriptor per record,
+`index` wraps tcsum_pcap_index (include/tcsum_pcap.h, libtcsum_pcap.so): one descriptor per record,
 pointing at the record's IPv4 packet inside the file, plus what the stack's
 rx front end does with the frame before ipv4_in (plat/netif_pcap.c:9-38,
 net/src/ether.c:14-25,62-101).  `rx_verify` then runs the batched rx gates
@@ -29,7 +29,7 @@ def index(buf):
     memory (bytes, mmap, or a u8 numpy array); raises on a file that is not
     one, or that ends inside a record."""
     a = _as_u8(buf)
-    L = _lib.lib()
+    L = _lib.pcap_lib()
     n = ctypes.c_uint32(0)
     rc = L.tcsum_pcap_index(a.ctypes.data, a.nbytes, None, None, 0, ctypes.byref(n))
     if rc not in (_lib.OK, _lib.ERR_MEM):

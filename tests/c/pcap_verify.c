@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include "tcsum.h"
+#include "tcsum_pcap.h"
 
 int main(int argc, char **argv)
 {

@@ -18,9 +18,9 @@ def libpath():
     return build.build()
 
 
-def declared_functions():
+def declared_functions(headers=HEADERS):
     names = set()
-    for h in HEADERS:
+    for h in headers:
         text = open(os.path.join(ROOT, "include", h)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         text = re.sub(r"//[^\n]*", "", text)
@@ -52,6 +52,23 @@ def test_binding_table_matches_headers(libpath):
     L = _lib.lib()  # loads libamdhip64 too; no device is touched
     for name in _lib.SIGNATURES:
         assert getattr(L, name)
+
+
+def test_capture_helper_is_a_library_of_its_own(libpath):
+    """tcsum_pcap.h (capture files, not the checksum path) is exported by
+    libtcsum_pcap.so, which has no GPU code, and not by the product library."""
+    from tcp_amd import _lib
+    names = declared_functions(["tcsum_pcap.h"])
+    assert names == set(_lib.PCAP_SIGNATURES) == {"tcsum_pcap_index"}
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.PCAP_LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    assert names <= {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    prod = subprocess.run(["nm", "-D", "--defined-only", libpath], capture_output=True, text=True,
+                          check=True).stdout
+    assert "tcsum_pcap_index" not in prod
+    deps = subprocess.run(["ldd", _lib.PCAP_LIB_PATH], capture_output=True, text=True).stdout
+    assert "amdhip" not in deps and "libtcsum.so" not in deps
+    assert getattr(_lib.pcap_lib(), "tcsum_pcap_index")
 
 
 def test_descriptor_layouts():

@@ -77,7 +77,7 @@ def test_truncated_records_are_the_captured_bytes(pcap):
 def test_file_level_errors(pcap):
     import ctypes
     from tcp_amd import _lib
-    L = _lib.lib()
+    L = _lib.pcap_lib()
     body = bytes(range(64))
     buf, offs, _ = PB.build([body] * 5, PB.ETHER)
     n = ctypes.c_uint32(0)
@@ -141,7 +141,7 @@ def test_parallel_walk_equals_sequential(pcap, monkeypatch, seed):
             monkeypatch.delenv("TCSUM_PCAP_PIECE_KB", raising=False)
         pk = np.zeros(n, PKT_DTYPE)
         got = ctypes.c_uint32(0)
-        rc = _lib.lib().tcsum_pcap_index(buf[:cut], cut, pk.ctypes.data, None, n, ctypes.byref(got))
+        rc = _lib.pcap_lib().tcsum_pcap_index(buf[:cut], cut, pk.ctypes.data, None, n, ctypes.byref(got))
         assert rc == SIZE and got.value == n // 2
         np.testing.assert_array_equal(pk[: n // 2], one[0][: n // 2])
 
@@ -268,7 +268,7 @@ def test_pcapng_interfaces_sections_fcs(pcap):
 def test_pcapng_errors(pcap):
     import ctypes
     from tcp_amd import _lib, PKT_DTYPE
-    L = _lib.lib()
+    L = _lib.pcap_lib()
     body = bytes(range(64))
     buf, offs, _ = PB.build_ng([body] * 5, (PB.ETHER,), extra_blocks=False)
     pk = np.zeros(5, PKT_DTYPE)

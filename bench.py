@@ -87,6 +87,43 @@ def algorithmic_bytes(batch) -> int:
     return batch.total_bytes + per * batch.n
 
 
+# Counter bytes per byte of each access class the step kernels make, measured
+# by scripts/pmc_calib.py on MI355X (known byte counts, each class alone after
+# an L2 flush; profiles/r03/pmc_calib.json).  Keys: the class
+# kernels of scripts/pmc_calib.hip.  None until measured: pmc_traffic then
+# falls back to the guide's blanket x2 for FETCH_SIZE.
+PMC_CALIB = None
+
+
+def access_classes(batch) -> dict:
+    """Bytes one step moves per access class: (calibration class, counter) ->
+    bytes.  Every packet byte is one streaming 16-B-per-lane nontemporal read;
+    descriptors are read by lane groups; results are dense stores; the
+    deferred tx fill adds its scratch (8 B per packet written, then read by
+    k_tx_scatter with the descriptor offsets) and the scattered field writes."""
+    n = batch.n
+    c = {("k_stream<true>", "FETCH_SIZE"): batch.total_bytes}
+    if batch.kind == "peso":
+        c[("k_desc<24>", "FETCH_SIZE")] = 24 * n
+        res = "k_store_wg16" if batch.config == "tso" else "k_store_dense<unsigned short>"
+        c[(res, "WRITE_SIZE")] = 2 * n
+        return c
+    c[("k_desc<16>", "FETCH_SIZE")] = 16 * n
+    if batch.op == "sums":
+        c[("k_store_dense<unsigned int>", "WRITE_SIZE")] = 4 * n
+    elif batch.op == "rx":
+        c[("k_store_dense<unsigned char>", "WRITE_SIZE")] = n
+    elif batch.op == "txo":
+        c[("k_store_dense<unsigned int>", "WRITE_SIZE")] = 4 * n
+        c[("k_store_dense<unsigned char>", "WRITE_SIZE")] = n
+    else:  # tx, deferred: fill (values + positions) -> k_tx_scatter
+        c[("k_store_dense<unsigned long>", "WRITE_SIZE")] = 8 * n
+        c[("k_load<unsigned int, 4>", "FETCH_SIZE")] = 8 * n
+        c[("k_load<unsigned long, 16>", "FETCH_SIZE")] = 8 * n
+        c[("k_store_field<2>", "WRITE_SIZE")] = 4 * n  # IPv4 + TCP/UDP field: every synthetic packet has both
+    return c
+
+
 def launch(tc, batch, arena, descs, out, flags=None):
     if batch.kind == "peso":
         tc.batch_peso(arena, descs, batch.n, batch.total_bytes, out=out)
@@ -266,7 +303,7 @@ def pmc_traffic(config: str):
     (MI355X_MICROARCH.md §HBM) -> x2; both counters are in KiB."""
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(prof):
-        return None, "rocprofv3 not found"
+        return None, "rocprofv3 not found", None
     vals = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix=f"tcsum_pmc_{counter}_")
@@ -277,7 +314,7 @@ def pmc_traffic(config: str):
             subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
                            env=dict(os.environ, TMPDIR=d))
         except (subprocess.SubprocessError, OSError) as e:
-            return None, f"rocprofv3 {counter} pass failed: {type(e).__name__}"
+            return None, f"rocprofv3 {counter} pass failed: {type(e).__name__}", None
         files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
         keep = os.environ.get("TCSUM_PMC_KEEP")  # directory to keep the raw counter CSVs in
         if keep:
@@ -293,10 +330,25 @@ def pmc_traffic(config: str):
                         per.setdefault(name.split("(")[0], []).append(float(row["Counter_Value"]))
         shutil.rmtree(d, ignore_errors=True)
         if not per:
-            return None, f"no {counter} rows for the checksum kernel"
+            return None, f"no {counter} rows for the checksum kernel", None
         vals[counter] = sum(sorted(v)[len(v) // 2] for v in per.values())
-    traffic = vals["FETCH_SIZE"] * 1024 * 2 + vals["WRITE_SIZE"] * 1024
-    return traffic, None
+    raw = {k: v * 1024 for k, v in vals.items()}  # KiB -> bytes, as the counters report them
+    if PMC_CALIB is None:
+        traffic = raw["FETCH_SIZE"] * 2 + raw["WRITE_SIZE"]
+        return traffic, None, {"raw": raw, "method": "blanket x2 on FETCH_SIZE (uncalibrated)"}
+    # per counter: the bytes the step's classes move, scaled by how far the
+    # counter is from what those classes report on their own (calibrated)
+    from tcp_amd import workload
+    classes = access_classes(workload.make_batch(config))
+    traffic, detail = 0.0, {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        nominal = sum(b for (k, c), b in classes.items() if c == counter)
+        expect = sum(b * PMC_CALIB[k] for (k, c), b in classes.items() if c == counter)
+        ratio = raw[counter] / expect if expect else 1.0
+        traffic += nominal * ratio
+        detail[counter] = {"raw": round(raw[counter]), "expected_raw": round(expect), "nominal": nominal,
+                           "measured_vs_expected": round(ratio, 4)}
+    return traffic, None, {"per_counter": detail, "method": "per access class (scripts/pmc_calib.py)"}
 
 
 def rocprof_trace(config: str, steps: int, warmup: int, settle_ms: float):
@@ -731,10 +783,10 @@ def main():
         return
     n_gpus = max(world, 1)
 
-    traffic, pmc_note = None, "skipped"
+    traffic, pmc_note, pmc_detail = None, "skipped", None
     trace, trace_note = None, "skipped"
     if not args.pmc_child and world == 1 and not args.no_pmc:
-        traffic, pmc_note = pmc_traffic(args.config)  # before this process touches the GPU
+        traffic, pmc_note, pmc_detail = pmc_traffic(args.config)  # before this process touches the GPU
     if not args.pmc_child and world == 1 and not args.no_trace:
         trace, trace_note = rocprof_trace(args.config, args.steps, args.warmup, args.settle_ms)
 
@@ -783,6 +835,7 @@ def main():
         roof["traffic_note"] = pmc_note
     else:
         roof["traffic_vs_algorithmic"] = round(traffic / algorithmic_bytes(b), 4)
+        roof["traffic_accounting"] = pmc_detail
     if trace is None:
         roof["rocprof_frac"] = None
         roof["rocprof_note"] = trace_note

@@ -89,6 +89,18 @@ __global__ __launch_bounds__(256) void k_sparse16(const uint8_t *__restrict__ a,
     sink_it(v.x ^ v.y ^ v.z ^ v.w, sink);
 }
 
+// dense loads of T per lane (k_tx_scatter's value / position arrays), and
+// 8 B per lane at a 16-B stride (its descriptor offsets)
+template <typename T, int STRIDE>
+__global__ __launch_bounds__(256) void k_load(const uint8_t *__restrict__ a, uint32_t n, uint32_t *sink)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n)
+        return;
+    const T v = *reinterpret_cast<const T *>(a + (uint64_t)STRIDE * i);
+    sink_it((uint32_t)v ^ (uint32_t)((uint64_t)v >> 16 >> 16), sink);
+}
+
 // dense stores of T per lane (results: u8 verdicts, u16 sums, u32 pairs, 8-B scratch)
 template <typename T>
 __global__ __launch_bounds__(256) void k_store_dense(T *__restrict__ o, uint32_t n)
@@ -168,6 +180,10 @@ int main()
         flush_l2();
         hipLaunchKernelGGL(k_sparse16, dim3(pblocks), dim3(256), 0, 0, pkts, kPkts, kStride, sink);
         flush_l2();
+        hipLaunchKernelGGL((k_load<uint32_t, 4>), dim3(pblocks), dim3(256), 0, 0, dense, kPkts, sink);
+        flush_l2();
+        hipLaunchKernelGGL((k_load<uint64_t, 16>), dim3(pblocks), dim3(256), 0, 0, desc, kPkts, sink);
+        flush_l2();
         hipLaunchKernelGGL(k_store_dense<uint8_t>, dim3(pblocks), dim3(256), 0, 0, dense, kPkts);
         flush_l2();
         hipLaunchKernelGGL(k_store_dense<uint16_t>, dim3(pblocks), dim3(256), 0, 0, (uint16_t *)dense, kPkts);
@@ -190,6 +206,8 @@ int main()
     note("k_desc<24>", "24-B descriptor (16 + 8 B loads) per 16-lane group", 24.0 * kPkts, 0);
     note("k_sparse16@1500", "one default-policy 16-B chunk per packet, stride 1500", 16.0 * kPkts, 0);
     note("k_sparse16@4532", "one default-policy 16-B chunk per packet, stride 4532", 16.0 * kPkts, 0);
+    note("k_load<unsigned int, 4>", "dense u32 load per lane", 4.0 * kPkts, 0);
+    note("k_load<unsigned long, 16>", "8-B load per lane at a 16-B stride", 8.0 * kPkts, 0);
     note("k_store_dense<unsigned char>", "dense u8 per lane", 1.0 * kPkts, 1);
     note("k_store_dense<unsigned short>", "dense u16 per lane", 2.0 * kPkts, 1);
     note("k_store_dense<unsigned int>", "dense u32 per lane", 4.0 * kPkts, 1);

@@ -1714,10 +1714,10 @@ static hipError_t seg_u(int G, int U, int persist, uint32_t xg, uint32_t n, cons
     if (G == 256) { // one range per workgroup
         const dim3 grid(n);
         const uint8_t *a = static_cast<const uint8_t *>(arena);
-        // TCSUM_WGX=W,GL,U: k_segments_wgx's shapes (checksum_peso batches)
+        // TCSUM_WGX=W/GL/U: k_segments_wgx's shapes (checksum_peso batches)
         if (const char *x = MODE == MODE_PESO ? getenv("TCSUM_WGX") : nullptr) {
             int w = 0, gl = -1, u = 0;
-            if (sscanf(x, "%d,%d,%d", &w, &gl, &u) != 3)
+            if (sscanf(x, "%d%*[/x,]%d%*[/x,]%d", &w, &gl, &u) != 3)
                 return hipErrorInvalidValue;
 #define TCSUM_WGX(WW, GG, UU)                                                                                \
     if (w == WW && gl == GG && u == UU) {                                                                    \

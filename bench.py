@@ -345,10 +345,14 @@ def pmc_traffic(config: str):
     if PMC_CALIB is None:
         traffic = raw["FETCH_SIZE"] * 2 + raw["WRITE_SIZE"]
         return traffic, None, {"raw": raw, "method": "blanket x2 on FETCH_SIZE (uncalibrated)"}
-    # per counter: the bytes the step's classes move, scaled by how far the
-    # counter is from what those classes report on their own (calibrated)
     from tcp_amd import workload
-    classes = access_classes(workload.make_batch(config))
+    traffic, detail = calibrated_traffic(access_classes(workload.make_batch(config)), raw)
+    return traffic, None, {"per_counter": detail, "method": "per access class (scripts/pmc_calib.py)"}
+
+
+def calibrated_traffic(classes: dict, raw: dict):
+    """Per counter: the bytes the step's classes move, scaled by how far the
+    raw counter is from what those classes report on their own (PMC_CALIB)."""
     traffic, detail = 0.0, {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         nominal = sum(b for (k, c), b in classes.items() if c == counter)
@@ -357,7 +361,7 @@ def pmc_traffic(config: str):
         traffic += nominal * ratio
         detail[counter] = {"raw": round(raw[counter]), "expected_raw": round(expect), "nominal": nominal,
                            "measured_vs_expected": round(ratio, 4)}
-    return traffic, None, {"per_counter": detail, "method": "per access class (scripts/pmc_calib.py)"}
+    return traffic, detail
 
 
 def rocprof_trace(config: str, steps: int, warmup: int, settle_ms: float):

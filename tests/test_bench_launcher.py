@@ -85,3 +85,24 @@ def test_spawn_ranks_failing_rank_ends_the_others(tmp_path):
     assert D.spawn_ranks(2, [str(prog)]) == 3
     assert time.monotonic() - t0 < 30
     assert D.spawn_ranks(2, [str(prog)], extra_env={"RANK": "0"}, timeout=1.0) == 124  # both sleep: time-out
+
+
+def test_calibrated_traffic_accounting():
+    """bench.py's per-class counter accounting: raw counters equal to what the
+    classes report on their own give exactly the classes' bytes; 5 % more
+    FETCH_SIZE gives 5 % more read traffic; every class a config uses has a
+    calibration entry."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from tcp_amd import workload
+    for cfg in ("mtu", "tso", "mixed", "mixed_tx", "mixed_rx", "mixed_txo"):
+        cls = bench.access_classes(workload.make_batch(cfg, n=4096))
+        assert all(k in bench.PMC_CALIB for k, _ in cls)
+        exp = {c: sum(b * bench.PMC_CALIB[k] for (k, cc), b in cls.items() if cc == c)
+               for c in ("FETCH_SIZE", "WRITE_SIZE")}
+        nominal = sum(cls.values())
+        t, detail = bench.calibrated_traffic(cls, exp)
+        assert abs(t - nominal) < 1e-6 * nominal
+        t5, _ = bench.calibrated_traffic(cls, dict(exp, FETCH_SIZE=exp["FETCH_SIZE"] * 1.05))
+        reads = sum(b for (k, c), b in cls.items() if c == "FETCH_SIZE")
+        assert abs(t5 - nominal - 0.05 * reads) < 1e-6 * nominal

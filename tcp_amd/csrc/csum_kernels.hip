@@ -1728,6 +1728,8 @@ static hipError_t seg_u(int G, int U, int persist, uint32_t xg, uint32_t n, cons
             TCSUM_WGX(4, 0, 16) TCSUM_WGX(8, 0, 8) TCSUM_WGX(16, 0, 4) TCSUM_WGX(4, 16, 16) TCSUM_WGX(8, 16, 8)
             TCSUM_WGX(16, 16, 4) TCSUM_WGX(16, 16, 6) TCSUM_WGX(8, 64, 8) TCSUM_WGX(16, 64, 4)
             TCSUM_WGX(4, 16, 6) TCSUM_WGX(4, 16, 8) TCSUM_WGX(4, 0, 8) TCSUM_WGX(4, 0, 4)
+            TCSUM_WGX(16, 64, 2) TCSUM_WGX(8, 64, 4) TCSUM_WGX(4, 64, 4) TCSUM_WGX(16, 32, 4) TCSUM_WGX(16, 128, 4)
+            TCSUM_WGX(16, 256, 4) TCSUM_WGX(16, 64, 3) TCSUM_WGX(8, 64, 2)
 #undef TCSUM_WGX
             return hipErrorInvalidValue;
         }

@@ -483,7 +483,10 @@ __global__ __launch_bounds__(256) void k_segments_wg(const uint8_t *__restrict__
 // ranges take more passes.  Edges as in frame_issue: lane 0 loads the first
 // chunk and lane 1 the last with the default policy, masked; every interior
 // chunk is nontemporal and whole.
-template <int W, int GL, int U, int MODE>
+// PROBE: the same loads with the sums, the reduction and the store replaced
+// by an XOR fold into a sink (`out`) stored on a 2^-32 fluke
+// (tcsum_probe_segments for this geometry).
+template <int W, int GL, int U, int MODE, bool PROBE = false>
 __global__ __launch_bounds__(W * 64) void k_segments_wgx(const uint8_t *__restrict__ arena,
                                                          const void *__restrict__ descs, uint32_t n,
                                                          uint16_t *__restrict__ out, uint32_t aux, uint32_t xg)
@@ -513,6 +516,24 @@ __global__ __launch_bounds__(W * 64) void k_segments_wgx(const uint8_t *__restri
     for (int u = 0; u < U; ++u) {
         const uint32_t j = lane_off + u * ustep;
         v[u] = load16<true>(ib + (j < ni ? j : ilast));
+    }
+    if constexpr (PROBE) {
+        issue_fence();
+        u32x4 x = ev;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            x ^= v[u];
+        for (uint32_t b0 = CPP; b0 < ni; b0 += CPP) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t j = b0 + lane_off + u * ustep;
+                x ^= load16<true>(ib + (j < ni ? j : ilast));
+            }
+        }
+        const uint32_t f = x.x ^ x.y ^ x.z ^ x.w;
+        if (f == 0x9E3779B9u)
+            reinterpret_cast<uint32_t *>(out)[0] = f;
+        return;
     }
     uint32_t q16 = 0;
     if constexpr (MODE == MODE_PESO)
@@ -555,6 +576,161 @@ __global__ __launch_bounds__(W * 64) void k_segments_wgx(const uint8_t *__restri
         for (int w = 0; w < W; ++w)
             s += part[w]; // < 16 * 2^23
         out[seg] = finalize<MODE>(s, reinterpret_cast<uintptr_t>(p), d, aux, q16);
+    }
+}
+
+// One wave per K consecutive ranges, its 64 lanes on the K ranges' chunks
+// taken as ONE list (range 0's chunks, then range 1's, ...): load u of lane l
+// in pass p is chunk 64 * (U * p + u) + l of that list, so every load
+// instruction of the wave covers 64 consecutive chunks -- 1 KiB of contiguous
+// bytes when the ranges are packed -- and the wave's footprint is its K
+// ranges end to end: configs[2]'s fastest shape (k_segments_wgx<16, 64, 4>,
+// each wave one contiguous 4 KiB) applied to short ranges, where k_segments
+// puts 64/G separate ranges under every load instruction.  Lanes 0 and 1
+// load the list's first and last chunk with the default policy (shared with
+// the neighbouring waves' ranges in a packed arena, frame_issue's edges);
+// every other chunk is nontemporal, and a chunk two ranges of the wave share
+// is loaded by two neighbouring lanes, i.e. once.  Each lane sums a chunk into
+// the accumulator of its range; K wave reductions; lane k finalizes range k;
+// the workgroup's W * K results leave in one store (k_segments' gathered store).
+template <int W, int K, int U, int MODE>
+__global__ __launch_bounds__(W * 64) void k_segments_wv(const uint8_t *__restrict__ arena,
+                                                        const void *__restrict__ descs, uint32_t n,
+                                                        uint16_t *__restrict__ out, uint32_t aux, uint32_t xg)
+{
+    static_assert(MODE != MODE_EXACT && K >= 1 && K <= 8 && W * K <= 64, "shape");
+    constexpr uint32_t PER = W * K;
+    __shared__ uint16_t res[PER];
+    __shared__ uint32_t arrived;
+    if (threadIdx.x == 0)
+        arrived = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    const uint32_t seg0 = (blk * W + wave) * K; // no 32-bit wrap: n < 2^32, PER <= 64
+    const bool mine = lane < K && seg0 + lane < n;
+    const SegDesc d = load_desc<MODE>(descs, seg0 + (lane < K ? lane : 0u), mine); // len 0 unless mine
+    const uint8_t *p = arena + d.off;
+    const uint32_t s0 = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
+    const uint32_t nch = d.len ? (uint32_t)(((uint64_t)d.len + s0 + 15) >> 4) : 0u;
+    // the K ranges, wave-uniform: list offsets P[k], chunk counts, bases, byte ends
+    uint32_t P[K + 1], NC[K], S0[K], E[K];
+    const u32x4 *B[K];
+    P[0] = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        NC[k] = (uint32_t)__builtin_amdgcn_readlane((int)nch, k);
+        S0[k] = (uint32_t)__builtin_amdgcn_readlane((int)s0, k);
+        E[k] = (uint32_t)__builtin_amdgcn_readlane((int)(d.len + s0), k); // ranges < 4 GiB here (pick_geometry)
+        const uint64_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)reinterpret_cast<uintptr_t>(p), k);
+        const uint64_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(reinterpret_cast<uintptr_t>(p) >> 32), k);
+        B[k] = reinterpret_cast<const u32x4 *>(((hi << 32) | lo) - S0[k]);
+        P[k + 1] = P[k] + NC[k];
+    }
+    const uint32_t NCH = P[K];
+    // which range / chunk a list position is
+    auto locate = [&](uint32_t v, uint32_t &k, uint32_t &c, const u32x4 *&a) {
+        k = 0;
+#pragma unroll
+        for (int j = 1; j < K; ++j)
+            k += v >= P[j] ? 1u : 0u;
+        uint32_t pk = P[0];
+        const u32x4 *bk = B[0];
+#pragma unroll
+        for (int j = 1; j < K; ++j) {
+            pk = k == (uint32_t)j ? P[j] : pk;
+            bk = k == (uint32_t)j ? B[j] : bk;
+        }
+        c = v - pk;
+        a = bk + c;
+    };
+    // edges: lane 0 the list's first chunk, lane 1 its last, default policy
+    const uint32_t ev_v = lane == 0 ? 0u : (NCH ? NCH - 1u : 0u);
+    uint32_t ek, ec;
+    const u32x4 *ea;
+    locate(ev_v, ek, ec, ea);
+    const bool has_edge = lane < 2 && NCH > 0 && (lane == 0 || NCH >= 2);
+    const u32x4 ev = load16<false>(NCH ? ea : &g_zero_chunk);
+    // interior list positions [1, NCH - 1), nontemporal
+    const uint32_t ni = NCH > 2 ? NCH - 2 : 0u;
+    u32x4 v[U];
+    uint32_t vk[U], vc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t j = u * 64u + lane;
+        const u32x4 *a;
+        locate(1u + (j < ni ? j : (ni ? ni - 1u : 0u)), vk[u], vc[u], a);
+        v[u] = load16<true>(ni ? a : &g_zero_chunk);
+    }
+    uint32_t q16 = 0;
+    if constexpr (MODE == MODE_PESO)
+        q16 = pinned(peso_pseudo16(d));
+    issue_fence();
+    uint32_t acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        acc[k] = 0;
+    // a chunk's sum, masked to its range where the chunk is the range's first or last
+    auto add = [&](u32x4 x, uint32_t k, uint32_t c, bool on) {
+        uint32_t nc = NC[0], s0k = S0[0], ek_ = E[0];
+#pragma unroll
+        for (int j = 1; j < K; ++j) {
+            nc = k == (uint32_t)j ? NC[j] : nc;
+            s0k = k == (uint32_t)j ? S0[j] : s0k;
+            ek_ = k == (uint32_t)j ? E[j] : ek_;
+        }
+        uint32_t t;
+        if (c == 0 || c + 1 == nc) { // rare: the range's edge chunks
+            const int lo = c == 0 ? (int)s0k : 0;
+            const int hi = c + 1 == nc ? (int)(ek_ - 16u * c) : 16;
+            t = on ? chunk_sum_masked(0u, x, lo, hi) : 0u;
+        } else {
+            t = chunk_sum_w(0u, x, on ? 0x00010001u : 0u);
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            acc[j] += k == (uint32_t)j ? t : 0u;
+    };
+    add(ev, ek, ec, has_edge);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        add(v[u], vk[u], vc[u], u * 64u + lane < ni);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        acc[k] = fold_step(acc[k]);
+    for (uint32_t b0 = 64u * U; b0 < ni; b0 += 64u * U) {
+        u32x4 w[U];
+        uint32_t wk[U], wc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = b0 + u * 64u + lane;
+            const u32x4 *a;
+            locate(1u + (j < ni ? j : ni - 1u), wk[u], wc[u], a);
+            w[u] = load16<true>(a);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            add(w[u], wk[u], wc[u], b0 + u * 64u + lane < ni);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            acc[k] = fold_step(acc[k]);
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t t = group_sum<64>(acc[k]);
+        s = lane == (uint32_t)k ? t : s;
+    }
+    if (lane < K)
+        res[wave * K + lane] = finalize<MODE>(s, reinterpret_cast<uintptr_t>(p), d, aux, q16);
+    uint32_t order = 0;
+    if (lane == 0)
+        order = __hip_atomic_fetch_add(&arrived, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    order = __builtin_amdgcn_readfirstlane(order);
+    if (order == W - 1u && lane < PER) { // the last wave: every entry is in LDS
+        const uint32_t sl = blk * PER + lane;
+        if (sl < n)
+            out[sl] = res[lane];
     }
 }
 
@@ -1536,6 +1712,13 @@ hipError_t launch_probe_desc(const void *arena, const void *descs, uint32_t n, u
     const Geometry g = pick_geometry(mean_len);
     const uint32_t xg = (uint32_t)g.xcd;
     const uint8_t *a = static_cast<const uint8_t *>(arena);
+    if (g.lanes == 1024 && g.loads == 4) { // k_segments_wgx<16, 32, 4>'s loads
+        if (n >= (1u << 22))
+            return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_segments_wgx<16, 32, 4, MODE_PESO, true>), dim3(n), dim3(1024), 0, stream, a, descs, n,
+                           reinterpret_cast<uint16_t *>(sink), 0u, xg);
+        return hipGetLastError();
+    }
     const char *pe = getenv("TCSUM_PROBE_PACE");
     const uint32_t pace = pe ? (uint32_t)strtoul(pe, nullptr, 0) : 0u;
 #define TCSUM_PD(GG, UU)                                                                                     \
@@ -1649,7 +1832,14 @@ Geometry pick_geometry(uint64_t mean_len)
     Geometry g{32, 4, 0, 64};
     const uint64_t chunks = mean_len / 16 + 1;
     const uint64_t interior = chunks > 2 ? chunks - 2 : 0;
-    if (chunks >= 2048) {
+    if (chunks >= 3072) {
+        // >= 48 KiB (TSO): one range per 16-wave workgroup, 32-lane groups on
+        // 2-KiB sub-ranges, 4 loads per lane: a 64-KiB range is one pass of
+        // the workgroup -- 3.6 % faster than k_segments_wg on configs[2]
+        // (profiles/r03/ab_tso_shapes2*.txt: 2,242 against 2,326 us)
+        g.lanes = 1024;
+        g.loads = 4;
+    } else if (chunks >= 2048) {
         g.lanes = 256; // one range per workgroup (k_segments_wg): 1.8 % over G=64 on configs[2]
         g.loads = 16;
     } else if (interior > 128) {
@@ -1681,6 +1871,23 @@ template <int MODE>
 static hipError_t seg_u(int G, int U, int persist, uint32_t xg, uint32_t n, const void *arena, const void *descs,
                         uint16_t *out, uint32_t aux, hipStream_t s)
 {
+    // TCSUM_WV=W/K/U: k_segments_wv, K ranges per wave (measurement)
+    if (const char *x = getenv("TCSUM_WV")) {
+        int w = 0, k = 0, u = 0;
+        if (sscanf(x, "%d%*[/x,]%d%*[/x,]%d", &w, &k, &u) != 3)
+            return hipErrorInvalidValue;
+        const uint8_t *a = static_cast<const uint8_t *>(arena);
+#define TCSUM_WV(WW, KK, UU)                                                                                 \
+    if (w == WW && k == KK && u == UU) {                                                                     \
+        hipLaunchKernelGGL((k_segments_wv<WW, KK, UU, MODE>), dim3((n + WW * KK - 1) / (WW * KK)), dim3(WW * 64), 0, \
+                           s, a, descs, n, out, aux, xg);                                                    \
+        return hipGetLastError();                                                                            \
+    }
+        TCSUM_WV(4, 4, 6) TCSUM_WV(4, 2, 3) TCSUM_WV(4, 1, 2) TCSUM_WV(16, 4, 6) TCSUM_WV(16, 2, 3) TCSUM_WV(16, 1, 2)
+        TCSUM_WV(8, 4, 6) TCSUM_WV(4, 8, 12) TCSUM_WV(4, 3, 5)
+#undef TCSUM_WV
+        return hipErrorInvalidValue;
+    }
 #define TCSUM_SEG(GG, UU)                                                                            \
     if (G == GG && U == UU) {                                                                      \
         const uint32_t per_block = 256u / GG;                                                      \
@@ -1711,6 +1918,13 @@ static hipError_t seg_u(int G, int U, int persist, uint32_t xg, uint32_t n, cons
     TCSUM_SEG_U(64)
 #undef TCSUM_SEG_U
 #undef TCSUM_SEG
+    if (G == 1024) { // one range per 16-wave workgroup, 2 KiB sub-ranges (TSO)
+        if (U != 4)
+            return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_segments_wgx<16, 32, 4, MODE>), dim3(n), dim3(1024), 0, s,
+                           static_cast<const uint8_t *>(arena), descs, n, out, aux, xg);
+        return hipGetLastError();
+    }
     if (G == 256) { // one range per workgroup
         const dim3 grid(n);
         const uint8_t *a = static_cast<const uint8_t *>(arena);
@@ -1756,7 +1970,11 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
         return hipSuccess;
     {
         const uint32_t lanes = mode == MODE_EXACT ? 64u : (uint32_t)g.lanes;
-        const uint64_t per_launch = kMaxBlocks * (256u / (lanes ? lanes : 64u));
+        // ranges per launch: 2^32 - 1 work-items (256 / G ranges per 256-thread
+        // block; one range per block of 256 or 1024 threads)
+        const uint64_t per_launch = lanes >= 1024 ? (1ull << 22) - 1
+                                    : lanes >= 256 ? kMaxBlocks
+                                                   : kMaxBlocks * (256u / (lanes ? lanes : 64u));
         if (n > per_launch) {
             const size_t dsz = mode == MODE_PESO ? sizeof(tcsum_peso_t) : sizeof(tcsum_seg_t);
             for (uint64_t i0 = 0; i0 < n; i0 += per_launch) {

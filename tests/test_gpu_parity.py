@@ -18,7 +18,8 @@ import golden_io as G
 pytestmark = pytest.mark.gpu
 
 GEOMS_SEG = [(g, u, p) for g in (4, 8, 16, 32, 64) for u in (1, 3, 4, 16) for p in (0, 1, 2)] + \
-    [(256, u, 0) for u in (4, 8, 16)]  # one range per workgroup (k_segments_wg)
+    [(256, u, 0) for u in (4, 8, 16)] + \
+    [(1024, 4, 0)]  # one range per workgroup: k_segments_wg; k_segments_wgx<16, 32, 4> (TSO)
 GEOMS_IP = [(g, u) for g in (16, 32, 64) for u in (1, 2, 3, 4, 6, 8, 16)]
 
 
@@ -1057,7 +1058,7 @@ def test_measurement_probes_leave_arena_and_sink_alone(torch, tc, config):
     assert torch.equal(arena, before)
 
 
-@pytest.mark.parametrize("g,u", [(4, 1), (8, 4), (16, 6), (32, 6), (64, 16), (256, 16)])
+@pytest.mark.parametrize("g,u", [(4, 1), (8, 4), (16, 6), (32, 6), (64, 16), (256, 16), (1024, 4)])
 def test_ragged_batch_sizes_write_only_their_results(tc, torch, oracle, geometry, g, u):
     """Batch sizes that leave the last workgroup partly empty (k_segments
     stores a workgroup's results from its last wave, k_ipv4 per packet): every

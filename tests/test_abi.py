@@ -109,11 +109,13 @@ def test_geometry_choice(libpath):
     from tcp_amd import pick_geometry
     assert pick_geometry(1500) == (16, 6)
     assert pick_geometry(4500) == (32, 6)
-    assert pick_geometry(65536) == (256, 16)
+    assert pick_geometry(40000) == (256, 16)
+    assert pick_geometry(65536) == (1024, 4)
     assert pick_geometry(64) == (4, 1)
     for n in range(0, 70000, 37):  # every choice is an instantiated kernel
         g, u = pick_geometry(n)
-        assert (g in (4, 8, 16, 32, 64) and u in (1, 2, 3, 4, 6, 8, 16)) or (g == 256 and u in (4, 8, 16))
+        assert (g in (4, 8, 16, 32, 64) and u in (1, 2, 3, 4, 6, 8, 16)) or (g == 256 and u in (4, 8, 16)) \
+            or (g, u) == (1024, 4)
 
 
 def test_device_count_without_gpu(libpath):

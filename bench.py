@@ -114,8 +114,10 @@ def access_classes(batch) -> dict:
     c = {("k_stream<true>", "FETCH_SIZE"): batch.total_bytes}
     if batch.kind == "peso":
         c[("k_desc<24>", "FETCH_SIZE")] = 24 * n
-        res = "k_store_wg16" if batch.config == "tso" else "k_store_dense<unsigned short>"
-        c[(res, "WRITE_SIZE")] = 2 * n
+        # one u16 per range; consecutive ranges' workgroups share an XCD (xcd_block), so
+        # their results merge in its L2 like a dense store (k_store_wg16's 16 B per
+        # store is the round-robin case)
+        c[("k_store_dense<unsigned short>", "WRITE_SIZE")] = 2 * n
         return c
     c[("k_desc<16>", "FETCH_SIZE")] = 16 * n
     if batch.op == "sums":

@@ -579,161 +579,6 @@ __global__ __launch_bounds__(W * 64) void k_segments_wgx(const uint8_t *__restri
     }
 }
 
-// One wave per K consecutive ranges, its 64 lanes on the K ranges' chunks
-// taken as ONE list (range 0's chunks, then range 1's, ...): load u of lane l
-// in pass p is chunk 64 * (U * p + u) + l of that list, so every load
-// instruction of the wave covers 64 consecutive chunks -- 1 KiB of contiguous
-// bytes when the ranges are packed -- and the wave's footprint is its K
-// ranges end to end: configs[2]'s fastest shape (k_segments_wgx<16, 64, 4>,
-// each wave one contiguous 4 KiB) applied to short ranges, where k_segments
-// puts 64/G separate ranges under every load instruction.  Lanes 0 and 1
-// load the list's first and last chunk with the default policy (shared with
-// the neighbouring waves' ranges in a packed arena, frame_issue's edges);
-// every other chunk is nontemporal, and a chunk two ranges of the wave share
-// is loaded by two neighbouring lanes, i.e. once.  Each lane sums a chunk into
-// the accumulator of its range; K wave reductions; lane k finalizes range k;
-// the workgroup's W * K results leave in one store (k_segments' gathered store).
-template <int W, int K, int U, int MODE>
-__global__ __launch_bounds__(W * 64) void k_segments_wv(const uint8_t *__restrict__ arena,
-                                                        const void *__restrict__ descs, uint32_t n,
-                                                        uint16_t *__restrict__ out, uint32_t aux, uint32_t xg)
-{
-    static_assert(MODE != MODE_EXACT && K >= 1 && K <= 8 && W * K <= 64, "shape");
-    constexpr uint32_t PER = W * K;
-    __shared__ uint16_t res[PER];
-    __shared__ uint32_t arrived;
-    if (threadIdx.x == 0)
-        arrived = 0;
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
-    const uint32_t seg0 = (blk * W + wave) * K; // no 32-bit wrap: n < 2^32, PER <= 64
-    const bool mine = lane < K && seg0 + lane < n;
-    const SegDesc d = load_desc<MODE>(descs, seg0 + (lane < K ? lane : 0u), mine); // len 0 unless mine
-    const uint8_t *p = arena + d.off;
-    const uint32_t s0 = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
-    const uint32_t nch = d.len ? (uint32_t)(((uint64_t)d.len + s0 + 15) >> 4) : 0u;
-    // the K ranges, wave-uniform: list offsets P[k], chunk counts, bases, byte ends
-    uint32_t P[K + 1], NC[K], S0[K], E[K];
-    const u32x4 *B[K];
-    P[0] = 0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        NC[k] = (uint32_t)__builtin_amdgcn_readlane((int)nch, k);
-        S0[k] = (uint32_t)__builtin_amdgcn_readlane((int)s0, k);
-        E[k] = (uint32_t)__builtin_amdgcn_readlane((int)(d.len + s0), k); // ranges < 4 GiB here (pick_geometry)
-        const uint64_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)reinterpret_cast<uintptr_t>(p), k);
-        const uint64_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(reinterpret_cast<uintptr_t>(p) >> 32), k);
-        B[k] = reinterpret_cast<const u32x4 *>(((hi << 32) | lo) - S0[k]);
-        P[k + 1] = P[k] + NC[k];
-    }
-    const uint32_t NCH = P[K];
-    // which range / chunk a list position is
-    auto locate = [&](uint32_t v, uint32_t &k, uint32_t &c, const u32x4 *&a) {
-        k = 0;
-#pragma unroll
-        for (int j = 1; j < K; ++j)
-            k += v >= P[j] ? 1u : 0u;
-        uint32_t pk = P[0];
-        const u32x4 *bk = B[0];
-#pragma unroll
-        for (int j = 1; j < K; ++j) {
-            pk = k == (uint32_t)j ? P[j] : pk;
-            bk = k == (uint32_t)j ? B[j] : bk;
-        }
-        c = v - pk;
-        a = bk + c;
-    };
-    // edges: lane 0 the list's first chunk, lane 1 its last, default policy
-    const uint32_t ev_v = lane == 0 ? 0u : (NCH ? NCH - 1u : 0u);
-    uint32_t ek, ec;
-    const u32x4 *ea;
-    locate(ev_v, ek, ec, ea);
-    const bool has_edge = lane < 2 && NCH > 0 && (lane == 0 || NCH >= 2);
-    const u32x4 ev = load16<false>(NCH ? ea : &g_zero_chunk);
-    // interior list positions [1, NCH - 1), nontemporal
-    const uint32_t ni = NCH > 2 ? NCH - 2 : 0u;
-    u32x4 v[U];
-    uint32_t vk[U], vc[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint32_t j = u * 64u + lane;
-        const u32x4 *a;
-        locate(1u + (j < ni ? j : (ni ? ni - 1u : 0u)), vk[u], vc[u], a);
-        v[u] = load16<true>(ni ? a : &g_zero_chunk);
-    }
-    uint32_t q16 = 0;
-    if constexpr (MODE == MODE_PESO)
-        q16 = pinned(peso_pseudo16(d));
-    issue_fence();
-    uint32_t acc[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        acc[k] = 0;
-    // a chunk's sum, masked to its range where the chunk is the range's first or last
-    auto add = [&](u32x4 x, uint32_t k, uint32_t c, bool on) {
-        uint32_t nc = NC[0], s0k = S0[0], ek_ = E[0];
-#pragma unroll
-        for (int j = 1; j < K; ++j) {
-            nc = k == (uint32_t)j ? NC[j] : nc;
-            s0k = k == (uint32_t)j ? S0[j] : s0k;
-            ek_ = k == (uint32_t)j ? E[j] : ek_;
-        }
-        uint32_t t;
-        if (c == 0 || c + 1 == nc) { // rare: the range's edge chunks
-            const int lo = c == 0 ? (int)s0k : 0;
-            const int hi = c + 1 == nc ? (int)(ek_ - 16u * c) : 16;
-            t = on ? chunk_sum_masked(0u, x, lo, hi) : 0u;
-        } else {
-            t = chunk_sum_w(0u, x, on ? 0x00010001u : 0u);
-        }
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-            acc[j] += k == (uint32_t)j ? t : 0u;
-    };
-    add(ev, ek, ec, has_edge);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-        add(v[u], vk[u], vc[u], u * 64u + lane < ni);
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        acc[k] = fold_step(acc[k]);
-    for (uint32_t b0 = 64u * U; b0 < ni; b0 += 64u * U) {
-        u32x4 w[U];
-        uint32_t wk[U], wc[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t j = b0 + u * 64u + lane;
-            const u32x4 *a;
-            locate(1u + (j < ni ? j : ni - 1u), wk[u], wc[u], a);
-            w[u] = load16<true>(a);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            add(w[u], wk[u], wc[u], b0 + u * 64u + lane < ni);
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            acc[k] = fold_step(acc[k]);
-    }
-    uint32_t s = 0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint32_t t = group_sum<64>(acc[k]);
-        s = lane == (uint32_t)k ? t : s;
-    }
-    if (lane < K)
-        res[wave * K + lane] = finalize<MODE>(s, reinterpret_cast<uintptr_t>(p), d, aux, q16);
-    uint32_t order = 0;
-    if (lane == 0)
-        order = __hip_atomic_fetch_add(&arrived, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-    order = __builtin_amdgcn_readfirstlane(order);
-    if (order == W - 1u && lane < PER) { // the last wave: every entry is in LDS
-        const uint32_t sl = blk * PER + lane;
-        if (sl < n)
-            out[sl] = res[lane];
-    }
-}
-
 // Persistent form: a resident grid walks the batch; each wave prefetches its
 // next descriptor while the current packets' bytes are in flight, so the
 // descriptor -> data dependence costs one latency per wave, not per packet.
@@ -1871,23 +1716,6 @@ template <int MODE>
 static hipError_t seg_u(int G, int U, int persist, uint32_t xg, uint32_t n, const void *arena, const void *descs,
                         uint16_t *out, uint32_t aux, hipStream_t s)
 {
-    // TCSUM_WV=W/K/U: k_segments_wv, K ranges per wave (measurement)
-    if (const char *x = getenv("TCSUM_WV")) {
-        int w = 0, k = 0, u = 0;
-        if (sscanf(x, "%d%*[/x,]%d%*[/x,]%d", &w, &k, &u) != 3)
-            return hipErrorInvalidValue;
-        const uint8_t *a = static_cast<const uint8_t *>(arena);
-#define TCSUM_WV(WW, KK, UU)                                                                                 \
-    if (w == WW && k == KK && u == UU) {                                                                     \
-        hipLaunchKernelGGL((k_segments_wv<WW, KK, UU, MODE>), dim3((n + WW * KK - 1) / (WW * KK)), dim3(WW * 64), 0, \
-                           s, a, descs, n, out, aux, xg);                                                    \
-        return hipGetLastError();                                                                            \
-    }
-        TCSUM_WV(4, 4, 6) TCSUM_WV(4, 2, 3) TCSUM_WV(4, 1, 2) TCSUM_WV(16, 4, 6) TCSUM_WV(16, 2, 3) TCSUM_WV(16, 1, 2)
-        TCSUM_WV(8, 4, 6) TCSUM_WV(4, 8, 12) TCSUM_WV(4, 3, 5)
-#undef TCSUM_WV
-        return hipErrorInvalidValue;
-    }
 #define TCSUM_SEG(GG, UU)                                                                            \
     if (G == GG && U == UU) {                                                                      \
         const uint32_t per_block = 256u / GG;                                                      \

@@ -1048,7 +1048,8 @@ def test_measurement_probes_leave_arena_and_sink_alone(torch, tc, config):
     sink = torch.zeros(1, dtype=torch.uint32, device=arena.device)
     tc.probe_read(arena, b.arena_bytes, sink)
     g, u = tc.pick_geometry(b.total_bytes // b.n)
-    tc.probe_tile(arena, b.arena_bytes, g, u, sink)
+    if g <= 256:  # the tile probe has the <= 256-lane shapes (bench.py skips it otherwise)
+        tc.probe_tile(arena, b.arena_bytes, g, u, sink)
     if b.kind == "peso":
         tc.probe_segments(arena, descs, b.n, b.total_bytes, sink)
     else:

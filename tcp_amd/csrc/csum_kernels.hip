@@ -407,13 +407,13 @@ __device__ __forceinline__ uint16_t finalize(uint32_t acc, uintptr_t start, cons
 // headline ran 1.1 % slower -- as slow as its loads plus the stores' tail in
 // every wave; with the gathered store it matches the same kernel with no
 // store at all (profiles/r02/ab_store.txt).  A nontemporal store cost 4 %.
-template <int G, int U, int MODE>
-__global__ __launch_bounds__(256) void k_segments(const uint8_t *__restrict__ arena,
-                                                  const void *__restrict__ descs, uint32_t n,
-                                                  uint16_t *__restrict__ out, uint32_t aux, uint32_t xg)
+template <int G, int U, int MODE, int T = 256>
+__global__ __launch_bounds__(T) void k_segments(const uint8_t *__restrict__ arena,
+                                                const void *__restrict__ descs, uint32_t n,
+                                                uint16_t *__restrict__ out, uint32_t aux, uint32_t xg)
 {
-    static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G");
-    constexpr uint32_t PER = 256u / G; // ranges per workgroup
+    static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0 && (T == 256 || T == 1024) && T / G <= 64, "G, T");
+    constexpr uint32_t PER = T / G; // ranges per workgroup
     __shared__ uint16_t res[PER];
     __shared__ uint32_t arrived;
     if (threadIdx.x == 0)
@@ -436,7 +436,7 @@ __global__ __launch_bounds__(256) void k_segments(const uint8_t *__restrict__ ar
     if ((threadIdx.x & 63u) == 0) // release: this wave's res[] entries before the count
         order = __hip_atomic_fetch_add(&arrived, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
     order = __builtin_amdgcn_readfirstlane(order);
-    if (order == 3u) { // the last wave: every entry is in LDS
+    if (order == T / 64u - 1u) { // the last wave: every entry is in LDS
         const uint32_t l = threadIdx.x & 63u;
         const uint32_t sl = blk * PER + l;
         if (l < PER && sl < n)
@@ -1716,6 +1716,19 @@ template <int MODE>
 static hipError_t seg_u(int G, int U, int persist, uint32_t xg, uint32_t n, const void *arena, const void *descs,
                         uint16_t *out, uint32_t aux, hipStream_t s)
 {
+    // TCSUM_WG1024=1: k_segments with 16-wave workgroups (measurement)
+    if (const char *x = getenv("TCSUM_WG1024"); x && atoi(x) && persist == 0) {
+        const uint8_t *a = static_cast<const uint8_t *>(arena);
+#define TCSUM_SEG1K(GG, UU)                                                                                  \
+    if (G == GG && U == UU) {                                                                                \
+        hipLaunchKernelGGL((k_segments<GG, UU, MODE, 1024>), dim3((n + 1024 / GG - 1) / (1024 / GG)), dim3(1024), 0, s, \
+                           a, descs, n, out, aux, xg);                                                       \
+        return hipGetLastError();                                                                            \
+    }
+        TCSUM_SEG1K(16, 6) TCSUM_SEG1K(32, 6) TCSUM_SEG1K(16, 4) TCSUM_SEG1K(32, 4)
+#undef TCSUM_SEG1K
+        return hipErrorInvalidValue;
+    }
 #define TCSUM_SEG(GG, UU)                                                                            \
     if (G == GG && U == UU) {                                                                      \
         const uint32_t per_block = 256u / GG;                                                      \

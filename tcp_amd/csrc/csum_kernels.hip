@@ -1015,14 +1015,14 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     }
 }
 
-template <int G, int U, int IPM>
-__global__ __launch_bounds__(256) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
-                                              uint32_t n, uint32_t *__restrict__ out,
-                                              uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
-                                              uint32_t opts, uint32_t xg)
+template <int G, int U, int IPM, int T = 256>
+__global__ __launch_bounds__(T) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
+                                            uint32_t n, uint32_t *__restrict__ out,
+                                            uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
+                                            uint32_t opts, uint32_t xg)
 {
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
-    ipv4_packet<G, U, IPM>(arena, pkts, blk * (256u / G) + threadIdx.x / G, n, out, flags_out, verdict_out,
+    ipv4_packet<G, U, IPM>(arena, pkts, blk * (uint32_t)(T / G) + threadIdx.x / G, n, out, flags_out, verdict_out,
                            opts); // no 32-bit wrap for any n
 }
 
@@ -1843,6 +1843,19 @@ static hipError_t ipv4_u(int G, int U, dim3 grid, uint8_t *arena, const tcsum_pk
                          uint32_t *out, uint8_t *flags, int8_t *verdict, uint32_t opts, uint32_t xg,
                          hipStream_t s)
 {
+    // TCSUM_WG1024=1: 16-wave workgroups (measurement)
+    if (const char *x = getenv("TCSUM_WG1024"); x && atoi(x)) {
+        const dim3 g1k((n + 1024u / G - 1) / (1024u / G));
+#define TCSUM_IP1K(GG, UU)                                                                                   \
+    if (G == GG && U == UU) {                                                                                \
+        hipLaunchKernelGGL((k_ipv4<GG, UU, IPM, 1024>), g1k, dim3(1024), 0, s, arena, pkts, n, out, flags, verdict, \
+                           opts, xg);                                                                        \
+        return hipGetLastError();                                                                            \
+    }
+        TCSUM_IP1K(16, 6) TCSUM_IP1K(32, 6)
+#undef TCSUM_IP1K
+        return hipErrorInvalidValue;
+    }
 #define TCSUM_IP(GG, UU)                                                                             \
     if (G == GG && U == UU) {                                                                      \
         hipLaunchKernelGGL((k_ipv4<GG, UU, IPM>), grid, dim3(256), 0, s, arena, pkts, n, out, flags, \

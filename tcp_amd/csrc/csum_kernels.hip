@@ -1716,19 +1716,6 @@ template <int MODE>
 static hipError_t seg_u(int G, int U, int persist, uint32_t xg, uint32_t n, const void *arena, const void *descs,
                         uint16_t *out, uint32_t aux, hipStream_t s)
 {
-    // TCSUM_WG1024=1: k_segments with 16-wave workgroups (measurement)
-    if (const char *x = getenv("TCSUM_WG1024"); x && atoi(x) && persist == 0) {
-        const uint8_t *a = static_cast<const uint8_t *>(arena);
-#define TCSUM_SEG1K(GG, UU)                                                                                  \
-    if (G == GG && U == UU) {                                                                                \
-        hipLaunchKernelGGL((k_segments<GG, UU, MODE, 1024>), dim3((n + 1024 / GG - 1) / (1024 / GG)), dim3(1024), 0, s, \
-                           a, descs, n, out, aux, xg);                                                       \
-        return hipGetLastError();                                                                            \
-    }
-        TCSUM_SEG1K(16, 6) TCSUM_SEG1K(32, 6) TCSUM_SEG1K(16, 4) TCSUM_SEG1K(32, 4)
-#undef TCSUM_SEG1K
-        return hipErrorInvalidValue;
-    }
 #define TCSUM_SEG(GG, UU)                                                                            \
     if (G == GG && U == UU) {                                                                      \
         const uint32_t per_block = 256u / GG;                                                      \
@@ -1843,19 +1830,6 @@ static hipError_t ipv4_u(int G, int U, dim3 grid, uint8_t *arena, const tcsum_pk
                          uint32_t *out, uint8_t *flags, int8_t *verdict, uint32_t opts, uint32_t xg,
                          hipStream_t s)
 {
-    // TCSUM_WG1024=1: 16-wave workgroups (measurement)
-    if (const char *x = getenv("TCSUM_WG1024"); x && atoi(x)) {
-        const dim3 g1k((n + 1024u / G - 1) / (1024u / G));
-#define TCSUM_IP1K(GG, UU)                                                                                   \
-    if (G == GG && U == UU) {                                                                                \
-        hipLaunchKernelGGL((k_ipv4<GG, UU, IPM, 1024>), g1k, dim3(1024), 0, s, arena, pkts, n, out, flags, verdict, \
-                           opts, xg);                                                                        \
-        return hipGetLastError();                                                                            \
-    }
-        TCSUM_IP1K(16, 6) TCSUM_IP1K(32, 6)
-#undef TCSUM_IP1K
-        return hipErrorInvalidValue;
-    }
 #define TCSUM_IP(GG, UU)                                                                             \
     if (G == GG && U == UU) {                                                                      \
         hipLaunchKernelGGL((k_ipv4<GG, UU, IPM>), grid, dim3(256), 0, s, arena, pkts, n, out, flags, \

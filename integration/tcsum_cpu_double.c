@@ -56,8 +56,12 @@ uint16_t checksum16(int offset, void *buf, uint16_t len, uint32_t pre_sum, int c
 
 uint16_t pktbuf_checksum16(pktbuf_t *buf, int len, int pre_sum, int complement)
 {
-    if (len < 0 || buf->total_size - buf->pos < len)
+    if (buf->total_size - buf->pos < len)
         return 0; /* pktbuf.c:650-655 */
+    if (len <= 0) { /* no block is walked: the u16 pre_sum, complemented or not (pktbuf.c:657-669) */
+        const uint16_t s = (uint16_t)pre_sum;
+        return complement ? (uint16_t)~s : s;
+    }
     uint8_t *tmp = (uint8_t *)malloc(len ? (size_t)len : 1u);
     if (!tmp || (len && pktbuf_read(buf, tmp, len) != NET_ERR_OK)) {
         free(tmp);

@@ -106,3 +106,23 @@ def test_calibrated_traffic_accounting():
         t5, _ = bench.calibrated_traffic(cls, dict(exp, FETCH_SIZE=exp["FETCH_SIZE"] * 1.05))
         reads = sum(b for (k, c), b in cls.items() if c == "FETCH_SIZE")
         assert abs(t5 - nominal - 0.05 * reads) < 1e-6 * nominal
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [4, 8])
+def test_launcher_rehearsal_many_ranks(world):
+    """configs[4]'s layout (8 ranks, one per GPU) rehearsed on CPU: every rank
+    times its own consecutive slice of the one global stream, rank 0 alone
+    prints, the devices are distinct and every self-check is clean."""
+    r = run(["--gpus", str(world), "--cpu-rehearsal", "--steps", "2", "--warmup", "1"], timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == world and len(line["devices"]) == world
+    assert len({d["uuid"] for d in line["devices"]}) == world
+    ranks = sorted(line["ranks"], key=lambda x: x["rank"])
+    assert [x["rank"] for x in ranks] == list(range(world))
+    for a, b in zip(ranks, ranks[1:]):
+        assert b["byte_base"] >= a["byte_base"] + a["payload_bytes"]
+    assert line["self_check"]["mismatches"] == 0

@@ -412,7 +412,8 @@ __global__ __launch_bounds__(T) void k_segments(const uint8_t *__restrict__ aren
                                                 const void *__restrict__ descs, uint32_t n,
                                                 uint16_t *__restrict__ out, uint32_t aux, uint32_t xg)
 {
-    static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0 && (T == 256 || T == 1024) && T / G <= 64, "G, T");
+    static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0 && T >= 64 && T <= 1024 && T % 64 == 0 && T / G <= 64,
+                  "G, T");
     constexpr uint32_t PER = T / G; // ranges per workgroup
     __shared__ uint16_t res[PER];
     __shared__ uint32_t arrived;
@@ -1716,6 +1717,19 @@ template <int MODE>
 static hipError_t seg_u(int G, int U, int persist, uint32_t xg, uint32_t n, const void *arena, const void *descs,
                         uint16_t *out, uint32_t aux, hipStream_t s)
 {
+    // TCSUM_WGT=T: the headline geometry with T-thread workgroups (measurement)
+    if (const char *x = getenv("TCSUM_WGT"); x && G == 16 && U == 6 && persist == 0) {
+        const int t = atoi(x);
+        const uint8_t *a = static_cast<const uint8_t *>(arena);
+#define TCSUM_SEGT(TT)                                                                                        \
+    if (t == TT) {                                                                                            \
+        hipLaunchKernelGGL((k_segments<16, 6, MODE, TT>), dim3((n + TT / 16 - 1) / (TT / 16)), dim3(TT), 0, s, a, \
+                           descs, n, out, aux, xg);                                                           \
+        return hipGetLastError();                                                                             \
+    }
+        TCSUM_SEGT(64) TCSUM_SEGT(128) TCSUM_SEGT(512)
+#undef TCSUM_SEGT
+    }
 #define TCSUM_SEG(GG, UU)                                                                            \
     if (G == GG && U == UU) {                                                                      \
         const uint32_t per_block = 256u / GG;                                                      \

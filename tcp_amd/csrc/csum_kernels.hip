@@ -1717,19 +1717,6 @@ template <int MODE>
 static hipError_t seg_u(int G, int U, int persist, uint32_t xg, uint32_t n, const void *arena, const void *descs,
                         uint16_t *out, uint32_t aux, hipStream_t s)
 {
-    // TCSUM_WGT=T: the headline geometry with T-thread workgroups (measurement)
-    if (const char *x = getenv("TCSUM_WGT"); x && G == 16 && U == 6 && persist == 0) {
-        const int t = atoi(x);
-        const uint8_t *a = static_cast<const uint8_t *>(arena);
-#define TCSUM_SEGT(TT)                                                                                        \
-    if (t == TT) {                                                                                            \
-        hipLaunchKernelGGL((k_segments<16, 6, MODE, TT>), dim3((n + TT / 16 - 1) / (TT / 16)), dim3(TT), 0, s, a, \
-                           descs, n, out, aux, xg);                                                           \
-        return hipGetLastError();                                                                             \
-    }
-        TCSUM_SEGT(64) TCSUM_SEGT(128) TCSUM_SEGT(512)
-#undef TCSUM_SEGT
-    }
 #define TCSUM_SEG(GG, UU)                                                                            \
     if (G == GG && U == UU) {                                                                      \
         const uint32_t per_block = 256u / GG;                                                      \

@@ -580,6 +580,230 @@ __global__ __launch_bounds__(W * 64) void k_segments_wgx(const uint8_t *__restri
     }
 }
 
+// ---------------------------------------------------------------- packed stream
+//
+// Ranges packed back to back (offset[i+1] == offset[i] + len[i], e.g. a batch
+// of MTU segments laid out contiguously) are one byte stream with boundaries
+// in it.  k_segments_pk lets a 16-wave workgroup stream K consecutive ranges
+// (<= 64 KiB together) in the TSO kernel's load shape -- 32-lane groups each
+// walking a 2-KiB sub-range, 4 loads per lane, the whole region in one pass --
+// instead of giving every range its own lane group.
+//
+// Per-range sums come from prefix sums at the boundaries.  Chunk c of the
+// region (16-B aligned, address order) has the full word sum f(c); with
+// E(c) = sum of f over the chunks before c, the prefix of the region's bytes
+// before boundary x (byte offset from the first chunk) is
+//     P(x) = E(x / 16) + (bytes [0, x % 16) of chunk x / 16),
+// and range r's sum is P(x[r+1]) - P(x[r]): exact u32 arithmetic (a 64-KiB
+// region sums to < 2^31), so the bytes of the neighbouring regions that share
+// the first and last chunk cancel and no chunk is masked except at a boundary.
+// The address-parity weighting and the odd-start rotation are k_segments'.
+//
+// E is a scan in the load order: within a 2-KiB sub-range load u of lane l
+// is chunk u*32 + l, so E = (sub-ranges before) + (loads u' < u of this
+// sub-range) + (lanes l' < l of load u) -- a 32-lane DPP scan per load, the
+// half-wave totals by readlane.  Wave 0 alone loads the K descriptors (the
+// others read only the first and last, as scalars, to place their loads),
+// checks that they are packed and marks each boundary's byte in a 4-bit-per-
+// chunk table in LDS; after one barrier every lane writes, per chunk, its
+// sub-range prefix (+ the bytes before a marked boundary, summed by the lane
+// that holds the chunk, so no byte is loaded twice); after a second, wave 0
+// adds the sub-range prefixes, differences the boundary prefixes and stores
+// the K results with one coalesced store.
+//
+// Ranges shorter than 17 B (two boundaries in one chunk), gaps or overlaps
+// between neighbours, or a region over 64 KiB send the workgroup down the
+// per-range path (32 lanes per range): always correct, only slower.
+__device__ __forceinline__ uint32_t scan32(uint32_t x)
+{
+    // inclusive scan inside each 32-lane half: row_shr 1, 2, 4, 8 (16-lane
+    // rows), then row_bcast:15 adds row 0's total into row 1 (and 2's into 3)
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    return x;
+}
+
+// Word sum of the chunk's bytes [0, b), b = 0..16.
+__device__ __forceinline__ uint32_t chunk_prefix_sum(u32x4 v, uint32_t b)
+{
+    const int bits = (int)(8u * b);
+    const uint32_t m0 = bits >= 32 ? ~0u : (1u << bits) - 1u;
+    const uint32_t m1 = bits >= 64 ? ~0u : bits <= 32 ? 0u : (1u << (bits - 32)) - 1u;
+    const uint32_t m2 = bits >= 96 ? ~0u : bits <= 64 ? 0u : (1u << (bits - 64)) - 1u;
+    const uint32_t m3 = bits >= 128 ? ~0u : bits <= 96 ? 0u : (1u << (bits - 96)) - 1u;
+    uint32_t acc = add_halves(0u, v.x & m0);
+    acc = add_halves(acc, v.y & m1);
+    acc = add_halves(acc, v.z & m2);
+    return add_halves(acc, v.w & m3);
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t lane)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)lane);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+constexpr uint32_t kPkWaves = 16, kPkLoads = 4, kPkChunks = kPkWaves * 64 * kPkLoads; // 64 KiB per pass
+constexpr uint32_t kPkMaxRanges = 63; // boundaries 0..K live in the lanes of one wave
+
+// off and len of descriptor i (the same 12 bytes lead both layouts); called
+// with a workgroup-uniform index, so it is a scalar load
+template <int MODE>
+__device__ __forceinline__ void desc_span(const void *__restrict__ descs, uint32_t i, uint64_t &off, uint32_t &len)
+{
+    const uint8_t *x = static_cast<const uint8_t *>(descs) + (MODE == MODE_PESO ? 24ull : 16ull) * i;
+    const uint2 o = *reinterpret_cast<const uint2 *>(x);
+    off = (uint64_t)o.x | ((uint64_t)o.y << 32);
+    len = *reinterpret_cast<const uint32_t *>(x + 8);
+}
+
+template <int MODE, int W = kPkWaves, int U = kPkLoads, bool PROBE = false>
+__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) void k_segments_pk(
+    const uint8_t *__restrict__ arena, const void *__restrict__ descs, uint32_t n, uint16_t *__restrict__ out,
+    uint32_t aux, uint32_t xg, uint32_t K)
+{
+    static_assert(MODE != MODE_EXACT, "the exact u32 sum stays on k_segments");
+    constexpr uint32_t T = W * 64u, CH = T * U, SR = 32u * U; // chunks per pass, per sub-range
+    __shared__ uint32_t ex[CH];          // per chunk: its sub-range's word sum before the boundary in it
+    __shared__ uint32_t nib[CH / 8];     // per chunk, 4 bits: byte 1..15 of a boundary inside it, 0 = none
+    __shared__ uint32_t subtot[2 * W];   // per sub-range (32 lanes x U loads)
+    __shared__ uint32_t packed_flag;
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    const uint32_t first = blk * K;
+    const uint32_t kw = n - first < K ? n - first : K; // >= 1: grid = ceil(n / K)
+    // the region: from the first range's first byte to the last range's end
+    uint64_t r0, offl;
+    uint32_t len0, lenl;
+    desc_span<MODE>(descs, first, r0, len0);
+    desc_span<MODE>(descs, first + kw - 1u, offl, lenl);
+    const uint64_t rend = offl + lenl;
+    const uint8_t *p = arena + r0;
+    const uint32_t s0 = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
+    // [r0, rend) runs from a byte of the first range to a byte of the last, so
+    // it lies inside the arena whatever the ranges between do: its chunks are
+    // safe to load before the stream is known to be packed
+    const bool span_ok = len0 != 0 && lenl != 0 && rend > r0 && rend - r0 <= (uint64_t)(CH * 16u - s0);
+    const uint32_t span = span_ok ? (uint32_t)(rend - r0) : 0u;
+    const uint32_t nch = span_ok ? (s0 + span + 15u) >> 4 : 0u;
+    const uint32_t sub = t >> 5, l = t & 31u, hf = (t >> 5) & 1u;
+    const u32x4 *base = span_ok ? reinterpret_cast<const u32x4 *>(p - s0) : &g_zero_chunk;
+    u32x4 v[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t c = sub * SR + u * 32u + l;
+        v[u] = load16<true>(base + (c < nch ? c : (nch ? nch - 1u : 0u)));
+    }
+    issue_fence();
+    // wave 0: the K descriptors (lane r: range r), whether they are a packed
+    // stream, and boundary r's chunk and byte -- marked in the nibble table
+    // for the chunk's owner when it falls inside the chunk
+    const bool mine = lane < kw;
+    SegDesc d{0, 0, 0, 0, 0, 0};
+    uint32_t bc = 0, bb = 0, q16 = 0;
+    if (w == 0) {
+#pragma unroll
+        for (uint32_t i = lane; i < CH / 8; i += 64)
+            nib[i] = 0;
+        d = load_desc<MODE>(descs, first + lane, mine);
+        const uint64_t end = d.off + d.len;
+        const uint32_t nlo = (uint32_t)__shfl_down((int)(uint32_t)d.off, 1, 64);
+        const uint32_t nhi = (uint32_t)__shfl_down((int)(uint32_t)(d.off >> 32), 1, 64);
+        const uint64_t next = (uint64_t)nlo | ((uint64_t)nhi << 32);
+        const bool ok = !mine || (d.len >= 17u && (lane == kw - 1u || end == next));
+        const bool packed = span_ok && __ballot(!ok) == 0;
+        // boundary x[r] in bytes from the first chunk, r = 0..kw; a chunk-aligned
+        // end is byte 16 of the last chunk (its prefix: the whole region)
+        uint32_t x = s0 + (uint32_t)(d.off - r0);
+        if (lane == kw)
+            x = s0 + span;
+        bc = x >> 4;
+        bb = x & 15u;
+        if (bc == nch) {
+            bc = nch - 1u;
+            bb = 16u;
+        }
+        if (!(packed && lane <= kw))
+            bc = bb = 0;
+        if constexpr (MODE == MODE_PESO)
+            q16 = peso_pseudo16(d);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (bb != 0 && bb != 16)
+            __hip_atomic_fetch_or(&nib[bc >> 3], bb << (4u * (bc & 7u)), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0)
+            packed_flag = packed ? 1u : 0u;
+    }
+    if constexpr (PROBE) { // measurement: the same loads, no arithmetic
+        u32x4 z = v[0];
+#pragma unroll
+        for (uint32_t u = 1; u < U; ++u)
+            z ^= v[u];
+        const uint32_t f = z.x ^ z.y ^ z.z ^ z.w ^ q16;
+        if (f == 0x9E3779B9u)
+            reinterpret_cast<uint32_t *>(out)[0] = f;
+        return;
+    }
+    __syncthreads();
+    if (!packed_flag) { // workgroup-uniform: ranges one by one, 32 lanes each
+        const uint32_t h = t >> 5, gl = t & 31u;
+        for (uint32_t r = h; r < kw; r += 2 * W) {
+            const SegDesc e = load_desc<MODE>(descs, first + r, true);
+            uint32_t q = 0;
+            uint32_t acc = sum_range<32, 4, false>(arena, e.off, e.len, gl, [&] {
+                if constexpr (MODE == MODE_PESO)
+                    q = pinned(peso_pseudo16(e));
+            });
+            acc = group_sum<32>(acc);
+            if (gl == 0)
+                out[first + r] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + e.off), e, aux, q);
+        }
+        return;
+    }
+    uint32_t nw[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u)
+        nw[u] = nib[(sub * SR + u * 32u + l) >> 3];
+    // every wave: chunk sums, their scans over each 32-lane half; per chunk the
+    // word sum of its sub-range before it, plus, in a chunk holding a boundary,
+    // the chunk's bytes before the boundary
+    uint32_t a = 0; // this lane's half-wave: chunks of loads u' < u
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t c = sub * SR + u * 32u + l;
+        const uint32_t f = chunk_sum_w(0u, v[u], c < nch ? 0x00010001u : 0u); // < 2^20
+        const uint32_t sc = scan32(f);
+        uint32_t e = a + (sc - f);
+        const uint32_t b = (nw[u] >> (4u * (l & 7u))) & 15u;
+        if (__ballot(b != 0))
+            e += chunk_prefix_sum(v[u], b);
+        ex[c] = e;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)sc, 31);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)sc, 63);
+        a += hf ? hi : lo;
+    }
+    if (l == 0)
+        subtot[sub] = a;
+    __syncthreads();
+    if (w != 0)
+        return;
+    // wave 0: P(x[r]) = sub-ranges before + ex[chunk]; range r's sum is
+    // P(x[r+1]) - P(x[r])
+    const uint32_t st = lane < 2u * W ? subtot[lane] : 0u;
+    const uint32_t si = scan32(st);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)si, 31);
+    const uint32_t sp = (uint32_t)__shfl((int)(si - st), (int)(bc / SR), 64);
+    const uint32_t pr = bb == 16u ? total : sp + ex[bc];
+    const uint32_t pn = (uint32_t)__shfl_down((int)pr, 1, 64);
+    if (mine)
+        out[first + lane] = finalize<MODE>(pn - pr, reinterpret_cast<uintptr_t>(arena + d.off), d, aux, q16);
+}
+
 // Persistent form: a resident grid walks the batch; each wave prefetches its
 // next descriptor while the current packets' bytes are in flight, so the
 // descriptor -> data dependence costs one latency per wave, not per packet.
@@ -1710,6 +1934,15 @@ Geometry pick_geometry(uint64_t mean_len)
         g.persist = atoi(s);
     if (const char *s = getenv("TCSUM_XCD"))
         g.xcd = atoi(s);
+    // packed stream (k_segments_pk): K ranges of this mean length fill one
+    // 64-KiB pass; measurement switch while it is A/B'd
+    if (const char *s = getenv("TCSUM_PACKED"); s && atoi(s) && mean_len >= 17) {
+        const char *pw = getenv("TCSUM_PK_W");
+        const char *pu = getenv("TCSUM_PK_U");
+        const uint64_t pass = 16ull * 64u * (pw ? atoi(pw) : kPkWaves) * (pu ? atoi(pu) : kPkLoads);
+        const uint64_t k = (pass - 15u) / mean_len;
+        g.packed = (int)(k > kPkMaxRanges ? kPkMaxRanges : k);
+    }
     return g;
 }
 
@@ -1801,7 +2034,8 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
         const uint32_t lanes = mode == MODE_EXACT ? 64u : (uint32_t)g.lanes;
         // ranges per launch: 2^32 - 1 work-items (256 / G ranges per 256-thread
         // block; one range per block of 256 or 1024 threads)
-        const uint64_t per_launch = lanes >= 1024 ? (1ull << 22) - 1
+        const uint64_t per_launch = g.packed > 0 && mode != MODE_EXACT ? ((1ull << 22) - 1) * (uint64_t)g.packed
+                                    : lanes >= 1024 ? (1ull << 22) - 1
                                     : lanes >= 256 ? kMaxBlocks
                                                    : kMaxBlocks * (256u / (lanes ? lanes : 64u));
         if (n > per_launch) {
@@ -1815,6 +2049,32 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
             }
             return hipSuccess;
         }
+    }
+    if (g.packed > 0 && mode != MODE_EXACT) {
+        const uint32_t K = (uint32_t)g.packed > kPkMaxRanges ? kPkMaxRanges : (uint32_t)g.packed;
+        const uint8_t *a = static_cast<const uint8_t *>(arena);
+        // measurement: TCSUM_PK_W / TCSUM_PK_U workgroup waves and loads per lane
+        const char *pw = getenv("TCSUM_PK_W");
+        const char *pu = getenv("TCSUM_PK_U");
+        const int W = pw ? atoi(pw) : (int)kPkWaves, Ul = pu ? atoi(pu) : (int)kPkLoads;
+        const char *pr = getenv("TCSUM_PK_PROBE"); // measurement: the loads only
+        const bool probe = mode == MODE_PESO && pr && atoi(pr);
+        const uint32_t xgc = (uint32_t)g.xcd;
+#define TCSUM_PK(WW, UU)                                                                                        \
+    if (W == WW && Ul == UU) {                                                                                  \
+        const dim3 gr((n + K - 1) / K), bl(WW * 64);                                                            \
+        if (mode == MODE_SEG)                                                                                   \
+            hipLaunchKernelGGL((k_segments_pk<MODE_SEG, WW, UU>), gr, bl, 0, stream, a, descs, n, out, aux, xgc, K); \
+        else if (probe)                                                                                         \
+            hipLaunchKernelGGL((k_segments_pk<MODE_PESO, WW, UU, true>), gr, bl, 0, stream, a, descs, n, out, aux, \
+                               xgc, K);                                                                         \
+        else                                                                                                    \
+            hipLaunchKernelGGL((k_segments_pk<MODE_PESO, WW, UU>), gr, bl, 0, stream, a, descs, n, out, aux, xgc, K); \
+        return hipGetLastError();                                                                               \
+    }
+        TCSUM_PK(16, 4) TCSUM_PK(16, 3) TCSUM_PK(16, 2) TCSUM_PK(8, 4) TCSUM_PK(8, 3) TCSUM_PK(8, 2) TCSUM_PK(4, 4) TCSUM_PK(4, 3) TCSUM_PK(12, 3)
+#undef TCSUM_PK
+        return hipErrorInvalidValue;
     }
     if (mode == MODE_EXACT) {
         hipLaunchKernelGGL((k_segments<64, 8, MODE_EXACT>), dim3((n + 3) / 4), dim3(256), 0, stream,

@@ -22,6 +22,8 @@ struct Geometry {
     int persist; // 0: one pass per wave; 1: resident grid + descriptor prefetch;
                  // 2: resident grid, two ranges in flight per wave (k_segments_pp)
     int xcd;     // consecutive workgroups kept on one XCD (1: dispatch order)
+    int packed;  // K > 0: checksum_peso / pktbuf_checksum16 batches as a packed
+                 // stream, K consecutive ranges per 16-wave workgroup (k_segments_pk)
 };
 
 Geometry pick_geometry(uint64_t mean_len);

@@ -1,0 +1,154 @@
+"""k_segments_pk -- ranges packed back to back summed as one stream -- against
+the oracle (the CPU restatement of net/src/tools.c:24-75 and
+net/src/pktbuf.c:646-670, pinned to the reference's fixtures).
+
+The packed path takes a workgroup's K consecutive ranges when every one is at
+least 17 B, each starts where the previous one ends and together they fit a
+64-KiB pass; any other workgroup goes down its per-range path.  Both paths
+and their mix inside one batch are checked bit for bit, with ranges starting
+at every byte parity and chunk phase.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "gpu tests need an MI355X"
+    return t
+
+
+@pytest.fixture(scope="module")
+def tc(torch):
+    from tcp_amd import build
+    build.build()
+    import tcp_amd
+    tcp_amd.plat_init(0)
+    return tcp_amd
+
+
+@pytest.fixture(params=[16, 8])
+def packed(monkeypatch, request):
+    """The packed kernel, 16-wave (64-KiB passes) and 8-wave (32-KiB)."""
+    monkeypatch.setenv("TCSUM_PACKED", "1")
+    monkeypatch.setenv("TCSUM_PK_W", str(request.param))
+
+
+def _arena(rng, size):
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    for _ in range(30):  # runs of 0x00 / 0xFF: sums of 0 and 0xFFFF
+        a = int(rng.integers(0, size - 3000))
+        host[a: a + int(rng.integers(1, 3000))] = rng.choice([0, 0xFF])
+    return host
+
+
+def _peso(tc, offs, lens, rng):
+    p = np.zeros(len(lens), tc.PESO_DTYPE)
+    p["offset"], p["len"] = offs, lens
+    p["src"] = rng.integers(0, 256, (len(lens), 4))
+    p["dst"] = rng.integers(0, 256, (len(lens), 4))
+    p["protocol"] = rng.choice([6, 17], len(lens))
+    return p
+
+
+def _packed_offs(lens, start):
+    return start + np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.uint64)
+
+
+@pytest.mark.parametrize("start", [0, 1, 7, 12, 15])
+@pytest.mark.parametrize("n", [1, 2, 42, 43, 44, 86, 4097])
+def test_packed_mtu_vs_oracle(tc, torch, oracle, packed, n, start):
+    """1500-B ranges packed from an arbitrary first byte (odd starts: every
+    other range starts at an odd address); n around multiples of K = 43."""
+    rng = np.random.default_rng(n * 16 + start)
+    lens = np.full(n, 1500, np.uint32)
+    host = _arena(rng, start + 1500 * n + 4096)
+    p = _peso(tc, _packed_offs(lens, start), lens, rng)
+    out = tc.batch_peso(torch.from_numpy(host).cuda(), tc.descs_to_device(p), n, int(lens.sum()))
+    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_packed_ragged_lengths(tc, torch, oracle, packed, seed):
+    """Packed ranges of 17..3000 B (odd lengths: the parity flips range by
+    range), the hint's mean setting K; some workgroups' regions exceed 64 KiB
+    and take the per-range path."""
+    rng = np.random.default_rng(500 + seed)
+    n = 6000
+    lens = rng.integers(17, 3001, n).astype(np.uint32)
+    start = int(rng.integers(0, 64))
+    host = _arena(rng, start + int(lens.sum()) + 4096)
+    p = _peso(tc, _packed_offs(lens, start), lens, rng)
+    hint = int(rng.choice([int(lens.sum()), 1500 * n, 700 * n]))  # K from the hint only
+    out = tc.batch_peso(torch.from_numpy(host).cuda(), tc.descs_to_device(p), n, hint)
+    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
+
+
+@pytest.mark.parametrize("layout", ["short", "gap", "overlap", "reversed", "zero"])
+def test_packed_fallback_workgroups(tc, torch, oracle, packed, layout):
+    """Workgroups whose ranges are not a packed stream -- a range under 17 B,
+    a gap, an overlap, descending offsets, a zero-length range -- are summed
+    per range; their neighbours stay on the packed path."""
+    rng = np.random.default_rng(["short", "gap", "overlap", "reversed", "zero"].index(layout))
+    n = 43 * 40
+    lens = np.full(n, 1500, np.uint32)
+    offs = _packed_offs(lens, 64).astype(np.int64)
+    bad = rng.choice(n, 25, replace=False)
+    for i in bad:
+        if layout == "short":
+            lens[i] = int(rng.integers(1, 17))
+        elif layout == "zero":
+            lens[i] = 0
+        elif layout == "gap":
+            offs[i:] += int(rng.integers(1, 40))
+        elif layout == "overlap":
+            offs[i:] -= int(rng.integers(1, 40))
+    if layout == "reversed":
+        offs = offs[::-1].copy()
+    host = _arena(rng, int(offs.max()) + 1500 + 4096)
+    p = _peso(tc, offs.astype(np.uint64), lens, rng)
+    out = tc.batch_peso(torch.from_numpy(host).cuda(), tc.descs_to_device(p), n, 1500 * n)
+    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
+
+
+@pytest.mark.parametrize("comp", [0, 1])
+def test_packed_segments_mode(tc, torch, oracle, packed, comp):
+    """tcsum_batch_segments (pktbuf_checksum16: u16 pre_sum, optional
+    complement) on packed ranges."""
+    rng = np.random.default_rng(31 + comp)
+    n = 5000
+    lens = rng.integers(900, 2200, n).astype(np.uint32)
+    host = _arena(rng, 3 + int(lens.sum()) + 4096)
+    s = np.zeros(n, tc.SEG_DTYPE)
+    s["offset"], s["len"] = _packed_offs(lens, 3), lens
+    s["pre_sum"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    out = tc.batch_segments(torch.from_numpy(host).cuda(), tc.descs_to_device(s), n, comp, int(lens.sum()))
+    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_segments(host, s, comp, nthreads=8))
+
+
+def test_packed_exact_region_edges(tc, torch, oracle, packed):
+    """Regions that end exactly on a chunk boundary (the end prefix is the
+    last chunk's whole sum) and that fill the 64-KiB pass to the byte."""
+    rng = np.random.default_rng(3)
+    # K = 63 for mean 1040; 63 x 1040 = 65,520 B: with start 0 the region ends
+    # chunk-aligned; 16 + 65,520 = the whole pass
+    for start, L in ((0, 1040), (16, 1040), (1, 1040), (0, 1024), (8, 1488)):
+        n = 63 * 5 + 1
+        lens = np.full(n, L, np.uint32)
+        host = _arena(rng, start + L * n + 4096)
+        p = _peso(tc, _packed_offs(lens, start), lens, rng)
+        out = tc.batch_peso(torch.from_numpy(host).cuda(), tc.descs_to_device(p), n, L * n)
+        np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
+
+
+def test_packed_full_mtu_config(tc, torch, oracle, packed):
+    """configs[1] at full size (1M x 1500 B) through the packed kernel: every
+    result equal to the oracle and to the per-range kernel."""
+    from tcp_amd import workload
+    b = workload.make_batch("mtu")
+    arena, descs = workload.materialize(b)
+    out = tc.batch_peso(arena, descs, b.n, b.total_bytes).cpu().numpy()
+    np.testing.assert_array_equal(out, oracle.batch_peso(arena.cpu().numpy(), b.descs, nthreads=16))

@@ -582,38 +582,43 @@ __global__ __launch_bounds__(W * 64) void k_segments_wgx(const uint8_t *__restri
 
 // ---------------------------------------------------------------- packed stream
 //
-// Ranges packed back to back (offset[i+1] == offset[i] + len[i], e.g. a batch
-// of MTU segments laid out contiguously) are one byte stream with boundaries
-// in it.  k_segments_pk lets a 16-wave workgroup stream K consecutive ranges
-// (<= 64 KiB together) in the TSO kernel's load shape -- 32-lane groups each
-// walking a 2-KiB sub-range, 4 loads per lane, the whole region in one pass --
-// instead of giving every range its own lane group.
+// Ranges laid out one after another in the arena (a batch of MTU segments
+// packed back to back: offset[i+1] == offset[i] + len[i]; or with padding
+// between them) are one byte stream.  k_segments_pk gives a workgroup of W
+// waves K consecutive ranges and streams the region from the first range's
+// first byte to the last range's end in the TSO kernel's load shape -- 32-lane
+// groups each walking a contiguous sub-range, U loads per lane -- instead of
+// giving every range its own lane group; a region longer than one pass
+// (W * 64 * U chunks) is walked pass by pass, the next pass's loads in flight
+// while the current one is combined.
 //
-// Per-range sums come from prefix sums at the boundaries.  Chunk c of the
-// region (16-B aligned, address order) has the full word sum f(c); with
-// E(c) = sum of f over the chunks before c, the prefix of the region's bytes
-// before boundary x (byte offset from the first chunk) is
-//     P(x) = E(x / 16) + (bytes [0, x % 16) of chunk x / 16),
-// and range r's sum is P(x[r+1]) - P(x[r]): exact u32 arithmetic (a 64-KiB
-// region sums to < 2^31), so the bytes of the neighbouring regions that share
-// the first and last chunk cancel and no chunk is masked except at a boundary.
-// The address-parity weighting and the odd-start rotation are k_segments'.
+// Per-range sums come from prefix sums.  Chunk c of the region (16-B aligned,
+// address order) has the full word sum f(c); with E(c) = the sum of f over the
+// chunks before c, the word sum of the region's bytes before byte x (counted
+// from the first chunk) is
+//     P(x) = E(x / 16) + (word sum of bytes [0, x % 16) of chunk x / 16),
+// and range r's sum is P(end_r) - P(start_r): exact u32 arithmetic (a pass of
+// <= 64 KiB sums to < 2^31 and P wraps mod 2^32 consistently), so bytes that
+// belong to no range -- padding, the neighbouring regions' bytes in the first
+// and last chunk -- cancel, and no chunk is masked.  Any layout works as long
+// as every range lies inside the region: gaps, overlaps, duplicates, ranges of
+// 0..16 bytes.  The address-parity weighting and the odd-start rotation are
+// k_segments'.
 //
-// E is a scan in the load order: within a 2-KiB sub-range load u of lane l
-// is chunk u*32 + l, so E = (sub-ranges before) + (loads u' < u of this
-// sub-range) + (lanes l' < l of load u) -- a 32-lane DPP scan per load, the
-// half-wave totals by readlane.  Wave 0 alone loads the K descriptors (the
-// others read only the first and last, as scalars, to place their loads),
-// checks that they are packed and marks each boundary's byte in a 4-bit-per-
-// chunk table in LDS; after one barrier every lane writes, per chunk, its
-// sub-range prefix (+ the bytes before a marked boundary, summed by the lane
-// that holds the chunk, so no byte is loaded twice); after a second, wave 0
-// adds the sub-range prefixes, differences the boundary prefixes and stores
-// the K results with one coalesced store.
+// E is a scan in the load order: within a sub-range load u of lane l is chunk
+// u*32 + l, so E = (sub-ranges before) + (loads u' < u of this sub-range) +
+// (lanes l' < l of load u) -- a 32-lane DPP scan per load, the half-wave
+// totals by readlane.  Every lane writes, per chunk, its sub-range prefix and
+// the chunk itself to LDS; after one barrier, lane r of wave w (range 64w + r,
+// whose descriptor it loaded while the bytes were in flight) adds the
+// sub-range prefixes and the bytes before its start and end from the LDS copy
+// of their chunks.  The waves place their loads from the first and last
+// descriptor only (scalar loads), so the data loads wait on one descriptor
+// latency, as in the per-range kernels.
 //
-// Ranges shorter than 17 B (two boundaries in one chunk), gaps or overlaps
-// between neighbours, or a region over 64 KiB send the workgroup down the
-// per-range path (32 lanes per range): always correct, only slower.
+// A workgroup whose region is longer than 64 passes, or one of whose ranges
+// lies outside it (a shuffled batch), sums range by range with the widest lane
+// groups that give every range one: always correct, only slower.
 __device__ __forceinline__ uint32_t scan32(uint32_t x)
 {
     // inclusive scan inside each 32-lane half: row_shr 1, 2, 4, 8 (16-lane
@@ -647,8 +652,8 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t lane)
     return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
-constexpr uint32_t kPkWaves = 16, kPkLoads = 4, kPkChunks = kPkWaves * 64 * kPkLoads; // 64 KiB per pass
-constexpr uint32_t kPkMaxRanges = 63; // boundaries 0..K live in the lanes of one wave
+constexpr uint32_t kPkWaves = 4, kPkLoads = 3; // 4 waves x 64 lanes x 3 loads x 16 B = 12 KiB per pass
+constexpr uint32_t kPkMaxRanges = 64; // ranges per wave of the workgroup (lane r of wave w: range 64w + r)
 
 // off and len of descriptor i (the same 12 bytes lead both layouts); called
 // with a workgroup-uniform index, so it is a scalar load
@@ -661,17 +666,41 @@ __device__ __forceinline__ void desc_span(const void *__restrict__ descs, uint32
     len = *reinterpret_cast<const uint32_t *>(x + 8);
 }
 
+// The per-range path for a workgroup whose ranges are not one region:
+// groups of G lanes, G the widest power of two with one group per range.
+template <int MODE, int G, int UL = 4>
+__device__ __forceinline__ void pk_ranges(const uint8_t *__restrict__ arena, const void *__restrict__ descs,
+                                          uint16_t *__restrict__ out, uint32_t aux, uint32_t first, uint32_t kw,
+                                          uint32_t T)
+{
+    const uint32_t t = threadIdx.x, gl = t & (G - 1u);
+    for (uint32_t r = t / G; r < kw; r += T / G) {
+        const SegDesc e = load_desc<MODE>(descs, first + r, true);
+        uint32_t q = 0;
+        uint32_t acc = sum_range<G, UL, false>(arena, e.off, e.len, gl, [&] {
+            if constexpr (MODE == MODE_PESO)
+                q = pinned(peso_pseudo16(e));
+        });
+        acc = group_sum<G>(acc);
+        if (gl == 0)
+            out[first + r] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + e.off), e, aux, q);
+    }
+}
+
+constexpr uint32_t kPkMaxPasses = 64; // longer regions go range by range
+
 template <int MODE, int W = kPkWaves, int U = kPkLoads, bool PROBE = false>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) void k_segments_pk(
     const uint8_t *__restrict__ arena, const void *__restrict__ descs, uint32_t n, uint16_t *__restrict__ out,
     uint32_t aux, uint32_t xg, uint32_t K)
 {
     static_assert(MODE != MODE_EXACT, "the exact u32 sum stays on k_segments");
+    static_assert(W <= 16, "the sub-range totals are scanned by 32 lanes");
     constexpr uint32_t T = W * 64u, CH = T * U, SR = 32u * U; // chunks per pass, per sub-range
-    __shared__ uint32_t ex[CH];          // per chunk: its sub-range's word sum before the boundary in it
-    __shared__ uint32_t nib[CH / 8];     // per chunk, 4 bits: byte 1..15 of a boundary inside it, 0 = none
+    __shared__ u32x4 dat[CH];            // the pass's chunks, for the boundary bytes
+    __shared__ uint32_t ex[CH];          // per chunk: its sub-range's word sum before it
     __shared__ uint32_t subtot[2 * W];   // per sub-range (32 lanes x U loads)
-    __shared__ uint32_t packed_flag;
+    __shared__ uint32_t region_ok[W];     // per wave: its ranges lie in the region
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
     const uint32_t first = blk * K;
@@ -686,10 +715,13 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     const uint32_t s0 = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
     // [r0, rend) runs from a byte of the first range to a byte of the last, so
     // it lies inside the arena whatever the ranges between do: its chunks are
-    // safe to load before the stream is known to be packed
-    const bool span_ok = len0 != 0 && lenl != 0 && rend > r0 && rend - r0 <= (uint64_t)(CH * 16u - s0);
+    // safe to load before the ranges are known to lie inside it
+    const bool span_ok = len0 != 0 && lenl != 0 && rend > r0 &&
+                         rend - r0 <= (uint64_t)kPkMaxPasses * CH * 16u - s0;
+    bool ranges = !span_ok; // workgroup-uniform: sum range by range instead
     const uint32_t span = span_ok ? (uint32_t)(rend - r0) : 0u;
     const uint32_t nch = span_ok ? (s0 + span + 15u) >> 4 : 0u;
+    const uint32_t npass = (nch + CH - 1u) / CH;
     const uint32_t sub = t >> 5, l = t & 31u, hf = (t >> 5) & 1u;
     const u32x4 *base = span_ok ? reinterpret_cast<const u32x4 *>(p - s0) : &g_zero_chunk;
     u32x4 v[U];
@@ -699,109 +731,117 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
         v[u] = load16<true>(base + (c < nch ? c : (nch ? nch - 1u : 0u)));
     }
     issue_fence();
-    // wave 0: the K descriptors (lane r: range r), whether they are a packed
-    // stream, and boundary r's chunk and byte -- marked in the nibble table
-    // for the chunk's owner when it falls inside the chunk
-    const bool mine = lane < kw;
+    // every wave: its share of the K descriptors (lane r: range 64w + r),
+    // whether each lies in the region, and its start and end in bytes from the
+    // first chunk
+    const uint32_t rr = w * 64u + lane;
+    const bool mine = rr < kw;
+    const bool has = w * 64u < kw; // wave-uniform
     SegDesc d{0, 0, 0, 0, 0, 0};
-    uint32_t bc = 0, bb = 0, q16 = 0;
-    if (w == 0) {
-#pragma unroll
-        for (uint32_t i = lane; i < CH / 8; i += 64)
-            nib[i] = 0;
-        d = load_desc<MODE>(descs, first + lane, mine);
-        const uint64_t end = d.off + d.len;
-        const uint32_t nlo = (uint32_t)__shfl_down((int)(uint32_t)d.off, 1, 64);
-        const uint32_t nhi = (uint32_t)__shfl_down((int)(uint32_t)(d.off >> 32), 1, 64);
-        const uint64_t next = (uint64_t)nlo | ((uint64_t)nhi << 32);
-        const bool ok = !mine || (d.len >= 17u && (lane == kw - 1u || end == next));
-        const bool packed = span_ok && __ballot(!ok) == 0;
-        // boundary x[r] in bytes from the first chunk, r = 0..kw; a chunk-aligned
-        // end is byte 16 of the last chunk (its prefix: the whole region)
-        uint32_t x = s0 + (uint32_t)(d.off - r0);
-        if (lane == kw)
-            x = s0 + span;
-        bc = x >> 4;
-        bb = x & 15u;
-        if (bc == nch) {
-            bc = nch - 1u;
-            bb = 16u;
-        }
-        if (!(packed && lane <= kw))
-            bc = bb = 0;
+    uint32_t xs = 0, xe = 0, q16 = 0;
+    if (has) {
+        d = load_desc<MODE>(descs, first + rr, mine);
+        const bool inside = !mine || (d.off >= r0 && d.off + d.len <= rend);
+        const bool ok = __ballot(!inside) == 0;
+        xs = ok ? s0 + (uint32_t)(d.off - r0) : 0u;
+        xe = ok ? xs + d.len : 0u;
         if constexpr (MODE == MODE_PESO)
             q16 = peso_pseudo16(d);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (bb != 0 && bb != 16)
-            __hip_atomic_fetch_or(&nib[bc >> 3], bb << (4u * (bc & 7u)), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WORKGROUP);
         if (lane == 0)
-            packed_flag = packed ? 1u : 0u;
+            region_ok[w] = ok ? 1u : 0u;
+    } else if (lane == 0) {
+        region_ok[w] = 1u;
     }
     if constexpr (PROBE) { // measurement: the same loads, no arithmetic
         u32x4 z = v[0];
 #pragma unroll
         for (uint32_t u = 1; u < U; ++u)
             z ^= v[u];
-        const uint32_t f = z.x ^ z.y ^ z.z ^ z.w ^ q16;
+        const uint32_t f = z.x ^ z.y ^ z.z ^ z.w ^ q16 ^ xe;
         if (f == 0x9E3779B9u)
             reinterpret_cast<uint32_t *>(out)[0] = f;
         return;
     }
-    __syncthreads();
-    if (!packed_flag) { // workgroup-uniform: ranges one by one, 32 lanes each
-        const uint32_t h = t >> 5, gl = t & 31u;
-        for (uint32_t r = h; r < kw; r += 2 * W) {
-            const SegDesc e = load_desc<MODE>(descs, first + r, true);
-            uint32_t q = 0;
-            uint32_t acc = sum_range<32, 4, false>(arena, e.off, e.len, gl, [&] {
-                if constexpr (MODE == MODE_PESO)
-                    q = pinned(peso_pseudo16(e));
-            });
-            acc = group_sum<32>(acc);
-            if (gl == 0)
-                out[first + r] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + e.off), e, aux, q);
+    uint32_t run = 0, ps = 0, pe = 0; // word sum of the passes before; P(start), P(end)
+    for (uint32_t pass = 0; !ranges && pass < npass; ++pass) { // workgroup-uniform
+        const uint32_t cb = pass * CH;
+        // every wave: chunk sums, their scans over each 32-lane half; per chunk
+        // the word sum of its sub-range before it, and the chunk itself
+        uint32_t a = 0; // this lane's half-wave: chunks of loads u' < u
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t c = sub * SR + u * 32u + l;
+            const uint32_t f = chunk_sum_w(0u, v[u], cb + c < nch ? 0x00010001u : 0u); // < 2^20
+            const uint32_t sc = scan32(f);
+            ex[c] = a + (sc - f);
+            dat[c] = v[u];
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)sc, 31);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)sc, 63);
+            a += hf ? hi : lo;
         }
+        if (l == 0)
+            subtot[sub] = a;
+        if (pass + 1u < npass) { // the next pass's bytes stream during the barrier and wave 0's sums
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t c = cb + CH + sub * SR + u * 32u + l;
+                v[u] = load16<true>(base + (c < nch ? c : nch - 1u));
+            }
+        }
+        __syncthreads();
+        if (pass == 0) {
+            bool all = true;
+#pragma unroll
+            for (uint32_t i = 0; i < W; ++i)
+                all = all && region_ok[i] != 0u;
+            if (!all) {
+                ranges = true;
+                break;
+            }
+        }
+        if (has) {
+            // P(x) = passes before + sub-ranges before + ex[chunk] + the chunk's
+            // bytes before x; the end of the region (x = 16 * nch) is byte 16 of
+            // the last chunk
+            const uint32_t st = lane < 2u * W ? subtot[lane] : 0u;
+            const uint32_t si = scan32(st);
+            const uint32_t sx = si - st;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t x = k ? xe : xs;
+                uint32_t cx = x >> 4, bx = x & 15u;
+                if (cx == nch) {
+                    cx = nch - 1u;
+                    bx = 16u;
+                }
+                const bool here = cx >= cb && cx < cb + CH;
+                const uint32_t lc = here ? cx - cb : 0u;
+                const uint32_t sp = (uint32_t)__shfl((int)sx, (int)(lc / SR), 64);
+                const uint32_t px = run + sp + ex[lc] + chunk_prefix_sum(dat[lc], bx);
+                if (k)
+                    pe = here ? px : pe;
+                else
+                    ps = here ? px : ps;
+            }
+            run += (uint32_t)__builtin_amdgcn_readlane((int)si, 31);
+        }
+        if (pass + 1u < npass)
+            __syncthreads(); // the next pass overwrites dat / ex / subtot
+    }
+    if (ranges) { // G lanes per range: the widest power of two that gives every range a group
+        const uint32_t lanes_per = T / kw;
+        if (lanes_per >= 64)
+            pk_ranges<MODE, 64>(arena, descs, out, aux, first, kw, T);
+        else if (lanes_per >= 32)
+            pk_ranges<MODE, 32, 3>(arena, descs, out, aux, first, kw, T);
+        else if (lanes_per >= 16)
+            pk_ranges<MODE, 16>(arena, descs, out, aux, first, kw, T);
+        else
+            pk_ranges<MODE, 8>(arena, descs, out, aux, first, kw, T);
         return;
     }
-    uint32_t nw[U];
-#pragma unroll
-    for (uint32_t u = 0; u < U; ++u)
-        nw[u] = nib[(sub * SR + u * 32u + l) >> 3];
-    // every wave: chunk sums, their scans over each 32-lane half; per chunk the
-    // word sum of its sub-range before it, plus, in a chunk holding a boundary,
-    // the chunk's bytes before the boundary
-    uint32_t a = 0; // this lane's half-wave: chunks of loads u' < u
-#pragma unroll
-    for (uint32_t u = 0; u < U; ++u) {
-        const uint32_t c = sub * SR + u * 32u + l;
-        const uint32_t f = chunk_sum_w(0u, v[u], c < nch ? 0x00010001u : 0u); // < 2^20
-        const uint32_t sc = scan32(f);
-        uint32_t e = a + (sc - f);
-        const uint32_t b = (nw[u] >> (4u * (l & 7u))) & 15u;
-        if (__ballot(b != 0))
-            e += chunk_prefix_sum(v[u], b);
-        ex[c] = e;
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)sc, 31);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)sc, 63);
-        a += hf ? hi : lo;
-    }
-    if (l == 0)
-        subtot[sub] = a;
-    __syncthreads();
-    if (w != 0)
-        return;
-    // wave 0: P(x[r]) = sub-ranges before + ex[chunk]; range r's sum is
-    // P(x[r+1]) - P(x[r])
-    const uint32_t st = lane < 2u * W ? subtot[lane] : 0u;
-    const uint32_t si = scan32(st);
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)si, 31);
-    const uint32_t sp = (uint32_t)__shfl((int)(si - st), (int)(bc / SR), 64);
-    const uint32_t pr = bb == 16u ? total : sp + ex[bc];
-    const uint32_t pn = (uint32_t)__shfl_down((int)pr, 1, 64);
     if (mine)
-        out[first + lane] = finalize<MODE>(pn - pr, reinterpret_cast<uintptr_t>(arena + d.off), d, aux, q16);
+        out[first + rr] = finalize<MODE>(pe - ps, reinterpret_cast<uintptr_t>(arena + d.off), d, aux, q16);
 }
 
 // Persistent form: a resident grid walks the batch; each wave prefetches its
@@ -1782,6 +1822,16 @@ hipError_t launch_probe_desc(const void *arena, const void *descs, uint32_t n, u
     const Geometry g = pick_geometry(mean_len);
     const uint32_t xg = (uint32_t)g.xcd;
     const uint8_t *a = static_cast<const uint8_t *>(arena);
+    if (g.packed > 0) { // k_segments_pk's loads (the default shape)
+        const uint32_t K = (uint32_t)g.packed < kPkMaxRanges * kPkWaves ? (uint32_t)g.packed
+                                                                          : kPkMaxRanges * kPkWaves;
+        if ((n + K - 1) / K >= (1u << 24))
+            return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_segments_pk<MODE_PESO, kPkWaves, kPkLoads, true>), dim3((n + K - 1) / K),
+                           dim3(kPkWaves * 64), 0, stream, a, descs, n, reinterpret_cast<uint16_t *>(sink), 0u, xg,
+                           K);
+        return hipGetLastError();
+    }
     if (g.lanes == 1024 && g.loads == 4) { // k_segments_wgx<16, 32, 4>'s loads
         if (n >= (1u << 22))
             return hipErrorInvalidValue;
@@ -1934,14 +1984,29 @@ Geometry pick_geometry(uint64_t mean_len)
         g.persist = atoi(s);
     if (const char *s = getenv("TCSUM_XCD"))
         g.xcd = atoi(s);
-    // packed stream (k_segments_pk): K ranges of this mean length fill one
-    // 64-KiB pass; measurement switch while it is A/B'd
-    if (const char *s = getenv("TCSUM_PACKED"); s && atoi(s) && mean_len >= 17) {
+    // packed stream (k_segments_pk) for checksum_peso / pktbuf_checksum16
+    // batches of ranges up to ~4 KiB: K ranges of this mean length fill one
+    // 12-KiB pass of a 4-wave workgroup (1500 B: K = 8).  One-process A/Bs on
+    // 1.5-GB batches (profiles/r03/ab_pk_layouts.txt): packed 1500-B ranges
+    // 0.98 of k_segments<16,6>'s time, 576 B 0.73, 200 B 0.48, 64 B 0.70,
+    // 4000 B 0.94, ragged 64..2936 B 0.96, with 0..63-B gaps 1.00; with
+    // K < 3 (mean > ~4 KiB) it lost (9000 B 1.04, ragged 64..9000 B 1.20), and
+    // a shuffled batch (ranges outside the region: range by range) costs 1.13.
+    // TCSUM_PACKED=0 turns it off; TCSUM_PK_W / TCSUM_PK_U pick another
+    // shape (measurement).
+    // (a forced per-range geometry -- TCSUM_G / TCSUM_U / TCSUM_P -- keeps it off
+    // unless TCSUM_PACKED=1 asks for it)
+    const char *pks = getenv("TCSUM_PACKED");
+    const bool forced = getenv("TCSUM_G") || getenv("TCSUM_U") || getenv("TCSUM_P");
+    if ((pks ? atoi(pks) != 0 : !forced) && mean_len > 0) {
         const char *pw = getenv("TCSUM_PK_W");
         const char *pu = getenv("TCSUM_PK_U");
-        const uint64_t pass = 16ull * 64u * (pw ? atoi(pw) : kPkWaves) * (pu ? atoi(pu) : kPkLoads);
+        const uint64_t w = pw ? (uint64_t)atoi(pw) : kPkWaves;
+        const uint64_t pass = 16ull * 64u * w * (pu ? (uint64_t)atoi(pu) : kPkLoads);
         const uint64_t k = (pass - 15u) / mean_len;
-        g.packed = (int)(k > kPkMaxRanges ? kPkMaxRanges : k);
+        const uint64_t kmax = (uint64_t)kPkMaxRanges * w;
+        if (k >= 3)
+            g.packed = (int)(k > kmax ? kmax : k);
     }
     return g;
 }
@@ -2051,7 +2116,7 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
         }
     }
     if (g.packed > 0 && mode != MODE_EXACT) {
-        const uint32_t K = (uint32_t)g.packed > kPkMaxRanges ? kPkMaxRanges : (uint32_t)g.packed;
+        const uint32_t K = (uint32_t)g.packed; // <= 64 per wave: capped by pick_geometry
         const uint8_t *a = static_cast<const uint8_t *>(arena);
         // measurement: TCSUM_PK_W / TCSUM_PK_U workgroup waves and loads per lane
         const char *pw = getenv("TCSUM_PK_W");
@@ -2062,17 +2127,19 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
         const uint32_t xgc = (uint32_t)g.xcd;
 #define TCSUM_PK(WW, UU)                                                                                        \
     if (W == WW && Ul == UU) {                                                                                  \
-        const dim3 gr((n + K - 1) / K), bl(WW * 64);                                                            \
+        const uint32_t Kc = K < 64u * WW ? K : 64u * WW;                                                        \
+        const dim3 gr((n + Kc - 1) / Kc), bl(WW * 64);                                                          \
         if (mode == MODE_SEG)                                                                                   \
-            hipLaunchKernelGGL((k_segments_pk<MODE_SEG, WW, UU>), gr, bl, 0, stream, a, descs, n, out, aux, xgc, K); \
+            hipLaunchKernelGGL((k_segments_pk<MODE_SEG, WW, UU>), gr, bl, 0, stream, a, descs, n, out, aux, xgc, Kc); \
         else if (probe)                                                                                         \
             hipLaunchKernelGGL((k_segments_pk<MODE_PESO, WW, UU, true>), gr, bl, 0, stream, a, descs, n, out, aux, \
-                               xgc, K);                                                                         \
+                               xgc, Kc);                                                                         \
         else                                                                                                    \
-            hipLaunchKernelGGL((k_segments_pk<MODE_PESO, WW, UU>), gr, bl, 0, stream, a, descs, n, out, aux, xgc, K); \
+            hipLaunchKernelGGL((k_segments_pk<MODE_PESO, WW, UU>), gr, bl, 0, stream, a, descs, n, out, aux, xgc, Kc); \
         return hipGetLastError();                                                                               \
     }
-        TCSUM_PK(16, 4) TCSUM_PK(16, 3) TCSUM_PK(16, 2) TCSUM_PK(8, 4) TCSUM_PK(8, 3) TCSUM_PK(8, 2) TCSUM_PK(4, 4) TCSUM_PK(4, 3) TCSUM_PK(12, 3)
+        TCSUM_PK(4, 3) TCSUM_PK(4, 2) TCSUM_PK(4, 4) TCSUM_PK(2, 3) TCSUM_PK(2, 4) TCSUM_PK(2, 6) TCSUM_PK(8, 3)
+        TCSUM_PK(16, 4)
 #undef TCSUM_PK
         return hipErrorInvalidValue;
     }

@@ -2,11 +2,11 @@
 the oracle (the CPU restatement of net/src/tools.c:24-75 and
 net/src/pktbuf.c:646-670, pinned to the reference's fixtures).
 
-The packed path takes a workgroup's K consecutive ranges when every one is at
-least 17 B, each starts where the previous one ends and together they fit a
-64-KiB pass; any other workgroup goes down its per-range path.  Both paths
-and their mix inside one batch are checked bit for bit, with ranges starting
-at every byte parity and chunk phase.
+A workgroup streams the region from its first range's first byte to its
+last range's end (pass by pass, up to 64 passes) when every one of its K
+ranges lies inside that region; any other workgroup goes range by range.
+Both paths and their mix inside one batch are checked bit for bit, with
+ranges starting at every byte parity and chunk phase.
 """
 import numpy as np
 import pytest
@@ -30,11 +30,13 @@ def tc(torch):
     return tcp_amd
 
 
-@pytest.fixture(params=[16, 8])
+@pytest.fixture(params=[(8, 3), (16, 4), (4, 3)])
 def packed(monkeypatch, request):
-    """The packed kernel, 16-wave (64-KiB passes) and 8-wave (32-KiB)."""
+    """The packed kernel in three workgroup shapes (waves x loads per lane)."""
+    w, u = request.param
     monkeypatch.setenv("TCSUM_PACKED", "1")
-    monkeypatch.setenv("TCSUM_PK_W", str(request.param))
+    monkeypatch.setenv("TCSUM_PK_W", str(w))
+    monkeypatch.setenv("TCSUM_PK_U", str(u))
 
 
 def _arena(rng, size):
@@ -87,16 +89,27 @@ def test_packed_ragged_lengths(tc, torch, oracle, packed, seed):
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
 
 
-@pytest.mark.parametrize("layout", ["short", "gap", "overlap", "reversed", "zero"])
-def test_packed_fallback_workgroups(tc, torch, oracle, packed, layout):
-    """Workgroups whose ranges are not a packed stream -- a range under 17 B,
-    a gap, an overlap, descending offsets, a zero-length range -- are summed
-    per range; their neighbours stay on the packed path."""
-    rng = np.random.default_rng(["short", "gap", "overlap", "reversed", "zero"].index(layout))
+LAYOUTS = ["short", "tiny", "gap", "aligned", "overlap", "duplicate", "zero", "reversed", "far", "shuffled"]
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_packed_irregular_layouts(tc, torch, oracle, packed, layout):
+    """Ranges that are not a clean packed stream.  Inside the region from the
+    workgroup's first range to its last (short and 1..16-B ranges, gaps,
+    16-B aligned starts, overlaps, duplicates, zero lengths) they are summed
+    from the stream's prefixes; ranges outside it (descending order, a last
+    range megabytes away, a shuffled batch) send the workgroup range by
+    range."""
+    rng = np.random.default_rng(LAYOUTS.index(layout))
     n = 43 * 40
-    lens = np.full(n, 1500, np.uint32)
-    offs = _packed_offs(lens, 64).astype(np.int64)
-    bad = rng.choice(n, 25, replace=False)
+    lens = np.full(n, 1500, np.int64)
+    if layout == "tiny":
+        lens = rng.integers(1, 17, n)
+    offs = np.concatenate([[64], 64 + np.cumsum(lens[:-1])]).astype(np.int64)
+    bad = rng.choice(n, 60, replace=False)
+    if layout == "aligned":
+        lens = rng.integers(1000, 2000, n)
+        offs = 64 + np.concatenate([[0], np.cumsum((lens[:-1] + 15) // 16 * 16)])
     for i in bad:
         if layout == "short":
             lens[i] = int(rng.integers(1, 17))
@@ -106,11 +119,33 @@ def test_packed_fallback_workgroups(tc, torch, oracle, packed, layout):
             offs[i:] += int(rng.integers(1, 40))
         elif layout == "overlap":
             offs[i:] -= int(rng.integers(1, 40))
+        elif layout == "duplicate" and i > 0:
+            offs[i], lens[i] = offs[i - 1], lens[i - 1]
+        elif layout == "far":
+            offs[i] += 8 << 20
     if layout == "reversed":
         offs = offs[::-1].copy()
-    host = _arena(rng, int(offs.max()) + 1500 + 4096)
-    p = _peso(tc, offs.astype(np.uint64), lens, rng)
-    out = tc.batch_peso(torch.from_numpy(host).cuda(), tc.descs_to_device(p), n, 1500 * n)
+    if layout == "shuffled":
+        perm = rng.permutation(n)
+        offs, lens = offs[perm], lens[perm]
+    host = _arena(rng, int((offs + lens).max()) + 4096)
+    p = _peso(tc, offs.astype(np.uint64), lens.astype(np.uint32), rng)
+    out = tc.batch_peso(torch.from_numpy(host).cuda(), tc.descs_to_device(p), n, int(lens.sum()))
+    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
+
+
+@pytest.mark.parametrize("hint_mean", [300, 1500, 9000])
+def test_packed_multi_pass_regions(tc, torch, oracle, packed, hint_mean):
+    """Regions longer than one pass (ranges up to 70 KB; K from a small hinted
+    mean), streamed pass by pass with the next pass's loads in flight; and
+    regions over the pass limit, range by range."""
+    rng = np.random.default_rng(hint_mean)
+    n = 900
+    lens = np.where(rng.random(n) < 0.2, rng.integers(20000, 70000, n), rng.integers(1, 3000, n)).astype(np.uint32)
+    start = int(rng.integers(0, 16))
+    host = _arena(rng, start + int(lens.sum()) + 4096)
+    p = _peso(tc, _packed_offs(lens, start), lens, rng)
+    out = tc.batch_peso(torch.from_numpy(host).cuda(), tc.descs_to_device(p), n, hint_mean * n)
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
 
 

@@ -689,7 +689,7 @@ __device__ __forceinline__ void pk_ranges(const uint8_t *__restrict__ arena, con
 
 constexpr uint32_t kPkMaxPasses = 64; // longer regions go range by range
 
-template <int MODE, int W = kPkWaves, int U = kPkLoads, bool PROBE = false, bool VDESC = false>
+template <int MODE, int W = kPkWaves, int U = kPkLoads, bool PROBE = false>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) void k_segments_pk(
     const uint8_t *__restrict__ arena, const void *__restrict__ descs, uint32_t n, uint16_t *__restrict__ out,
     uint32_t aux, uint32_t xg, uint32_t K)
@@ -708,18 +708,12 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     // the region: from the first range's first byte to the last range's end
     uint64_t r0, offl;
     uint32_t len0, lenl;
-    if constexpr (VDESC) { // measurement: the two descriptors by vector loads (lanes 0 and 1)
-        uint64_t o;
-        uint32_t ln;
-        desc_span<MODE>(descs, first + (lane == 1u ? kw - 1u : 0u), o, ln);
-        r0 = readlane64(o, 0);
-        offl = readlane64(o, 1);
-        len0 = (uint32_t)__builtin_amdgcn_readlane((int)ln, 0);
-        lenl = (uint32_t)__builtin_amdgcn_readlane((int)ln, 1);
-    } else {
-        desc_span<MODE>(descs, first, r0, len0);
-        desc_span<MODE>(descs, first + kw - 1u, offl, lenl);
-    }
+    // scalar loads: their short latency is what the data loads wait on
+    // (fetching the two descriptors with vector loads instead cut the read
+    // traffic from 1.0165x to 1.0018x the algorithmic bytes but ran 11 %
+    // slower, profiles/r03/packed/ab_vdesc_w8.txt)
+    desc_span<MODE>(descs, first, r0, len0);
+    desc_span<MODE>(descs, first + kw - 1u, offl, lenl);
     const uint64_t rend = offl + lenl;
     const uint8_t *p = arena + r0;
     const uint32_t s0 = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
@@ -2148,13 +2142,6 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
             hipLaunchKernelGGL((k_segments_pk<MODE_PESO, WW, UU>), gr, bl, 0, stream, a, descs, n, out, aux, xgc, Kc); \
         return hipGetLastError();                                                                               \
     }
-        if (const char *pe = getenv("TCSUM_PK_VDESC"); pe && atoi(pe) && W == (int)kPkWaves && Ul == (int)kPkLoads &&
-                                                      mode == MODE_PESO && !probe) {
-            const uint32_t Kc = K < 64u * kPkWaves ? K : 64u * kPkWaves;
-            hipLaunchKernelGGL((k_segments_pk<MODE_PESO, kPkWaves, kPkLoads, false, true>), dim3((n + Kc - 1) / Kc),
-                               dim3(kPkWaves * 64), 0, stream, a, descs, n, out, aux, xgc, Kc);
-            return hipGetLastError();
-        }
         TCSUM_PK(4, 3) TCSUM_PK(4, 2) TCSUM_PK(4, 4) TCSUM_PK(2, 3) TCSUM_PK(2, 4) TCSUM_PK(2, 6) TCSUM_PK(8, 3)
         TCSUM_PK(16, 4)
 #undef TCSUM_PK

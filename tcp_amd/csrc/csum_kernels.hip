@@ -616,8 +616,9 @@ __global__ __launch_bounds__(W * 64) void k_segments_wgx(const uint8_t *__restri
 // descriptor only (scalar loads), so the data loads wait on one descriptor
 // latency, as in the per-range kernels.
 //
-// A workgroup whose region is longer than 64 passes, or one of whose ranges
-// lies outside it (a shuffled batch), sums range by range with the widest lane
+// A workgroup whose region is longer than 64 passes, one of whose ranges lies
+// outside it (a shuffled batch) or is 128 KiB or longer (its word sum could
+// reach 2^32, where the u32 prefixes stop being exact), sums range by range with the widest lane
 // groups that give every range one: always correct, only slower.
 __device__ __forceinline__ uint32_t scan32(uint32_t x)
 {
@@ -745,7 +746,9 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     uint32_t xs = 0, xe = 0, q16 = 0;
     if (has) {
         d = load_desc<MODE>(descs, first + rr, mine);
-        const bool inside = !mine || (d.off >= r0 && d.off + d.len <= rend);
+        // P wraps mod 2^32 across passes, so a difference is exact only for a
+        // range whose word sum stays below 2^32: < 128 KiB (<= 65536 words)
+        const bool inside = !mine || (d.off >= r0 && d.off + d.len <= rend && d.len < (1u << 17));
         const bool ok = __ballot(!inside) == 0;
         xs = ok ? s0 + (uint32_t)(d.off - r0) : 0u;
         xe = ok ? xs + d.len : 0u;
@@ -2011,6 +2014,8 @@ Geometry pick_geometry(uint64_t mean_len)
         const uint64_t kmax = (uint64_t)kPkMaxRanges * w;
         if (k >= 3)
             g.packed = (int)(k > kmax ? kmax : k);
+        if (const char *pkk = getenv("TCSUM_PK_K"); pkk && atoi(pkk) > 0) // measurement: ranges per workgroup
+            g.packed = (int)((uint64_t)atoi(pkk) > kmax ? kmax : (uint64_t)atoi(pkk));
     }
     return g;
 }
@@ -2143,7 +2148,7 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
         return hipGetLastError();                                                                               \
     }
         TCSUM_PK(4, 3) TCSUM_PK(4, 2) TCSUM_PK(4, 4) TCSUM_PK(2, 3) TCSUM_PK(2, 4) TCSUM_PK(2, 6) TCSUM_PK(8, 3)
-        TCSUM_PK(16, 4)
+        TCSUM_PK(16, 4) TCSUM_PK(8, 4)
 #undef TCSUM_PK
         return hipErrorInvalidValue;
     }

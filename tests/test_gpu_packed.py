@@ -149,6 +149,23 @@ def test_packed_multi_pass_regions(tc, torch, oracle, packed, hint_mean):
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
 
 
+def test_packed_long_range_word_sum_past_2_32(tc, torch, oracle, packed):
+    """A 200-KB range of 0xFF bytes among 1500-B ones: its word sum exceeds
+    2^32, where the stream's u32 prefix differences stop being exact -- its
+    workgroup must sum range by range (ranges of 128 KiB and longer)."""
+    rng = np.random.default_rng(17)
+    n = 300
+    lens = np.full(n, 1500, np.uint32)
+    lens[[37, 150]] = [200000, 131071]
+    host = _arena(rng, int(lens.sum()) + 4096)
+    offs = _packed_offs(lens, 3)
+    for i in (37, 150):
+        host[int(offs[i]): int(offs[i]) + int(lens[i])] = 0xFF
+    p = _peso(tc, offs, lens, rng)
+    out = tc.batch_peso(torch.from_numpy(host).cuda(), tc.descs_to_device(p), n, 1500 * n)
+    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
+
+
 @pytest.mark.parametrize("comp", [0, 1])
 def test_packed_segments_mode(tc, torch, oracle, packed, comp):
     """tcsum_batch_segments (pktbuf_checksum16: u16 pre_sum, optional

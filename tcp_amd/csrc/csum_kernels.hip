@@ -656,52 +656,6 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t lane)
 constexpr uint32_t kPkWaves = 4, kPkLoads = 3; // 4 waves x 64 lanes x 3 loads x 16 B = 12 KiB per pass
 constexpr uint32_t kPkMaxRanges = 64; // ranges per wave of the workgroup (lane r of wave w: range 64w + r)
 
-// Descriptors base .. base + cnt - 1 (cnt <= 64, wave-uniform) into lanes
-// 0 .. cnt - 1 through scalar loads (measurement: TCSUM_PK_SD); other lanes
-// get a dead descriptor (len 0).
-template <int MODE>
-__device__ __forceinline__ SegDesc load_desc_uniform(const void *__restrict__ descs, uint32_t base, uint32_t cnt,
-                                                     uint32_t lane)
-{
-    constexpr uint32_t DW = MODE == MODE_PESO ? 6u : 4u;
-    const uint32_t *q = static_cast<const uint32_t *>(descs) + (uint64_t)__builtin_amdgcn_readfirstlane((int)base) * DW;
-    uint32_t x[DW];
-#pragma unroll
-    for (uint32_t k = 0; k < DW; ++k)
-        x[k] = 0;
-    // blocks of eight descriptors as one uniform struct read (s_load_dwordx16
-    // and friends, issued together); a last partial block one by one
-    struct Blk {
-        uint32_t w[8 * DW];
-    };
-    uint32_t r0 = 0;
-    for (; r0 + 8u <= cnt; r0 += 8) {
-        const Blk b = *reinterpret_cast<const Blk *>(q + r0 * DW);
-#pragma unroll
-        for (uint32_t i = 0; i < 8; ++i)
-#pragma unroll
-            for (uint32_t k = 0; k < DW; ++k)
-                x[k] = lane == r0 + i ? b.w[i * DW + k] : x[k];
-    }
-    for (uint32_t r = r0; r < cnt; ++r)
-#pragma unroll
-        for (uint32_t k = 0; k < DW; ++k)
-            x[k] = lane == r ? q[r * DW + k] : x[k];
-    SegDesc d;
-    d.off = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
-    d.len = x[2];
-    if constexpr (MODE == MODE_PESO) {
-        d.src = x[3];
-        d.dst = x[4];
-        d.proto = x[5] & 0xFFu;
-        d.pre = 0;
-    } else {
-        d.pre = x[3];
-        d.src = d.dst = d.proto = 0;
-    }
-    return d;
-}
-
 // off and len of descriptor i (the same 12 bytes lead both layouts); called
 // with a workgroup-uniform index, so it is a scalar load
 template <int MODE>
@@ -736,7 +690,7 @@ __device__ __forceinline__ void pk_ranges(const uint8_t *__restrict__ arena, con
 
 constexpr uint32_t kPkMaxPasses = 64; // longer regions go range by range
 
-template <int MODE, int W = kPkWaves, int U = kPkLoads, bool PROBE = false, bool SD = false>
+template <int MODE, int W = kPkWaves, int U = kPkLoads, bool PROBE = false>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) void k_segments_pk(
     const uint8_t *__restrict__ arena, const void *__restrict__ descs, uint32_t n, uint16_t *__restrict__ out,
     uint32_t aux, uint32_t xg, uint32_t K)
@@ -791,13 +745,7 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     SegDesc d{0, 0, 0, 0, 0, 0};
     uint32_t xs = 0, xe = 0, q16 = 0;
     if (has) {
-        if constexpr (SD)
-            d = load_desc_uniform<MODE>(descs, first + w * 64u,
-                                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(kw - w * 64u < 64u ? kw - w * 64u
-                                                                                                          : 64u)),
-                                        lane);
-        else
-            d = load_desc<MODE>(descs, first + rr, mine);
+        d = load_desc<MODE>(descs, first + rr, mine);
         // P wraps mod 2^32 across passes, so a difference is exact only for a
         // range whose word sum stays below 2^32: < 128 KiB (<= 65536 words)
         const bool inside = !mine || (d.off >= r0 && d.off + d.len <= rend && d.len < (1u << 17));
@@ -2199,13 +2147,6 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
             hipLaunchKernelGGL((k_segments_pk<MODE_PESO, WW, UU>), gr, bl, 0, stream, a, descs, n, out, aux, xgc, Kc); \
         return hipGetLastError();                                                                               \
     }
-        if (const char *ps1 = getenv("TCSUM_PK_SD"); ps1 && atoi(ps1) && W == (int)kPkWaves && Ul == (int)kPkLoads &&
-                                                    mode == MODE_PESO && !probe) {
-            const uint32_t Kc = K < 64u * kPkWaves ? K : 64u * kPkWaves;
-            hipLaunchKernelGGL((k_segments_pk<MODE_PESO, kPkWaves, kPkLoads, false, true>), dim3((n + Kc - 1) / Kc),
-                               dim3(kPkWaves * 64), 0, stream, a, descs, n, out, aux, xgc, Kc);
-            return hipGetLastError();
-        }
         TCSUM_PK(4, 3) TCSUM_PK(4, 2) TCSUM_PK(4, 4) TCSUM_PK(2, 3) TCSUM_PK(2, 4) TCSUM_PK(2, 6) TCSUM_PK(8, 3)
         TCSUM_PK(16, 4) TCSUM_PK(8, 4)
 #undef TCSUM_PK

@@ -2014,8 +2014,6 @@ Geometry pick_geometry(uint64_t mean_len)
         const uint64_t kmax = (uint64_t)kPkMaxRanges * w;
         if (k >= 3)
             g.packed = (int)(k > kmax ? kmax : k);
-        if (const char *pkk = getenv("TCSUM_PK_K"); pkk && atoi(pkk) > 0) // measurement: ranges per workgroup
-            g.packed = (int)((uint64_t)atoi(pkk) > kmax ? kmax : (uint64_t)atoi(pkk));
     }
     return g;
 }
@@ -2127,12 +2125,11 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
     if (g.packed > 0 && mode != MODE_EXACT) {
         const uint32_t K = (uint32_t)g.packed; // <= 64 per wave: capped by pick_geometry
         const uint8_t *a = static_cast<const uint8_t *>(arena);
-        // measurement: TCSUM_PK_W / TCSUM_PK_U workgroup waves and loads per lane
+        // TCSUM_PK_W / TCSUM_PK_U: the shapes the parity tests cover besides
+        // the default (measurement otherwise)
         const char *pw = getenv("TCSUM_PK_W");
         const char *pu = getenv("TCSUM_PK_U");
         const int W = pw ? atoi(pw) : (int)kPkWaves, Ul = pu ? atoi(pu) : (int)kPkLoads;
-        const char *pr = getenv("TCSUM_PK_PROBE"); // measurement: the loads only
-        const bool probe = mode == MODE_PESO && pr && atoi(pr);
         const uint32_t xgc = (uint32_t)g.xcd;
 #define TCSUM_PK(WW, UU)                                                                                        \
     if (W == WW && Ul == UU) {                                                                                  \
@@ -2140,15 +2137,11 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
         const dim3 gr((n + Kc - 1) / Kc), bl(WW * 64);                                                          \
         if (mode == MODE_SEG)                                                                                   \
             hipLaunchKernelGGL((k_segments_pk<MODE_SEG, WW, UU>), gr, bl, 0, stream, a, descs, n, out, aux, xgc, Kc); \
-        else if (probe)                                                                                         \
-            hipLaunchKernelGGL((k_segments_pk<MODE_PESO, WW, UU, true>), gr, bl, 0, stream, a, descs, n, out, aux, \
-                               xgc, Kc);                                                                         \
         else                                                                                                    \
             hipLaunchKernelGGL((k_segments_pk<MODE_PESO, WW, UU>), gr, bl, 0, stream, a, descs, n, out, aux, xgc, Kc); \
         return hipGetLastError();                                                                               \
     }
-        TCSUM_PK(4, 3) TCSUM_PK(4, 2) TCSUM_PK(4, 4) TCSUM_PK(2, 3) TCSUM_PK(2, 4) TCSUM_PK(2, 6) TCSUM_PK(8, 3)
-        TCSUM_PK(16, 4) TCSUM_PK(8, 4)
+        TCSUM_PK(4, 3) TCSUM_PK(8, 3) TCSUM_PK(16, 2)
 #undef TCSUM_PK
         return hipErrorInvalidValue;
     }

@@ -30,7 +30,7 @@ def tc(torch):
     return tcp_amd
 
 
-@pytest.fixture(params=[(8, 3), (16, 4), (4, 3)])
+@pytest.fixture(params=[(8, 3), (16, 2), (4, 3)])
 def packed(monkeypatch, request):
     """The packed kernel in three workgroup shapes (waves x loads per lane)."""
     w, u = request.param

@@ -204,3 +204,39 @@ def test_packed_full_mtu_config(tc, torch, oracle, packed):
     arena, descs = workload.materialize(b)
     out = tc.batch_peso(arena, descs, b.n, b.total_bytes).cpu().numpy()
     np.testing.assert_array_equal(out, oracle.batch_peso(arena.cpu().numpy(), b.descs, nthreads=16))
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_packed_fuzz(tc, torch, oracle, seed):
+    """Seeded fuzz over the default shape: batches built from runs of packed
+    ranges, gaps, overlaps, zero and 1..16-B ranges, long ranges (up to
+    200 KB), descending and shuffled stretches, at random arena phases, with
+    random length hints (K) -- checksum_peso and pktbuf_checksum16 (random
+    pre_sum and complement) against the oracle."""
+    rng = np.random.default_rng(4242 + seed)
+    n = int(rng.integers(200, 4000))
+    kind = rng.integers(0, 10, n)
+    lens = np.where(kind < 6, rng.integers(17, 3000, n),
+                    np.where(kind < 8, rng.integers(0, 17, n),
+                             np.where(kind < 9, rng.integers(3000, 20000, n), rng.integers(20000, 200000, n))))
+    step = lens + np.where(rng.random(n) < 0.2, rng.integers(-40, 64, n), 0)
+    offs = int(rng.integers(0, 64)) + np.concatenate([[0], np.cumsum(np.maximum(step[:-1], 0))])
+    for _ in range(int(rng.integers(0, 4))):  # a shuffled or reversed stretch
+        a = int(rng.integers(0, n - 1))
+        b = min(n, a + int(rng.integers(2, 200)))
+        idx = np.arange(a, b)
+        perm = idx[::-1] if rng.random() < 0.5 else rng.permutation(idx)
+        offs[a:b], lens[a:b] = offs[perm], lens[perm]
+    size = int((offs + lens).max()) + 4096
+    host = _arena(rng, size)
+    arena = torch.from_numpy(host).cuda()
+    hint = int(rng.choice([int(lens.sum()), 300 * n, 1500 * n, 4000 * n]))
+    p = _peso(tc, offs.astype(np.uint64), lens.astype(np.uint32), rng)
+    out = tc.batch_peso(arena, tc.descs_to_device(p), n, hint)
+    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
+    s = np.zeros(n, tc.SEG_DTYPE)
+    s["offset"], s["len"] = offs, lens
+    s["pre_sum"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    comp = int(rng.integers(0, 2))
+    out = tc.batch_segments(arena, tc.descs_to_device(s), n, comp, hint)
+    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_segments(host, s, comp, nthreads=8))

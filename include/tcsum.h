@@ -87,7 +87,9 @@ typedef struct tcsum_pkt {
 /* ------------------------------------------------ device-resident batches */
 
 /* out[i] = pktbuf_checksum16 over segs[i] with complement (0/1).
- * total_bytes_hint = sum of lens if known (selects the lane mapping), else 0. */
+ * total_bytes_hint = sum of lens if known, else 0 (read as 1500-B ranges): the
+ * mean length selects the kernel -- up to ~4 KiB, ranges listed in arena order
+ * are streamed as one region per workgroup (k_segments_pk), any order exact. */
 int tcsum_batch_segments(const void *arena /*[dev]*/, const tcsum_seg_t *segs /*[dev]*/,
                          uint32_t n, uint16_t *out /*[dev]*/, int complement,
                          uint64_t total_bytes_hint, void *stream);

@@ -498,6 +498,25 @@ static int run_tx(uint32_t c0, uint32_t c1, const char *name)
 }
 
 /* feed rx cases [c0, c1); check the verdicts; replies checked against the oracle fill */
+/* Until no frame has been injected for quiet_s (at most max_s): the replies
+ * the stack sends to received frames leave through xmit_thread after the
+ * receive phase that caused them has returned, and a fault phase that counts
+ * the frames injected since its start must not count them. */
+static void wait_tx_quiet(double quiet_s, double max_s)
+{
+    uint32_t last = pcapd_injected_count();
+    double t_last = now_s();
+    for (double t0 = now_s(); now_s() - t0 < max_s; usleep(1000)) {
+        const uint32_t c = pcapd_injected_count();
+        if (c != last) {
+            last = c;
+            t_last = now_s();
+        } else if (now_s() - t_last >= quiet_s) {
+            return;
+        }
+    }
+}
+
 static int run_rx(uint32_t c0, uint32_t c1, const char *name)
 {
     uint32_t v0 = verdicts(), fed = 0;
@@ -520,6 +539,13 @@ static int run_rx(uint32_t c0, uint32_t c1, const char *name)
                   fed);
             return 0;
         }
+        /* the replies this group caused hold pool blocks until xmit_thread has
+         * sent them: let them leave before the next group needs blocks, or
+         * recv_thread's pktbuf_alloc fails and drops a frame (the reference's
+         * pool is 100 blocks, net_cfg.h) */
+        for (double tq = now_s(); fixq_count(&wire->out_q) > 0 && now_s() - tq < 5.0;)
+            usleep(200);
+        wait_tx_quiet(0.003, 2.0);
     }
     const double dt = now_s() - t0;
     uint32_t bad = 0, first = 0, hist[32] = {0};
@@ -620,6 +646,7 @@ static void run_faults(void)
     net_csum_gpu_stats_t s0, s1;
 
     /* (1) the engine fails one tx fill */
+    wait_tx_quiet(0.2, 10.0);
     stats(&s0);
     uint64_t inj_fail0 = pcapd_inject_failures();
     tx_wait_t w = {pcapd_injected_count(), G + (uint32_t)inj_fail0, s0.tx_dropped};
@@ -652,6 +679,7 @@ static void run_faults(void)
           "symbols, all %u verdicts equal", (unsigned long long)(s1.rx_fail_batches - s0.rx_fail_batches), R);
 
     /* (3) one pcap_inject fails: the reference's own handling (logged, frame lost) */
+    wait_tx_quiet(0.2, 10.0); /* the replies to the fault_rx frames leave first */
     stats(&s0);
     w.base = pcapd_injected_count();
     w.dropped0 = s0.tx_dropped;

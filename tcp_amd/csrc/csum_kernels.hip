@@ -788,7 +788,7 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
         }
         if (l == 0)
             subtot[sub] = a;
-        if (pass + 1u < npass) { // the next pass's bytes stream during the barrier and wave 0's sums
+        if (pass + 1u < npass) { // the next pass's bytes stream during the barrier and the prefix sums
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u) {
                 const uint32_t c = cb + CH + sub * SR + u * 32u + l;

@@ -225,13 +225,8 @@ def probe_compare(torch, tc, batch, product, arena, steps, rounds=5, descs=None)
     if tile_ok:
         kinds["tile"] = lambda: tc.probe_tile(arena, nbytes, g, u, sink)
 
-        def tile_dep():  # each unit's loads behind one dependent 16-B read, like the product's descriptor
-            os.environ["TCSUM_PROBE_DEP"] = "1"
-            try:
-                tc.probe_tile(arena, nbytes, g, u, sink)
-            finally:
-                del os.environ["TCSUM_PROBE_DEP"]
-        kinds["tile_dep"] = tile_dep
+        # each unit's loads behind one dependent 16-B read, like the product's descriptor
+        kinds["tile_dep"] = lambda: tc.probe_tile(arena, nbytes, g, u, sink, dep=True)
     if batch.kind == "peso" and descs is not None:
         kinds["segments"] = lambda: tc.probe_segments(arena, descs, batch.n, batch.total_bytes, sink)
     elif descs is not None:

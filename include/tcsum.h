@@ -23,6 +23,11 @@
  *     yields network-order bytes (net/src/tools.c:24-54).
  *   - Return codes are the reference's net_err_t values
  *     (net/net/net_err.h:8-29): 0 = OK, negative = error.
+ *   - One arena per batch: every byte from a batch's lowest range start to
+ *     its highest range end must be readable device memory (one
+ *     allocation).  The stream kernels read the bytes between neighbouring
+ *     ranges -- padding, gaps -- and discard them; ranges may sit anywhere
+ *     in that span, in any order, overlap or repeat.
  */
 #ifndef TCSUM_H
 #define TCSUM_H

@@ -1,8 +1,10 @@
 /*
- * tcsum_synth.h -- on-device synthetic packet batches and a read probe, for
- * tests and bench.py.
+ * tcsum_synth.h -- libtcsum_bench.so: on-device synthetic packet batches and
+ * the load probes, for tests and bench.py.
  *
- * Not part of the checksum path.  The byte stream is the one the CPU oracle
+ * Not part of the checksum path: a separate library (tcp_amd/csrc/
+ * bench_kernels.hip), so that libtcsum.so holds only the kernels its router
+ * launches.  The byte stream is the one the CPU oracle
  * reproduces (oracle/csum_oracle.c: orc_synth_fill): byte p of the stream is
  * byte (p & 7) of splitmix64(seed + (p >> 3)), so host and device see the same
  * packets without a transfer.
@@ -42,17 +44,18 @@ int tcsum_probe_read(const void *p /*[dev]*/, uint64_t nbytes, uint32_t *sink /*
  * share a unit of lanes*loads consecutive 16-B chunks (lane l loads chunks
  * u*lanes + l), 256/lanes units per workgroup, workgroups in the product's
  * XCD-grouped order (k_segments / k_ipv4 / k_segments_wg minus descriptors,
- * masking and sums).  lanes x loads in {16,32} x {4,6,8}, 64 x {4,8},
- * 256 x {4,8,16}; otherwise TCSUM_ERR_PARAM. */
-int tcsum_probe_tile(const void *p /*[dev]*/, uint64_t nbytes, int lanes, int loads, uint32_t *sink /*[dev]*/,
-                     void *stream);
+ * masking and sums).  dep != 0: each unit's loads wait behind one dependent
+ * 16-B read, as the product's wait for their descriptor.  lanes x loads in
+ * {16,32} x {4,6,8}, 64 x {4,8}, 256 x {4,8,16}; otherwise TCSUM_ERR_PARAM. */
+int tcsum_probe_tile(const void *p /*[dev]*/, uint64_t nbytes, int lanes, int loads, int dep,
+                     uint32_t *sink /*[dev]*/, void *stream);
 
 /* tcsum_batch_peso's loads and nothing else: the same descriptors, lanes,
  * edge / interior cache policies and workgroup order, with the sums, the
  * reduction and the result store replaced by an XOR fold -- the rate the
- * checksum kernel would run at if its arithmetic were free.  Geometries the
- * batch call picks for the configs (16 x 3..8, 32 x 4/6, 8 x 4, 256 x 16);
- * otherwise TCSUM_ERR_PARAM. */
+ * checksum kernel would run at if its arithmetic were free.  It follows the
+ * route libtcsum.so's router takes (tcsum_debug_route): the packed stream,
+ * the TSO workgroup shape or a per-range shape. */
 int tcsum_probe_segments(const void *arena /*[dev]*/, const tcsum_peso_t *segs /*[dev]*/, uint32_t n,
                          uint64_t total_bytes_hint, uint32_t *sink /*[dev]*/, void *stream);
 
@@ -65,7 +68,7 @@ int tcsum_probe_segments(const void *arena /*[dev]*/, const tcsum_peso_t *segs /
  * fill's own rules) and then the fill's k_tx_scatter storing the fields; the
  * stored values are the XOR fold, so every IPv4 / L4 checksum field of the
  * batch is left holding junk (the arena is written despite the const).
- * Geometries 16 x 3..8, 32 x 4/6, 64 x 16; else TCSUM_ERR_PARAM. */
+ * The per-packet shape k_ipv4 takes for the mean length. */
 int tcsum_probe_ipv4(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,
                      uint64_t total_bytes_hint, int mode, uint32_t *sink /*[dev]*/, void *stream);
 

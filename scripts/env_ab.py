@@ -1,9 +1,12 @@
-"""A/B of launch-time switches (environment variables read per launch by
-libtcsum.so) in ONE process: interleaved rounds, median us per launch, and
-every variant's results must equal the default's.
+"""A/B of route knobs (include/tcsum_debug.h, set per variant with
+tcsum_debug_set; round 4 replaced the environment variables rounds 1-3 read)
+in ONE process: interleaved rounds, median us per launch, and every
+variant's results must equal the default's.
 
-  python scripts/env_ab.py CONFIG VAR=VALUE[,VAR=VALUE...] ...
-  e.g. python scripts/env_ab.py mixed_tx TCSUM_TX_SPLIT=0
+  python scripts/env_ab.py CONFIG KNOB=VALUE[,KNOB=VALUE...] ...
+  e.g. python scripts/env_ab.py mixed_tx tx_split=0
+  (the old names TCSUM_G / TCSUM_U / TCSUM_XCD / TCSUM_PACKED / TCSUM_TX_SPLIT
+  are accepted and mapped to lanes / loads / xcd / packed / tx_split)
 CONFIG: mtu | tso | mixed | mixed_tx | mixed_rx | mixed_txo
 """
 import os
@@ -40,17 +43,14 @@ def run():
         tc.batch_ipv4(arena, descs, n, b.total_bytes, out=out, want_flags=False)
 
 
+OLD = {"TCSUM_G": "lanes", "TCSUM_U": "loads", "TCSUM_XCD": "xcd", "TCSUM_PACKED": "packed",
+       "TCSUM_TX_SPLIT": "tx_split", "TCSUM_FLAT": "flat"}
+
+
 def with_env(env, fn):
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
+    knobs = {OLD.get(k, k): int(v) for k, v in env.items()}
+    with tc.debug(**knobs):
         return fn()
-    finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
 
 
 # a tx fill writes the packets: every variant, run on the unfilled arena, must

@@ -1,13 +1,15 @@
 """tcp_amd -- MI355X-native Internet-checksum engine for the wj9806/tcp stack.
 
 The product is tcp_amd/libtcsum.so (C ABI: include/tcsum.h,
-include/tcsum_legacy.h); this package is its Python face.
+include/tcsum_legacy.h, include/tcsum_debug.h); this package is its Python
+face.  Synthetic batches and load probes come from libtcsum_bench.so
+(include/tcsum_synth.h).
 """
 from .csum import (PESO_DTYPE, PKT_DTYPE, SEG_DTYPE, batch_ipv4, batch_ipv4_rx_verify, batch_ipv4_tx_fill,
                    batch_ipv4_tx_offload, tx_apply_batch, batch_peso, batch_segments,
                    checksum16, checksum_peso, descs_to_device, device_count, host_batch_peso, host_batch_peso_multi,
                    HostArena, host_register, host_unregister, host_batch_ipv4, host_batch_ipv4_rx_verify, host_batch_ipv4_tx_fill,
-                   pick_geometry, pktbuf_checksum16, plat_init, probe_ipv4, probe_read, probe_segments, probe_tile, queue_server, release, call_server, synth_fill,
+                   pick_geometry, route, debug, debug_get, debug_set, pktbuf_checksum16, plat_init, probe_ipv4, probe_read, probe_segments, probe_tile, queue_server, release, call_server, synth_fill,
                    synth_ipv4)
 from .pktbuf import IpAddr, PktBuf
 from . import pcap, workload
@@ -16,6 +18,7 @@ __all__ = [
     "checksum16", "checksum_peso", "pktbuf_checksum16", "batch_segments", "batch_peso", "batch_ipv4",
     "batch_ipv4_tx_fill", "batch_ipv4_tx_offload", "tx_apply_batch", "batch_ipv4_rx_verify",
     "host_batch_peso", "host_batch_peso_multi", "HostArena", "host_register", "host_unregister", "host_batch_ipv4", "host_batch_ipv4_tx_fill", "host_batch_ipv4_rx_verify",
-    "synth_fill", "synth_ipv4", "descs_to_device", "device_count", "pick_geometry",
+    "synth_fill", "synth_ipv4", "descs_to_device", "device_count", "pick_geometry", "route", "debug",
+    "debug_get", "debug_set",
     "plat_init", "probe_ipv4", "probe_read", "probe_segments", "probe_tile", "queue_server", "release", "call_server", "PktBuf", "IpAddr", "SEG_DTYPE", "PESO_DTYPE", "PKT_DTYPE", "pcap", "workload",
 ]

@@ -1,7 +1,9 @@
 """ctypes binding of libtcsum.so (the C ABI declared in include/*.h).
 
-The library is loaded from this package directory only; if it is missing the
-import of any compute entry point raises -- there is no CPU fallback.
+The libraries are loaded from this package directory only; if one is missing
+the import of any compute entry point raises -- there is no CPU fallback.
+libtcsum.so is the product; libtcsum_bench.so (include/tcsum_synth.h) holds
+the synthetic-data and load-probe kernels the tests and bench.py use.
 """
 from __future__ import annotations
 
@@ -53,16 +55,24 @@ SIGNATURES = {
     "tcsum_device_count": (_I, []),
     "tcsum_pick_geometry": (None, [_U64, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "tcsum_version": (ctypes.c_char_p, []),
+    "tcsum_release": (_I, [_I]),
     # tcsum_legacy.h
     "checksum16": (_U16, [_I, _V, _U16, _U32, _I]),
     "checksum_peso": (_U16, [_V, _V, _V, ctypes.c_uint8]),
     "pktbuf_checksum16": (_U16, [_V, _I, _I, _I]),
-    # tcsum_synth.h
+    # tcsum_debug.h (tests and measurement only)
+    "tcsum_debug_set": (_I, [ctypes.c_char_p, ctypes.c_int64]),
+    "tcsum_debug_get": (ctypes.c_int64, [ctypes.c_char_p]),
+    "tcsum_debug_route": (None, [_U64, ctypes.POINTER(ctypes.c_int32)]),
+}
+
+# tcsum_synth.h: libtcsum_bench.so (synthetic batches, load probes)
+BENCH_LIB_PATH = os.path.join(PKG, "libtcsum_bench.so")
+BENCH_SIGNATURES = {
     "tcsum_synth_fill": (_I, [_V, _U64, _U64, _U64, _V]),
     "tcsum_synth_ipv4": (_I, [_V, _V, _U32, _U64, _V]),
     "tcsum_probe_read": (_I, [_V, _U64, _V, _V]),
-    "tcsum_probe_tile": (_I, [_V, _U64, _I, _I, _V, _V]),
-    "tcsum_release": (_I, [_I]),
+    "tcsum_probe_tile": (_I, [_V, _U64, _I, _I, _I, _V, _V]),
     "tcsum_probe_segments": (_I, [_V, _V, _U32, _U64, _V, _V]),
     "tcsum_probe_ipv4": (_I, [_V, _V, _U32, _U64, _I, _V, _V]),
 }
@@ -74,6 +84,7 @@ PCAP_SIGNATURES = {
 }
 
 _lib = None
+_bench_lib = None
 _pcap_lib = None
 
 
@@ -99,6 +110,22 @@ def lib() -> ctypes.CDLL:
             f.argtypes = args
         _lib = L
     return _lib
+
+
+def bench_lib() -> ctypes.CDLL:
+    """The measurement / synthetic-data library (include/tcsum_synth.h)."""
+    global _bench_lib
+    if _bench_lib is None:
+        lib()  # its dependency, bound to torch's HIP runtime first
+        if not os.path.exists(BENCH_LIB_PATH):
+            raise RuntimeError(f"{BENCH_LIB_PATH} is missing: build it with __graft_entry__.build()")
+        L = ctypes.CDLL(BENCH_LIB_PATH)
+        for name, (res, args) in BENCH_SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _bench_lib = L
+    return _bench_lib
 
 
 def pcap_lib() -> ctypes.CDLL:

@@ -1,0 +1,499 @@
+// bench_kernels.hip -- libtcsum_bench.so: measurement and test-data kernels
+// (include/tcsum_synth.h).  Not part of the checksum path: the load-only
+// probes that price the product kernels' own load shapes, the plain read
+// probes of the roofline's achievable side, and the on-device synthetic
+// packet generator the tests, smoke() and bench.py share with the oracle.
+#include "csum_device.h"
+#include "tcsum_debug.h"
+#include "tcsum_synth.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+namespace tcsum {
+
+// k_ipv4's loads and nothing else (measurement: tcsum_probe_ipv4): the 16-B
+// descriptor, the two or three default-policy header chunks (four for rx),
+// the line-aligned nontemporal data pass -- same lanes, same clamping, same
+// XCD order -- folded by XOR into a sink stored on a 2^-32 fluke.  The rate
+// the IPv4 kernels would run at if their arithmetic and stores were free.
+// PM_TX adds exactly the deferred tx fill's writes (the ceiling for a kernel
+// that must write): every packet's 8 bytes of scratch -- a value word and the
+// field positions k_ipv4<IP_TX> derives from the header (same rules) -- and
+// then k_tx_scatter, the product's own scatter, writing the fields.  The
+// values are the XOR fold, so the packets' checksum fields end up junk.
+enum ProbeMode : int { PM_SUMS = 0, PM_RX = 1, PM_TX = 2 };
+template <int G, int U, int PM>
+__global__ __launch_bounds__(256) void k_probe_ipv4(const uint8_t *__restrict__ arena,
+                                                    const tcsum_pkt_t *__restrict__ pkts, uint32_t n,
+                                                    uint32_t *__restrict__ sink, uint32_t xg,
+                                                    uint32_t *__restrict__ vals, uint32_t *__restrict__ posv)
+{
+    constexpr bool RX = PM == PM_RX;
+    const uint32_t gl = threadIdx.x & (G - 1);
+    const uint32_t pk = xcd_block(blockIdx.x, gridDim.x, xg) * (256u / G) + threadIdx.x / G;
+    const bool live = pk < n;
+    const u32x4 dv = *reinterpret_cast<const u32x4 *>(pkts + (live ? pk : 0u));
+    const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+    const uint32_t frame = live ? dv.z : 0u;
+    const bool big_enough = frame >= 20;
+    const uint8_t *pp = arena + off;
+    const uintptr_t start = reinterpret_cast<uintptr_t>(pp);
+    const uint32_t s0 = (uint32_t)(start & 15u);
+    const u32x4 *base = reinterpret_cast<const u32x4 *>(pp - s0);
+    const uint32_t frame_ld = frame < 65600u ? frame : 65600u;
+    const uint32_t nch = big_enough ? (frame_ld + s0 + 15) >> 4 : 0u;
+    const u32x4 *hb = big_enough ? base : &g_zero_chunk;
+    const u32x4 h0 = load16<false>(hb);
+    const u32x4 h1 = load16<false>(hb + (big_enough ? 1u : 0u));
+    u32x4 h2;
+    if constexpr (RX) {
+        const u32x4 c2 = load16<false>(nch > 2 ? base + 2 : &g_zero_chunk);
+        const u32x4 c3 = load16<false>(nch > 3 && s0 >= 12 ? base + 3 : &g_zero_chunk);
+        h2 = c2 ^ c3;
+    } else {
+        h2 = load16<false>(hb + (big_enough ? (s0 > 12 ? 2u : 1u) : 0u));
+    }
+    const uint32_t sl = (uint32_t)(start & 127u);
+    const uint32_t dch = big_enough ? (frame_ld + sl + 15) >> 4 : 0u;
+    const u32x4 *dbase = dch ? reinterpret_cast<const u32x4 *>(pp - sl) : &g_zero_chunk;
+    const uint32_t dlast = dch ? dch - 1u : 0u;
+    u32x4 x = h0 ^ h1 ^ h2;
+    for (uint32_t b0 = 0; b0 < (dch ? dch : 1u); b0 += G * U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t idx = b0 + u * G + gl;
+            x ^= load16<true>(dbase + (idx < dch ? idx : dlast));
+        }
+    }
+    const uint32_t acc = x.x ^ x.y ^ x.z ^ x.w;
+    if constexpr (PM == PM_TX) {
+        // the positions k_ipv4<IP_TX> stores with IP_OPT_DEFER (ipv4_packet)
+        const Hdr5 hd = header_dwords(h0, h1, h2, s0);
+        const uint32_t b0h = hd.d0 & 0xFFu, ihl4 = (b0h & 0xFu) << 2;
+        const uint32_t tl = (((hd.d0 >> 16) & 0xFFu) << 8) | (hd.d0 >> 24);
+        const uint32_t b6 = (hd.d1 >> 16) & 0xFFu, b7 = hd.d1 >> 24;
+        const bool frag = (b6 & 0x20u) || (((b6 & 0x1Fu) << 8) | b7);
+        const uint32_t proto = (hd.d2 >> 8) & 0xFFu;
+        const bool bad = !big_enough || (b0h >> 4) != 4 || ihl4 < 20 || ihl4 > frame || tl < 20 || tl > frame ||
+                         tl < ihl4;
+        uint32_t hl = ihl4 < 20 ? 20u : ihl4;
+        hl = hl > frame ? frame : hl;
+        uint32_t end = tl < hl ? hl : tl;
+        end = end > frame ? frame : end;
+        uint32_t min_l4;
+        const uint32_t fld = l4_field(proto, min_l4);
+        const bool field_on = !bad && !frag && fld && end - hl >= min_l4;
+        if (live && gl == 0) {
+            vals[pk] = acc;
+            posv[pk] = bad ? 0u : (1u << 16) | (field_on ? hl + fld : 0u);
+        }
+    } else if (acc == 0x9E3779B9u) {
+        sink[0] = acc;
+    }
+}
+
+// ---------------------------------------------------------------- synthetic
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_synth_fill(uint8_t *__restrict__ arena, uint64_t nbytes,
+                                                    uint64_t word_base, uint64_t seed)
+{
+    const uint64_t units = (nbytes + 15) / 16;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < units; i += (uint64_t)gridDim.x * 256ull) {
+        const uint64_t w0 = splitmix64(seed + word_base + 2 * i);
+        const uint64_t w1 = splitmix64(seed + word_base + 2 * i + 1);
+        if (16 * i + 16 <= nbytes) {
+            uint64_t *p = reinterpret_cast<uint64_t *>(arena + 16 * i);
+            p[0] = w0;
+            p[1] = w1;
+        } else {
+            for (uint64_t b = 16 * i; b < nbytes; ++b)
+                arena[b] = (uint8_t)((b - 16 * i < 8 ? w0 : w1) >> (8 * (b & 7)));
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_synth_ipv4(uint8_t *__restrict__ arena,
+                                                    const tcsum_pkt_t *__restrict__ pkts,
+                                                    uint32_t n, uint64_t seed)
+{
+    const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t len = pkts[i].len;
+    if (len < 20)
+        return;
+    uint8_t *p = arena + pkts[i].offset;
+    const uint64_t h = splitmix64(seed ^ (0x1000000ull + i));
+    const uint64_t a = splitmix64(h);
+    const uint32_t tl = len > 0xFFFFu ? 0xFFFFu : len;
+    p[0] = 0x45;
+    p[1] = 0;
+    p[2] = (uint8_t)(tl >> 8);
+    p[3] = (uint8_t)tl;
+    p[4] = (uint8_t)(h >> 8);
+    p[5] = (uint8_t)h;
+    p[6] = 0x40;
+    p[7] = 0;
+    p[8] = 64;
+    p[9] = (h >> 20) & 1u ? 17 : 6;
+    p[10] = 0;
+    p[11] = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        p[12 + k] = (uint8_t)(a >> (8 * k));
+    // L4 header fields the receive gates read (tcp_in.c:87-103, udp.c:337):
+    // nonzero ports; TCP data offset 5 with ACK (+ PSH half the time); UDP
+    // length.  The rest of the L4 bytes stay the synthetic stream.
+    if (len < 40u) // room for a TCP header (the configs start at 64 B)
+        return;
+    const uint64_t b = splitmix64(a);
+    const uint32_t sport = 1u + (uint32_t)(b % 65535u), dport = 1u + (uint32_t)((b >> 20) % 65535u);
+    p[20] = (uint8_t)(sport >> 8);
+    p[21] = (uint8_t)sport;
+    p[22] = (uint8_t)(dport >> 8);
+    p[23] = (uint8_t)dport;
+    if (p[9] == 6) {
+        p[32] = 0x50;
+        p[33] = (b >> 40) & 1u ? 0x18 : 0x10;
+    } else {
+        const uint32_t ul = tl - 20u;
+        p[24] = (uint8_t)(ul >> 8);
+        p[25] = (uint8_t)ul;
+    }
+}
+
+// ---------------------------------------------------------------- read probe
+//
+// The "achievable" side of the roofline: a plain streaming read of the same
+// bytes with the same load shape (nontemporal dwordx4, one contiguous
+// 64*U-chunk tile per wave), XOR-folded so the loads stay live; a store only
+// happens if the fold hits a magic value.
+template <int U, bool NT = true>
+__global__ __launch_bounds__(256) void k_probe_read(const u32x4 *__restrict__ p, uint64_t nchunks,
+                                                    uint32_t *__restrict__ sink, uint32_t xg)
+{
+    const uint64_t wave = (xcd_block(blockIdx.x, gridDim.x, xg) * 256ull + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t base = wave * 64ull * U;
+    uint32_t acc = 0;
+    u32x4 v[U];
+    // unconditional loads, index clamped to the last chunk (as the checksum
+    // kernels do): a bounds test per load would put each one behind its own
+    // exec-mask branch
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t idx = base + u * 64ull + lane;
+        v[u] = load16<NT>(p + (idx < nchunks ? idx : nchunks - 1));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    if (acc == 0x9E3779B9u)
+        sink[0] = acc;
+}
+
+// The same plain read in the product's own tile shape: G lanes share a
+// "unit" of G*U consecutive chunks (lane gl loads chunks u*G + gl, u < U),
+// 256/G units per workgroup, workgroups in the product's XCD-grouped order --
+// k_segments / k_ipv4 minus descriptors, edge masking and sums (G = 256: one
+// unit per workgroup, k_segments_wg's shape).  The ceiling the product kernel
+// is compared with, on the same bytes.
+// DEP: each unit first reads a 16-B "descriptor" (its own first chunk, so no
+// extra bytes) and issues the tile's loads only behind it, as the product
+// kernels wait for their descriptor before the data loads.
+template <int G, int U, bool DEP>
+__global__ __launch_bounds__(256) void k_probe_tile(const u32x4 *__restrict__ p, uint64_t nchunks,
+                                                    uint32_t *__restrict__ sink, uint32_t xg)
+{
+    const uint64_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    const uint32_t gl = threadIdx.x & (G - 1);
+    uint64_t base = (blk * (256u / G) + threadIdx.x / G) * (uint64_t)(G * U);
+    if constexpr (DEP) {
+        const u32x4 d = p[base < nchunks ? base : nchunks - 1];
+        uint32_t zero;
+        asm volatile("v_and_b32 %0, 0, %1" : "=v"(zero) : "v"(d.x)); // 0, but only once d is here
+        base += zero;
+    }
+    uint32_t acc = 0;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) { // unconditional, clamped (see k_probe_read)
+        const uint64_t idx = base + (uint64_t)(u * G) + gl;
+        v[u] = load16<true>(p + (idx < nchunks ? idx : nchunks - 1));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    if (acc == 0x9E3779B9u)
+        sink[0] = acc;
+}
+
+// The product's own load shape and nothing else: k_segments / k_segments_wg
+// on the real checksum_peso descriptors -- descriptor, then the range's
+// default-policy edge chunks and nontemporal interior chunks, same lanes, same
+// XCD order -- with the sums, the group reduction and the result store
+// replaced by an XOR fold (stored only on a 2^-32 fluke).  What the kernel
+// would run at if its arithmetic were free.
+template <int G, int U>
+__global__ __launch_bounds__(256) void k_probe_desc(const uint8_t *__restrict__ arena,
+                                                    const void *__restrict__ descs, uint32_t n,
+                                                    uint32_t *__restrict__ sink, uint32_t xg)
+{
+    const uint32_t gl = threadIdx.x & (G - 1);
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    const uint32_t seg = G == 256 ? blk : blk * (256u / G) + threadIdx.x / G;
+    const SegDesc d = load_desc<MODE_PESO>(descs, seg, seg < n);
+    Frame<U> f;
+    frame_issue<G, U>(f, arena, d.off, d.len, gl);
+    issue_fence();
+    uint32_t acc = f.ev.x ^ f.ev.y ^ f.ev.z ^ f.ev.w;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        acc ^= f.v[u].x ^ f.v[u].y ^ f.v[u].z ^ f.v[u].w;
+    for (uint32_t b0 = G * U; b0 < f.ni; b0 += G * U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = b0 + u * G + gl;
+            const u32x4 w = load16<true>(f.ibase + (j < f.ni ? j : f.ilast));
+            acc ^= w.x ^ w.y ^ w.z ^ w.w;
+        }
+    }
+    if (acc == 0x9E3779B9u)
+        sink[0] = acc;
+}
+
+// The product's route (libtcsum.so's router with its debug knobs applied).
+static Geometry route(uint64_t mean_len)
+{
+    int32_t r[5];
+    tcsum_debug_route(mean_len, r);
+    return Geometry{r[0], r[1], r[2], r[3], r[4]};
+}
+
+static hipError_t launch_probe_desc(const void *arena, const void *descs, uint32_t n, uint64_t mean_len,
+                                    uint32_t *sink, hipStream_t stream)
+{
+    if (n == 0)
+        return hipSuccess;
+    const Geometry g = route(mean_len);
+    const uint32_t xg = (uint32_t)g.xcd;
+    const uint8_t *a = static_cast<const uint8_t *>(arena);
+    if (g.packed > 0) { // k_segments_pk's loads
+        const uint32_t K = (uint32_t)g.packed < kPkMaxRanges * kPkWaves ? (uint32_t)g.packed
+                                                                          : kPkMaxRanges * kPkWaves;
+        if ((n + K - 1) / K >= (1u << 24))
+            return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_segments_pk<MODE_PESO, kPkWaves, kPkLoads, true>), dim3((n + K - 1) / K),
+                           dim3(kPkWaves * 64), 0, stream, a, descs, n, reinterpret_cast<uint16_t *>(sink), 0u, xg,
+                           K);
+        return hipGetLastError();
+    }
+    if (g.lanes == 1024 && g.loads == 4) { // k_segments_wgx<16, 32, 4>'s loads
+        if (n >= (1u << 22))
+            return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_segments_wgx<16, 32, 4, MODE_PESO, true>), dim3(n), dim3(1024), 0, stream, a, descs, n,
+                           reinterpret_cast<uint16_t *>(sink), 0u, xg);
+        return hipGetLastError();
+    }
+#define TCSUM_PD(GG, UU)                                                                                     \
+    if (g.lanes == GG && g.loads == UU) {                                                                    \
+        const uint32_t per_block = GG == 256 ? 1u : 256u / GG;                                               \
+        if ((n + per_block - 1) / per_block >= (1u << 24))                                                   \
+            return hipErrorInvalidValue;                                                                     \
+        hipLaunchKernelGGL((k_probe_desc<GG, UU>), dim3((n + per_block - 1) / per_block), dim3(256), 0, stream, a, \
+                           descs, n, sink, xg);                                                              \
+        return hipGetLastError();                                                                            \
+    }
+    TCSUM_PD(4, 1) TCSUM_PD(4, 2) TCSUM_PD(8, 4) TCSUM_PD(16, 3) TCSUM_PD(16, 4) TCSUM_PD(16, 6) TCSUM_PD(16, 8)
+    TCSUM_PD(32, 6) TCSUM_PD(256, 16)
+#undef TCSUM_PD
+    return hipErrorInvalidValue;
+}
+
+static hipError_t launch_probe_tile(const void *p, uint64_t nbytes, int G, int U, bool dep, uint32_t *sink,
+                                    hipStream_t stream)
+{
+    const uint64_t nchunks = nbytes / 16;
+    if (nchunks == 0)
+        return hipSuccess;
+    const uint32_t xg = (uint32_t)route(1500).xcd; // the product's order
+    const dim3 grid((uint32_t)((nchunks + 256ull * U - 1) / (256ull * U)));
+    const u32x4 *q = static_cast<const u32x4 *>(p);
+#define TCSUM_PT(GG, UU)                                                                         \
+    if (G == GG && U == UU) {                                                                  \
+        if (dep)                                                                               \
+            hipLaunchKernelGGL((k_probe_tile<GG, UU, true>), grid, dim3(256), 0, stream, q, nchunks, sink, xg); \
+        else                                                                                   \
+            hipLaunchKernelGGL((k_probe_tile<GG, UU, false>), grid, dim3(256), 0, stream, q, nchunks, sink, xg); \
+        return hipGetLastError();                                                              \
+    }
+    TCSUM_PT(16, 4) TCSUM_PT(16, 6) TCSUM_PT(16, 8) TCSUM_PT(32, 4) TCSUM_PT(32, 6) TCSUM_PT(32, 8)
+    TCSUM_PT(64, 4) TCSUM_PT(64, 8) TCSUM_PT(256, 4) TCSUM_PT(256, 8) TCSUM_PT(256, 16)
+#undef TCSUM_PT
+    return hipErrorInvalidValue;
+}
+
+// Plain streaming read: 4 nontemporal 16-B loads per lane, one contiguous
+// 1-KiB tile per wave, dispatch order -- the fastest plain read measured
+// (profiles/r01/probe_variants.txt, xcd_tune.txt).
+static hipError_t launch_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, hipStream_t stream)
+{
+    const uint64_t nchunks = nbytes / 16;
+    if (nchunks == 0)
+        return hipSuccess;
+    const uint64_t per_block = 4ull * 64 * 4;
+    const dim3 grid((uint32_t)((nchunks + per_block - 1) / per_block));
+    hipLaunchKernelGGL(k_probe_read<4>, grid, dim3(256), 0, stream, static_cast<const u32x4 *>(p), nchunks, sink, 1u);
+    return hipGetLastError();
+}
+
+static hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t mean_len,
+                                    int mode, uint32_t *sink, hipStream_t stream)
+{
+    if (n == 0)
+        return hipSuccess;
+    if (mode < PM_SUMS || mode > PM_TX)
+        return hipErrorInvalidValue;
+    Geometry g = route(mean_len); // launch_ipv4's geometry rules
+    if (g.lanes < 16)
+        g.lanes = 16;
+    if (g.lanes > 64)
+        g.lanes = 64;
+    if (mode == PM_RX && g.lanes == 32 && tcsum_debug_get("lanes") < 0)
+        g.lanes = 16;
+    const uint32_t per_block = 256u / (uint32_t)g.lanes;
+    const uint64_t blocks = ((uint64_t)n + per_block - 1) / per_block;
+    if (blocks >= (1u << 24))
+        return hipErrorInvalidValue;
+    const uint8_t *a = static_cast<const uint8_t *>(arena);
+    const uint32_t xg = (uint32_t)g.xcd;
+    // PM_TX: the deferred fill's scratch (values, positions)
+    uint32_t *side = nullptr;
+    if (mode == PM_TX) {
+        const hipError_t e = hipMallocAsync(reinterpret_cast<void **>(&side), (size_t)n * 8u, stream);
+        if (e != hipSuccess)
+            return e;
+    }
+    uint32_t *vals = side, *posv = side ? side + n : nullptr;
+    hipError_t e = hipErrorInvalidValue;
+#define TCSUM_PI(GG, UU)                                                                                     \
+    if (e == hipErrorInvalidValue && g.lanes == GG && g.loads == UU) {                                       \
+        if (mode == PM_RX)                                                                                   \
+            hipLaunchKernelGGL((k_probe_ipv4<GG, UU, PM_RX>), dim3((uint32_t)blocks), dim3(256), 0, stream, a,   \
+                               pkts, n, sink, xg, vals, posv);                                              \
+        else if (mode == PM_TX)                                                                              \
+            hipLaunchKernelGGL((k_probe_ipv4<GG, UU, PM_TX>), dim3((uint32_t)blocks), dim3(256), 0, stream, a,   \
+                               pkts, n, sink, xg, vals, posv);                                              \
+        else                                                                                                 \
+            hipLaunchKernelGGL((k_probe_ipv4<GG, UU, PM_SUMS>), dim3((uint32_t)blocks), dim3(256), 0, stream, a, \
+                               pkts, n, sink, xg, vals, posv);                                              \
+        e = hipGetLastError();                                                                               \
+    }
+    TCSUM_PI(16, 1) TCSUM_PI(16, 2) TCSUM_PI(16, 3) TCSUM_PI(16, 4) TCSUM_PI(16, 6) TCSUM_PI(16, 8)
+    TCSUM_PI(32, 6) TCSUM_PI(64, 4) TCSUM_PI(64, 16)
+#undef TCSUM_PI
+    if (mode == PM_TX) {
+        if (e == hipSuccess) { // the product's scatter, on the probe's values and positions
+            hipLaunchKernelGGL(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, const_cast<uint8_t *>(a),
+                               pkts, n, vals, posv);
+            e = hipGetLastError();
+        }
+        const hipError_t f = hipFreeAsync(side, stream);
+        e = e != hipSuccess ? e : f;
+    }
+    return e;
+}
+
+static hipError_t launch_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, uint64_t seed,
+                                    hipStream_t stream)
+{
+    if (nbytes == 0)
+        return hipSuccess;
+    const uint64_t units = (nbytes + 15) / 16;
+    uint64_t blocks = (units + 255) / 256;
+    if (blocks > 65536)
+        blocks = 65536;
+    hipLaunchKernelGGL(k_synth_fill, dim3((uint32_t)blocks), dim3(256), 0, stream,
+                       static_cast<uint8_t *>(arena), nbytes, byte_base / 8, seed);
+    return hipGetLastError();
+}
+
+static hipError_t launch_synth_ipv4(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t seed,
+                                    hipStream_t stream)
+{
+    if (n == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_synth_ipv4, dim3((n + 255) / 256), dim3(256), 0, stream,
+                       static_cast<uint8_t *>(arena), pkts, n, seed);
+    return hipGetLastError();
+}
+
+} // namespace tcsum
+
+// ===================================================================== ABI
+
+static uint64_t mean_of(uint64_t total, uint32_t n) { return total && n ? total / n : 1500; }
+
+static int rc_of(hipError_t e)
+{
+    return e == hipSuccess ? TCSUM_OK : e == hipErrorInvalidValue ? TCSUM_ERR_PARAM : TCSUM_ERR_SYS;
+}
+
+extern "C" {
+
+int tcsum_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, uint64_t seed, void *stream)
+{
+    if (!arena || (reinterpret_cast<uintptr_t>(arena) & 15u) || (byte_base & 15u))
+        return TCSUM_ERR_PARAM;
+    return rc_of(tcsum::launch_synth_fill(arena, nbytes, byte_base, seed, static_cast<hipStream_t>(stream)));
+}
+
+int tcsum_synth_ipv4(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t seed, void *stream)
+{
+    if (n && (!arena || !pkts))
+        return TCSUM_ERR_PARAM;
+    return rc_of(tcsum::launch_synth_ipv4(arena, pkts, n, seed, static_cast<hipStream_t>(stream)));
+}
+
+int tcsum_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, void *stream)
+{
+    if (!p || !sink || (reinterpret_cast<uintptr_t>(p) & 15u))
+        return TCSUM_ERR_PARAM;
+    return rc_of(tcsum::launch_probe_read(p, nbytes, sink, static_cast<hipStream_t>(stream)));
+}
+
+int tcsum_probe_segments(const void *arena, const tcsum_peso_t *segs, uint32_t n, uint64_t total_bytes_hint,
+                         uint32_t *sink, void *stream)
+{
+    if (!arena || !segs || !sink)
+        return TCSUM_ERR_PARAM;
+    return rc_of(tcsum::launch_probe_desc(arena, segs, n, mean_of(total_bytes_hint, n), sink,
+                                          static_cast<hipStream_t>(stream)));
+}
+
+int tcsum_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t total_bytes_hint, int mode,
+                     uint32_t *sink, void *stream)
+{
+    if (!arena || !pkts || !sink || mode < 0 || mode > 2)
+        return TCSUM_ERR_PARAM;
+    return rc_of(tcsum::launch_probe_ipv4(arena, pkts, n, mean_of(total_bytes_hint, n), mode, sink,
+                                          static_cast<hipStream_t>(stream)));
+}
+
+int tcsum_probe_tile(const void *p, uint64_t nbytes, int lanes, int loads, int dep, uint32_t *sink, void *stream)
+{
+    if (!p || !sink || (reinterpret_cast<uintptr_t>(p) & 15u))
+        return TCSUM_ERR_PARAM;
+    return rc_of(tcsum::launch_probe_tile(p, nbytes, lanes, loads, dep != 0, sink, static_cast<hipStream_t>(stream)));
+}
+
+} // extern "C"

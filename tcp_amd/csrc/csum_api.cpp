@@ -1,5 +1,5 @@
 // csum_api.cpp -- the C ABI of libtcsum.so (include/tcsum.h, tcsum_legacy.h,
-// tcsum_synth.h): argument checks, per-device context, pinned staging, and
+// tcsum_debug.h): argument checks, per-device context, pinned staging, and
 // the legacy drop-in entry points.  Every checksum is computed by the gfx950
 // kernels in csum_kernels.hip; nothing here sums bytes.
 #include <hip/hip_runtime.h>
@@ -21,7 +21,7 @@
 #include "csum_launch.h"
 #include "tcsum.h"
 #include "tcsum_legacy.h"
-#include "tcsum_synth.h"
+#include "tcsum_debug.h"
 
 // The drop-in symbols are called with the reference's own structs: the
 // mirror types must have the reference's LP64 layout (net/net/list.h:9-34,
@@ -129,14 +129,10 @@ constexpr size_t kCallStageMax = 1u << 16;
 // Launch-path drop-in calls up to this many bytes pass their descriptor (and
 // up to kCallInline bytes) in the kernel arguments: one wave, one pass
 // (k_once / k_inline16).  TCSUM_ARGS_LAUNCH=0: the descriptor in pinned
-// memory, as before (measurement; read per call so one process can run both,
-// tests/test_gpu_parity.py).
+// memory, as before (debug knob "args_launch", include/tcsum_debug.h; read per
+// call so one process can run both, tests/test_gpu_parity.py).
 constexpr size_t kOnceMax = 16u << 10;
-bool args_launch()
-{
-    const char *s = getenv("TCSUM_ARGS_LAUNCH");
-    return !(s && atoi(s) == 0);
-}
+bool args_launch() { return tcsum::knob(tcsum::KNOB_ARGS_LAUNCH) != 0; }
 
 Ctx g_ctx[kMaxDev];
 std::mutex g_default_mu;
@@ -247,14 +243,13 @@ void ensure_stage(Ctx &c, size_t bytes)
 // number into pinned memory behind the last kernel and the host spins on that
 // word: 13.5-15.5 us per drop-in call against 16.9-17.6 us blocking in
 // hipStreamSynchronize (profiles/r02/legacy_latency_poll.txt).
-// TCSUM_SYNC=block: the latter.  The spin is only the fast path: after 10 s
+// Debug knob "sync_block" = 1: the latter.  The spin is only the fast path: after 10 s
 // (a contended GPU, a profiler serialising kernels) the wait continues in
 // hipStreamSynchronize, so a caller never gets control back while its kernels
 // may still read or write its buffers; only a real device error is returned.
 hipError_t stream_wait(Ctx &c)
 {
-    static const bool block = getenv("TCSUM_SYNC") && strcmp(getenv("TCSUM_SYNC"), "block") == 0;
-    if (block)
+    if (tcsum::knob(tcsum::KNOB_SYNC_BLOCK) > 0)
         return hipStreamSynchronize(c.stream);
     uint32_t *flag = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(c.result) + 32);
     void *dflag = reinterpret_cast<uint8_t *>(c.d_result) + 32;
@@ -422,6 +417,65 @@ int tcsum_host_unregister(void *p)
     return TCSUM_OK;
 }
 
+// ------------------------------------------------------------ debug knobs
+
+static const struct {
+    const char *key;
+    tcsum::Knob k;
+} kKnobs[] = {
+    {"lanes", tcsum::KNOB_LANES},         {"loads", tcsum::KNOB_LOADS},
+    {"xcd", tcsum::KNOB_XCD},             {"packed", tcsum::KNOB_PACKED},
+    {"flat", tcsum::KNOB_FLAT},           {"tx_split", tcsum::KNOB_TX_SPLIT},
+    {"args_launch", tcsum::KNOB_ARGS_LAUNCH}, {"sync_block", tcsum::KNOB_SYNC_BLOCK},
+    {"e2e_trace", tcsum::KNOB_E2E_TRACE}, {"e2e_chunk_mb", tcsum::KNOB_E2E_CHUNK_MB},
+};
+
+static int knob_of(const char *key)
+{
+    if (key)
+        for (const auto &e : kKnobs)
+            if (strcmp(e.key, key) == 0)
+                return e.k;
+    return -1;
+}
+
+int tcsum_debug_set(const char *key, int64_t value)
+{
+    const int k = knob_of(key);
+    if (k < 0 || value < -1)
+        return TCSUM_ERR_PARAM;
+    tcsum::set_knob((tcsum::Knob)k, value);
+    return TCSUM_OK;
+}
+
+int64_t tcsum_debug_get(const char *key)
+{
+    if (key && strcmp(key, "scratch_reserved") == 0) { // the calling thread's current device
+        int dev = 0;
+        return hipGetDevice(&dev) == hipSuccess ? (int64_t)tcsum::scratch_reserved(dev) : -2;
+    }
+    const int k = knob_of(key);
+    return k < 0 ? -2 : tcsum::knob((tcsum::Knob)k);
+}
+
+void tcsum_debug_route(uint64_t mean_len, int32_t out[5])
+{
+    const Geometry g = tcsum::pick_geometry(mean_len);
+    if (out) {
+        out[0] = g.lanes;
+        out[1] = g.loads;
+        out[2] = g.xcd;
+        out[3] = g.packed;
+        out[4] = g.flat;
+    }
+}
+
+// hipErrorInvalidValue from a launcher: a shape or size it refuses
+static int rc_of(hipError_t e)
+{
+    return e == hipSuccess ? TCSUM_OK : e == hipErrorInvalidValue ? TCSUM_ERR_PARAM : TCSUM_ERR_SYS;
+}
+
 static uint64_t mean_of(uint64_t total, uint32_t n) { return total && n ? total / n : 1500; }
 
 // device tx fills of at least this many packets defer their stores (mode 4)
@@ -437,7 +491,7 @@ int tcsum_batch_segments(const void *arena, const tcsum_seg_t *segs, uint32_t n,
     const hipError_t e = tcsum::launch_segments(tcsum::MODE_SEG, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
                                                 arena, segs, n, out, complement ? 1u : 0u,
                                                 static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
+    return rc_of(e);
 }
 
 int tcsum_batch_peso(const void *arena, const tcsum_peso_t *segs, uint32_t n, uint16_t *out,
@@ -449,7 +503,7 @@ int tcsum_batch_peso(const void *arena, const tcsum_peso_t *segs, uint32_t n, ui
         return TCSUM_ERR_PARAM;
     const hipError_t e = tcsum::launch_segments(tcsum::MODE_PESO, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
                                                 arena, segs, n, out, 0u, static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
+    return rc_of(e);
 }
 
 int tcsum_batch_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
@@ -462,7 +516,7 @@ int tcsum_batch_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uin
     const hipError_t e = tcsum::launch_ipv4(0, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
                                             const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts,
                                             n, out, flags, nullptr, static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
+    return rc_of(e);
 }
 
 int tcsum_batch_ipv4_tx_fill(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out, uint8_t *flags,
@@ -476,11 +530,11 @@ int tcsum_batch_ipv4_tx_fill(void *arena, const tcsum_pkt_t *pkts, uint32_t n, u
     // the field stores in one short second launch (mode 4) -- 4-6 % faster on
     // configs[3] than storing each packet's fields as its sums finish, which
     // trickles a million isolated writes through the read stream (DESIGN.md
-    // §6, tx fill).  Small batches keep one launch.  TCSUM_TX_SPLIT=0/1 forces.
+    // §6, tx fill).  Small batches keep one launch.  Debug knob "tx_split" forces.
     // Under hipGraph capture the single-launch form is taken: it allocates
     // nothing (this header's convention).
-    const char *sp = getenv("TCSUM_TX_SPLIT");
-    bool split = sp ? atoi(sp) != 0 : n >= kTxSplitMin;
+    const int64_t ks = tcsum::knob(tcsum::KNOB_TX_SPLIT);
+    bool split = ks >= 0 ? ks != 0 : n >= kTxSplitMin;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (split && hipStreamIsCapturing(static_cast<hipStream_t>(stream), &cap) == hipSuccess &&
         cap != hipStreamCaptureStatusNone)
@@ -488,7 +542,7 @@ int tcsum_batch_ipv4_tx_fill(void *arena, const tcsum_pkt_t *pkts, uint32_t n, u
     const hipError_t e = tcsum::launch_ipv4(split ? 4 : 1, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
                                             static_cast<uint8_t *>(arena), pkts, n, out, flags, nullptr,
                                             static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
+    return rc_of(e);
 }
 
 int tcsum_batch_ipv4_tx_fill_scratch(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
@@ -503,7 +557,7 @@ int tcsum_batch_ipv4_tx_fill_scratch(void *arena, const tcsum_pkt_t *pkts, uint3
                                                        static_cast<uint8_t *>(arena), pkts, n, out, flags,
                                                        static_cast<uint32_t *>(scratch),
                                                        static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
+    return rc_of(e);
 }
 
 int tcsum_batch_ipv4_tx_offload(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
@@ -517,7 +571,7 @@ int tcsum_batch_ipv4_tx_offload(const void *arena, const tcsum_pkt_t *pkts, uint
     const hipError_t e = tcsum::launch_ipv4(3, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
                                             const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts,
                                             n, out, flags, nullptr, static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
+    return rc_of(e);
 }
 
 // Host side of the offload contract: the stores k_ipv4<IP_TX> makes, driven
@@ -573,63 +627,7 @@ int tcsum_batch_ipv4_rx_verify(const void *arena, const tcsum_pkt_t *pkts, uint3
     const hipError_t e = tcsum::launch_ipv4(2, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
                                             const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts,
                                             n, out, flags, verdict, static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
-}
-
-int tcsum_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, uint64_t seed, void *stream)
-{
-    if (!arena || (reinterpret_cast<uintptr_t>(arena) & 15u) || (byte_base & 15u))
-        return TCSUM_ERR_PARAM;
-    return tcsum::launch_synth_fill(arena, nbytes, byte_base, seed, static_cast<hipStream_t>(stream)) ==
-                   hipSuccess
-               ? TCSUM_OK
-               : TCSUM_ERR_SYS;
-}
-
-int tcsum_synth_ipv4(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t seed, void *stream)
-{
-    if (n && (!arena || !pkts))
-        return TCSUM_ERR_PARAM;
-    return tcsum::launch_synth_ipv4(arena, pkts, n, seed, static_cast<hipStream_t>(stream)) == hipSuccess
-               ? TCSUM_OK
-               : TCSUM_ERR_SYS;
-}
-
-int tcsum_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, void *stream)
-{
-    if (!p || !sink || (reinterpret_cast<uintptr_t>(p) & 15u))
-        return TCSUM_ERR_PARAM;
-    return tcsum::launch_probe_read(p, nbytes, sink, static_cast<hipStream_t>(stream)) == hipSuccess
-               ? TCSUM_OK
-               : TCSUM_ERR_SYS;
-}
-
-int tcsum_probe_segments(const void *arena, const tcsum_peso_t *segs, uint32_t n, uint64_t total_bytes_hint,
-                         uint32_t *sink, void *stream)
-{
-    if (!arena || !segs || !sink)
-        return TCSUM_ERR_PARAM;
-    const hipError_t e = tcsum::launch_probe_desc(arena, segs, n, mean_of(total_bytes_hint, n), sink,
-                                                  static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? TCSUM_OK : e == hipErrorInvalidValue ? TCSUM_ERR_PARAM : TCSUM_ERR_SYS;
-}
-
-int tcsum_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t total_bytes_hint, int mode,
-                     uint32_t *sink, void *stream)
-{
-    if (!arena || !pkts || !sink || mode < 0 || mode > 2)
-        return TCSUM_ERR_PARAM;
-    const hipError_t e = tcsum::launch_probe_ipv4(arena, pkts, n, mean_of(total_bytes_hint, n), mode,
-                                                  sink, static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? TCSUM_OK : e == hipErrorInvalidValue ? TCSUM_ERR_PARAM : TCSUM_ERR_SYS;
-}
-
-int tcsum_probe_tile(const void *p, uint64_t nbytes, int lanes, int loads, uint32_t *sink, void *stream)
-{
-    if (!p || !sink || (reinterpret_cast<uintptr_t>(p) & 15u))
-        return TCSUM_ERR_PARAM;
-    const hipError_t e = tcsum::launch_probe_tile(p, nbytes, lanes, loads, sink, static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? TCSUM_OK : e == hipErrorInvalidValue ? TCSUM_ERR_PARAM : TCSUM_ERR_SYS;
+    return rc_of(e);
 }
 
 // ------------------------------------------------------------ host batches
@@ -661,9 +659,8 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
 {
     if (n == 0)
         return TCSUM_OK;
-    // TCSUM_E2E_TRACE=1: host-side phase times of this call on stderr (measurement)
-    const char *tr = getenv("TCSUM_E2E_TRACE");
-    const bool trace = tr && atoi(tr);
+    // debug knob "e2e_trace" = 1: host-side phase times of this call on stderr (measurement)
+    const bool trace = tcsum::knob(tcsum::KNOB_E2E_TRACE) > 0;
     const auto t_start = std::chrono::steady_clock::now();
     auto stamp = [&](const char *what) {
         if (trace)
@@ -697,15 +694,15 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     // its copy's event on the kernel stream and runs under the next copy.
     // Every copy costs ~18 us of link idle before it (rocprofv3
     // --memory-copy-trace, profiles/r02/e2e_phase.txt), so chunks are large:
-    // a quarter of the batch, at least 64 MiB (TCSUM_E2E_CHUNK_MB: fixed size).
+    // a quarter of the batch, at least 64 MiB (debug knob "e2e_chunk_mb": fixed size).
     const uint32_t step = std::max<uint32_t>(1, n / 64); // the batch's bytes, estimated from 64 segments
     uint64_t sampled = 0, taken = 0;
     for (uint32_t i = 0; i < n; i += step, ++taken)
         sampled += segs[i].len;
     const uint64_t total_hint = sampled / taken * (uint64_t)n;
     uint64_t target = std::max<uint64_t>(64ull << 20, total_hint / 4);
-    if (const char *v = getenv("TCSUM_E2E_CHUNK_MB"))
-        target = (uint64_t)std::max(1, atoi(v)) << 20;
+    if (const int64_t v = tcsum::knob(tcsum::KNOB_E2E_CHUNK_MB); v > 0)
+        target = (uint64_t)v << 20;
     // The lead: the first blocks, up to 64 MiB of packet bytes, looked at on
     // this thread before anything else.  When they are dense (their span at
     // most 1.25x their bytes) their copy starts at once, into a buffer of
@@ -1448,11 +1445,18 @@ void reap_at_exit() { std::call_once(g_reap_once, [] { atexit(reap_servers); });
 // Give back every cached batch buffer of a device (tcsum_release): the HBM
 // copy of host spans and descriptors, and the pinned host-queue staging.  The
 // servers go first: their next job would name the freed buffers.
-int release_ctx(Ctx &c)
+int release_ctx(Ctx &c, int dev)
 {
     std::lock_guard<std::mutex> lk(c.mu);
-    if (!c.ready)
-        return TCSUM_OK;
+    if (!c.ready) {
+        // no context (only device-resident batch calls on caller streams ran
+        // here): the tx fill's scratch pool may still hold memory
+        if (!tcsum::scratch_reserved(dev))
+            return TCSUM_OK;
+        if (hipSetDevice(dev) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+            return TCSUM_ERR_SYS;
+        return tcsum::scratch_trim(dev) == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
+    }
     if (hipSetDevice(c.device) != hipSuccess)
         return TCSUM_ERR_SYS;
     if ((c.srv_running && srv_stop(c) != TCSUM_OK) || (c.cs_running && cs_stop(c) != TCSUM_OK))
@@ -1906,7 +1910,7 @@ uint16_t checksum16(int offset, void *buf, uint16_t len, uint32_t pre_sum, int c
     d->offset = par;
     d->len = len;
     d->pre_sum = pre_sum;
-    const hipError_t e = tcsum::launch_segments(tcsum::MODE_EXACT, Geometry{64, 8, 0, 1} /* unused for MODE_EXACT */, c.d_stage, c.d_desc,
+    const hipError_t e = tcsum::launch_segments(tcsum::MODE_EXACT, Geometry{64, 8, 1, 0, 0} /* unused for MODE_EXACT */, c.d_stage, c.d_desc,
                                                 1, c.d_result, (complement ? 1u : 0u) | (par << 1), c.stream);
     run_sync(c, e);
     return *c.result;
@@ -2002,7 +2006,7 @@ int tcsum_release(int device)
 {
     if (device < 0 || device >= kMaxDev)
         return TCSUM_ERR_PARAM;
-    return release_ctx(g_ctx[device]);
+    return release_ctx(g_ctx[device], device);
 }
 
 } // extern "C"

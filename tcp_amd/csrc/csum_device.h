@@ -1,0 +1,1245 @@
+// csum_device.h -- the gfx950 device code both libraries compile: arithmetic
+// helpers and the checksum kernels as templates.  libtcsum.so (csum_kernels.hip)
+// instantiates the shapes its router can pick; libtcsum_bench.so
+// (bench_kernels.hip) instantiates the load-only PROBE forms for measurement.
+// Included by exactly one translation unit of each library.
+//
+// csum_kernels.hip -- gfx950 kernels for the Internet checksum (RFC 1071 sum as
+// the wj9806/tcp stack computes it: net/src/tools.c:24-75, pktbuf.c:646-670).
+//
+// Arithmetic.  The reference adds the range as little-endian u16 words into a
+// u32 and folds with end-around carry.  For a range of bytes b[0..n) whose
+// byte parity starts at 0 that is
+//     S = pre + sum_i b[i] * 256^(i & 1),   fold(S) = S == 0 ? 0 : 1 + (S-1) % 0xFFFF.
+// 65536 == 1 (mod 0xFFFF), so any regrouping of the words gives the same
+// fold, and folding never turns a non-zero sum into zero.  The kernels
+//   * read the range as 16-byte-aligned chunks (global_load_dwordx4; an
+//     aligned chunk never crosses a page, so touching a chunk's bytes outside
+//     the range is safe and they are masked to zero),
+//   * add each dword's two halves with one v_dot2_u32_u16 (d . {1,1} + acc),
+//   * keep a u32 per lane, folded once per pass (never exact-overflows),
+//   * reduce the G lanes that share a packet with DPP-free xor shuffles,
+//   * and let the packet's first lane fold, rotate and complement.
+// Address parity vs logical parity: the loads weight a byte by the parity of
+// its ADDRESS; when the range starts at an odd address every byte is in the
+// other half of its word, and the folded sum is the 8-bit rotation of the
+// logical one (x*256 mod 0xFFFF), so one rotate fixes it.
+//
+// Lane mapping.  G lanes (4..64) share one packet and each issues U 16-byte
+// loads per pass before adding anything, so a wave keeps 64*U*16 bytes in
+// flight (8 KiB at U=8).  64/G packets ride in one wave; 4 waves per 256-thread
+// workgroup; no LDS and no barriers -- the reduction stays inside a wave.
+#pragma once
+
+#include "csum_launch.h"
+
+namespace tcsum {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// a.lo + a.hi + acc in one VALU op (v_dot2_u32_u16 with {1,1}).
+__device__ __forceinline__ uint32_t add_halves(uint32_t acc, uint32_t d)
+{
+    const u16x2 one = {1, 1};
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, d), one, acc, false);
+}
+
+__device__ __forceinline__ uint32_t chunk_sum(uint32_t acc, u32x4 v)
+{
+    acc = add_halves(acc, v.x);
+    acc = add_halves(acc, v.y);
+    acc = add_halves(acc, v.z);
+    return add_halves(acc, v.w);
+}
+
+// acc + d.lo * w.lo + d.hi * w.hi.  The operands are taken by value: clang
+// (ROCm 7.2) miscompiles __builtin_bit_cast applied directly to an
+// ext_vector element (v.y reads v.x), so never bit_cast `v.y` in place.
+__device__ __forceinline__ uint32_t dot_halves(uint32_t acc, uint32_t d, uint32_t w)
+{
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, d), __builtin_bit_cast(u16x2, w), acc, false);
+}
+
+// acc + w.lo * (sum of the chunk's low halves) + w.hi * (high halves), w in
+// {0x00010001, 0}: adds the chunk or nothing, without a branch.
+__device__ __forceinline__ uint32_t chunk_sum_w(uint32_t acc, u32x4 v, uint32_t w)
+{
+    acc = dot_halves(acc, v.x, w);
+    acc = dot_halves(acc, v.y, w);
+    acc = dot_halves(acc, v.z, w);
+    return dot_halves(acc, v.w, w);
+}
+
+// Four independent accumulators, one per dword of the chunk: the dot2 ops of
+// one chunk do not wait on each other (a single chain put an s_nop between
+// every two of them), and the last chunk to arrive costs one dot2 latency,
+// not four, in the wave's tail.
+struct Acc4 {
+    uint32_t x, y, z, w;
+};
+__device__ __forceinline__ void acc4_add(Acc4 &a, u32x4 v, uint32_t w)
+{
+    a.x = dot_halves(a.x, v.x, w);
+    a.y = dot_halves(a.y, v.y, w);
+    a.z = dot_halves(a.z, v.z, w);
+    a.w = dot_halves(a.w, v.w, w);
+}
+__device__ __forceinline__ uint32_t acc4_total(const Acc4 &a) { return (a.x + a.y) + (a.z + a.w); }
+
+// Keep only bytes [lo, hi) of a chunk (positions 0..16).
+__device__ __forceinline__ u32x4 mask_chunk(u32x4 v, int lo, int hi);
+
+// Bytes [a, b) of a dword (0 <= a, b <= 4); empty when b <= a.
+__device__ __forceinline__ uint32_t byte_mask(int a, int b)
+{
+    const uint64_t hi = (1ull << (8 * b)) - 1ull;
+    const uint64_t lo = (1ull << (8 * a)) - 1ull;
+    return (uint32_t)(hi & ~lo);
+}
+
+__device__ __forceinline__ int clamp4(int x) { return x < 0 ? 0 : (x > 4 ? 4 : x); }
+
+__device__ __forceinline__ u32x4 mask_chunk(u32x4 v, int lo, int hi)
+{
+    v.x &= byte_mask(clamp4(lo), clamp4(hi));
+    v.y &= byte_mask(clamp4(lo - 4), clamp4(hi - 4));
+    v.z &= byte_mask(clamp4(lo - 8), clamp4(hi - 8));
+    v.w &= byte_mask(clamp4(lo - 12), clamp4(hi - 12));
+    return v;
+}
+
+// Sum of the chunk's bytes [lo, hi) (positions 0..16 inside the chunk).
+__device__ __forceinline__ uint32_t chunk_sum_masked(uint32_t acc, u32x4 v, int lo, int hi)
+{
+    acc = add_halves(acc, v.x & byte_mask(clamp4(lo), clamp4(hi)));
+    acc = add_halves(acc, v.y & byte_mask(clamp4(lo - 4), clamp4(hi - 4)));
+    acc = add_halves(acc, v.z & byte_mask(clamp4(lo - 8), clamp4(hi - 8)));
+    return add_halves(acc, v.w & byte_mask(clamp4(lo - 12), clamp4(hi - 12)));
+}
+
+// One end-around step: keeps x == 0 iff input == 0, x mod 0xFFFF, x <= 0x1FFFE.
+__device__ __forceinline__ uint32_t fold_step(uint32_t x) { return (x & 0xFFFFu) + (x >> 16); }
+
+// tools.c:47-51 closed form.
+__device__ __forceinline__ uint32_t fold16(uint32_t x)
+{
+    x = fold_step(x);
+    x = fold_step(x);
+    return fold_step(x);
+}
+
+__device__ __forceinline__ uint32_t rot8(uint32_t x) { return ((x & 0xFFu) << 8) | (x >> 8); }
+
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
+
+template <bool NT>
+__device__ __forceinline__ u32x4 load16(const u32x4 *p)
+{
+    if constexpr (NT)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+
+// Keep every load issued so far above this point: the optimizer may neither
+// sink them into a later loop (IR level: memory clobber) nor reorder their
+// consumers before them (machine scheduler barrier).  Without it hipcc moved
+// the first pass of data loads behind an s_waitcnt vmcnt(0) on the header /
+// edge loads -- one extra full memory latency per wave.
+__device__ __forceinline__ void issue_fence()
+{
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// x + (x of another lane selected by a DPP control), all lanes active.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_add(uint32_t x)
+{
+    return x + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+
+// Sum over the G lanes that share a packet, in every lane of the group.
+// Inside a 16-lane DPP row the butterfly is four DPP adds (quad_perm xor1,
+// xor2; row_ror 4, 8: no LDS unit, no waits); only the cross-row steps
+// (G = 8's xor 4, G >= 32) go through ds_bpermute.
+template <int G>
+__device__ __forceinline__ uint32_t group_sum(uint32_t x)
+{
+    x = dpp_add<0xB1>(x); // quad_perm [1,0,3,2]: lane ^ 1
+    x = dpp_add<0x4E>(x); // quad_perm [2,3,0,1]: lane ^ 2
+    if constexpr (G == 8)
+        x += __shfl_xor(x, 4, 64);
+    if constexpr (G >= 16) {
+        x = dpp_add<0x124>(x); // row_ror:4 -- quad sums of lanes i, i-4
+        x = dpp_add<0x128>(x); // row_ror:8 -- + lanes i-8, i-12: the row sum
+    }
+    if constexpr (G >= 32)
+        x += __shfl_xor(x, 16, 64);
+    if constexpr (G >= 64)
+        x += __shfl_xor(x, 32, 64);
+    return x;
+}
+
+// XCD-grouped block order.  The dispatcher hands consecutive workgroups to
+// the 8 XCDs round-robin (MI355X_MICROARCH.md, workgroup dispatch), so with the
+// identity map the results of neighbouring packets -- one 128-byte line of
+// `out` -- are written by 4..16 workgroups on different XCDs, each L2 writing
+// its own partial copy of the line back to HBM, and the 16-byte chunk two
+// packed packets share is fetched by two L2s.  Remapped, every run of `xg`
+// consecutive logical blocks sits on one XCD (hardware blocks b, b+8, ...),
+// while the set of blocks in flight -- the HBM window the chip streams
+// through -- stays the same.  Bijective: a last, incomplete group of 8*xg
+// blocks keeps the identity map.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t xg)
+{
+    if (xg <= 1)
+        return b;
+    const uint32_t sg = 8u * xg;
+    if (b >= nb - nb % sg)
+        return b;
+    const uint32_t r = b % sg;
+    return b - r + (r & 7u) * xg + (r >> 3);
+}
+
+// ---------------------------------------------------------------- segments
+//
+// One descriptor per range.  MODE_SEG: pktbuf_checksum16 (u16 pre_sum);
+// MODE_EXACT: checksum16 (u32 pre_sum, u32 wrap, len <= 65535);
+// MODE_PESO: checksum_peso with the pseudo-header built here (tools.c:58-70).
+
+struct SegDesc {
+    uint64_t off;
+    uint32_t len, pre, src, dst, proto;
+};
+
+// Unconditional: a dead lane (seg >= n) reads descriptor 0 and gets len 0, so
+// no load sits behind a branch.
+template <int MODE>
+__device__ __forceinline__ SegDesc load_desc(const void *__restrict__ descs, uint32_t seg, bool live)
+{
+    SegDesc d;
+    const uint32_t i = live ? seg : 0u;
+    if constexpr (MODE == MODE_PESO) {
+        // 24 B = 16 + 8: two loads (the array is 8-byte aligned)
+        const uint8_t *x = static_cast<const uint8_t *>(descs) + 24ull * i;
+        const u32x4 a = *reinterpret_cast<const u32x4 *>(x);
+        const uint2 b = *reinterpret_cast<const uint2 *>(x + 16);
+        d.off = (uint64_t)a.x | ((uint64_t)a.y << 32);
+        d.len = a.z;
+        d.src = a.w;
+        d.dst = b.x;
+        d.proto = b.y & 0xFFu;
+        d.pre = 0;
+    } else {
+        const u32x4 a = *(reinterpret_cast<const u32x4 *>(descs) + i);
+        d.off = (uint64_t)a.x | ((uint64_t)a.y << 32);
+        d.len = a.z;
+        d.pre = a.w;
+        d.src = d.dst = d.proto = 0;
+    }
+    d.len = live ? d.len : 0u;
+    return d;
+}
+
+// A valid, 16-byte aligned chunk of zeros in the code object: lanes with no
+// bytes to read load from here, so every load is unconditional (no branch
+// around a load -> the compiler can count vmcnt exactly instead of vmcnt(0)).
+__device__ u32x4 g_zero_chunk = {0u, 0u, 0u, 0u};
+
+// One range's loads in flight for this lane (G lanes per range).  Lane 0
+// takes the first chunk and lane 1 the last, masked; the interior chunks
+// [1, nch-1) are whole, so the unrolled loop has no divergent branch: lanes
+// past the end re-read the last interior chunk (same lines as a live lane,
+// merged) and add it with weight 0.
+template <int U>
+struct Frame {
+    const u32x4 *ibase;
+    uint64_t e; // range end in bytes from the first chunk
+    uint32_t s0, ni, ilast, eidx;
+    bool has_edge;
+    u32x4 ev;
+    u32x4 v[U];
+};
+
+template <int G, int U>
+__device__ __forceinline__ void frame_issue(Frame<U> &f, const uint8_t *__restrict__ arena, uint64_t off,
+                                            uint32_t len, uint32_t gl)
+{
+    const uint8_t *p = arena + off; // derived from the kernel argument: global_load, not flat_load
+    f.s0 = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
+    const u32x4 *base = reinterpret_cast<const u32x4 *>(p - f.s0);
+    f.e = (uint64_t)len + f.s0;
+    const uint32_t nch = len ? (uint32_t)((f.e + 15) >> 4) : 0u;
+    f.ni = nch > 2 ? nch - 2 : 0u;
+    f.eidx = gl == 0 ? 0u : (nch ? nch - 1u : 0u);
+    f.has_edge = gl < 2 && nch > 0 && (gl == 0 || nch >= 2);
+    const u32x4 *ebase = nch ? base : &g_zero_chunk;
+    f.ibase = f.ni ? base + 1 : &g_zero_chunk;
+    f.ilast = f.ni ? f.ni - 1u : 0u;
+    // the edge chunks with the DEFAULT policy, the interior nontemporal: a
+    // packed range shares its first and last 128-B line with its neighbours,
+    // and a line fetched by a default-policy load stays in L2 until the
+    // neighbour's wave (same XCD, xcd_block) reads it -- configs[1] fetched
+    // 1.2 % more than the algorithmic bytes with nt edges, 0.05 % without,
+    // and ran 5 % faster (profiles/r01/ab_edge_policy.txt)
+    f.ev = load16<false>(ebase + (nch ? f.eidx : 0u));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t j = u * G + gl;
+        f.v[u] = load16<true>(f.ibase + (j < f.ni ? j : f.ilast));
+    }
+}
+
+template <int G, int U, bool EXACT>
+__device__ __forceinline__ uint32_t frame_consume(Frame<U> &f, uint32_t gl)
+{
+    uint32_t acc;
+    {
+        const uint64_t c = 16ull * f.eidx;
+        const int lo = f.has_edge && f.eidx == 0 ? (int)f.s0 : 0;
+        const int hi = f.has_edge ? (int)(f.e - c < 16 ? f.e - c : 16) : 0;
+        acc = chunk_sum_masked(0u, f.ev, lo, hi);
+    }
+    // pass 0: the loads frame_issue put in flight
+    {
+        Acc4 p{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            acc4_add(p, f.v[u], (uint32_t)(u * G) + gl < f.ni ? 0x00010001u : 0u);
+        const uint32_t part = acc4_total(p); // <= 4 * 16 * 131070 < 2^23
+        acc = EXACT ? acc + part : fold_step(acc + part);
+    }
+    // later passes load and sum inside one iteration: nothing vector-sized is
+    // carried around the loop, so its registers are pass 0's (a loop-carried
+    // f.v made hipcc keep two copies: 68 -> 52 VGPRs at U=6, 8 waves/SIMD)
+    for (uint32_t b0 = G * U; b0 < f.ni; b0 += G * U) {
+        u32x4 w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = b0 + u * G + gl;
+            w[u] = load16<true>(f.ibase + (j < f.ni ? j : f.ilast));
+        }
+        Acc4 p{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = b0 + u * G + gl;
+            acc4_add(p, w[u], j < f.ni ? 0x00010001u : 0u);
+        }
+        const uint32_t part = acc4_total(p);
+        acc = EXACT ? acc + part : fold_step(acc + part);
+    }
+    return acc;
+}
+
+// This lane's share of the word sum of arena[off, off+len).  `issued` runs
+// right after the first loads are in flight.
+template <int G, int U, bool EXACT, class Issued>
+__device__ __forceinline__ uint32_t sum_range(const uint8_t *__restrict__ arena, uint64_t off, uint32_t len,
+                                              uint32_t gl, Issued &&issued)
+{
+    Frame<U> f;
+    frame_issue<G, U>(f, arena, off, len, gl);
+    issued();
+    issue_fence();
+    return frame_consume<G, U, EXACT>(f, gl);
+}
+
+// checksum_peso's pseudo-header words, folded (tools.c:58-70): src, dst,
+// {0, proto}, htons((uint16_t)len).  Depends on the descriptor only, so the
+// kernels compute it while the range's bytes are in flight.
+__device__ __forceinline__ uint32_t peso_pseudo16(const SegDesc &d)
+{
+    uint32_t q = add_halves(0u, d.src);
+    q = add_halves(q, d.dst);
+    q += d.proto << 8;
+    q += bswap16(d.len & 0xFFFFu);
+    return fold16(q);
+}
+
+// Computed now, inside the load shadow: the empty asm pins the value here,
+// so the compiler cannot sink the arithmetic into the tail behind the last load.
+__device__ __forceinline__ uint32_t pinned(uint32_t x)
+{
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+// The packet's first lane turns the group's sum into the reference's u16.
+// MODE_PESO: q16 = peso_pseudo16(d) (ignored by the other modes).
+template <int MODE>
+__device__ __forceinline__ uint16_t finalize(uint32_t acc, uintptr_t start, const SegDesc &d, uint32_t aux,
+                                             uint32_t q16)
+{
+    uint32_t r;
+    if constexpr (MODE == MODE_EXACT) {
+        // tools.c:27-53: u32 accumulator from pre_sum; acc is the exact word
+        // sum (< 2^31 for len <= 65535).  The host stages the bytes so that
+        // address parity == logical parity (aux bit 1).
+        uint32_t s;
+        if (((start ^ (aux >> 1)) & 1u) == 0) {
+            s = d.pre + acc;
+        } else { // not reached from the C ABI; mod-0xFFFF result
+            const uint32_t f = rot8(fold16(acc));
+            s = fold_step(f + fold16(d.pre));
+        }
+        s = fold16(s);
+        r = (aux & 1u) ? (~s & 0xFFFFu) : s;
+    } else {
+        uint32_t f = fold16(acc);
+        if (start & 1u)
+            f = rot8(f);
+        if constexpr (MODE == MODE_SEG) {
+            const uint32_t t = fold_step(f + (d.pre & 0xFFFFu)); // pktbuf.c:657
+            r = (aux & 1u) ? (~t & 0xFFFFu) : t;
+        } else {
+            r = ~fold_step(f + q16) & 0xFFFFu; // pktbuf_checksum16(..., 1), tools.c:73
+        }
+    }
+    return (uint16_t)r;
+}
+
+// One wave-slice of packets per wave, one launch-wide pass.
+//
+// Results leave through the workgroup's LAST wave: each wave puts its packets'
+// u16 into LDS and bumps an LDS counter; the wave that brings it to 4 stores
+// all 256/G results with one coalesced store and the other three end at once.
+// With every wave storing its own 4 results (an 8-byte partial store each) the
+// headline ran 1.1 % slower -- as slow as its loads plus the stores' tail in
+// every wave; with the gathered store it matches the same kernel with no
+// store at all (profiles/r02/ab_store.txt).  A nontemporal store cost 4 %.
+template <int G, int U, int MODE, int T = 256>
+__global__ __launch_bounds__(T) void k_segments(const uint8_t *__restrict__ arena,
+                                                const void *__restrict__ descs, uint32_t n,
+                                                uint16_t *__restrict__ out, uint32_t aux, uint32_t xg)
+{
+    static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0 && T >= 64 && T <= 1024 && T % 64 == 0 && T / G <= 64,
+                  "G, T");
+    constexpr uint32_t PER = T / G; // ranges per workgroup
+    __shared__ uint16_t res[PER];
+    __shared__ uint32_t arrived;
+    if (threadIdx.x == 0)
+        arrived = 0;
+    __syncthreads();
+    const uint32_t gl = threadIdx.x & (G - 1);
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    const uint32_t seg = blk * PER + threadIdx.x / G; // no 32-bit wrap for any n
+    const bool live = seg < n;
+    const SegDesc d = load_desc<MODE>(descs, seg, live);
+    uint32_t q16 = 0;
+    uint32_t acc = sum_range<G, U, MODE == MODE_EXACT>(arena, d.off, d.len, gl, [&] {
+        if constexpr (MODE == MODE_PESO)
+            q16 = pinned(peso_pseudo16(d));
+    });
+    acc = group_sum<G>(acc);
+    if (gl == 0)
+        res[threadIdx.x / G] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + d.off), d, aux, q16);
+    uint32_t order = 0;
+    if ((threadIdx.x & 63u) == 0) // release: this wave's res[] entries before the count
+        order = __hip_atomic_fetch_add(&arrived, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    order = __builtin_amdgcn_readfirstlane(order);
+    if (order == T / 64u - 1u) { // the last wave: every entry is in LDS
+        const uint32_t l = threadIdx.x & 63u;
+        const uint32_t sl = blk * PER + l;
+        if (l < PER && sl < n)
+            out[sl] = res[l];
+    }
+}
+
+// One range per workgroup: all four waves on one range (G = 256), for ranges
+// of tens of KiB (TSO).  Each wave's share of a 64-KiB range is one pass of
+// U loads per lane -- the short-lived, one-pass shape of the fastest plain
+// read (profiles/r01/probe_variants.txt) -- and the waves' sums meet in LDS.
+template <int U, int MODE>
+__global__ __launch_bounds__(256) void k_segments_wg(const uint8_t *__restrict__ arena,
+                                                     const void *__restrict__ descs, uint32_t n,
+                                                     uint16_t *__restrict__ out, uint32_t aux, uint32_t xg)
+{
+    __shared__ uint32_t part[4];
+    const uint32_t gl = threadIdx.x;
+    const uint32_t seg = xcd_block(blockIdx.x, gridDim.x, xg); // grid == n: one range per workgroup
+    const bool live = seg < n;
+    const SegDesc d = load_desc<MODE>(descs, seg, live);
+    uint32_t q16 = 0;
+    uint32_t acc = sum_range<256, U, MODE == MODE_EXACT>(arena, d.off, d.len, gl, [&] {
+        if constexpr (MODE == MODE_PESO)
+            q16 = pinned(peso_pseudo16(d));
+    });
+    acc = group_sum<64>(acc); // < 2^23 (folded lanes) or exact
+    if ((gl & 63u) == 0)
+        part[gl >> 6] = acc;
+    __syncthreads();
+    if (gl == 0 && live)
+        out[seg] = finalize<MODE>(part[0] + part[1] + part[2] + part[3], reinterpret_cast<uintptr_t>(arena + d.off),
+                                  d, aux, q16);
+}
+
+// One range per workgroup of W waves, with the lane -> chunk map as a
+// parameter (measured against k_segments_wg for configs[2],
+// scripts/env_ab.py, profiles/r03/ab_tso_shapes*.txt): GL = 0 interleaves the whole workgroup (load u of
+// lane t is interior chunk u * 64W + t: each load instruction of the
+// workgroup covers 64W contiguous chunks, k_segments_wg's map); GL > 0 cuts
+// the range into sub-ranges of GL * U chunks, one per GL-lane group, each
+// walked like one headline packet (k_segments<16, 6>: load u of lane l is
+// chunk u * GL + l of its sub-range).  A pass covers 64W * U chunks; longer
+// ranges take more passes.  Edges as in frame_issue: lane 0 loads the first
+// chunk and lane 1 the last with the default policy, masked; every interior
+// chunk is nontemporal and whole.
+// PROBE: the same loads with the sums, the reduction and the store replaced
+// by an XOR fold into a sink (`out`) stored on a 2^-32 fluke
+// (tcsum_probe_segments for this geometry).
+template <int W, int GL, int U, int MODE, bool PROBE = false>
+__global__ __launch_bounds__(W * 64) void k_segments_wgx(const uint8_t *__restrict__ arena,
+                                                         const void *__restrict__ descs, uint32_t n,
+                                                         uint16_t *__restrict__ out, uint32_t aux, uint32_t xg)
+{
+    static_assert(MODE != MODE_EXACT, "the exact u32 sum stays on k_segments");
+    constexpr uint32_t T = W * 64u, CPP = T * U;
+    __shared__ uint32_t part[W];
+    const uint32_t t = threadIdx.x;
+    const uint32_t seg = xcd_block(blockIdx.x, gridDim.x, xg); // grid == n
+    const bool live = seg < n;
+    const SegDesc d = load_desc<MODE>(descs, seg, live);
+    const uint8_t *p = arena + d.off;
+    const uint32_t s0 = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
+    const u32x4 *base = reinterpret_cast<const u32x4 *>(p - s0);
+    const uint64_t e = (uint64_t)d.len + s0;
+    const uint32_t nch = d.len ? (uint32_t)((e + 15) >> 4) : 0u;
+    const uint32_t ni = nch > 2 ? nch - 2 : 0u;
+    const u32x4 *ib = ni ? base + 1 : &g_zero_chunk;
+    const uint32_t ilast = ni ? ni - 1u : 0u;
+    const uint32_t eidx = t == 0 ? 0u : (nch ? nch - 1u : 0u);
+    const bool has_edge = t < 2 && nch > 0 && (t == 0 || nch >= 2);
+    const u32x4 ev = load16<false>((nch ? base : &g_zero_chunk) + (nch ? eidx : 0u));
+    const uint32_t lane_off = GL ? (t / GL) * (GL * U) + (t % GL) : t;
+    constexpr uint32_t ustep = GL ? GL : T;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t j = lane_off + u * ustep;
+        v[u] = load16<true>(ib + (j < ni ? j : ilast));
+    }
+    if constexpr (PROBE) {
+        issue_fence();
+        u32x4 x = ev;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            x ^= v[u];
+        for (uint32_t b0 = CPP; b0 < ni; b0 += CPP) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t j = b0 + lane_off + u * ustep;
+                x ^= load16<true>(ib + (j < ni ? j : ilast));
+            }
+        }
+        const uint32_t f = x.x ^ x.y ^ x.z ^ x.w;
+        if (f == 0x9E3779B9u)
+            reinterpret_cast<uint32_t *>(out)[0] = f;
+        return;
+    }
+    uint32_t q16 = 0;
+    if constexpr (MODE == MODE_PESO)
+        q16 = pinned(peso_pseudo16(d));
+    issue_fence();
+    uint32_t acc;
+    {
+        const uint64_t c = 16ull * eidx;
+        const int lo = has_edge && eidx == 0 ? (int)s0 : 0;
+        const int hi = has_edge ? (int)(e - c < 16 ? e - c : 16) : 0;
+        acc = chunk_sum_masked(0u, ev, lo, hi);
+    }
+    {
+        Acc4 pa{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            acc4_add(pa, v[u], lane_off + u * ustep < ni ? 0x00010001u : 0u);
+        acc = fold_step(acc + acc4_total(pa));
+    }
+    for (uint32_t b0 = CPP; b0 < ni; b0 += CPP) {
+        u32x4 w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = b0 + lane_off + u * ustep;
+            w[u] = load16<true>(ib + (j < ni ? j : ilast));
+        }
+        Acc4 pa{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            acc4_add(pa, w[u], b0 + lane_off + u * ustep < ni ? 0x00010001u : 0u);
+        acc = fold_step(acc + acc4_total(pa));
+    }
+    acc = group_sum<64>(acc); // < 2^23
+    if ((t & 63u) == 0)
+        part[t >> 6] = acc;
+    __syncthreads();
+    if (t == 0 && live) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            s += part[w]; // < 16 * 2^23
+        out[seg] = finalize<MODE>(s, reinterpret_cast<uintptr_t>(p), d, aux, q16);
+    }
+}
+
+// ---------------------------------------------------------------- packed stream
+//
+// Ranges laid out one after another in the arena (a batch of MTU segments
+// packed back to back: offset[i+1] == offset[i] + len[i]; or with padding
+// between them) are one byte stream.  k_segments_pk gives a workgroup of W
+// waves K consecutive ranges and streams the region from the first range's
+// first byte to the last range's end in the TSO kernel's load shape -- 32-lane
+// groups each walking a contiguous sub-range, U loads per lane -- instead of
+// giving every range its own lane group; a region longer than one pass
+// (W * 64 * U chunks) is walked pass by pass, the next pass's loads in flight
+// while the current one is combined.
+//
+// Per-range sums come from prefix sums.  Chunk c of the region (16-B aligned,
+// address order) has the full word sum f(c); with E(c) = the sum of f over the
+// chunks before c, the word sum of the region's bytes before byte x (counted
+// from the first chunk) is
+//     P(x) = E(x / 16) + (word sum of bytes [0, x % 16) of chunk x / 16),
+// and range r's sum is P(end_r) - P(start_r): exact u32 arithmetic (a pass of
+// <= 64 KiB sums to < 2^31 and P wraps mod 2^32 consistently), so bytes that
+// belong to no range -- padding, the neighbouring regions' bytes in the first
+// and last chunk -- cancel, and no chunk is masked.  Any layout works as long
+// as every range lies inside the region: gaps, overlaps, duplicates, ranges of
+// 0..16 bytes.  The address-parity weighting and the odd-start rotation are
+// k_segments'.
+//
+// E is a scan in the load order: within a sub-range load u of lane l is chunk
+// u*32 + l, so E = (sub-ranges before) + (loads u' < u of this sub-range) +
+// (lanes l' < l of load u) -- a 32-lane DPP scan per load, the half-wave
+// totals by readlane.  Every lane writes, per chunk, its sub-range prefix and
+// the chunk itself to LDS; after one barrier, lane r of wave w (range 64w + r,
+// whose descriptor it loaded while the bytes were in flight) adds the
+// sub-range prefixes and the bytes before its start and end from the LDS copy
+// of their chunks.  The waves place their loads from the first and last
+// descriptor only (scalar loads), so the data loads wait on one descriptor
+// latency, as in the per-range kernels.
+//
+// A workgroup whose region is longer than 64 passes, one of whose ranges lies
+// outside it (a shuffled batch) or is 128 KiB or longer (its word sum could
+// reach 2^32, where the u32 prefixes stop being exact), sums range by range with the widest lane
+// groups that give every range one: always correct, only slower.
+__device__ __forceinline__ uint32_t scan32(uint32_t x)
+{
+    // inclusive scan inside each 32-lane half: row_shr 1, 2, 4, 8 (16-lane
+    // rows), then row_bcast:15 adds row 0's total into row 1 (and 2's into 3)
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    return x;
+}
+
+// Word sum of the chunk's bytes [0, b), b = 0..16.
+__device__ __forceinline__ uint32_t chunk_prefix_sum(u32x4 v, uint32_t b)
+{
+    const int bits = (int)(8u * b);
+    const uint32_t m0 = bits >= 32 ? ~0u : (1u << bits) - 1u;
+    const uint32_t m1 = bits >= 64 ? ~0u : bits <= 32 ? 0u : (1u << (bits - 32)) - 1u;
+    const uint32_t m2 = bits >= 96 ? ~0u : bits <= 64 ? 0u : (1u << (bits - 64)) - 1u;
+    const uint32_t m3 = bits >= 128 ? ~0u : bits <= 96 ? 0u : (1u << (bits - 96)) - 1u;
+    uint32_t acc = add_halves(0u, v.x & m0);
+    acc = add_halves(acc, v.y & m1);
+    acc = add_halves(acc, v.z & m2);
+    return add_halves(acc, v.w & m3);
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t lane)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)lane);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+constexpr uint32_t kPkWaves = 4, kPkLoads = 3; // 4 waves x 64 lanes x 3 loads x 16 B = 12 KiB per pass
+constexpr uint32_t kPkMaxRanges = 64; // ranges per wave of the workgroup (lane r of wave w: range 64w + r)
+
+// off and len of descriptor i (the same 12 bytes lead both layouts); called
+// with a workgroup-uniform index, so it is a scalar load
+template <int MODE>
+__device__ __forceinline__ void desc_span(const void *__restrict__ descs, uint32_t i, uint64_t &off, uint32_t &len)
+{
+    const uint8_t *x = static_cast<const uint8_t *>(descs) + (MODE == MODE_PESO ? 24ull : 16ull) * i;
+    const uint2 o = *reinterpret_cast<const uint2 *>(x);
+    off = (uint64_t)o.x | ((uint64_t)o.y << 32);
+    len = *reinterpret_cast<const uint32_t *>(x + 8);
+}
+
+// The per-range path for a workgroup whose ranges are not one region:
+// groups of G lanes, G the widest power of two with one group per range.
+template <int MODE, int G, int UL = 4>
+__device__ __forceinline__ void pk_ranges(const uint8_t *__restrict__ arena, const void *__restrict__ descs,
+                                          uint16_t *__restrict__ out, uint32_t aux, uint32_t first, uint32_t kw,
+                                          uint32_t T)
+{
+    const uint32_t t = threadIdx.x, gl = t & (G - 1u);
+    for (uint32_t r = t / G; r < kw; r += T / G) {
+        const SegDesc e = load_desc<MODE>(descs, first + r, true);
+        uint32_t q = 0;
+        uint32_t acc = sum_range<G, UL, false>(arena, e.off, e.len, gl, [&] {
+            if constexpr (MODE == MODE_PESO)
+                q = pinned(peso_pseudo16(e));
+        });
+        acc = group_sum<G>(acc);
+        if (gl == 0)
+            out[first + r] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + e.off), e, aux, q);
+    }
+}
+
+constexpr uint32_t kPkMaxPasses = 64; // longer regions go range by range
+
+template <int MODE, int W = kPkWaves, int U = kPkLoads, bool PROBE = false>
+__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) void k_segments_pk(
+    const uint8_t *__restrict__ arena, const void *__restrict__ descs, uint32_t n, uint16_t *__restrict__ out,
+    uint32_t aux, uint32_t xg, uint32_t K)
+{
+    static_assert(MODE != MODE_EXACT, "the exact u32 sum stays on k_segments");
+    static_assert(W <= 16, "the sub-range totals are scanned by 32 lanes");
+    constexpr uint32_t T = W * 64u, CH = T * U, SR = 32u * U; // chunks per pass, per sub-range
+    __shared__ u32x4 dat[CH];            // the pass's chunks, for the boundary bytes
+    __shared__ uint32_t ex[CH];          // per chunk: its sub-range's word sum before it
+    __shared__ uint32_t subtot[2 * W];   // per sub-range (32 lanes x U loads)
+    __shared__ uint32_t region_ok[W];     // per wave: its ranges lie in the region
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    const uint32_t first = blk * K;
+    const uint32_t kw = n - first < K ? n - first : K; // >= 1: grid = ceil(n / K)
+    // the region: from the first range's first byte to the last range's end
+    uint64_t r0, offl;
+    uint32_t len0, lenl;
+    // scalar loads: their short latency is what the data loads wait on
+    // (fetching the two descriptors with vector loads instead cut the read
+    // traffic from 1.0165x to 1.0018x the algorithmic bytes but ran 11 %
+    // slower, profiles/r03/packed/ab_vdesc_w8.txt)
+    desc_span<MODE>(descs, first, r0, len0);
+    desc_span<MODE>(descs, first + kw - 1u, offl, lenl);
+    const uint64_t rend = offl + lenl;
+    const uint8_t *p = arena + r0;
+    const uint32_t s0 = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
+    // [r0, rend) runs from a byte of the first range to a byte of the last, so
+    // it lies inside the arena whatever the ranges between do: its chunks are
+    // safe to load before the ranges are known to lie inside it
+    const bool span_ok = len0 != 0 && lenl != 0 && rend > r0 &&
+                         rend - r0 <= (uint64_t)kPkMaxPasses * CH * 16u - s0;
+    bool ranges = !span_ok; // workgroup-uniform: sum range by range instead
+    const uint32_t span = span_ok ? (uint32_t)(rend - r0) : 0u;
+    const uint32_t nch = span_ok ? (s0 + span + 15u) >> 4 : 0u;
+    const uint32_t npass = (nch + CH - 1u) / CH;
+    const uint32_t sub = t >> 5, l = t & 31u, hf = (t >> 5) & 1u;
+    const u32x4 *base = span_ok ? reinterpret_cast<const u32x4 *>(p - s0) : &g_zero_chunk;
+    u32x4 v[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t c = sub * SR + u * 32u + l;
+        v[u] = load16<true>(base + (c < nch ? c : (nch ? nch - 1u : 0u)));
+    }
+    issue_fence();
+    // every wave: its share of the K descriptors (lane r: range 64w + r),
+    // whether each lies in the region, and its start and end in bytes from the
+    // first chunk
+    const uint32_t rr = w * 64u + lane;
+    const bool mine = rr < kw;
+    const bool has = w * 64u < kw; // wave-uniform
+    SegDesc d{0, 0, 0, 0, 0, 0};
+    uint32_t xs = 0, xe = 0, q16 = 0;
+    if (has) {
+        d = load_desc<MODE>(descs, first + rr, mine);
+        // P wraps mod 2^32 across passes, so a difference is exact only for a
+        // range whose word sum stays below 2^32: < 128 KiB (<= 65536 words)
+        const bool inside = !mine || (d.off >= r0 && d.off + d.len <= rend && d.len < (1u << 17));
+        const bool ok = __ballot(!inside) == 0;
+        xs = ok ? s0 + (uint32_t)(d.off - r0) : 0u;
+        xe = ok ? xs + d.len : 0u;
+        if constexpr (MODE == MODE_PESO)
+            q16 = peso_pseudo16(d);
+        if (lane == 0)
+            region_ok[w] = ok ? 1u : 0u;
+    } else if (lane == 0) {
+        region_ok[w] = 1u;
+    }
+    if constexpr (PROBE) { // measurement: the same loads, no arithmetic
+        u32x4 z = v[0];
+#pragma unroll
+        for (uint32_t u = 1; u < U; ++u)
+            z ^= v[u];
+        const uint32_t f = z.x ^ z.y ^ z.z ^ z.w ^ q16 ^ xe;
+        if (f == 0x9E3779B9u)
+            reinterpret_cast<uint32_t *>(out)[0] = f;
+        return;
+    }
+    uint32_t run = 0, ps = 0, pe = 0; // word sum of the passes before; P(start), P(end)
+    for (uint32_t pass = 0; !ranges && pass < npass; ++pass) { // workgroup-uniform
+        const uint32_t cb = pass * CH;
+        // every wave: chunk sums, their scans over each 32-lane half; per chunk
+        // the word sum of its sub-range before it, and the chunk itself
+        uint32_t a = 0; // this lane's half-wave: chunks of loads u' < u
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t c = sub * SR + u * 32u + l;
+            const uint32_t f = chunk_sum_w(0u, v[u], cb + c < nch ? 0x00010001u : 0u); // < 2^20
+            const uint32_t sc = scan32(f);
+            ex[c] = a + (sc - f);
+            dat[c] = v[u];
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)sc, 31);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)sc, 63);
+            a += hf ? hi : lo;
+        }
+        if (l == 0)
+            subtot[sub] = a;
+        if (pass + 1u < npass) { // the next pass's bytes stream during the barrier and the prefix sums
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t c = cb + CH + sub * SR + u * 32u + l;
+                v[u] = load16<true>(base + (c < nch ? c : nch - 1u));
+            }
+        }
+        __syncthreads();
+        if (pass == 0) {
+            bool all = true;
+#pragma unroll
+            for (uint32_t i = 0; i < W; ++i)
+                all = all && region_ok[i] != 0u;
+            if (!all) {
+                ranges = true;
+                break;
+            }
+        }
+        if (has) {
+            // P(x) = passes before + sub-ranges before + ex[chunk] + the chunk's
+            // bytes before x; the end of the region (x = 16 * nch) is byte 16 of
+            // the last chunk
+            const uint32_t st = lane < 2u * W ? subtot[lane] : 0u;
+            const uint32_t si = scan32(st);
+            const uint32_t sx = si - st;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t x = k ? xe : xs;
+                uint32_t cx = x >> 4, bx = x & 15u;
+                if (cx == nch) {
+                    cx = nch - 1u;
+                    bx = 16u;
+                }
+                const bool here = cx >= cb && cx < cb + CH;
+                const uint32_t lc = here ? cx - cb : 0u;
+                const uint32_t sp = (uint32_t)__shfl((int)sx, (int)(lc / SR), 64);
+                const uint32_t px = run + sp + ex[lc] + chunk_prefix_sum(dat[lc], bx);
+                if (k)
+                    pe = here ? px : pe;
+                else
+                    ps = here ? px : ps;
+            }
+            run += (uint32_t)__builtin_amdgcn_readlane((int)si, 31);
+        }
+        if (pass + 1u < npass)
+            __syncthreads(); // the next pass overwrites dat / ex / subtot
+    }
+    if (ranges) { // G lanes per range: the widest power of two that gives every range a group
+        const uint32_t lanes_per = T / kw;
+        if (lanes_per >= 64)
+            pk_ranges<MODE, 64>(arena, descs, out, aux, first, kw, T);
+        else if (lanes_per >= 32)
+            pk_ranges<MODE, 32, 3>(arena, descs, out, aux, first, kw, T);
+        else if (lanes_per >= 16)
+            pk_ranges<MODE, 16>(arena, descs, out, aux, first, kw, T);
+        else
+            pk_ranges<MODE, 8>(arena, descs, out, aux, first, kw, T);
+        return;
+    }
+    if (mine)
+        out[first + rr] = finalize<MODE>(pe - ps, reinterpret_cast<uintptr_t>(arena + d.off), d, aux, q16);
+}
+
+// ---------------------------------------------------------------- IPv4
+//
+// Both checksums of a captured IPv4 packet in one pass over its bytes, in one
+// of three modes:
+//   IP_SUMS  header + L4 values (ipv4.c:243 / tcp_in.c:80 / udp.c:410 /
+//            icmpv4.c:36) and is_pkt_ok flags;
+//   IP_TX    the stack's tx fill, in place: checksum fields read as zero,
+//            values stored into them (ipv4.c:643,656, tcp_out.c:19-20,
+//            udp.c:320-321, icmpv4.c:45-58); with IP_OPT_NO_STORE the same
+//            values go to `out` only (tx offload: the host applies them);
+//   IP_RX    the stack's rx gates: net_err_t verdict per packet
+//            (ipv4.c:475-515, is_pkt_ok ipv4.c:220-250, tcp_in.c:69-85,
+//            udp.c:386-415, icmpv4.c:29-43,71-77).
+// The 20 fixed header bytes come from two or three aligned chunks realigned
+// with v_alignbyte; the data pass splits every chunk between the header range
+// [0,hl), the L4 range [hl,end) and the 2-byte checksum fields.
+enum IpMode : int { IP_SUMS = 0, IP_TX = 1, IP_RX = 2 };
+// k_ipv4 `opts` bits (runtime, uniform over the grid)
+constexpr uint32_t IP_OPT_NO_STORE = 1u; // IP_TX: compute the fill's values, leave the packets alone
+// IP_TX, deferred stores (launch_ipv4 mode 4): the values go to `out` and each
+// packet's store positions to a side array (through the verdict pointer, which
+// tx never uses); k_tx_scatter then writes them into the packets in a second,
+// short launch (tx fill)
+constexpr uint32_t IP_OPT_DEFER = 2u;
+// launch_ipv4 mode 3: IP_TX kernels with IP_OPT_NO_STORE
+constexpr int IP_TX_OFFLOAD = 3;
+// launch_ipv4 mode 4: the tx fill as k_ipv4<IP_TX> with IP_OPT_DEFER + k_tx_scatter
+constexpr int IP_TX_SPLIT = 4;
+
+// The 20 fixed header bytes at byte s0 (0..15) of the three aligned chunks
+// h0, h1, h2, as five dwords: hd[k] = bytes [s0 + 4k, s0 + 4k + 4).  Two
+// stages of selects on named scalars pick dwords q = s0 >> 2 .. q + 5, then
+// v_alignbyte shifts by s0 & 3.  (Written over an array, w[q + k], clang
+// turned the selects back into a dynamically indexed alloca and promoted it
+// to 20 KiB of LDS per workgroup: ds_write/ds_read on every packet.)
+struct Hdr5 {
+    uint32_t d0, d1, d2, d3, d4;
+};
+__device__ __forceinline__ Hdr5 header_dwords(u32x4 h0, u32x4 h1, u32x4 h2, uint32_t s0)
+{
+    const bool b1 = s0 & 4u, b2 = s0 & 8u;
+    const uint32_t y0 = b1 ? h0.y : h0.x, y1 = b1 ? h0.z : h0.y, y2 = b1 ? h0.w : h0.z, y3 = b1 ? h1.x : h0.w;
+    const uint32_t y4 = b1 ? h1.y : h1.x, y5 = b1 ? h1.z : h1.y, y6 = b1 ? h1.w : h1.z, y7 = b1 ? h2.x : h1.w;
+    const uint32_t x0 = b2 ? y2 : y0, x1 = b2 ? y3 : y1, x2 = b2 ? y4 : y2;
+    const uint32_t x3 = b2 ? y5 : y3, x4 = b2 ? y6 : y4, x5 = b2 ? y7 : y5;
+    const uint32_t r = s0 & 3u;
+    return Hdr5{__builtin_amdgcn_alignbyte(x1, x0, r), __builtin_amdgcn_alignbyte(x2, x1, r),
+                __builtin_amdgcn_alignbyte(x3, x2, r), __builtin_amdgcn_alignbyte(x4, x3, r),
+                __builtin_amdgcn_alignbyte(x5, x4, r)};
+}
+
+// Sum of the chunk's bytes that fall in [r0, r1) (offsets from the chunk base c;
+// all positions are bytes from the packet's first chunk, < 2^17).
+__device__ __forceinline__ uint32_t region_sum(u32x4 v, int c, int r0, int r1)
+{
+    const int lo = r0 - c, hi = r1 - c;
+    const int a = lo < 0 ? 0 : (lo > 16 ? 16 : lo);
+    const int b = hi < 0 ? 0 : (hi > 16 ? 16 : hi);
+    return chunk_sum_masked(0u, v, a, b);
+}
+
+// L4 checksum field offset and minimum header length by protocol
+// (tcp.h:71, udp.h:24, icmpv4.h:28); 0 when the protocol has none here.
+__device__ __forceinline__ uint32_t l4_field(uint32_t proto, uint32_t &min_len)
+{
+    min_len = proto == 6 ? 20u : proto == 17 ? 8u : proto == 1 ? 4u : 0u;
+    return proto == 6 ? 16u : proto == 17 ? 6u : proto == 1 ? 2u : 0u;
+}
+
+// Packet `pk` (one per G-lane group; pk >= n: a dead group that reads
+// descriptor 0 and writes nothing).  Every lane of the wave must call it: the
+// group reduction crosses lanes.
+template <int G, int U, int IPM>
+__device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
+                                            uint32_t pk, uint32_t n, uint32_t *__restrict__ out,
+                                            uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
+                                            uint32_t opts)
+{
+    const uint32_t gl = threadIdx.x & (G - 1);
+    const bool live = pk < n;
+
+    // unconditional loads throughout (dead lanes read descriptor 0 / the zero chunk)
+    const u32x4 dv = *reinterpret_cast<const u32x4 *>(pkts + (live ? pk : 0u));
+    const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+    const uint32_t frame = live ? dv.z : 0u;
+    const bool big_enough = frame >= 20;
+    uint8_t *pp = arena + off;
+    const uintptr_t start = reinterpret_cast<uintptr_t>(pp);
+    const uint32_t s0 = (uint32_t)(start & 15u);
+    const u32x4 *base = reinterpret_cast<const u32x4 *>(pp - s0);
+
+    // IPv4 bytes past 65,535 (the largest total_len) never count: bound the
+    // loads there, so every position below fits comfortably in 32 bits
+    const uint32_t frame_ld = frame < 65600u ? frame : 65600u;
+    const uint32_t nch = big_enough ? (frame_ld + s0 + 15) >> 4 : 0u;
+
+    // fixed header: bytes [s0, s0 + 20) of base[0..2]
+    const u32x4 *hb = big_enough ? base : &g_zero_chunk;
+    const uint32_t h1i = big_enough ? 1u : 0u;
+    // header loads: default cache policy (nontemporal like the data pass that
+    // loads the same chunks: no different in time or traffic,
+    // profiles/r02/ab_hdr_nt_*.txt)
+    auto hload = [](const u32x4 *q) { return load16<false>(q); };
+    const u32x4 h0 = hload(hb);
+    const u32x4 h1 = hload(hb + h1i);
+    u32x4 h2, c2 = u32x4(0u), c3 = u32x4(0u);
+    if constexpr (IPM == IP_RX) {
+        // chunks 2 and 3 as well: an IHL-5 packet's TCP/UDP ports, data offset
+        // and flags (L4 bytes 0-3, 12-13) lie in chunks 1..3
+        c2 = hload(nch > 2 ? base + 2 : &g_zero_chunk);
+        c3 = hload(nch > 3 && s0 >= 12 ? base + 3 : &g_zero_chunk);
+        h2 = s0 > 12 ? c2 : u32x4(0u);
+    } else {
+        const u32x4 h2v = hload(hb + (big_enough ? (s0 > 12 ? 2u : 1u) : 0u));
+        h2 = s0 > 12 ? h2v : u32x4(0u);
+    }
+    // The data pass counts chunks from the packet's 128-B line, not from its
+    // 16-B chunk: the G*U-chunk span of each pass then ends on a line
+    // boundary, so no line is split between two passes (a split line is
+    // fetched once per pass: the nontemporal first fetch is gone from L2 by
+    // the time the next pass, a memory latency later, wants the other half).
+    // Chunks of that line before the packet are loaded (same line, same page)
+    // but fall outside every byte range below.
+    const uint32_t sl = (uint32_t)(start & 127u);
+    const uint32_t dch = big_enough ? (frame_ld + sl + 15) >> 4 : 0u;
+    const u32x4 *dbase = dch ? reinterpret_cast<const u32x4 *>(pp - sl) : &g_zero_chunk;
+    const uint32_t dlast = dch ? dch - 1u : 0u;
+
+    // first pass of data loads before the header is consumed: its latency
+    // overlaps them (vmcnt counts in issue order)
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t idx = u * G + gl;
+        v[u] = load16<true>(dbase + (idx < dch ? idx : dlast));
+    }
+    issue_fence();
+
+    const Hdr5 hd = header_dwords(h0, h1, h2, s0);
+    const uint32_t b0h = hd.d0 & 0xFFu;
+    const uint32_t version = b0h >> 4;
+    const uint32_t ihl4 = (b0h & 0xFu) << 2;
+    const uint32_t tl = (((hd.d0 >> 16) & 0xFFu) << 8) | (hd.d0 >> 24);
+    const uint32_t b6 = (hd.d1 >> 16) & 0xFFu, b7 = hd.d1 >> 24;
+    const bool frag = (b6 & 0x20u) || (((b6 & 0x1Fu) << 8) | b7);
+    const uint32_t proto = (hd.d2 >> 8) & 0xFFu;
+    const uint32_t stored_ip = hd.d2 >> 16;
+    uint32_t fl = 0;
+    if (version != 4)
+        fl |= TCSUM_PKT_BAD_VERSION;
+    if (ihl4 < 20 || ihl4 > frame)
+        fl |= TCSUM_PKT_BAD_HDRLEN;
+    if (tl < 20 || tl > frame || tl < ihl4)
+        fl |= TCSUM_PKT_BAD_TOTLEN;
+    if (frag)
+        fl |= TCSUM_PKT_FRAGMENT;
+    uint32_t hl = ihl4 < 20 ? 20u : ihl4;
+    hl = hl > frame ? frame : hl;
+    uint32_t end = tl < hl ? hl : tl;
+    end = end > frame ? frame : end;
+    uint32_t min_l4;
+    const uint32_t fld = l4_field(proto, min_l4);
+    if (fld && end - hl < min_l4)
+        fl |= TCSUM_PKT_L4_SHORT;
+    const bool bad = !big_enough ||
+                     (fl & (TCSUM_PKT_BAD_VERSION | TCSUM_PKT_BAD_HDRLEN | TCSUM_PKT_BAD_TOTLEN));
+    // the L4 checksum field this mode treats specially (tx: zero + store;
+    // rx: is it zero?) -- none for fragments, short L4, or ICMP on rx
+    const bool field_on = IPM != IP_SUMS && !bad && !frag && fld && !(fl & TCSUM_PKT_L4_SHORT) &&
+                          !(IPM == IP_RX && proto == 1);
+    // The L4 pseudo-header (tools.c:58-70), folded now: src, dst (packet bytes
+    // 12..19), {0, proto}, the L4 length; kept as one register past the data pass
+    uint32_t pseudo = 0;
+    if (proto == 6 || proto == 17)
+        pseudo = fold16(add_halves(add_halves(0u, hd.d3), hd.d4) + (proto << 8) + bswap16((end - hl) & 0xFFFFu));
+    if (big_enough && proto != 6 && proto != 17 && proto != 1)
+        fl |= TCSUM_PKT_PROTO_OTHER;
+
+    // rx: every gate that needs no sum, decided now, in the reference's order
+    // (the verdict at the end only places the two checksum tests between them):
+    //   pre  -- ipv4_in before the header checksum test (ipv4.c:475, 222-240)
+    //   mid  -- the L4 input before its checksum test (tcp_in.c:70-74 and
+    //           pktbuf_remove_header, udp.c:386-403, icmpv4.c:68)
+    //   post -- the L4 input after it (tcp_in.c:87-103)
+    // packed as three int8 in one register.
+    uint32_t vcodes = 0;
+    if constexpr (IPM == IP_RX) {
+        int vpre = 0, vmid = 0, vpost = 0;
+        if (!big_enough)
+            vpre = TCSUM_ERR_SIZE; // pktbuf_set_cont(buf, 20), ipv4.c:475
+        else if (version != 4)
+            vpre = TCSUM_ERR_NOT_SUPPORT; // ipv4.c:222-226
+        else if (ihl4 < 20 || tl < 20 || frame < tl)
+            vpre = TCSUM_ERR_SIZE; // ipv4.c:228-240
+        else if (frag)
+            vmid = 0; // ipv4.c:506-509: queued for reassembly, OK past the header test
+        else if (proto == 6 || proto == 17) { // TCP: pktbuf_remove_header + tcp_in (ipv4.c:450-452); UDP: udp_in
+            // the header words (L4 bytes 0-3: ports; 12-15: data offset,
+            // flags) from the 32 bytes at chunk (s0 + ihl4) / 16: chunks 1..3
+            // already in registers for IHL 5, two more loads otherwise
+            uint32_t ports = 0, oflags = 0;
+            if (tl >= ihl4 + 8u) {
+                const uint32_t o = s0 + ihl4, cw = o >> 4;
+                u32x4 wa, wb;
+                if (ihl4 == 20) {
+                    wa = cw == 1 ? h1 : c2;
+                    wb = cw == 1 ? c2 : c3;
+                } else {
+                    wa = load16<false>(base + cw);
+                    wb = load16<false>(cw + 1 < nch ? base + cw + 1 : &g_zero_chunk);
+                }
+                const Hdr5 l4h = header_dwords(wa, wb, u32x4(0u), o & 15u);
+                ports = l4h.d0;
+                oflags = l4h.d3;
+            }
+            const uint32_t sport = ports & 0xFFFFu, dport = ports >> 16, fword = oflags & 0xFFFFu;
+            if (proto == 6) {
+                if (ihl4 > tl)
+                    vmid = TCSUM_ERR_SIZE; // the reference runs off its block list (pktbuf.c:264-281)
+                else if (tl - ihl4 < 20)
+                    vmid = TCSUM_ERR_SYS; // pktbuf_set_cont fails: tcp_in returns -1, tcp_in.c:70-74
+                else if (tl - ihl4 < (((oflags & 0xFFu) >> 4) << 2))
+                    vpost = TCSUM_ERR_SIZE; // tcp_in.c:87-91
+                else if (sport == 0 || dport == 0 || fword == 0)
+                    vpost = TCSUM_ERR_BROKEN; // tcp_in.c:93-103
+            } else {
+                if (tl < ihl4 + 8)
+                    vmid = TCSUM_ERR_SIZE; // pktbuf_set_cont(buf, 8 + ihl), udp.c:386-391
+                else if (dport == 0)
+                    vmid = TCSUM_ERR_UNREACHABLE; // no socket has port 0: udp.c:337-340, :399-403
+            }
+        } else if (proto == 1) { // icmpv4_in, ipv4.c:427; its checksum test cannot fail (A10)
+            vmid = tl < ihl4 + 4 ? TCSUM_ERR_SIZE : 0; // pktbuf_set_cont(buf, ihl + 4), icmpv4.c:68
+        } // other protocols: raw_in, no checksum (ipv4.c:460-469)
+        vcodes = (uint32_t)(uint8_t)vpre | ((uint32_t)(uint8_t)vmid << 8) | ((uint32_t)(uint8_t)vpost << 16) |
+                 (stored_ip != 0 ? 1u << 24 : 0u);
+    }
+
+    // byte ranges, from the data pass's line base (end <= tl <= 65535 whenever
+    // it matters; clamp so a huge bogus frame cannot overflow)
+    const int h_end = (int)(hl < 65600u ? hl : 65600u) + (int)sl;
+    const int l_end = (int)(end < 65600u ? end : 65600u) + (int)sl;
+    const int f0 = field_on ? (int)(hl + fld) + (int)sl : -64;
+    const int i0 = (int)sl + 10; // IPv4 header checksum field
+
+    uint32_t acc_h = 0, acc_l = 0, acc_f = 0;
+    // one pass of U chunks per lane starting at chunk b0 (pass 0: the loads
+    // already in flight; later passes load and sum inside one iteration, so
+    // no vector registers are carried around the loop -- see frame_consume)
+    auto pass = [&](const u32x4 (&vv)[U], uint32_t b0) {
+        uint32_t ph = 0, pl = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t idx = b0 + u * G + gl;
+            const bool valid = idx < dch;
+            const int c = (int)(16u * idx);
+            const bool inner = valid && c >= h_end && c + 16 <= l_end && (f0 + 2 <= c || f0 >= c + 16);
+            if (valid && !inner) { // header chunks, the field chunk(s), the last chunk: rare
+                uint32_t th = region_sum(vv[u], c, (int)sl, h_end);
+                uint32_t tl4 = region_sum(vv[u], c, h_end, l_end);
+                if (field_on) {
+                    const uint32_t tf = region_sum(vv[u], c, f0, f0 + 2);
+                    if (IPM == IP_TX)
+                        tl4 -= tf; // tcp_out.c:19 / udp.c:320 / icmpv4.c:58 zero it first
+                    else
+                        acc_f += tf;
+                }
+                if (IPM == IP_TX)
+                    th -= region_sum(vv[u], c, i0, i0 + 2); // ipv4.c:643
+                ph += th;
+                pl += tl4;
+            }
+            pl = chunk_sum_w(pl, vv[u], inner ? 0x00010001u : 0u);
+        }
+        acc_h += ph; // header <= 60 bytes: no overflow
+        acc_l = fold_step(acc_l + pl);
+    };
+    if (dch)
+        pass(v, 0u);
+    for (uint32_t b0 = G * U; b0 < dch; b0 += G * U) {
+        u32x4 w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t idx = b0 + u * G + gl;
+            w[u] = load16<true>(dbase + (idx < dch ? idx : dlast));
+        }
+        pass(w, b0);
+    }
+    acc_h = group_sum<G>(acc_h);
+    acc_l = group_sum<G>(acc_l);
+    if (IPM == IP_RX)
+        acc_f = group_sum<G>(acc_f);
+
+    if (live && gl == 0) {
+        uint32_t ip = 0, l4 = 0;
+        if (!big_enough) {
+            fl = TCSUM_PKT_SHORT;
+        } else {
+            const bool odd = start & 1u;
+            uint32_t fh = fold16(acc_h);
+            uint32_t f4 = fold16(acc_l);
+            if (odd) {
+                fh = rot8(fh);
+                f4 = rot8(f4);
+            }
+            ip = ~fh & 0xFFFFu;
+            if (proto == 6 || proto == 17)
+                l4 = ~fold_step(f4 + pseudo) & 0xFFFFu;
+            else if (proto == 1)
+                l4 = ~f4 & 0xFFFFu;
+        }
+        if constexpr (IPM == IP_TX) {
+            if (opts & IP_OPT_DEFER) // bit 16: the IPv4 field; low 16: the L4 field's offset (0: none)
+                reinterpret_cast<uint32_t *>(verdict_out)[pk] = bad ? 0u : (1u << 16) | (field_on ? hl + fld : 0u);
+            else if (!bad && !(opts & IP_OPT_NO_STORE)) { // stored in host order, like the struct fields
+                pp[10] = (uint8_t)ip;
+                pp[11] = (uint8_t)(ip >> 8);
+                if (field_on) {
+                    pp[hl + fld] = (uint8_t)l4;
+                    pp[hl + fld + 1] = (uint8_t)(l4 >> 8);
+                }
+            }
+        }
+        if constexpr (IPM == IP_RX) {
+            // The first gate that rejects, in the reference's order: ipv4_in /
+            // is_pkt_ok, then the L4 input ip_normal_in dispatches to
+            // (ipv4.c:420-470), up to socket lookup.  Pinned by the reference
+            // stack's own verdicts (tests/golden/ipv4_rx_*, oracle/stack_gen.c).
+            const int vpre = (int8_t)(vcodes & 0xFFu), vmid = (int8_t)((vcodes >> 8) & 0xFFu);
+            const int vpost = (int8_t)((vcodes >> 16) & 0xFFu);
+            int v8;
+            if (vpre)
+                v8 = vpre;
+            else if ((vcodes >> 24) && ip != 0)
+                v8 = TCSUM_ERR_BROKEN; // ipv4.c:241-249
+            else if (vmid)
+                v8 = vmid;
+            else if (acc_f != 0 && l4 != 0)
+                v8 = TCSUM_ERR_BROKEN; // tcp_in.c:77-85, udp.c:407-415 (field_on: TCP/UDP only)
+            else
+                v8 = vpost;
+            verdict_out[pk] = (int8_t)v8;
+        }
+        if (out)
+            out[pk] = ip | (l4 << 16);
+        if (flags_out)
+            flags_out[pk] = (uint8_t)fl;
+    }
+}
+
+template <int G, int U, int IPM, int T = 256>
+__global__ __launch_bounds__(T) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
+                                            uint32_t n, uint32_t *__restrict__ out,
+                                            uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
+                                            uint32_t opts, uint32_t xg)
+{
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    ipv4_packet<G, U, IPM>(arena, pkts, blk * (uint32_t)(T / G) + threadIdx.x / G, n, out, flags_out, verdict_out,
+                           opts); // no 32-bit wrap for any n
+}
+
+// The deferred tx stores (IP_OPT_DEFER): one lane per packet writes the values
+// k_ipv4 left in `csums` at the positions it left in `pos` (bit 16: the IPv4
+// header field; low 16 bits: the L4 field's offset, 0 for none).  All the
+// packets' field writes then reach memory in one short burst instead of one at
+// a time through the read stream (u16 or nontemporal stores: no different;
+// system-scope write-through stores: slower; profiles/r02/ab_tx_split*.txt).
+__global__ __launch_bounds__(256) void k_tx_scatter(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
+                                                    uint32_t n, const uint32_t *__restrict__ csums,
+                                                    const uint32_t *__restrict__ pos)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t q = pos[i];
+    if (!q)
+        return;
+    const uint32_t v = csums[i];
+    uint8_t *pp = arena + pkts[i].offset;
+    pp[10] = (uint8_t)v; // ipv4.c:643,656, host order like the struct field
+    pp[11] = (uint8_t)(v >> 8);
+    const uint32_t f = q & 0xFFFFu;
+    if (f) { // tcp_out.c:19-20 / udp.c:320-321 / icmpv4.c:45-58
+        pp[f] = (uint8_t)(v >> 16);
+        pp[f + 1] = (uint8_t)(v >> 24);
+    }
+}
+
+} // namespace tcsum

@@ -17,14 +17,31 @@ enum Mode : int {
 };
 
 struct Geometry {
-    int lanes; // G: lanes that share one packet (4..64, power of two)
-    int loads; // U: 16-byte loads in flight per lane per pass
-    int persist; // 0: one pass per wave; 1: resident grid + descriptor prefetch;
-                 // 2: resident grid, two ranges in flight per wave (k_segments_pp)
-    int xcd;     // consecutive workgroups kept on one XCD (1: dispatch order)
-    int packed;  // K > 0: checksum_peso / pktbuf_checksum16 batches as a packed
-                 // stream, K consecutive ranges per 16-wave workgroup (k_segments_pk)
+    int lanes;  // G: lanes that share one packet (4..64, power of two; 256 / 1024: one range per workgroup)
+    int loads;  // U: 16-byte loads in flight per lane per pass
+    int xcd;    // consecutive workgroups kept on one XCD (1: dispatch order)
+    int packed; // K > 0: checksum_peso / pktbuf_checksum16 batches as a packed
+                // stream, K consecutive ranges per 4-wave workgroup (k_segments_pk)
+    int flat;   // 1: byte-window stream (k_flat_*): fixed byte windows per workgroup
 };
+
+// Test and measurement overrides (include/tcsum_debug.h): -1 = the router's
+// own choice.  Read on launch paths; set only by tcsum_debug_set.
+enum Knob : int {
+    KNOB_LANES = 0,  // per-range lanes (G)
+    KNOB_LOADS,      // per-range loads per lane (U)
+    KNOB_XCD,        // XCD run length
+    KNOB_PACKED,     // 0 / 1: k_segments_pk off / on
+    KNOB_FLAT,       // 0 / 1: the byte-window stream off / on
+    KNOB_TX_SPLIT,   // 0 / 1: tx fill stores in the kernel / deferred to k_tx_scatter
+    KNOB_ARGS_LAUNCH, // 0: drop-in launch path with its descriptor in pinned memory
+    KNOB_SYNC_BLOCK, // 1: drop-in calls block in hipStreamSynchronize instead of spinning
+    KNOB_E2E_TRACE,  // 1: tcsum_host_batch_peso prints phase stamps
+    KNOB_E2E_CHUNK_MB, // tcsum_host_batch_peso chunk size
+    KNOB_COUNT
+};
+int64_t knob(Knob k);
+void set_knob(Knob k, int64_t v);
 
 Geometry pick_geometry(uint64_t mean_len);
 
@@ -47,6 +64,7 @@ hipError_t launch_ipv4_tx_to(Geometry g, uint8_t *arena, uint8_t *store, const t
 // bytes): no allocation, so it can be captured in a hipGraph.
 // give back the tx fill's pooled scratch of device dev (tcsum_release)
 hipError_t scratch_trim(int dev);
+uint64_t scratch_reserved(int dev);
 
 hipError_t launch_ipv4_tx_scratch(Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
                                   uint8_t *flags, uint32_t *scratch, hipStream_t stream);
@@ -109,20 +127,5 @@ hipError_t launch_once(Mode mode, const uint8_t *stage, uint32_t off, uint32_t l
 
 hipError_t launch_call_server(CallBox *box /*device-visible address*/, const uint8_t *stage /*device-visible*/,
                               uint32_t last, uint64_t idle_ticks, hipStream_t stream);
-
-hipError_t launch_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, uint64_t seed,
-                             hipStream_t stream);
-
-hipError_t launch_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, hipStream_t stream);
-hipError_t launch_probe_desc(const void *arena, const void *descs, uint32_t n, uint64_t mean_len, uint32_t *sink,
-                             hipStream_t stream);
-// mode 0: tcsum_batch_ipv4's loads; 1: rx verify's; 2: the deferred tx fill's
-// loads + its scratch writes + k_tx_scatter (writes junk into the fields)
-hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t mean_len, int mode,
-                             uint32_t *sink, hipStream_t stream);
-hipError_t launch_probe_tile(const void *p, uint64_t nbytes, int lanes, int loads, uint32_t *sink, hipStream_t stream);
-
-hipError_t launch_synth_ipv4(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t seed,
-                             hipStream_t stream);
 
 } // namespace tcsum

@@ -303,12 +303,12 @@ def host_batch_ipv4_rx_verify(host_arena, pkts: np.ndarray, device: int = 0, dev
 
 def synth_fill(arena, nbytes: int | None = None, byte_base: int = 0, seed: int = 20240807, stream=None):
     n = arena.numel() if nbytes is None else nbytes
-    _lib.check(_lib.lib().tcsum_synth_fill(arena.data_ptr(), n, byte_base, seed, _stream_ptr(stream)),
+    _lib.check(_lib.bench_lib().tcsum_synth_fill(arena.data_ptr(), n, byte_base, seed, _stream_ptr(stream)),
                "tcsum_synth_fill")
 
 
 def synth_ipv4(arena, pkts, n: int, seed: int = 20240807, stream=None):
-    _lib.check(_lib.lib().tcsum_synth_ipv4(arena.data_ptr(), pkts.data_ptr(), n, seed, _stream_ptr(stream)),
+    _lib.check(_lib.bench_lib().tcsum_synth_ipv4(arena.data_ptr(), pkts.data_ptr(), n, seed, _stream_ptr(stream)),
                "tcsum_synth_ipv4")
 
 
@@ -318,19 +318,20 @@ def probe_read(buf, nbytes: int | None = None, sink=None, stream=None):
     if sink is None:
         sink = torch.zeros(1, dtype=torch.uint32, device=buf.device)
     n = buf.numel() * buf.element_size() if nbytes is None else nbytes
-    _lib.check(_lib.lib().tcsum_probe_read(buf.data_ptr(), n, sink.data_ptr(), _stream_ptr(stream)),
+    _lib.check(_lib.bench_lib().tcsum_probe_read(buf.data_ptr(), n, sink.data_ptr(), _stream_ptr(stream)),
                "tcsum_probe_read")
     return sink
 
 
-def probe_tile(buf, nbytes: int, lanes: int, loads: int, sink=None, stream=None):
+def probe_tile(buf, nbytes: int, lanes: int, loads: int, sink=None, stream=None, dep: bool = False):
     """Plain streaming read of `buf` in the product kernels' tile shape
-    (tcsum_probe_tile): the ceiling the checksum kernel is compared with."""
+    (tcsum_probe_tile): the ceiling the checksum kernel is compared with;
+    dep=True puts each unit's loads behind one dependent 16-B read."""
     torch = _torch()
     if sink is None:
         sink = torch.zeros(1, dtype=torch.uint32, device=buf.device)
-    _lib.check(_lib.lib().tcsum_probe_tile(buf.data_ptr(), nbytes, lanes, loads, sink.data_ptr(),
-                                           _stream_ptr(stream)), "tcsum_probe_tile")
+    _lib.check(_lib.bench_lib().tcsum_probe_tile(buf.data_ptr(), nbytes, lanes, loads, 1 if dep else 0,
+                                                 sink.data_ptr(), _stream_ptr(stream)), "tcsum_probe_tile")
     return sink
 
 
@@ -339,7 +340,7 @@ def probe_segments(arena, segs, n: int, total_bytes: int, sink=None, stream=None
     torch = _torch()
     if sink is None:
         sink = torch.zeros(1, dtype=torch.uint32, device=arena.device)
-    _lib.check(_lib.lib().tcsum_probe_segments(arena.data_ptr(), segs.data_ptr(), n, total_bytes, sink.data_ptr(),
+    _lib.check(_lib.bench_lib().tcsum_probe_segments(arena.data_ptr(), segs.data_ptr(), n, total_bytes, sink.data_ptr(),
                                                _stream_ptr(stream)), "tcsum_probe_segments")
     return sink
 
@@ -352,7 +353,7 @@ def probe_ipv4(arena, pkts, n: int, total_bytes: int, rx: bool = False, sink=Non
     if sink is None:
         sink = torch.zeros(1, dtype=torch.uint32, device=arena.device)
     mode = 2 if tx else 1 if rx else 0
-    _lib.check(_lib.lib().tcsum_probe_ipv4(arena.data_ptr(), pkts.data_ptr(), n, total_bytes, mode,
+    _lib.check(_lib.bench_lib().tcsum_probe_ipv4(arena.data_ptr(), pkts.data_ptr(), n, total_bytes, mode,
                                            sink.data_ptr(), _stream_ptr(stream)), "tcsum_probe_ipv4")
     return sink
 
@@ -361,6 +362,44 @@ def pick_geometry(mean_len: int):
     g, u = ctypes.c_int(), ctypes.c_int()
     _lib.lib().tcsum_pick_geometry(mean_len, ctypes.byref(g), ctypes.byref(u))
     return g.value, u.value
+
+
+def route(mean_len: int) -> dict:
+    """The route the batch calls take for a mean range length (debug knobs
+    applied): lanes, loads, xcd, packed K (0 = off), flat (tcsum_debug_route)."""
+    r = (ctypes.c_int32 * 5)()
+    _lib.lib().tcsum_debug_route(mean_len, r)
+    return dict(zip(("lanes", "loads", "xcd", "packed", "flat"), list(r)))
+
+
+def debug_set(key: str, value: int) -> None:
+    """Force a route knob for this process (include/tcsum_debug.h; tests and
+    measurement only; -1 gives the choice back to the router)."""
+    _lib.check(_lib.lib().tcsum_debug_set(key.encode(), int(value)), f"tcsum_debug_set({key})")
+
+
+def debug_get(key: str) -> int:
+    return int(_lib.lib().tcsum_debug_get(key.encode()))
+
+
+class debug:
+    """Context manager: `with tc.debug(lanes=16, loads=6): ...` sets the knobs
+    and restores their previous values on exit."""
+
+    def __init__(self, **knobs):
+        self.knobs = knobs
+        self.saved = {}
+
+    def __enter__(self):
+        for k, v in self.knobs.items():
+            self.saved[k] = debug_get(k)
+            debug_set(k, -1 if v is None else v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.saved.items():
+            debug_set(k, v)
+        return False
 
 
 def device_count() -> int:

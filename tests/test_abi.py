@@ -9,7 +9,8 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = ["tcsum.h", "tcsum_legacy.h", "tcsum_synth.h"]
+HEADERS = ["tcsum.h", "tcsum_legacy.h", "tcsum_debug.h"]  # libtcsum.so
+BENCH_HEADERS = ["tcsum_synth.h"]  # libtcsum_bench.so
 
 
 @pytest.fixture(scope="module")
@@ -34,24 +35,87 @@ def test_headers_declare_the_drop_in_trio():
     names = declared_functions()
     assert {"checksum16", "checksum_peso", "pktbuf_checksum16"} <= names
     assert {"tcsum_batch_segments", "tcsum_batch_peso", "tcsum_batch_ipv4", "tcsum_host_batch_peso",
-            "tcsum_plat_init", "tcsum_host_alloc", "tcsum_host_free", "tcsum_synth_fill",
-            "tcsum_synth_ipv4"} <= names
+            "tcsum_plat_init", "tcsum_host_alloc", "tcsum_host_free", "tcsum_debug_set"} <= names
+    assert {"tcsum_synth_fill", "tcsum_synth_ipv4", "tcsum_probe_read"} <= declared_functions(BENCH_HEADERS)
+
+
+def _exports(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if " T " in line}
 
 
 def test_every_declared_symbol_is_exported(libpath):
-    out = subprocess.run(["nm", "-D", "--defined-only", libpath], capture_output=True, text=True,
-                         check=True).stdout
-    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
-    missing = declared_functions() - exported
-    assert not missing, missing
+    """Each library exports exactly what its headers declare (export maps)."""
+    from tcp_amd import _lib
+    assert _exports(libpath) == declared_functions()
+    assert _exports(_lib.BENCH_LIB_PATH) == declared_functions(BENCH_HEADERS)
 
 
 def test_binding_table_matches_headers(libpath):
     from tcp_amd import _lib
     assert set(_lib.SIGNATURES) == declared_functions()
+    assert set(_lib.BENCH_SIGNATURES) == declared_functions(BENCH_HEADERS)
     L = _lib.lib()  # loads libamdhip64 too; no device is touched
     for name in _lib.SIGNATURES:
         assert getattr(L, name)
+    B = _lib.bench_lib()
+    for name in _lib.BENCH_SIGNATURES:
+        assert getattr(B, name)
+
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def code_object_kernels(path):
+    """Demangled names of the gfx950 kernels in a library's code object."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        fat, dev = os.path.join(d, "fat.bin"), os.path.join(d, "dev.o")
+        subprocess.run([f"{LLVM}/llvm-objcopy", "-O", "binary", "--only-section=.hip_fatbin", path, fat], check=True)
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={dev}"], check=True)
+        syms = subprocess.run([f"{LLVM}/llvm-readelf", "--symbols", dev], capture_output=True, text=True,
+                              check=True).stdout
+    names = {ln.split()[-1] for ln in syms.splitlines() if ln.split() and ln.split()[-1].endswith(".kd")}
+    out = subprocess.run(["c++filt"], input="\n".join(sorted(names)), capture_output=True, text=True).stdout
+    return {n.replace(" [clone .kd]", "") for n in out.splitlines() if n}
+
+
+@pytest.mark.skipif(not os.path.exists(f"{LLVM}/clang-offload-bundler"), reason="no ROCm llvm tools")
+def test_product_code_object_holds_only_product_kernels(libpath):
+    """libtcsum.so's code object: the kernels its router launches, the two
+    resident servers and the drop-in one-shots -- no load probes, no
+    synthetic-data kernels, no measurement-only shapes."""
+    from tcp_amd import _lib
+    prod = code_object_kernels(libpath)
+    families = ("tcsum::k_segments<", "tcsum::k_segments_wg<", "tcsum::k_segments_wgx<16, 32, 4,",
+                "tcsum::k_segments_pk<", "tcsum::k_ipv4<", "tcsum::k_tx_scatter(", "tcsum::k_server<",
+                "tcsum::k_call(", "tcsum::k_inline16<", "tcsum::k_once<", "tcsum::k_flat_")
+    stray = [k for k in prod if not any(f in k for f in families) or "true>" in k]
+    assert not stray, stray
+    assert not any("k_probe" in k or "k_synth" in k or "k_segments_p<" in k or "k_segments_pp<" in k for k in prod)
+    bench = code_object_kernels(_lib.BENCH_LIB_PATH)
+    assert any("k_probe_read" in k for k in bench) and any("k_synth_fill" in k for k in bench)
+
+
+def test_environment_does_not_route(libpath):
+    """Round 1-3's TCSUM_G / TCSUM_U / TCSUM_PACKED ... environment overrides
+    are gone: a child process with them set gets the router's own choice."""
+    code = ("import tcp_amd as tc; r = tc.route(1500); "
+            "assert (r['lanes'], r['loads'], r['packed']) == (16, 6, 8), r; print('ok')")
+    env = dict(os.environ, TCSUM_G="4", TCSUM_U="1", TCSUM_PACKED="0", TCSUM_XCD="1", TCSUM_P="2")
+    r = subprocess.run([os.sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr
+
+
+def test_debug_knobs(libpath):
+    import tcp_amd as tc
+    assert tc.debug_get("lanes") == -1 and tc.debug_get("no_such_knob") == -2
+    with tc.debug(lanes=32, loads=6):
+        assert tc.route(1500)["lanes"] == 32 and tc.route(1500)["packed"] == 0
+    assert tc.route(1500)["lanes"] == 16 and tc.debug_get("lanes") == -1
+    from tcp_amd import _lib
+    assert _lib.lib().tcsum_debug_set(b"no_such_knob", 1) == _lib.ERR_PARAM
 
 
 def test_capture_helper_is_a_library_of_its_own(libpath):
@@ -112,10 +176,9 @@ def test_geometry_choice(libpath):
     assert pick_geometry(40000) == (256, 16)
     assert pick_geometry(65536) == (1024, 4)
     assert pick_geometry(64) == (4, 1)
+    shapes = {(4, 1), (4, 2), (8, 4), (16, 3), (16, 4), (16, 6), (16, 8), (32, 6), (256, 16), (1024, 4)}
     for n in range(0, 70000, 37):  # every choice is an instantiated kernel
-        g, u = pick_geometry(n)
-        assert (g in (4, 8, 16, 32, 64) and u in (1, 2, 3, 4, 6, 8, 16)) or (g == 256 and u in (4, 8, 16)) \
-            or (g, u) == (1024, 4)
+        assert pick_geometry(n) in shapes
 
 
 def test_device_count_without_gpu(libpath):
@@ -149,7 +212,7 @@ def test_batch_argument_errors_without_device(libpath):
                                               ctypes.c_void_p(66), 64, 0, None) == _lib.ERR_PARAM  # misaligned
     assert L.tcsum_batch_ipv4_rx_verify(None, None, 4, None, None, None, 0, None) == _lib.ERR_PARAM
     assert L.tcsum_batch_peso(None, None, 0, None, 0, None) == _lib.OK  # empty batch
-    assert L.tcsum_synth_fill(ctypes.c_void_p(8), 16, 0, 1, None) == _lib.ERR_PARAM  # misaligned
+    assert _lib.bench_lib().tcsum_synth_fill(ctypes.c_void_p(8), 16, 0, 1, None) == _lib.ERR_PARAM  # misaligned
     from tcp_amd import PESO_DTYPE
     seg = np.zeros(1, PESO_DTYPE)
     seg["offset"], seg["len"] = 10, 100

@@ -4,6 +4,7 @@ pageable (staged) -- give byte-for-byte the reference's tx fill, its rx
 verdicts and both checksums (tests/golden/ipv4_*.bin, written by the
 reference's own ipv4/tcp/udp/icmp checksum code paths), and the same answers
 as the device-resident calls."""
+import os
 import numpy as np
 import pytest
 
@@ -378,3 +379,28 @@ def test_host_paths_fuzz(tc, oracle, monkeypatch, seed):
         np.testing.assert_array_equal(np.array(view[: data.size]), want)
     finally:
         del keep
+
+
+def test_release_trims_the_tx_scratch_pool_without_a_context(tc):
+    """a process that only runs device-resident tx fills on its
+    own streams never creates the library's device context; tcsum_release
+    must still give the deferred fill's pooled scratch back."""
+    import subprocess
+    import sys
+    code = r"""
+import sys; sys.path.insert(0, %r)
+import torch, tcp_amd as tc
+from tcp_amd import workload
+b = workload.make_batch("mixed", n=200000)
+arena, descs = workload.materialize(b)
+tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)  # >= 131072: deferred
+torch.cuda.synchronize()
+before = tc.debug_get("scratch_reserved")
+tc.release(0)
+print("reserved", before, tc.debug_get("scratch_reserved"))
+""" % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("reserved")][-1]
+    before, after = map(int, line.split()[1:])
+    assert before >= 200000 * 4 and after == 0, line

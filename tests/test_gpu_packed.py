@@ -30,13 +30,12 @@ def tc(torch):
     return tcp_amd
 
 
-@pytest.fixture(params=[(8, 3), (16, 2), (4, 3)])
-def packed(monkeypatch, request):
-    """The packed kernel in three workgroup shapes (waves x loads per lane)."""
-    w, u = request.param
-    monkeypatch.setenv("TCSUM_PACKED", "1")
-    monkeypatch.setenv("TCSUM_PK_W", str(w))
-    monkeypatch.setenv("TCSUM_PK_U", str(u))
+@pytest.fixture(params=["packed"])
+def packed(tc, request):
+    """The stream kernel under test (debug knobs, include/tcsum_debug.h)."""
+    tc.debug_set("packed", 1)
+    yield request.param
+    tc.debug_set("packed", -1)
 
 
 def _arena(rng, size):

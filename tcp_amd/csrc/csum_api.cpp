@@ -515,7 +515,7 @@ int tcsum_batch_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uin
         return TCSUM_ERR_PARAM;
     const hipError_t e = tcsum::launch_ipv4(0, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
                                             const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts,
-                                            n, out, flags, nullptr, static_cast<hipStream_t>(stream));
+                                            n, out, flags, nullptr, static_cast<hipStream_t>(stream), total_bytes_hint);
     return rc_of(e);
 }
 
@@ -541,7 +541,7 @@ int tcsum_batch_ipv4_tx_fill(void *arena, const tcsum_pkt_t *pkts, uint32_t n, u
         split = false;
     const hipError_t e = tcsum::launch_ipv4(split ? 4 : 1, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
                                             static_cast<uint8_t *>(arena), pkts, n, out, flags, nullptr,
-                                            static_cast<hipStream_t>(stream));
+                                            static_cast<hipStream_t>(stream), total_bytes_hint);
     return rc_of(e);
 }
 
@@ -570,7 +570,7 @@ int tcsum_batch_ipv4_tx_offload(const void *arena, const tcsum_pkt_t *pkts, uint
     // the kernel never writes the arena in this mode
     const hipError_t e = tcsum::launch_ipv4(3, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
                                             const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts,
-                                            n, out, flags, nullptr, static_cast<hipStream_t>(stream));
+                                            n, out, flags, nullptr, static_cast<hipStream_t>(stream), total_bytes_hint);
     return rc_of(e);
 }
 
@@ -626,7 +626,7 @@ int tcsum_batch_ipv4_rx_verify(const void *arena, const tcsum_pkt_t *pkts, uint3
     // the kernel never writes the arena in this mode
     const hipError_t e = tcsum::launch_ipv4(2, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
                                             const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts,
-                                            n, out, flags, verdict, static_cast<hipStream_t>(stream));
+                                            n, out, flags, verdict, static_cast<hipStream_t>(stream), total_bytes_hint);
     return rc_of(e);
 }
 

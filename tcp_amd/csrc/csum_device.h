@@ -923,6 +923,195 @@ __device__ __forceinline__ uint32_t l4_field(uint32_t proto, uint32_t &min_len)
     return proto == 6 ? 16u : proto == 17 ? 6u : proto == 1 ? 2u : 0u;
 }
 
+// What the fixed IPv4 header (and, rx, the TCP/UDP header words) decide
+// before any sum: the is_pkt_ok flags, the header and L4 byte ranges, the
+// checksum field this mode treats specially, the folded pseudo-header and
+// (rx) every sum-free gate.  Shared by k_ipv4 and the byte-window stream
+// k_flat_ipv4 so that both decide exactly alike.
+struct IpHdr {
+    uint32_t fl;     // TCSUM_PKT_* (SHORT is set at the end)
+    uint32_t hl;     // header bytes summed: IHL*4, clamped to [20, frame]
+    uint32_t end;    // L4 range end: total_len clamped to [hl, frame]
+    uint32_t proto;
+    uint32_t fld;    // the L4 checksum field's offset in the L4 header (0: none)
+    uint32_t pseudo; // TCP/UDP pseudo-header, folded (tools.c:58-70)
+    uint32_t vcodes; // rx: three int8 gate codes + (stored header checksum != 0) << 24
+    bool bad;        // SHORT / BAD_*: nothing stored, no field
+    bool field_on;   // the L4 field this mode zeroes (tx) or tests (rx)
+};
+
+// hd: the 20 fixed header bytes; l4words(ihl4): the Hdr5 of the 16 bytes at
+// packet offset ihl4 (the TCP/UDP header's first bytes; called for rx only).
+template <int IPM, class L4Words>
+__device__ __forceinline__ IpHdr ip_parse(const Hdr5 &hd, uint32_t frame, bool big_enough, L4Words &&l4words)
+{
+    IpHdr h;
+    const uint32_t b0h = hd.d0 & 0xFFu;
+    const uint32_t version = b0h >> 4;
+    const uint32_t ihl4 = (b0h & 0xFu) << 2;
+    const uint32_t tl = (((hd.d0 >> 16) & 0xFFu) << 8) | (hd.d0 >> 24);
+    const uint32_t b6 = (hd.d1 >> 16) & 0xFFu, b7 = hd.d1 >> 24;
+    const bool frag = (b6 & 0x20u) || (((b6 & 0x1Fu) << 8) | b7);
+    const uint32_t proto = (hd.d2 >> 8) & 0xFFu;
+    const uint32_t stored_ip = hd.d2 >> 16;
+    uint32_t fl = 0;
+    if (version != 4)
+        fl |= TCSUM_PKT_BAD_VERSION;
+    if (ihl4 < 20 || ihl4 > frame)
+        fl |= TCSUM_PKT_BAD_HDRLEN;
+    if (tl < 20 || tl > frame || tl < ihl4)
+        fl |= TCSUM_PKT_BAD_TOTLEN;
+    if (frag)
+        fl |= TCSUM_PKT_FRAGMENT;
+    uint32_t hl = ihl4 < 20 ? 20u : ihl4;
+    hl = hl > frame ? frame : hl;
+    uint32_t end = tl < hl ? hl : tl;
+    end = end > frame ? frame : end;
+    uint32_t min_l4;
+    const uint32_t fld = l4_field(proto, min_l4);
+    if (fld && end - hl < min_l4)
+        fl |= TCSUM_PKT_L4_SHORT;
+    const bool bad = !big_enough ||
+                     (fl & (TCSUM_PKT_BAD_VERSION | TCSUM_PKT_BAD_HDRLEN | TCSUM_PKT_BAD_TOTLEN));
+    // the L4 checksum field this mode treats specially (tx: zero + store;
+    // rx: is it zero?) -- none for fragments, short L4, or ICMP on rx
+    const bool field_on = IPM != IP_SUMS && !bad && !frag && fld && !(fl & TCSUM_PKT_L4_SHORT) &&
+                          !(IPM == IP_RX && proto == 1);
+    // The L4 pseudo-header (tools.c:58-70), folded now: src, dst (packet bytes
+    // 12..19), {0, proto}, the L4 length; kept as one register past the data pass
+    uint32_t pseudo = 0;
+    if (proto == 6 || proto == 17)
+        pseudo = fold16(add_halves(add_halves(0u, hd.d3), hd.d4) + (proto << 8) + bswap16((end - hl) & 0xFFFFu));
+    if (big_enough && proto != 6 && proto != 17 && proto != 1)
+        fl |= TCSUM_PKT_PROTO_OTHER;
+
+    // rx: every gate that needs no sum, decided now, in the reference's order
+    // (the verdict at the end only places the two checksum tests between them):
+    //   pre  -- ipv4_in before the header checksum test (ipv4.c:475, 222-240)
+    //   mid  -- the L4 input before its checksum test (tcp_in.c:70-74 and
+    //           pktbuf_remove_header, udp.c:386-403, icmpv4.c:68)
+    //   post -- the L4 input after it (tcp_in.c:87-103)
+    // packed as three int8 in one register.
+    uint32_t vcodes = 0;
+    if constexpr (IPM == IP_RX) {
+        int vpre = 0, vmid = 0, vpost = 0;
+        if (!big_enough)
+            vpre = TCSUM_ERR_SIZE; // pktbuf_set_cont(buf, 20), ipv4.c:475
+        else if (version != 4)
+            vpre = TCSUM_ERR_NOT_SUPPORT; // ipv4.c:222-226
+        else if (ihl4 < 20 || tl < 20 || frame < tl)
+            vpre = TCSUM_ERR_SIZE; // ipv4.c:228-240
+        else if (frag)
+            vmid = 0; // ipv4.c:506-509: queued for reassembly, OK past the header test
+        else if (proto == 6 || proto == 17) { // TCP: pktbuf_remove_header + tcp_in (ipv4.c:450-452); UDP: udp_in
+            // the header words: L4 bytes 0-3 (ports) and 12-15 (data offset, flags)
+            uint32_t ports = 0, oflags = 0;
+            if (tl >= ihl4 + 8u) {
+                const Hdr5 l4h = l4words(ihl4);
+                ports = l4h.d0;
+                oflags = l4h.d3;
+            }
+            const uint32_t sport = ports & 0xFFFFu, dport = ports >> 16, fword = oflags & 0xFFFFu;
+            if (proto == 6) {
+                if (ihl4 > tl)
+                    vmid = TCSUM_ERR_SIZE; // the reference runs off its block list (pktbuf.c:264-281)
+                else if (tl - ihl4 < 20)
+                    vmid = TCSUM_ERR_SYS; // pktbuf_set_cont fails: tcp_in returns -1, tcp_in.c:70-74
+                else if (tl - ihl4 < (((oflags & 0xFFu) >> 4) << 2))
+                    vpost = TCSUM_ERR_SIZE; // tcp_in.c:87-91
+                else if (sport == 0 || dport == 0 || fword == 0)
+                    vpost = TCSUM_ERR_BROKEN; // tcp_in.c:93-103
+            } else {
+                if (tl < ihl4 + 8)
+                    vmid = TCSUM_ERR_SIZE; // pktbuf_set_cont(buf, 8 + ihl), udp.c:386-391
+                else if (dport == 0)
+                    vmid = TCSUM_ERR_UNREACHABLE; // no socket has port 0: udp.c:337-340, :399-403
+            }
+        } else if (proto == 1) { // icmpv4_in, ipv4.c:427; its checksum test cannot fail (A10)
+            vmid = tl < ihl4 + 4 ? TCSUM_ERR_SIZE : 0; // pktbuf_set_cont(buf, ihl + 4), icmpv4.c:68
+        } // other protocols: raw_in, no checksum (ipv4.c:460-469)
+        vcodes = (uint32_t)(uint8_t)vpre | ((uint32_t)(uint8_t)vmid << 8) | ((uint32_t)(uint8_t)vpost << 16) |
+                 (stored_ip != 0 ? 1u << 24 : 0u);
+    }
+    h.fl = fl;
+    h.hl = hl;
+    h.end = end;
+    h.proto = proto;
+    h.fld = fld;
+    h.pseudo = pseudo;
+    h.vcodes = vcodes;
+    h.bad = bad;
+    h.field_on = field_on;
+    return h;
+}
+
+// The packet's results from its header sum and L4 sum (acc_h, acc_l: word
+// sums by address parity, any grouping -- fold16 keeps "zero iff all bytes
+// zero"), odd = the packet's start address parity, acc_f (rx): nonzero iff
+// the stored L4 checksum field is.  Stores out / flags / verdict, and the tx
+// fill's fields (in place, or their positions for k_tx_scatter with
+// IP_OPT_DEFER).
+template <int IPM>
+__device__ __forceinline__ void ip_finish(const IpHdr &ih, uint32_t fl, bool big_enough, uint32_t odd,
+                                          uint32_t acc_h, uint32_t acc_l, uint32_t acc_f, uint8_t *pp, uint32_t pk,
+                                          uint32_t *__restrict__ out, uint8_t *__restrict__ flags_out,
+                                          int8_t *__restrict__ verdict_out, uint32_t opts)
+{
+    uint32_t ip = 0, l4 = 0;
+    if (!big_enough) {
+        fl = TCSUM_PKT_SHORT;
+    } else {
+        uint32_t fh = fold16(acc_h);
+        uint32_t f4 = fold16(acc_l);
+        if (odd) {
+            fh = rot8(fh);
+            f4 = rot8(f4);
+        }
+        ip = ~fh & 0xFFFFu;
+        if (ih.proto == 6 || ih.proto == 17)
+            l4 = ~fold_step(f4 + ih.pseudo) & 0xFFFFu;
+        else if (ih.proto == 1)
+            l4 = ~f4 & 0xFFFFu;
+    }
+    if constexpr (IPM == IP_TX) {
+        if (opts & IP_OPT_DEFER) // bit 16: the IPv4 field; low 16: the L4 field's offset (0: none)
+            reinterpret_cast<uint32_t *>(verdict_out)[pk] = ih.bad ? 0u : (1u << 16) | (ih.field_on ? ih.hl + ih.fld : 0u);
+        else if (!ih.bad && !(opts & IP_OPT_NO_STORE)) { // stored in host order, like the struct fields
+            pp[10] = (uint8_t)ip;
+            pp[11] = (uint8_t)(ip >> 8);
+            if (ih.field_on) {
+                pp[ih.hl + ih.fld] = (uint8_t)l4;
+                pp[ih.hl + ih.fld + 1] = (uint8_t)(l4 >> 8);
+            }
+        }
+    }
+    if constexpr (IPM == IP_RX) {
+        // The first gate that rejects, in the reference's order: ipv4_in /
+        // is_pkt_ok, then the L4 input ip_normal_in dispatches to
+        // (ipv4.c:420-470), up to socket lookup.  Pinned by the reference
+        // stack's own verdicts (tests/golden/ipv4_rx_*, oracle/stack_gen.c).
+        const uint32_t vcodes = ih.vcodes;
+        const int vpre = (int8_t)(vcodes & 0xFFu), vmid = (int8_t)((vcodes >> 8) & 0xFFu);
+        const int vpost = (int8_t)((vcodes >> 16) & 0xFFu);
+        int v8;
+        if (vpre)
+            v8 = vpre;
+        else if ((vcodes >> 24) && ip != 0)
+            v8 = TCSUM_ERR_BROKEN; // ipv4.c:241-249
+        else if (vmid)
+            v8 = vmid;
+        else if (acc_f != 0 && l4 != 0)
+            v8 = TCSUM_ERR_BROKEN; // tcp_in.c:77-85, udp.c:407-415 (field_on: TCP/UDP only)
+        else
+            v8 = vpost;
+        verdict_out[pk] = (int8_t)v8;
+    }
+    if (out)
+        out[pk] = ip | (l4 << 16);
+    if (flags_out)
+        flags_out[pk] = (uint8_t)fl;
+}
+
 // Packet `pk` (one per G-lane group; pk >= n: a dead group that reads
 // descriptor 0 and writes nothing).  Every lane of the wave must call it: the
 // group reduction crosses lanes.
@@ -993,104 +1182,26 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     issue_fence();
 
     const Hdr5 hd = header_dwords(h0, h1, h2, s0);
-    const uint32_t b0h = hd.d0 & 0xFFu;
-    const uint32_t version = b0h >> 4;
-    const uint32_t ihl4 = (b0h & 0xFu) << 2;
-    const uint32_t tl = (((hd.d0 >> 16) & 0xFFu) << 8) | (hd.d0 >> 24);
-    const uint32_t b6 = (hd.d1 >> 16) & 0xFFu, b7 = hd.d1 >> 24;
-    const bool frag = (b6 & 0x20u) || (((b6 & 0x1Fu) << 8) | b7);
-    const uint32_t proto = (hd.d2 >> 8) & 0xFFu;
-    const uint32_t stored_ip = hd.d2 >> 16;
-    uint32_t fl = 0;
-    if (version != 4)
-        fl |= TCSUM_PKT_BAD_VERSION;
-    if (ihl4 < 20 || ihl4 > frame)
-        fl |= TCSUM_PKT_BAD_HDRLEN;
-    if (tl < 20 || tl > frame || tl < ihl4)
-        fl |= TCSUM_PKT_BAD_TOTLEN;
-    if (frag)
-        fl |= TCSUM_PKT_FRAGMENT;
-    uint32_t hl = ihl4 < 20 ? 20u : ihl4;
-    hl = hl > frame ? frame : hl;
-    uint32_t end = tl < hl ? hl : tl;
-    end = end > frame ? frame : end;
-    uint32_t min_l4;
-    const uint32_t fld = l4_field(proto, min_l4);
-    if (fld && end - hl < min_l4)
-        fl |= TCSUM_PKT_L4_SHORT;
-    const bool bad = !big_enough ||
-                     (fl & (TCSUM_PKT_BAD_VERSION | TCSUM_PKT_BAD_HDRLEN | TCSUM_PKT_BAD_TOTLEN));
-    // the L4 checksum field this mode treats specially (tx: zero + store;
-    // rx: is it zero?) -- none for fragments, short L4, or ICMP on rx
-    const bool field_on = IPM != IP_SUMS && !bad && !frag && fld && !(fl & TCSUM_PKT_L4_SHORT) &&
-                          !(IPM == IP_RX && proto == 1);
-    // The L4 pseudo-header (tools.c:58-70), folded now: src, dst (packet bytes
-    // 12..19), {0, proto}, the L4 length; kept as one register past the data pass
-    uint32_t pseudo = 0;
-    if (proto == 6 || proto == 17)
-        pseudo = fold16(add_halves(add_halves(0u, hd.d3), hd.d4) + (proto << 8) + bswap16((end - hl) & 0xFFFFu));
-    if (big_enough && proto != 6 && proto != 17 && proto != 1)
-        fl |= TCSUM_PKT_PROTO_OTHER;
-
-    // rx: every gate that needs no sum, decided now, in the reference's order
-    // (the verdict at the end only places the two checksum tests between them):
-    //   pre  -- ipv4_in before the header checksum test (ipv4.c:475, 222-240)
-    //   mid  -- the L4 input before its checksum test (tcp_in.c:70-74 and
-    //           pktbuf_remove_header, udp.c:386-403, icmpv4.c:68)
-    //   post -- the L4 input after it (tcp_in.c:87-103)
-    // packed as three int8 in one register.
-    uint32_t vcodes = 0;
-    if constexpr (IPM == IP_RX) {
-        int vpre = 0, vmid = 0, vpost = 0;
-        if (!big_enough)
-            vpre = TCSUM_ERR_SIZE; // pktbuf_set_cont(buf, 20), ipv4.c:475
-        else if (version != 4)
-            vpre = TCSUM_ERR_NOT_SUPPORT; // ipv4.c:222-226
-        else if (ihl4 < 20 || tl < 20 || frame < tl)
-            vpre = TCSUM_ERR_SIZE; // ipv4.c:228-240
-        else if (frag)
-            vmid = 0; // ipv4.c:506-509: queued for reassembly, OK past the header test
-        else if (proto == 6 || proto == 17) { // TCP: pktbuf_remove_header + tcp_in (ipv4.c:450-452); UDP: udp_in
-            // the header words (L4 bytes 0-3: ports; 12-15: data offset,
-            // flags) from the 32 bytes at chunk (s0 + ihl4) / 16: chunks 1..3
-            // already in registers for IHL 5, two more loads otherwise
-            uint32_t ports = 0, oflags = 0;
-            if (tl >= ihl4 + 8u) {
-                const uint32_t o = s0 + ihl4, cw = o >> 4;
-                u32x4 wa, wb;
-                if (ihl4 == 20) {
-                    wa = cw == 1 ? h1 : c2;
-                    wb = cw == 1 ? c2 : c3;
-                } else {
-                    wa = load16<false>(base + cw);
-                    wb = load16<false>(cw + 1 < nch ? base + cw + 1 : &g_zero_chunk);
-                }
-                const Hdr5 l4h = header_dwords(wa, wb, u32x4(0u), o & 15u);
-                ports = l4h.d0;
-                oflags = l4h.d3;
-            }
-            const uint32_t sport = ports & 0xFFFFu, dport = ports >> 16, fword = oflags & 0xFFFFu;
-            if (proto == 6) {
-                if (ihl4 > tl)
-                    vmid = TCSUM_ERR_SIZE; // the reference runs off its block list (pktbuf.c:264-281)
-                else if (tl - ihl4 < 20)
-                    vmid = TCSUM_ERR_SYS; // pktbuf_set_cont fails: tcp_in returns -1, tcp_in.c:70-74
-                else if (tl - ihl4 < (((oflags & 0xFFu) >> 4) << 2))
-                    vpost = TCSUM_ERR_SIZE; // tcp_in.c:87-91
-                else if (sport == 0 || dport == 0 || fword == 0)
-                    vpost = TCSUM_ERR_BROKEN; // tcp_in.c:93-103
-            } else {
-                if (tl < ihl4 + 8)
-                    vmid = TCSUM_ERR_SIZE; // pktbuf_set_cont(buf, 8 + ihl), udp.c:386-391
-                else if (dport == 0)
-                    vmid = TCSUM_ERR_UNREACHABLE; // no socket has port 0: udp.c:337-340, :399-403
-            }
-        } else if (proto == 1) { // icmpv4_in, ipv4.c:427; its checksum test cannot fail (A10)
-            vmid = tl < ihl4 + 4 ? TCSUM_ERR_SIZE : 0; // pktbuf_set_cont(buf, ihl + 4), icmpv4.c:68
-        } // other protocols: raw_in, no checksum (ipv4.c:460-469)
-        vcodes = (uint32_t)(uint8_t)vpre | ((uint32_t)(uint8_t)vmid << 8) | ((uint32_t)(uint8_t)vpost << 16) |
-                 (stored_ip != 0 ? 1u << 24 : 0u);
-    }
+    // rx: the TCP/UDP header words (L4 bytes 0-3: ports; 12-15: data offset,
+    // flags) from the 32 bytes at chunk (s0 + ihl4) / 16: chunks 1..3 already
+    // in registers for IHL 5, two more loads otherwise
+    // (the lambda captures by value: a reference capture takes the chunks'
+    // addresses, and clang then kept them in scratch memory)
+    const IpHdr ih = ip_parse<IPM>(hd, frame, big_enough, [=](uint32_t ihl4) {
+        const uint32_t o = s0 + ihl4, cw = o >> 4;
+        u32x4 wa, wb;
+        if (ihl4 == 20) {
+            wa = cw == 1 ? h1 : c2;
+            wb = cw == 1 ? c2 : c3;
+        } else {
+            wa = load16<false>(base + cw);
+            wb = load16<false>(cw + 1 < nch ? base + cw + 1 : &g_zero_chunk);
+        }
+        return header_dwords(wa, wb, u32x4(0u), o & 15u);
+    });
+    uint32_t fl = ih.fl;
+    const bool field_on = ih.field_on;
+    const uint32_t hl = ih.hl, end = ih.end, fld = ih.fld;
 
     // byte ranges, from the data pass's line base (end <= tl <= 65535 whenever
     // it matters; clamp so a huge bogus frame cannot overflow)
@@ -1147,61 +1258,9 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     if (IPM == IP_RX)
         acc_f = group_sum<G>(acc_f);
 
-    if (live && gl == 0) {
-        uint32_t ip = 0, l4 = 0;
-        if (!big_enough) {
-            fl = TCSUM_PKT_SHORT;
-        } else {
-            const bool odd = start & 1u;
-            uint32_t fh = fold16(acc_h);
-            uint32_t f4 = fold16(acc_l);
-            if (odd) {
-                fh = rot8(fh);
-                f4 = rot8(f4);
-            }
-            ip = ~fh & 0xFFFFu;
-            if (proto == 6 || proto == 17)
-                l4 = ~fold_step(f4 + pseudo) & 0xFFFFu;
-            else if (proto == 1)
-                l4 = ~f4 & 0xFFFFu;
-        }
-        if constexpr (IPM == IP_TX) {
-            if (opts & IP_OPT_DEFER) // bit 16: the IPv4 field; low 16: the L4 field's offset (0: none)
-                reinterpret_cast<uint32_t *>(verdict_out)[pk] = bad ? 0u : (1u << 16) | (field_on ? hl + fld : 0u);
-            else if (!bad && !(opts & IP_OPT_NO_STORE)) { // stored in host order, like the struct fields
-                pp[10] = (uint8_t)ip;
-                pp[11] = (uint8_t)(ip >> 8);
-                if (field_on) {
-                    pp[hl + fld] = (uint8_t)l4;
-                    pp[hl + fld + 1] = (uint8_t)(l4 >> 8);
-                }
-            }
-        }
-        if constexpr (IPM == IP_RX) {
-            // The first gate that rejects, in the reference's order: ipv4_in /
-            // is_pkt_ok, then the L4 input ip_normal_in dispatches to
-            // (ipv4.c:420-470), up to socket lookup.  Pinned by the reference
-            // stack's own verdicts (tests/golden/ipv4_rx_*, oracle/stack_gen.c).
-            const int vpre = (int8_t)(vcodes & 0xFFu), vmid = (int8_t)((vcodes >> 8) & 0xFFu);
-            const int vpost = (int8_t)((vcodes >> 16) & 0xFFu);
-            int v8;
-            if (vpre)
-                v8 = vpre;
-            else if ((vcodes >> 24) && ip != 0)
-                v8 = TCSUM_ERR_BROKEN; // ipv4.c:241-249
-            else if (vmid)
-                v8 = vmid;
-            else if (acc_f != 0 && l4 != 0)
-                v8 = TCSUM_ERR_BROKEN; // tcp_in.c:77-85, udp.c:407-415 (field_on: TCP/UDP only)
-            else
-                v8 = vpost;
-            verdict_out[pk] = (int8_t)v8;
-        }
-        if (out)
-            out[pk] = ip | (l4 << 16);
-        if (flags_out)
-            flags_out[pk] = (uint8_t)fl;
-    }
+    if (live && gl == 0)
+        ip_finish<IPM>(ih, fl, big_enough, (uint32_t)(start & 1u), acc_h, acc_l, acc_f, pp, pk, out, flags_out,
+                       verdict_out, opts);
 }
 
 template <int G, int U, int IPM, int T = 256>
@@ -1239,6 +1298,289 @@ __global__ __launch_bounds__(256) void k_tx_scatter(uint8_t *__restrict__ arena,
     if (f) { // tcp_out.c:19-20 / udp.c:320-321 / icmpv4.c:45-58
         pp[f] = (uint8_t)(v >> 16);
         pp[f + 1] = (uint8_t)(v >> 24);
+    }
+}
+
+
+// ---------------------------------------------------------------- byte-window stream (IPv4)
+//
+// k_ipv4 gives every packet its own lane group, so a pass of a 64..9000-B
+// packet ends wherever the packet ends: lanes idle in the last pass, and the
+// loads in flight follow the packet lengths.  k_flat_ipv4 cuts the batch's
+// BYTES instead: workgroup w streams window w, a fixed WB-byte stretch of the
+// arena (W waves x 64 lanes x U 16-B loads, the TSO kernel's load shape:
+// 32-lane groups walking contiguous sub-ranges), whatever packets lie there,
+// and sums each packet's part of it from prefix sums as k_segments_pk does:
+//
+//     P(x) = word sum of the window's bytes before x,
+//     part(window, [A, B)) = P(min(B, end)) - P(max(A, start)),
+//
+// exact in u32 (a window sums to < 2^31), so padding and the neighbours'
+// bytes cancel.  A packet belongs to the window its first byte lies in (its
+// "owner"); the windows its later bytes reach add their parts to one 64-bit
+// word per owner window with a single atomic -- folded part in the low half,
+// an arrival count in the high half -- and the last to arrive finishes the
+// packet (fold keeps "zero iff all bytes zero", and any regrouping of the
+// words is allowed, so the folded parts add up to the packet's fold).  Every
+// participant parses the packet's header itself (from the window's LDS copy
+// of its chunks, or from memory for a header outside the window), so nothing
+// else crosses workgroups.
+//
+// Which packets a window holds comes from k_flat_plan, one pass over the
+// descriptors before the stream: wfirst[w] = the first packet starting at or
+// after window w's first byte.  It also checks that the batch IS a stream --
+// descriptors in arena order, packets disjoint, the whole span inside the
+// grid the host sized from the byte hint -- and otherwise marks the plan
+// (plan->bad = this call's generation number), and every workgroup then sums
+// its share of the packets one by one (ipv4_packet), as k_ipv4 would.
+struct FlatPlan {
+    uint64_t base; // absolute address of window 0: the first packet's 128-B line
+    uint64_t end;  // absolute end of the stream (the last packet's loaded bytes)
+    uint32_t bad;  // == the call's generation: not a stream, per-packet mode
+    uint32_t rsv;
+};
+constexpr uint32_t kFlatMaxFrame = 65600; // bytes of a frame the IPv4 kernels load (k_ipv4: frame_ld)
+
+template <uint32_t WB>
+__global__ __launch_bounds__(256) void k_flat_plan(const uint8_t *__restrict__ arena,
+                                                   const tcsum_pkt_t *__restrict__ pkts, uint32_t n, uint32_t nw,
+                                                   FlatPlan *__restrict__ plan, uint32_t *__restrict__ wfirst,
+                                                   unsigned long long *__restrict__ slot, uint32_t gen)
+{
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t < nw)
+        slot[t] = 0ull;
+    if (t > n)
+        return;
+    const uint64_t a0 = reinterpret_cast<uintptr_t>(arena);
+    const uint64_t base = (a0 + pkts[0].offset) & ~127ull;
+    if (t == 0)
+        plan->base = base;
+    const uint64_t cover = (uint64_t)nw * WB;
+    bool bad = false;
+    uint64_t lo; // the windows whose first packet is t: (window of packet t-1's start, window of t's start]
+    if (t == 0) {
+        lo = 0;
+    } else {
+        const uint64_t sp = a0 + pkts[t - 1].offset;
+        lo = sp >= base ? (sp - base) / WB + 1u : ~0ull;
+    }
+    uint64_t hi = nw;
+    if (t < n) {
+        const tcsum_pkt_t d = pkts[t];
+        const uint64_t st = a0 + d.offset;
+        if (st < base) {
+            bad = true;
+        } else {
+            hi = (st - base) / WB;
+            if (t + 1u < n && a0 + pkts[t + 1].offset < st + d.len) // arena order, disjoint
+                bad = true;
+            if (t + 1u == n) {
+                const uint64_t e = st + (d.len < kFlatMaxFrame ? d.len : kFlatMaxFrame);
+                plan->end = e;
+                if (e - base > cover)
+                    bad = true;
+            }
+        }
+    }
+    if (!bad && lo <= hi) {
+        if (hi - lo > nw)
+            bad = true;
+        else
+            for (uint64_t w = lo; w <= hi && w <= nw; ++w)
+                wfirst[w] = t;
+    }
+    if (bad)
+        plan->bad = gen;
+}
+
+// Byte `i` (0..15) of a chunk (selects on named dwords: no dynamic indexing)
+__device__ __forceinline__ uint32_t chunk_byte(u32x4 v, uint32_t i)
+{
+    const uint32_t q = i >> 2;
+    const uint32_t d = q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
+    return (d >> (8u * (i & 3u))) & 0xFFu;
+}
+
+template <int IPM, int W, int U>
+__global__ __launch_bounds__(W * 64) void k_flat_ipv4(uint8_t *__restrict__ arena,
+                                                      const tcsum_pkt_t *__restrict__ pkts, uint32_t n,
+                                                      uint32_t *__restrict__ out, uint8_t *__restrict__ flags_out,
+                                                      int8_t *__restrict__ verdict_out, uint32_t opts, uint32_t xg,
+                                                      const FlatPlan *__restrict__ plan,
+                                                      const uint32_t *__restrict__ wfirst,
+                                                      unsigned long long *__restrict__ slot, uint32_t gen)
+{
+    static_assert(2 * W <= 32, "the sub-range totals are scanned by 32 lanes");
+    constexpr uint32_t T = W * 64u, CH = T * U, SR = 32u * U, WB = 16u * CH;
+    __shared__ u32x4 dat[CH];   // the window's chunks (headers, boundary bytes)
+    __shared__ uint32_t ex[CH]; // per chunk: its sub-range's word sum before it; slot 0 of a sub-range: its total
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    const uint64_t a0 = reinterpret_cast<uintptr_t>(arena);
+    if (plan->bad == gen) {
+        // not a stream: this workgroup's share of the packets, one by one
+        const uint32_t lo = (uint32_t)((uint64_t)n * blk / gridDim.x);
+        const uint32_t hi = (uint32_t)((uint64_t)n * (blk + 1u) / gridDim.x);
+        constexpr uint32_t G = 16, PER = T / G;
+        for (uint32_t p0 = lo; p0 < hi; p0 += PER) // workgroup-uniform
+            ipv4_packet<G, 4, IPM>(arena, pkts, p0 + t / G, hi, out, flags_out, verdict_out, opts);
+        return;
+    }
+    const uint64_t base = plan->base, send = plan->end;
+    const uint64_t wlo = base + (uint64_t)blk * WB;
+    if (wlo >= send) // past the stream (the grid is sized from the byte hint)
+        return;
+    // the window's loads: chunk c of the window is load u of lane l of
+    // sub-range c / SR; chunks past the stream re-read its last chunk (their
+    // bytes belong to no packet)
+    const int64_t rel0 = (int64_t)(wlo - a0); // from the arena pointer: global_load, not flat_load
+    const u32x4 *wbase = reinterpret_cast<const u32x4 *>(arena + rel0);
+    const uint32_t nchw = send - wlo >= WB ? CH : (uint32_t)((send - wlo + 15u) >> 4);
+    const uint32_t sub = t >> 5, l = t & 31u, hf = (t >> 5) & 1u;
+    u32x4 v[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t c = sub * SR + u * 32u + l;
+        v[u] = load16<true>(wbase + (c < nchw ? c : nchw - 1u));
+    }
+    issue_fence();
+    // the packets: the straddler from the left (if any) and those starting here
+    const uint32_t pf = wfirst[blk], pl = wfirst[blk + 1u];
+    const uint32_t j0 = pf > 0 ? pf - 1u : 0u;
+    const uint32_t m = pl - j0;
+    // packet i of the window goes to wave i % W, lane i / W (spread over the SIMDs)
+    const uint32_t i0 = lane * W + wv;
+    u32x4 dv0 = u32x4(0u);
+    if (i0 < m)
+        dv0 = *reinterpret_cast<const u32x4 *>(pkts + j0 + i0);
+
+    // chunk sums, scans over each 32-lane half, the chunks and prefixes into LDS
+    {
+        uint32_t a = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t c = sub * SR + u * 32u + l;
+            const uint32_t f = chunk_sum(0u, v[u]); // < 2^19
+            const uint32_t sc = scan32(f);
+            if (u != 0 || l != 0)
+                ex[c] = a + (sc - f);
+            dat[c] = v[u];
+            const uint32_t lo32 = (uint32_t)__builtin_amdgcn_readlane((int)sc, 31);
+            const uint32_t hi32 = (uint32_t)__builtin_amdgcn_readlane((int)sc, 63);
+            a += hf ? hi32 : lo32;
+        }
+        if (l == 0)
+            ex[sub * SR] = a; // the sub-range's total (its first chunk's prefix is 0)
+    }
+    __syncthreads();
+    // every wave: the sub-ranges' exclusive prefixes (lane k: sub-range k)
+    const uint32_t st = lane < 2u * W ? ex[lane * SR] : 0u;
+    const uint32_t si = scan32(st);
+    const uint32_t sx = si - st;
+    const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)si, 31);
+    // P(x), x = 0..WB bytes from the window's start; called by every lane of
+    // the wave (the shuffle), x = 0 for lanes without a packet
+    auto prefix = [=](uint32_t x) -> uint32_t {
+        const uint32_t c = x >> 4, b = x & 15u;
+        const uint32_t cc = c < CH ? c : CH - 1u;
+        const uint32_t sp = (uint32_t)__shfl((int)sx, (int)(cc / SR), 64);
+        if (c >= CH)
+            return wtot;
+        uint32_t e = sp + (cc % SR ? ex[cc] : 0u);
+        if (b)
+            e += chunk_prefix_sum(dat[cc], b);
+        return e;
+    };
+    const uint64_t whi = wlo + WB;
+    const uint32_t rounds = (m + T - 1u) / T; // workgroup-uniform
+    for (uint32_t r = 0; r < rounds; ++r) {
+        const uint32_t i = r * T + i0;
+        const bool act = i < m;
+        const u32x4 dv = r == 0 ? dv0 : (act ? *reinterpret_cast<const u32x4 *>(pkts + j0 + i) : u32x4(0u));
+        const uint32_t j = j0 + i;
+        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+        const uint32_t frame = act ? dv.z : 0u;
+        const uint64_t s = a0 + off;
+        const uint32_t frame_ld = frame < kFlatMaxFrame ? frame : kFlatMaxFrame;
+        const uint64_t ee = s + frame_ld;
+        // this window takes part: the packet starts here, or (packet j0 = pf - 1)
+        // reaches in from the left
+        const bool straddler = i == 0 && pf > 0;
+        const bool part_of = act && (!straddler || ee > wlo);
+        const bool owner = act && s >= wlo && s < whi;
+        const bool big_enough = frame >= 20;
+        const uint32_t s0 = (uint32_t)(s & 15u);
+        const uint64_t hc = s >> 4; // the packet's first chunk (absolute)
+        const uint32_t nchp = big_enough ? (frame_ld + s0 + 15u) >> 4 : 0u; // the packet's chunks
+        // chunk k of the packet: from the window's LDS copy, else from memory
+        auto fetch = [=](uint32_t k) -> u32x4 {
+            if (!part_of || k >= nchp)
+                return u32x4(0u);
+            const uint64_t g = hc + k;
+            const uint64_t rel = g - (wlo >> 4);
+            if (rel < CH)
+                return dat[rel];
+            return load16<false>(reinterpret_cast<const u32x4 *>(arena + (int64_t)((g << 4) - a0)));
+        };
+        const u32x4 h0 = fetch(0), h1 = fetch(1);
+        const u32x4 h2 = s0 > 12 ? fetch(2) : u32x4(0u);
+        const Hdr5 hd = header_dwords(h0, h1, h2, s0);
+        const IpHdr ih = ip_parse<IPM>(hd, frame, big_enough, [=](uint32_t ihl4) {
+            const uint32_t o = s0 + ihl4, cw = o >> 4;
+            return header_dwords(fetch(cw), fetch(cw + 1u), u32x4(0u), o & 15u);
+        });
+        // the L4 range's part in this window
+        const uint64_t A = s + ih.hl, B = s + ih.end;
+        const uint32_t xa = A <= wlo ? 0u : A >= whi ? WB : (uint32_t)(A - wlo);
+        const uint32_t xb = B <= wlo ? 0u : B >= whi ? WB : (uint32_t)(B - wlo);
+        const bool sums = part_of && big_enough;
+        uint32_t part = prefix(sums ? xb : 0u) - prefix(sums ? xa : 0u);
+        // the L4 checksum field: its bytes (tx subtracts those in this window:
+        // the fill reads it as zero; rx tests whether it is zero)
+        uint32_t acc_f = 0;
+        if (sums && ih.field_on) {
+#pragma unroll
+            for (uint32_t k = 0; k < 2; ++k) {
+                const uint32_t q = s0 + ih.hl + ih.fld + k; // from the packet's first chunk
+                const uint32_t b = chunk_byte(fetch(q >> 4), q & 15u);
+                const uint64_t F = s + ih.hl + ih.fld + k;
+                if (IPM == IP_TX && F >= wlo && F < whi)
+                    part -= b << (8u * (uint32_t)(F & 1u));
+                acc_f |= b;
+            }
+        }
+        if (!part_of || (!big_enough && !owner))
+            continue;
+        // windows this packet's bytes reach: its owner's and the ones after it
+        const uint64_t ws = (s - base) / WB;
+        const uint32_t kwin = frame_ld ? (uint32_t)((ee - 1u - base) / WB - ws + 1u) : 1u;
+        uint32_t acc_l = part;
+        if (big_enough && kwin > 1u) {
+            const uint32_t fp = fold16(part);
+            const unsigned long long old =
+                atomicAdd(&slot[ws], (1ull << 32) | (unsigned long long)fp);
+            if ((uint32_t)(old >> 32) + 1u != kwin)
+                continue; // another window finishes the packet
+            acc_l = (uint32_t)old + fp;
+        }
+        // the finisher: the header sum from the packet's first chunks
+        uint32_t acc_h = 0;
+        if (big_enough) {
+            const int h_end = (int)(s0 + ih.hl);
+#pragma unroll
+            for (uint32_t k = 0; k < 5; ++k) {
+                if ((int)(16u * k) < h_end) {
+                    const u32x4 hk = fetch(k);
+                    uint32_t th = region_sum(hk, (int)(16u * k), (int)s0, h_end);
+                    if (IPM == IP_TX)
+                        th -= region_sum(hk, (int)(16u * k), (int)s0 + 10, (int)s0 + 12); // ipv4.c:643
+                    acc_h += th;
+                }
+            }
+        }
+        ip_finish<IPM>(ih, ih.fl, big_enough, (uint32_t)(s & 1u), acc_h, acc_l, acc_f, arena + off, j, out,
+                       flags_out, verdict_out, opts);
     }
 }
 

@@ -52,8 +52,10 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
 // ip_mode: 0 sums, 1 tx fill (writes into arena), 2 rx verify (verdict required),
 //          3 tx offload (the tx fill's values into out only; out required),
 //          4 tx fill with its stores deferred to a second launch (k_tx_scatter)
+// total_bytes (the batch's byte count, 0 = unknown) lets g.flat take the
+// byte-window stream (k_flat_plan + k_flat_ipv4).
 hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
-                       uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream);
+                       uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream, uint64_t total_bytes = 0);
 
 // The tx fill (deferred stores) reading `arena` and storing the fields into
 // `store` (the same packets at another device-visible address).

@@ -1,0 +1,285 @@
+"""k_flat_ipv4 -- the byte-window stream for IPv4 batches (plan + stream,
+csum_device.h) -- against the reference's fixtures and the oracle (the CPU
+restatement of net/src/tools.c:24-75 / pktbuf.c:646-670 and of the receive
+gates of ipv4.c / tcp_in.c / udp.c / icmpv4.c, pinned to the reference's
+own outputs).
+
+Every workgroup sums a fixed byte window of the arena; packets that cross a
+window boundary are combined from the windows' parts through one atomic word
+per owner window, the last arriver finishing the packet.  The cases below put
+packets, headers, checksum fields and packet ends on and across window
+boundaries, make packets longer than several windows, crowd more packets into
+one window than it has lanes, and break the stream precondition (descriptors
+out of arena order, overlaps, a span the byte hint does not cover) so that
+the per-packet fallback inside the same launch runs.  Bit-exact throughout.
+"""
+import numpy as np
+import pytest
+
+import golden_io as G
+
+pytestmark = pytest.mark.gpu
+
+WB = 12288  # the window: 4 waves x 64 lanes x 3 loads x 16 B (kFlatWB)
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "gpu tests need an MI355X"
+    return t
+
+
+@pytest.fixture(scope="module")
+def tc(torch):
+    from tcp_amd import build
+    build.build()
+    import tcp_amd
+    tcp_amd.plat_init(0)
+    return tcp_amd
+
+
+@pytest.fixture(autouse=True)
+def flat(tc):
+    tc.debug_set("flat", 1)
+    assert tc.route(4500)["flat"] == 1
+    yield
+    tc.debug_set("flat", -1)
+    tc.debug_set("tx_split", -1)
+
+
+def to_dev(torch, a: np.ndarray, pad: int = 256):
+    t = torch.zeros(a.nbytes + pad, dtype=torch.uint8)
+    t[: a.nbytes] = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1))
+    return t.cuda()
+
+
+def _all_modes(tc, torch, oracle, host, pk, hint=None, tx=True):
+    """sums, rx verify, tx offload and both tx fill forms vs the oracle
+    (tx=False: overlapping packets, whose fill depends on the order)."""
+    n = pk.size
+    hint = int(pk["len"].astype(np.int64).sum()) if hint is None else hint
+    arena = to_dev(torch, host)
+    d = tc.descs_to_device(pk)
+    out, fl = tc.batch_ipv4(arena, d, n, hint)
+    exp, efl = oracle.batch_ipv4(host, pk, nthreads=8)
+    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+    np.testing.assert_array_equal(fl.cpu().numpy(), efl)
+    rout = torch.empty(n, dtype=torch.uint32, device="cuda")
+    verdict, vfl = tc.batch_ipv4_rx_verify(arena, d, n, hint, out=rout)
+    ev, evfl = oracle.batch_ipv4_rx_verify(host, pk, nthreads=8)
+    np.testing.assert_array_equal(verdict.cpu().numpy(), ev)
+    np.testing.assert_array_equal(vfl.cpu().numpy(), evfl)
+    np.testing.assert_array_equal(rout.cpu().numpy(), exp)  # rx reports the same sums
+    if not tx:
+        return
+    tout, tfl = tc.batch_ipv4_tx_offload(arena, d, n, hint)
+    filled = host.copy()
+    tc.tx_apply_batch(filled, pk, tout.cpu().numpy(), tfl.cpu().numpy())
+    want = host.copy()
+    oracle.batch_ipv4_tx_fill(want, pk, nthreads=8)
+    np.testing.assert_array_equal(filled, want)
+    for split in (0, 1):
+        tc.debug_set("tx_split", split)
+        a2 = to_dev(torch, host)
+        fout = torch.empty(n, dtype=torch.uint32, device="cuda")
+        tc.batch_ipv4_tx_fill(a2, d, n, hint, out=fout, want_flags=False)
+        np.testing.assert_array_equal(a2.cpu().numpy()[: host.size], filled)
+        np.testing.assert_array_equal(fout.cpu().numpy(), tout.cpu().numpy())
+    tc.debug_set("tx_split", -1)
+
+
+def _headers(rng, host, offs, lens, valid=0.85):
+    """Mostly plausible IPv4 headers (IHL 5..15, TCP/UDP/ICMP/other, stored
+    checksums zero sometimes, fragments sometimes) over the random bytes."""
+    for o, ln in zip(offs.tolist(), lens.tolist()):
+        if ln < 20:
+            continue
+        h = host[o: o + 20]
+        ihl = 5 if rng.random() < 0.8 else int(rng.integers(5, 16))
+        h[0] = (0x40 | ihl) if rng.random() < valid else int(rng.integers(0, 256))
+        tl = ln if rng.random() < 0.8 else int(rng.integers(0, 70000)) & 0xFFFF
+        h[2], h[3] = tl >> 8, tl & 0xFF
+        if rng.random() < 0.85:
+            h[6], h[7] = 0, 0
+        h[9] = int(rng.choice([6, 17, 1, 99]))
+        if rng.random() < 0.2:
+            h[10], h[11] = 0, 0
+        hl = 4 * (h[0] & 0xF)
+        if ln >= hl + 20 and rng.random() < 0.2:
+            host[o + hl + 16: o + hl + 18] = 0
+            host[o + hl + 6: o + hl + 8] = 0
+
+
+def _arena(rng, size):
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    for _ in range(30):  # runs of 0x00 / 0xFF: fold edge cases
+        a = int(rng.integers(0, max(1, size - 5000)))
+        host[a: a + int(rng.integers(1, 5000))] = rng.choice([0, 0xFF])
+    return host
+
+
+def _stream(lens, start=0, gaps=None):
+    step = lens + (0 if gaps is None else gaps)
+    return start + np.concatenate([[0], np.cumsum(step[:-1])]).astype(np.int64)
+
+
+def _pk(tc, offs, lens):
+    pk = np.zeros(len(lens), tc.PKT_DTYPE)
+    pk["offset"], pk["len"] = offs, lens
+    return pk
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_flat_fuzz_vs_oracle(tc, torch, oracle, seed):
+    """Packets of 0..9000 B (a third of them short), packed or with gaps, at a
+    random arena phase; every mode and both fill forms."""
+    rng = np.random.default_rng(7700 + seed)
+    n = int(rng.integers(500, 5000))
+    kind = rng.integers(0, 3, n)
+    lens = np.where(kind == 0, rng.integers(0, 80, n),
+                    np.where(kind == 1, rng.integers(20, 2048, n), rng.integers(20, 9001, n)))
+    gaps = rng.integers(0, 40, n) * (rng.random(n) < 0.3) if seed % 2 else None
+    offs = _stream(lens, int(rng.integers(0, 200)), gaps)
+    host = _arena(rng, int(offs[-1] + lens[-1]) + 512)
+    _headers(rng, host, offs, lens)
+    _all_modes(tc, torch, oracle, host, _pk(tc, offs, lens))
+
+
+@pytest.mark.parametrize("phase", [0, 1, 5, 10, 11, 12, 15, 16, 18, 19, 20, 35, 36, 37, 77, 78])
+def test_flat_boundaries(tc, torch, oracle, phase):
+    """A packet placed so that its header, its IPv4 checksum field, its L4
+    checksum field or its end lands on / across every window boundary, at
+    every offset near it: 2,000 packets of 700..1400 B laid out so that one
+    of them starts `phase` bytes before each boundary."""
+    rng = np.random.default_rng(phase)
+
+    def fill(total):  # packets of 700..1400 B that add up to `total` exactly
+        out = []
+        while total > 2100:
+            out.append(int(rng.integers(700, 1401)))
+            total -= out[-1]
+        if total <= 1400:
+            out.append(total)
+        else:
+            out += [total // 2, total - total // 2]
+        return out
+
+    # window boundaries sit at k * WB (the arena starts on a 128-B line): the
+    # first packet of every stretch starts `phase` bytes before a boundary
+    lens = fill(WB - phase)
+    while len(lens) < 2000:
+        lens += fill(WB)
+    lens = np.array(lens, np.int64)
+    offs = _stream(lens)
+    host = _arena(rng, int(offs[-1] + lens[-1]) + 512)
+    _headers(rng, host, offs, lens, valid=0.95)
+    _all_modes(tc, torch, oracle, host, _pk(tc, offs, lens))
+
+
+def test_flat_long_packets(tc, torch, oracle):
+    """Packets longer than one window and up to the IPv4 maximum (65,535 B)
+    -- spread over up to seven windows, their parts combined by the last
+    arriving one -- among short ones; frames longer than the IPv4 maximum."""
+    rng = np.random.default_rng(99)
+    n = 400
+    lens = np.where(rng.random(n) < 0.3, rng.integers(12000, 65536, n), rng.integers(20, 3000, n)).astype(np.int64)
+    lens[[5, 77]] = [70000, 131072]  # frames past total_len's range: loads stop at 65,600 B
+    offs = _stream(lens, 3)
+    host = _arena(rng, int(offs[-1] + lens[-1]) + 512)
+    _headers(rng, host, offs, lens, valid=0.95)
+    _all_modes(tc, torch, oracle, host, _pk(tc, offs, lens))
+
+
+def test_flat_crowded_windows(tc, torch, oracle):
+    """20..64-B packets: more packets start in one 12-KiB window than it has
+    lanes (256), so the window takes several rounds of them; and runs of
+    frames shorter than 20 B (SHORT) across boundaries."""
+    rng = np.random.default_rng(5)
+    n = 60000
+    lens = np.where(rng.random(n) < 0.1, rng.integers(0, 20, n), rng.integers(20, 65, n)).astype(np.int64)
+    offs = _stream(lens, 9)
+    host = _arena(rng, int(offs[-1] + lens[-1]) + 512)
+    _headers(rng, host, offs, lens)
+    _all_modes(tc, torch, oracle, host, _pk(tc, offs, lens))
+
+
+@pytest.mark.parametrize("layout", ["shuffled", "overlap", "reversed", "big_gaps", "tiny_hint"])
+def test_flat_not_a_stream_falls_back(tc, torch, oracle, layout):
+    """Batches the stream cannot take -- descriptors out of arena order,
+    overlapping packets, gaps the byte hint does not cover -- are found by the
+    plan and summed packet by packet in the same launch: still exact."""
+    rng = np.random.default_rng(["shuffled", "overlap", "reversed", "big_gaps", "tiny_hint"].index(layout))
+    n = 3000
+    lens = rng.integers(20, 9001, n).astype(np.int64)
+    offs = _stream(lens, 1, rng.integers(0, 2000, n) if layout == "big_gaps" else None)
+    if layout == "overlap":
+        offs[100:] -= 30
+    host = _arena(rng, int(offs.max() + lens.max()) + 512)
+    _headers(rng, host, offs, lens)
+    pk = _pk(tc, offs, lens)
+    if layout == "shuffled":
+        pk = pk[rng.permutation(n)]
+    elif layout == "reversed":
+        pk = pk[::-1].copy()
+    hint = int(lens.sum()) // 4 if layout == "tiny_hint" else None
+    _all_modes(tc, torch, oracle, host, pk, hint=hint, tx=layout != "overlap")
+
+
+@pytest.mark.parametrize("fixture", ["ipv4", "rx", "tx", "stack_tx"])
+def test_flat_reference_fixtures(tc, torch, fixture):
+    """The reference's own outputs (tests/golden) through the stream path."""
+    if fixture == "ipv4":
+        cases, pool = G.ipv4_cases()
+        pk = np.zeros(cases.size, tc.PKT_DTYPE)
+        pk["offset"], pk["len"] = cases["pool_off"], cases["frame_len"]
+        out, flags = tc.batch_ipv4(to_dev(torch, pool), tc.descs_to_device(pk), pk.size, int(pk["len"].sum()))
+        out = out.cpu().numpy()
+        np.testing.assert_array_equal(out & 0xFFFF, cases["ip"])
+        np.testing.assert_array_equal(out >> 16, cases["l4"])
+        np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+    elif fixture == "rx":
+        cases, pool = G.ipv4_rx_cases()
+        pk = G.pkt_descs(cases, tc.PKT_DTYPE)
+        verdict, flags = tc.batch_ipv4_rx_verify(to_dev(torch, pool), tc.descs_to_device(pk), cases.size,
+                                                 int(pk["len"].sum()))
+        np.testing.assert_array_equal(verdict.cpu().numpy(), cases["verdict"])
+        np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+    else:
+        cases, pin, pout = G.ipv4_tx_cases() if fixture == "tx" else G.stack_tx_cases()
+        pk = G.pkt_descs(cases, tc.PKT_DTYPE)
+        for split in (0, 1):
+            tc.debug_set("tx_split", split)
+            arena = to_dev(torch, pin)
+            flags = tc.batch_ipv4_tx_fill(arena, tc.descs_to_device(pk), cases.size, int(pk["len"].sum()))
+            np.testing.assert_array_equal(arena.cpu().numpy()[: pout.size], pout)
+            np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+
+
+@pytest.mark.parametrize("config", ["mixed", "mixed_aligned"])
+def test_flat_full_mixed_config(tc, torch, oracle, config):
+    """configs[3] at full size (1M packets, 4.4 GiB) through the stream:
+    both sums of every packet equal the oracle's; then fill, verify (all
+    OK), corrupt 2,000 packets, verify again against the oracle."""
+    from tcp_amd import workload
+    b = workload.make_batch(config)
+    arena, descs = workload.materialize(b)
+    out, fl = tc.batch_ipv4(arena, descs, b.n, b.total_bytes)
+    host = arena.cpu().numpy()
+    exp, efl = oracle.batch_ipv4(host, b.descs, nthreads=16)
+    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+    np.testing.assert_array_equal(fl.cpu().numpy(), efl)
+    del host
+    tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes)
+    verdict, _ = tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes)
+    assert (verdict.cpu().numpy() == 0).all()
+    rng = np.random.default_rng(55)
+    bad = rng.choice(b.n, 2000, replace=False)
+    pos = (b.descs["offset"][bad] + 20 + (rng.integers(0, 1 << 30, bad.size) % (b.descs["len"][bad] - 20)))
+    arena[torch.from_numpy(pos.astype(np.int64)).cuda()] ^= 0x04
+    verdict, flags = tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes)
+    v = verdict.cpu().numpy()
+    ev, ef = oracle.batch_ipv4_rx_verify(arena.cpu().numpy(), b.descs, nthreads=16)
+    np.testing.assert_array_equal(v, ev)
+    np.testing.assert_array_equal(flags.cpu().numpy(), ef)
+    assert (v[bad] == -13).mean() > 0.99

@@ -185,7 +185,17 @@ def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None, pro
         dist.barrier()
     torch.cuda.synchronize()
     ms = t0.elapsed_time(t1)  # events on the launch stream: pure kernel time of K launches
-    r = dict(batch=batch, arena=arena, descs=descs, out=out, flags=flags, ms=ms, wall_s=wall, steps=steps)
+    # untimed for the line: the same K launches again, each between its own
+    # pair of events -- the per-launch median the rocprof trace is compared with
+    pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for e0, e1 in pairs:
+        e0.record(stream)
+        launch(tc, batch, arena, descs, out, flags)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    per_launch = sorted(e0.elapsed_time(e1) for e0, e1 in pairs)
+    r = dict(batch=batch, arena=arena, descs=descs, out=out, flags=flags, ms=ms, wall_s=wall, steps=steps,
+             launch_median_ms=per_launch[len(per_launch) // 2])
     if probes:
         run_probes(torch, tc, r)
     return r
@@ -375,11 +385,15 @@ def rocprof_trace(config: str, steps: int, warmup: int, settle_ms: float):
            sys.executable, os.path.abspath(__file__), "--pmc-child", "--trace-child", "--config", config,
            "--steps", str(steps), "--warmup", str(warmup), "--settle-ms", str(settle_ms)]
     try:
-        subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
-                       env=dict(os.environ, TMPDIR=d))
+        res = subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                             env=dict(os.environ, TMPDIR=d), text=True)
     except (subprocess.SubprocessError, OSError) as e:
         shutil.rmtree(d, ignore_errors=True)
         return None, f"rocprofv3 kernel-trace pass failed: {type(e).__name__}"
+    child = {}
+    for ln in res.stdout.splitlines():
+        if ln.startswith("{") and "child_ms_per_step" in ln:
+            child = json.loads(ln)
     files = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
     keep = os.environ.get("TCSUM_PMC_KEEP")
     if keep:
@@ -409,17 +423,22 @@ def rocprof_trace(config: str, steps: int, warmup: int, settle_ms: float):
     durs = median_at_full_grid(name)
     # every kernel of a step (tx fill: the fill + k_tx_scatter), median each
     step_ns = sum(median_at_full_grid(k)[len(median_at_full_grid(k)) // 2] for k in total)
-    return (durs[len(durs) // 2], sum(durs) / len(durs), len(durs), name, step_ns, len(total)), None
+    return (durs[len(durs) // 2], sum(durs) / len(durs), len(durs), name, step_ns, len(total), child), None
 
 
 # ------------------------------------------------------------ CPU baseline
 
 def cpu_model():
-    """The GPU box's host CPU as /proc/cpuinfo names it (and its logical CPUs)."""
+    """The GPU box's host CPU as /proc/cpuinfo names it: model, logical CPUs,
+    sockets, NUMA nodes."""
     try:
         with open("/proc/cpuinfo") as f:
-            names = [ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")]
-        return f"{names[0]} ({len(names)} logical CPUs on the host)" if names else None
+            lines = f.readlines()
+        names = [ln.split(":", 1)[1].strip() for ln in lines if ln.startswith("model name")]
+        sockets = len({ln.split(":", 1)[1].strip() for ln in lines if ln.startswith("physical id")})
+        nodes = len(glob.glob("/sys/devices/system/node/node[0-9]*"))
+        return (f"{names[0]} ({len(names)} logical CPUs on the host, {sockets or '?'} socket(s), "
+                f"{nodes or '?'} NUMA node(s))") if names else None
     except OSError:
         return None
 
@@ -468,7 +487,9 @@ def cpu_baseline(torch, r, seconds, kind="reference", cache_sample=True):
         return host, segs, want, n
 
     threads_all = min(256, os.cpu_count() or 1)  # orc_time_peso runs at most 256 threads
-    res = {"unit": "GiB/s", "kind": kind, "cores": 1, "cores_all": threads_all, "host_cpu": cpu_model()}
+    res = {"unit": "GiB/s", "kind": kind, "cores": 1, "cores_all": threads_all, "host_cpu": cpu_model(),
+           "placement": "each timing thread pinned to its own logical CPU, its slice of the sample copied "
+                        "(first-touched) by that thread before the timed region: NUMA-local"}
     what = "segments" if b.kind == "peso" else "packets' L4 ranges"
     big = min(b.total_bytes, 1 << 30)
     legs = [("dram", big, seconds)] + ([("cache", 96 << 20, seconds / 2)] if cache_sample else [])
@@ -759,12 +780,16 @@ def rehearsal(args, rank, world) -> None:
     dev = {"ordinal": None, "pci": None, "uuid": f"cpu-rank-{rank}-pid-{os.getpid()}", "name": "cpu (rehearsal)"}
     ranks = D.gather_objects(dist, {"rank": rank, "byte_base": int(b.byte_base), "packets": int(b.n),
                                     "payload_bytes": int(b.total_bytes), "stand_in_sum": s, "device": dev,
+                                    "ms_per_step": dt * 1e3 / max(args.steps, 1),
                                     "self_check": {"segments": 1, "mismatches": bad}})
     if rank == 0:
         print(json.dumps({"rehearsal": "cpu-gloo (numpy stand-in for the kernel; not a measurement)",
                           "n_gpus": world, "steps": args.steps, "scaling": "weak",
                           "value": round(world * b.total_bytes * args.steps / t / GIB, 3),
                           "max_rank_s": t, "ranks": ranks, "devices": [r["device"] for r in ranks],
+                          "ranks_ms_per_step": [round(r["ms_per_step"], 4) for r in ranks],
+                          "ms_per_step_spread": {"min": round(min(r["ms_per_step"] for r in ranks), 4),
+                                                 "max": round(max(r["ms_per_step"] for r in ranks), 4)},
                           "self_check": {"segments_per_rank": 1,
                                          "mismatches": sum(r["self_check"]["mismatches"] for r in ranks)}}),
               flush=True)
@@ -818,14 +843,17 @@ def main():
     global SETTLE_MS
     SETTLE_MS = 0.0 if args.pmc_child and not args.trace_child else max(0.0, args.settle_ms)
     if args.pmc_child:  # no probes: the tx probe launches k_tx_scatter, a step kernel by name
-        time_config(torch, tc, workload, args.config, 0, args.steps, args.warmup, probes=False)
+        r = time_config(torch, tc, workload, args.config, 0, args.steps, args.warmup, probes=False)
+        # under rocprofv3: this process's own events, next to the trace's durations
+        print(json.dumps({"child_ms_per_step": r["ms"] / args.steps, "child_launch_median_ms": r["launch_median_ms"]}),
+              flush=True)
         return
 
     head = time_config(torch, tc, workload, args.config, rank, args.steps, args.warmup, dist, probes=False)
     ms = D.max_over_ranks(dist, head["ms"], device="cuda" if backend == "nccl" else "cpu")
     # after the timed region: every rank names its GPU and re-sums a sample of
     # its own slice against its timed results
-    mine = {"rank": rank, "device": device_identity(torch, dev),
+    mine = {"rank": rank, "device": device_identity(torch, dev), "ms_per_step": head["ms"] / args.steps,
             "self_check": self_check(torch, tc, workload, head, 20240807 + rank)}
     ranks = D.gather_objects(dist, mine)
     devices = [dict(r["device"], rank=r["rank"]) for r in ranks]
@@ -847,7 +875,7 @@ def main():
         roof["rocprof_frac"] = None
         roof["rocprof_note"] = trace_note
     else:  # the same algorithmic bytes over the profiled child's median launch
-        med_ns, mean_ns, nl, kname, step_ns, nk = trace
+        med_ns, mean_ns, nl, kname, step_ns, nk, child = trace
         roof["rocprof_frac"] = round(algorithmic_bytes(b) / (med_ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
         if nk > 1:  # the same bytes over every kernel of a step (their medians summed)
             roof["rocprof_step_frac"] = round(algorithmic_bytes(b) / (step_ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
@@ -856,6 +884,23 @@ def main():
                            "step_median_us": round(step_ns / 1e3, 1),
                            "source": "rocprofv3 --kernel-trace --stats of bench.py --config "
                                      f"{args.config} (same K/W/settle), run as a child of this bench"}
+        if child:
+            # the traced child's own HIP events on the same launches: how much
+            # the trace's per-dispatch durations exceed what the kernel takes
+            # inside the traced process, and how much tracing slows it
+            cl = child["child_launch_median_ms"] * 1e3
+            roof["rocprof"]["child_events_launch_median_us"] = round(cl, 1)
+            roof["rocprof"]["child_events_us_per_step"] = round(child["child_ms_per_step"] * 1e3, 1)
+            roof["rocprof"]["trace_over_child_events"] = round(med_ns / 1e3 / cl, 4)
+    # the line's frac: events over the K-launch window; per-launch event pairs
+    # (untimed, the same K launches again) and the trace are reported beside
+    # it, and frac_conservative is the lowest of the three
+    if head.get("launch_median_ms"):
+        roof["events_launch_median_us"] = round(head["launch_median_ms"] * 1e3, 1)
+        roof["events_launch_frac"] = round(algorithmic_bytes(b) / (head["launch_median_ms"] * 1e-3) / 1e9
+                                           / HBM_PEAK_GBS, 4)
+    roof["frac_conservative"] = min(x for x in (roof["frac"], roof.get("events_launch_frac"),
+                                                roof.get("rocprof_frac")) if x is not None)
 
     line = {
         "metric": METRIC,
@@ -877,6 +922,13 @@ def main():
                    "parallelism": f"{n_gpus} independent GPU shards, no collective"},
         "roofline": roof,
         "devices": devices,
+        # every rank's own time (the line's ms_per_step is their max): a
+        # straggler GPU shows here on its own
+        "ranks_ms_per_step": [round(r["ms_per_step"], 4) for r in ranks],
+        "ms_per_step_spread": {"min": round(min(r["ms_per_step"] for r in ranks), 4),
+                               "max": round(max(r["ms_per_step"] for r in ranks), 4),
+                               "max_over_min": round(max(r["ms_per_step"] for r in ranks)
+                                                     / max(1e-9, min(r["ms_per_step"] for r in ranks)), 4)},
         "self_check": {"segments_per_rank": mine["self_check"]["segments"], "mismatches": mism,
                        "what": "a seeded sample of each rank's segments re-summed in a separate launch after the "
                                "timed region, compared with the timed results (tx fill: filled again, must not "

@@ -72,6 +72,17 @@ int tcsum_probe_segments(const void *arena /*[dev]*/, const tcsum_peso_t *segs /
 int tcsum_probe_ipv4(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,
                      uint64_t total_bytes_hint, int mode, uint32_t *sink /*[dev]*/, void *stream);
 
+/* The byte-window stream (k_flat_plan + k_flat_ipv4, tcsum_batch_ipv4's
+ * sums) in a workgroup shape of `waves` x `loads` (4x3, 8x3, 8x4, 16x4, 16x2),
+ * for A/Bs: variant 0 = the product's arithmetic (out/flags as
+ * tcsum_batch_ipv4); 1 = the plan and the windows' loads only; 2 = + the
+ * prefix scans into LDS; 3 = everything but the combine of packets that
+ * cross windows (their values are then wrong).  out: n u32 (variant 0) or a
+ * sink u32 (1..3); flags may be NULL. */
+int tcsum_probe_flat(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,
+                     uint64_t total_bytes, int variant, int waves, int loads, uint32_t *out /*[dev]*/,
+                     uint8_t *flags /*[dev] or NULL*/, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

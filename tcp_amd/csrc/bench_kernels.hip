@@ -437,6 +437,55 @@ static hipError_t launch_synth_ipv4(void *arena, const tcsum_pkt_t *pkts, uint32
     return hipGetLastError();
 }
 
+// The byte-window stream in other workgroup shapes and as load probes
+// (k_flat_ipv4's PROBE forms): the plan pass, then one window per workgroup.
+template <int W, int U, int PROBE>
+static hipError_t flat_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t total, uint32_t *out,
+                             uint8_t *flags, hipStream_t stream)
+{
+    constexpr uint32_t WB = 16u * 64u * W * U;
+    const uint64_t nw = (total + 16ull * n + 256u + WB - 1u) / WB;
+    const size_t plan_bytes = sizeof(FlatPlan) + ((4 * (nw + 1) + 7) & ~size_t(7)) + 8 * nw;
+    uint8_t *scr = nullptr;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void **>(&scr), plan_bytes, stream);
+    if (e != hipSuccess)
+        return e;
+    FlatPlan *plan = reinterpret_cast<FlatPlan *>(scr);
+    uint32_t *wfirst = reinterpret_cast<uint32_t *>(scr + sizeof(FlatPlan));
+    unsigned long long *slot =
+        reinterpret_cast<unsigned long long *>(scr + sizeof(FlatPlan) + ((4 * (nw + 1) + 7) & ~size_t(7)));
+    static uint32_t gen = 0x80000000u; // apart from the product's
+    ++gen;
+    const uint64_t pthreads = (uint64_t)n + 1u > nw ? (uint64_t)n + 1u : nw;
+    hipLaunchKernelGGL((k_flat_plan<WB>), dim3((uint32_t)((pthreads + 255u) / 256u)), dim3(256), 0, stream, arena, pkts,
+                       n, (uint32_t)nw, plan, wfirst, slot, gen);
+    hipLaunchKernelGGL((k_flat_ipv4<IP_SUMS, W, U, PROBE>), dim3((uint32_t)nw), dim3(W * 64), 0, stream, arena, pkts, n,
+                       out, flags, (int8_t *)nullptr, 0u, 64u, plan, wfirst, slot, gen);
+    e = hipGetLastError();
+    const hipError_t f = hipFreeAsync(scr, stream);
+    return e != hipSuccess ? e : f;
+}
+
+static hipError_t launch_probe_flat(uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t total, int variant,
+                                    int waves, int loads, uint32_t *out, uint8_t *flags, hipStream_t stream)
+{
+    if (n == 0)
+        return hipSuccess;
+#define TCSUM_FL(WW, UU)                                                                                       \
+    if (waves == WW && loads == UU) {                                                                          \
+        switch (variant) {                                                                                     \
+        case 0: return flat_shape<WW, UU, 0>(arena, pkts, n, total, out, flags, stream);                       \
+        case 1: return flat_shape<WW, UU, 1>(arena, pkts, n, total, out, flags, stream);                       \
+        case 2: return flat_shape<WW, UU, 2>(arena, pkts, n, total, out, flags, stream);                       \
+        case 3: return flat_shape<WW, UU, 3>(arena, pkts, n, total, out, flags, stream);                       \
+        default: return hipErrorInvalidValue;                                                                  \
+        }                                                                                                      \
+    }
+    TCSUM_FL(4, 3) TCSUM_FL(8, 3) TCSUM_FL(8, 4) TCSUM_FL(16, 4) TCSUM_FL(16, 2)
+#undef TCSUM_FL
+    return hipErrorInvalidValue;
+}
+
 } // namespace tcsum
 
 // ===================================================================== ABI
@@ -486,6 +535,16 @@ int tcsum_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uin
     if (!arena || !pkts || !sink || mode < 0 || mode > 2)
         return TCSUM_ERR_PARAM;
     return rc_of(tcsum::launch_probe_ipv4(arena, pkts, n, mean_of(total_bytes_hint, n), mode, sink,
+                                          static_cast<hipStream_t>(stream)));
+}
+
+int tcsum_probe_flat(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t total_bytes, int variant,
+                     int waves, int loads, uint32_t *out, uint8_t *flags, void *stream)
+{
+    if (!arena || !pkts || !out || !total_bytes)
+        return TCSUM_ERR_PARAM;
+    return rc_of(tcsum::launch_probe_flat(const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts, n,
+                                          total_bytes, variant, waves, loads, out, flags,
                                           static_cast<hipStream_t>(stream)));
 }
 

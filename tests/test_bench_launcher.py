@@ -39,6 +39,10 @@ def test_launcher_world2_rehearsal():
     assert len(devs) == 2 and len({d["uuid"] for d in devs}) == 2
     # each rank re-ran its stand-in after the timed region: no mismatch
     assert line["self_check"]["mismatches"] == 0 and line["self_check"]["segments_per_rank"] >= 1
+    # every rank's own time, so a straggler shows by itself
+    assert len(line["ranks_ms_per_step"]) == 2 and all(t > 0 for t in line["ranks_ms_per_step"])
+    sp = line["ms_per_step_spread"]
+    assert sp["min"] == min(line["ranks_ms_per_step"]) and sp["max"] == max(line["ranks_ms_per_step"])
 
 
 def test_shared_gpu_is_refused():
@@ -126,3 +130,5 @@ def test_launcher_rehearsal_many_ranks(world):
     for a, b in zip(ranks, ranks[1:]):
         assert b["byte_base"] >= a["byte_base"] + a["payload_bytes"]
     assert line["self_check"]["mismatches"] == 0
+    assert len(line["ranks_ms_per_step"]) == world and line["ms_per_step_spread"]["max"] >= \
+        line["ms_per_step_spread"]["min"] > 0

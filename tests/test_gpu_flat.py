@@ -105,7 +105,7 @@ def _headers(rng, host, offs, lens, valid=0.85):
         h[9] = int(rng.choice([6, 17, 1, 99]))
         if rng.random() < 0.2:
             h[10], h[11] = 0, 0
-        hl = 4 * (h[0] & 0xF)
+        hl = 4 * int(h[0] & 0xF)
         if ln >= hl + 20 and rng.random() < 0.2:
             host[o + hl + 16: o + hl + 18] = 0
             host[o + hl + 6: o + hl + 8] = 0

@@ -91,6 +91,37 @@ typedef struct tcsum_pkt {
 
 /* ------------------------------------------------ device-resident batches */
 
+/* What a caller knows of where its ranges lie (tcsum_batch's hint). */
+#define TCSUM_LAYOUT_UNKNOWN 0  /* the calls below: the stream kernels check per workgroup */
+#define TCSUM_LAYOUT_ORDERED 1  /* descriptors in arena order, ranges disjoint (gaps allowed) */
+#define TCSUM_LAYOUT_SHUFFLED 2 /* no order to exploit: per-range / per-packet kernels only */
+
+typedef struct tcsum_hint {
+    uint64_t total_bytes; /* sum of the lengths; 0 = unknown (read as 1500-B ranges) */
+    uint32_t layout;      /* TCSUM_LAYOUT_* */
+    uint32_t rsv;         /* 0 */
+} tcsum_hint_t;
+
+/* tcsum_batch operations: the same computations as the named calls below. */
+#define TCSUM_OP_SEGMENTS 0        /* tcsum_batch_segments, complement 0: out u16[n], descs tcsum_seg_t */
+#define TCSUM_OP_SEGMENTS_COMP 1   /* tcsum_batch_segments, complement 1 */
+#define TCSUM_OP_PESO 2            /* tcsum_batch_peso: out u16[n], descs tcsum_peso_t */
+#define TCSUM_OP_IPV4 3            /* tcsum_batch_ipv4: out u32[n], flags (or NULL) */
+#define TCSUM_OP_IPV4_TX_FILL 4    /* tcsum_batch_ipv4_tx_fill: out (or NULL), flags (or NULL) */
+#define TCSUM_OP_IPV4_TX_OFFLOAD 5 /* tcsum_batch_ipv4_tx_offload: out and flags required */
+#define TCSUM_OP_IPV4_RX_VERIFY 6  /* tcsum_batch_ipv4_rx_verify: verdict required, out / flags or NULL */
+
+/* Every device-resident batch in one call, with the caller's layout hint
+ * (hint NULL: total unknown, layout UNKNOWN -- exactly the named calls).
+ * Results are the same whatever the hint, except that ORDERED promises what
+ * the kernels then rely on: a batch that breaks the promise is still summed
+ * exactly (the stream kernels check it) but may take a slower path.
+ * SHUFFLED skips the stream kernels, which a batch in no particular order
+ * would only leave again.  arena is written only by TCSUM_OP_IPV4_TX_FILL. */
+int tcsum_batch(int op, void *arena /*[dev]*/, const void *descs /*[dev]*/, uint32_t n, void *out /*[dev]*/,
+                uint8_t *flags /*[dev] or NULL*/, int8_t *verdict /*[dev] or NULL*/, const tcsum_hint_t *hint /*[host]*/,
+                void *stream);
+
 /* out[i] = pktbuf_checksum16 over segs[i] with complement (0/1).
  * total_bytes_hint = sum of lens if known, else 0 (read as 1500-B ranges): the
  * mean length selects the kernel -- up to ~4 KiB, ranges listed in arena order

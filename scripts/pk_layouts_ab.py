@@ -2,7 +2,8 @@
 checksum_peso batches of several layouts, one process, interleaved rounds,
 median us per launch; every variant's results must equal the default's.
 
-  python scripts/pk_layouts_ab.py [LAYOUT,LAYOUT...] VAR=VALUE[,VAR=VALUE...] ...
+  python scripts/pk_layouts_ab.py [LAYOUT,LAYOUT...] KEY=VALUE[,KEY=VALUE...] ...
+  (KEY: a debug knob of include/tcsum_debug.h, or lib=PATH for another build)
 
 Layouts (all ~1.5 GB, device-resident):
   mtu        configs[1]: 1M x 1500 B packed back to back
@@ -59,17 +60,35 @@ arena = torch.empty(TOTAL + (64 << 20), dtype=torch.uint8, device="cuda")
 tc.synth_fill(arena)
 
 
+OLD = {"TCSUM_G": "lanes", "TCSUM_U": "loads", "TCSUM_XCD": "xcd", "TCSUM_PACKED": "packed"}
+_libs = {}
+
+
 def with_env(env, fn):
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
+    """A variant: lib=PATH runs another build of libtcsum.so (built by
+    scripts/build_ab_lib.sh); every other KEY=VALUE is a debug knob
+    (include/tcsum_debug.h; rounds 1-3's TCSUM_* names map to them)."""
+    from tcp_amd import _lib
+    prev = _lib._lib
+    path = env.get("lib")
+    if path:
+        if path not in _libs:
+            import ctypes
+            L = ctypes.CDLL(os.path.abspath(path))
+            for name, (res, args) in _lib.SIGNATURES.items():
+                f = getattr(L, name, None)
+                if f is not None:
+                    f.restype, f.argtypes = res, args
+            _libs[path] = L
+        _lib._lib = _libs[path]
+    knobs = {OLD.get(k, k): int(v) for k, v in env.items() if k != "lib"}
     try:
+        if knobs and hasattr(_lib._lib, "tcsum_debug_set"):
+            with tc.debug(**knobs):
+                return fn()
         return fn()
     finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
+        _lib._lib = prev
 
 
 for name in NAMES:

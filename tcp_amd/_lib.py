@@ -28,6 +28,7 @@ _V, _U16, _U32, _U64, _I, _SZ = (ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint
                                   ctypes.c_int, ctypes.c_size_t)
 SIGNATURES = {
     # tcsum.h
+    "tcsum_batch": (_I, [_I, _V, _V, _U32, _V, _V, _V, _V, _V]),
     "tcsum_batch_segments": (_I, [_V, _V, _U32, _V, _I, _U64, _V]),
     "tcsum_batch_peso": (_I, [_V, _V, _U32, _V, _U64, _V]),
     "tcsum_batch_ipv4": (_I, [_V, _V, _U32, _V, _V, _U64, _V]),

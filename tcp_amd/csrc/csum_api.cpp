@@ -481,68 +481,108 @@ static uint64_t mean_of(uint64_t total, uint32_t n) { return total && n ? total 
 // device tx fills of at least this many packets defer their stores (mode 4)
 static constexpr uint32_t kTxSplitMin = 131072;
 
-int tcsum_batch_segments(const void *arena, const tcsum_seg_t *segs, uint32_t n, uint16_t *out,
-                         int complement, uint64_t total_bytes_hint, void *stream)
+// The route for a batch and what its caller knows of the layout
+// (tcsum_hint_t): SHUFFLED skips the stream kernels, which would find out
+// per workgroup; a debug knob set to 1 keeps its kernel on regardless.
+static Geometry route_for(uint64_t total, uint32_t n, uint32_t layout)
+{
+    Geometry g = tcsum::pick_geometry(mean_of(total, n));
+    if (layout == TCSUM_LAYOUT_SHUFFLED) {
+        if (tcsum::knob(tcsum::KNOB_PACKED) != 1)
+            g.packed = 0;
+        if (tcsum::knob(tcsum::KNOB_FLAT) != 1)
+            g.flat = 0;
+    }
+    return g;
+}
+
+int tcsum_batch(int op, void *arena, const void *descs, uint32_t n, void *out, uint8_t *flags, int8_t *verdict,
+                const tcsum_hint_t *hint, void *stream)
 {
     if (n == 0)
         return TCSUM_OK;
-    if (!arena || !segs || !out)
+    const uint64_t total = hint ? hint->total_bytes : 0;
+    const uint32_t layout = hint ? hint->layout : TCSUM_LAYOUT_UNKNOWN;
+    if (!arena || !descs || layout > TCSUM_LAYOUT_SHUFFLED)
         return TCSUM_ERR_PARAM;
-    const hipError_t e = tcsum::launch_segments(tcsum::MODE_SEG, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
-                                                arena, segs, n, out, complement ? 1u : 0u,
-                                                static_cast<hipStream_t>(stream));
-    return rc_of(e);
+    const Geometry g = route_for(total, n, layout);
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    uint8_t *a = static_cast<uint8_t *>(arena);
+    const tcsum_pkt_t *pk = static_cast<const tcsum_pkt_t *>(descs);
+    switch (op) {
+    case TCSUM_OP_SEGMENTS:
+    case TCSUM_OP_SEGMENTS_COMP:
+    case TCSUM_OP_PESO:
+        if (!out)
+            return TCSUM_ERR_PARAM;
+        return rc_of(tcsum::launch_segments(op == TCSUM_OP_PESO ? tcsum::MODE_PESO : tcsum::MODE_SEG, g, arena,
+                                            descs, n, static_cast<uint16_t *>(out),
+                                            op == TCSUM_OP_SEGMENTS_COMP ? 1u : 0u, st));
+    case TCSUM_OP_IPV4:
+        if (!out)
+            return TCSUM_ERR_PARAM;
+        return rc_of(tcsum::launch_ipv4(0, g, a, pk, n, static_cast<uint32_t *>(out), flags, nullptr, st, total));
+    case TCSUM_OP_IPV4_TX_FILL: {
+        // Large batches: every packet's values and store positions first, then
+        // all the field stores in one short second launch (mode 4) -- 4-6 %
+        // faster on configs[3] than storing each packet's fields as its sums
+        // finish, which trickles a million isolated writes through the read
+        // stream (tx fill).  Small batches keep one launch.
+        // Debug knob "tx_split" forces.  Under hipGraph capture the
+        // single-launch form is taken: it allocates nothing (tcsum.h).
+        const int64_t ks = tcsum::knob(tcsum::KNOB_TX_SPLIT);
+        bool split = ks >= 0 ? ks != 0 : n >= kTxSplitMin;
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        if (split && hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone)
+            split = false;
+        return rc_of(tcsum::launch_ipv4(split ? 4 : 1, g, a, pk, n, static_cast<uint32_t *>(out), flags, nullptr, st,
+                                        total));
+    }
+    case TCSUM_OP_IPV4_TX_OFFLOAD:
+        if (!out || !flags)
+            return TCSUM_ERR_PARAM;
+        // the kernel never writes the arena in this mode
+        return rc_of(tcsum::launch_ipv4(3, g, a, pk, n, static_cast<uint32_t *>(out), flags, nullptr, st, total));
+    case TCSUM_OP_IPV4_RX_VERIFY:
+        if (!verdict)
+            return TCSUM_ERR_PARAM;
+        // the kernel never writes the arena in this mode
+        return rc_of(tcsum::launch_ipv4(2, g, a, pk, n, static_cast<uint32_t *>(out), flags, verdict, st, total));
+    default:
+        return TCSUM_ERR_PARAM;
+    }
+}
+
+static int batch_unknown(int op, const void *arena, const void *descs, uint32_t n, void *out, uint8_t *flags,
+                         int8_t *verdict, uint64_t total_bytes_hint, void *stream)
+{
+    const tcsum_hint_t h{total_bytes_hint, TCSUM_LAYOUT_UNKNOWN, 0u};
+    return tcsum_batch(op, const_cast<void *>(arena), descs, n, out, flags, verdict, &h, stream);
+}
+
+int tcsum_batch_segments(const void *arena, const tcsum_seg_t *segs, uint32_t n, uint16_t *out,
+                         int complement, uint64_t total_bytes_hint, void *stream)
+{
+    return batch_unknown(complement ? TCSUM_OP_SEGMENTS_COMP : TCSUM_OP_SEGMENTS, arena, segs, n, out, nullptr,
+                         nullptr, total_bytes_hint, stream);
 }
 
 int tcsum_batch_peso(const void *arena, const tcsum_peso_t *segs, uint32_t n, uint16_t *out,
                      uint64_t total_bytes_hint, void *stream)
 {
-    if (n == 0)
-        return TCSUM_OK;
-    if (!arena || !segs || !out)
-        return TCSUM_ERR_PARAM;
-    const hipError_t e = tcsum::launch_segments(tcsum::MODE_PESO, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
-                                                arena, segs, n, out, 0u, static_cast<hipStream_t>(stream));
-    return rc_of(e);
+    return batch_unknown(TCSUM_OP_PESO, arena, segs, n, out, nullptr, nullptr, total_bytes_hint, stream);
 }
 
 int tcsum_batch_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
                      uint8_t *flags, uint64_t total_bytes_hint, void *stream)
 {
-    if (n == 0)
-        return TCSUM_OK;
-    if (!arena || !pkts || !out)
-        return TCSUM_ERR_PARAM;
-    const hipError_t e = tcsum::launch_ipv4(0, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
-                                            const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts,
-                                            n, out, flags, nullptr, static_cast<hipStream_t>(stream), total_bytes_hint);
-    return rc_of(e);
+    return batch_unknown(TCSUM_OP_IPV4, arena, pkts, n, out, flags, nullptr, total_bytes_hint, stream);
 }
 
 int tcsum_batch_ipv4_tx_fill(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out, uint8_t *flags,
                              uint64_t total_bytes_hint, void *stream)
 {
-    if (n == 0)
-        return TCSUM_OK;
-    if (!arena || !pkts)
-        return TCSUM_ERR_PARAM;
-    // Large batches: every packet's values and store positions first, then all
-    // the field stores in one short second launch (mode 4) -- 4-6 % faster on
-    // configs[3] than storing each packet's fields as its sums finish, which
-    // trickles a million isolated writes through the read stream (DESIGN.md
-    // §6, tx fill).  Small batches keep one launch.  Debug knob "tx_split" forces.
-    // Under hipGraph capture the single-launch form is taken: it allocates
-    // nothing (this header's convention).
-    const int64_t ks = tcsum::knob(tcsum::KNOB_TX_SPLIT);
-    bool split = ks >= 0 ? ks != 0 : n >= kTxSplitMin;
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (split && hipStreamIsCapturing(static_cast<hipStream_t>(stream), &cap) == hipSuccess &&
-        cap != hipStreamCaptureStatusNone)
-        split = false;
-    const hipError_t e = tcsum::launch_ipv4(split ? 4 : 1, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
-                                            static_cast<uint8_t *>(arena), pkts, n, out, flags, nullptr,
-                                            static_cast<hipStream_t>(stream), total_bytes_hint);
-    return rc_of(e);
+    return batch_unknown(TCSUM_OP_IPV4_TX_FILL, arena, pkts, n, out, flags, nullptr, total_bytes_hint, stream);
 }
 
 int tcsum_batch_ipv4_tx_fill_scratch(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
@@ -563,15 +603,7 @@ int tcsum_batch_ipv4_tx_fill_scratch(void *arena, const tcsum_pkt_t *pkts, uint3
 int tcsum_batch_ipv4_tx_offload(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
                                 uint8_t *flags, uint64_t total_bytes_hint, void *stream)
 {
-    if (n == 0)
-        return TCSUM_OK;
-    if (!arena || !pkts || !out || !flags)
-        return TCSUM_ERR_PARAM;
-    // the kernel never writes the arena in this mode
-    const hipError_t e = tcsum::launch_ipv4(3, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
-                                            const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts,
-                                            n, out, flags, nullptr, static_cast<hipStream_t>(stream), total_bytes_hint);
-    return rc_of(e);
+    return batch_unknown(TCSUM_OP_IPV4_TX_OFFLOAD, arena, pkts, n, out, flags, nullptr, total_bytes_hint, stream);
 }
 
 // Host side of the offload contract: the stores k_ipv4<IP_TX> makes, driven
@@ -619,15 +651,7 @@ int tcsum_tx_apply_batch(void *arena, uint64_t arena_bytes, const tcsum_pkt_t *p
 int tcsum_batch_ipv4_rx_verify(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, int8_t *verdict,
                                uint32_t *out, uint8_t *flags, uint64_t total_bytes_hint, void *stream)
 {
-    if (n == 0)
-        return TCSUM_OK;
-    if (!arena || !pkts || !verdict)
-        return TCSUM_ERR_PARAM;
-    // the kernel never writes the arena in this mode
-    const hipError_t e = tcsum::launch_ipv4(2, tcsum::pick_geometry(mean_of(total_bytes_hint, n)),
-                                            const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts,
-                                            n, out, flags, verdict, static_cast<hipStream_t>(stream), total_bytes_hint);
-    return rc_of(e);
+    return batch_unknown(TCSUM_OP_IPV4_RX_VERIFY, arena, pkts, n, out, flags, verdict, total_bytes_hint, stream);
 }
 
 // ------------------------------------------------------------ host batches

@@ -73,6 +73,35 @@ def _stream_ptr(stream) -> int | None:
     return s.cuda_stream
 
 
+LAYOUT_UNKNOWN, LAYOUT_ORDERED, LAYOUT_SHUFFLED = 0, 1, 2
+OP_SEGMENTS, OP_SEGMENTS_COMP, OP_PESO, OP_IPV4, OP_IPV4_TX_FILL, OP_IPV4_TX_OFFLOAD, OP_IPV4_RX_VERIFY = range(7)
+
+
+class Hint(ctypes.Structure):
+    """tcsum_hint_t: the batch's byte count and what the caller knows of its layout."""
+    _fields_ = [("total_bytes", ctypes.c_uint64), ("layout", ctypes.c_uint32), ("rsv", ctypes.c_uint32)]
+
+
+def batch(op: int, arena, descs, n: int, out=None, flags=None, verdict=None, total_bytes: int = 0,
+          layout: int = LAYOUT_UNKNOWN, stream=None):
+    """tcsum_batch: any device-resident batch with a layout hint (device
+    tensors; out / flags / verdict as the op needs them, allocated when None)."""
+    torch = _torch()
+    dev = arena.device
+    if out is None and op != OP_IPV4_RX_VERIFY and op != OP_IPV4_TX_FILL:
+        out = torch.empty(n, dtype=torch.uint16 if op <= OP_PESO else torch.uint32, device=dev)
+    if flags is None and op == OP_IPV4_TX_OFFLOAD:
+        flags = torch.empty(n, dtype=torch.uint8, device=dev)
+    if verdict is None and op == OP_IPV4_RX_VERIFY:
+        verdict = torch.empty(n, dtype=torch.int8, device=dev)
+    h = Hint(total_bytes, layout, 0)
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    rc = _lib.lib().tcsum_batch(op, arena.data_ptr(), descs.data_ptr(), n, ptr(out), ptr(flags), ptr(verdict),
+                                ctypes.byref(h), _stream_ptr(stream))
+    _lib.check(rc, "tcsum_batch")
+    return out, flags, verdict
+
+
 def batch_segments(arena, segs, n: int, complement: int, total_bytes: int = 0, out=None, stream=None):
     """out[i] = pktbuf_checksum16 over each tcsum_seg_t (device tensors)."""
     torch = _torch()

@@ -212,6 +212,14 @@ def test_batch_argument_errors_without_device(libpath):
                                               ctypes.c_void_p(66), 64, 0, None) == _lib.ERR_PARAM  # misaligned
     assert L.tcsum_batch_ipv4_rx_verify(None, None, 4, None, None, None, 0, None) == _lib.ERR_PARAM
     assert L.tcsum_batch_peso(None, None, 0, None, 0, None) == _lib.OK  # empty batch
+    from tcp_amd.csum import Hint
+    h = Hint(1500 * 4, 1, 0)
+    v = ctypes.c_void_p(64)
+    assert L.tcsum_batch(99, v, v, 4, v, None, None, ctypes.byref(h), None) == _lib.ERR_PARAM  # no such op
+    assert L.tcsum_batch(2, v, v, 4, v, None, None, ctypes.byref(Hint(0, 7, 0)), None) == _lib.ERR_PARAM  # layout
+    assert L.tcsum_batch(2, v, v, 4, None, None, None, ctypes.byref(h), None) == _lib.ERR_PARAM  # no out
+    assert L.tcsum_batch(6, v, v, 4, v, None, None, ctypes.byref(h), None) == _lib.ERR_PARAM  # rx: no verdict
+    assert L.tcsum_batch(2, v, v, 0, None, None, None, None, None) == _lib.OK
     assert _lib.bench_lib().tcsum_synth_fill(ctypes.c_void_p(8), 16, 0, 1, None) == _lib.ERR_PARAM  # misaligned
     from tcp_amd import PESO_DTYPE
     seg = np.zeros(1, PESO_DTYPE)

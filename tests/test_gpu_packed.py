@@ -239,3 +239,32 @@ def test_packed_fuzz(tc, torch, oracle, seed):
     comp = int(rng.integers(0, 2))
     out = tc.batch_segments(arena, tc.descs_to_device(s), n, comp, hint)
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_segments(host, s, comp, nthreads=8))
+
+
+@pytest.mark.parametrize("layout", ["mtu", "shuffled", "ragged_gaps"])
+def test_layout_hints_give_the_same_results(tc, torch, oracle, layout):
+    """tcsum_batch's layout hint changes only the kernel, never a result --
+    also when the caller's ORDERED promise is false (a shuffled batch)."""
+    rng = np.random.default_rng(["mtu", "shuffled", "ragged_gaps"].index(layout) + 100)
+    n = 20000
+    lens = np.full(n, 1500, np.int64) if layout != "ragged_gaps" else rng.integers(1, 3000, n)
+    offs = _packed_offs(lens, 5).astype(np.int64)
+    if layout == "ragged_gaps":
+        offs += np.cumsum(rng.integers(0, 40, n))
+    host = _arena(rng, int(offs.max() + lens.max()) + 4096)
+    p = _peso(tc, offs.astype(np.uint64), lens.astype(np.uint32), rng)
+    if layout == "shuffled":
+        p = p[rng.permutation(n)]
+    want = oracle.batch_peso(host, p, nthreads=8)
+    arena = torch.from_numpy(host).cuda()
+    d = tc.descs_to_device(p)
+    s = np.zeros(n, tc.SEG_DTYPE)
+    s["offset"], s["len"] = p["offset"], p["len"]
+    s["pre_sum"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    ds = tc.descs_to_device(s)
+    want_s = oracle.batch_segments(host, s, 1, nthreads=8)
+    for lay in (tc.LAYOUT_UNKNOWN, tc.LAYOUT_ORDERED, tc.LAYOUT_SHUFFLED):
+        out, _, _ = tc.batch(tc.OP_PESO, arena, d, n, total_bytes=int(lens.sum()), layout=lay)
+        np.testing.assert_array_equal(out.cpu().numpy(), want)
+        out, _, _ = tc.batch(tc.OP_SEGMENTS_COMP, arena, ds, n, total_bytes=int(lens.sum()), layout=lay)
+        np.testing.assert_array_equal(out.cpu().numpy(), want_s)

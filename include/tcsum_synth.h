@@ -77,11 +77,12 @@ int tcsum_probe_ipv4(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev
  * for A/Bs: variant 0 = the product's arithmetic (out/flags as
  * tcsum_batch_ipv4); 1 = the plan and the windows' loads only; 2 = + the
  * prefix scans into LDS; 3 = everything but the combine of packets that
- * cross windows (their values are then wrong).  out: n u32 (variant 0) or a
- * sink u32 (1..3); flags may be NULL. */
+ * cross windows (their values are then wrong).  out: out_words u32, at
+ * least n for variants 0 and 3 (they write every packet's word; fewer:
+ * TCSUM_ERR_PARAM), a one-word sink for 1 and 2; flags may be NULL. */
 int tcsum_probe_flat(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,
                      uint64_t total_bytes, int variant, int waves, int loads, uint32_t *out /*[dev]*/,
-                     uint8_t *flags /*[dev] or NULL*/, void *stream);
+                     uint64_t out_words, uint8_t *flags /*[dev] or NULL*/, void *stream);
 
 #ifdef __cplusplus
 }

@@ -39,9 +39,10 @@ def product_flat():
 
 def probe(variant, w, u):
     def f():
-        o = out if variant == 0 else sink
+        o = out if variant in (0, 3) else sink  # variants 0 and 3 write out[0..n): a 1-word sink would overflow
         _lib.check(B.tcsum_probe_flat(arena.data_ptr(), descs.data_ptr(), n, b.total_bytes, variant, w, u,
-                                      o.data_ptr(), None, torch.cuda.current_stream().cuda_stream), "probe_flat")
+                                      o.data_ptr(), o.numel(), None, torch.cuda.current_stream().cuda_stream),
+                   "probe_flat")
     return f
 
 

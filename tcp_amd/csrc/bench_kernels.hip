@@ -539,9 +539,11 @@ int tcsum_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uin
 }
 
 int tcsum_probe_flat(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t total_bytes, int variant,
-                     int waves, int loads, uint32_t *out, uint8_t *flags, void *stream)
+                     int waves, int loads, uint32_t *out, uint64_t out_words, uint8_t *flags, void *stream)
 {
-    if (!arena || !pkts || !out || !total_bytes)
+    // variants 0 and 3 store every packet's word (3: from each window's own
+    // part): out must hold n of them
+    if (!arena || !pkts || !out || !total_bytes || out_words < ((variant == 0 || variant == 3) ? n : 1u))
         return TCSUM_ERR_PARAM;
     return rc_of(tcsum::launch_probe_flat(const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts, n,
                                           total_bytes, variant, waves, loads, out, flags,

@@ -672,28 +672,14 @@ __device__ __forceinline__ void desc_span(const void *__restrict__ descs, uint32
 
 // The per-range path for a workgroup whose ranges are not one region:
 // groups of G lanes, G the widest power of two with one group per range.
-// sd != nullptr: the K descriptors are in LDS (two chunks per range, written
-// by desc_to_lds), so the data loads follow one LDS read instead of a second
-// trip to memory.
 template <int MODE, int G, int UL = 4>
 __device__ __forceinline__ void pk_ranges(const uint8_t *__restrict__ arena, const void *__restrict__ descs,
                                           uint16_t *__restrict__ out, uint32_t aux, uint32_t first, uint32_t kw,
-                                          uint32_t T, const u32x4 *sd = nullptr)
+                                          uint32_t T)
 {
     const uint32_t t = threadIdx.x, gl = t & (G - 1u);
     for (uint32_t r = t / G; r < kw; r += T / G) {
-        SegDesc e;
-        if (sd) {
-            const u32x4 a = sd[2u * r], b = sd[2u * r + 1u];
-            e.off = (uint64_t)a.x | ((uint64_t)a.y << 32);
-            e.len = a.z;
-            e.pre = a.w;
-            e.src = b.x;
-            e.dst = b.y;
-            e.proto = b.z;
-        } else {
-            e = load_desc<MODE>(descs, first + r, true);
-        }
+        const SegDesc e = load_desc<MODE>(descs, first + r, true);
         uint32_t q = 0;
         uint32_t acc = sum_range<G, UL, false>(arena, e.off, e.len, gl, [&] {
             if constexpr (MODE == MODE_PESO)
@@ -732,15 +718,6 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     // slower, profiles/r03/packed/ab_vdesc_w8.txt)
     desc_span<MODE>(descs, first, r0, len0);
     desc_span<MODE>(descs, first + kw - 1u, offl, lenl);
-    // every wave: its share of the K descriptors (lane r: range 64w + r),
-    // issued before the region is known, so that a workgroup whose ranges are
-    // not one region (a shuffled batch) has them at once
-    const uint32_t rr = w * 64u + lane;
-    const bool mine = rr < kw;
-    const bool has = w * 64u < kw; // wave-uniform
-    SegDesc d{0, 0, 0, 0, 0, 0};
-    if (has)
-        d = load_desc<MODE>(descs, first + rr, mine);
     const uint64_t rend = offl + lenl;
     const uint8_t *p = arena + r0;
     const uint32_t s0 = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
@@ -749,28 +726,7 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     // safe to load before the ranges are known to lie inside it
     const bool span_ok = len0 != 0 && lenl != 0 && rend > r0 &&
                          rend - r0 <= (uint64_t)kPkMaxPasses * CH * 16u - s0;
-    if (!span_ok) {
-        // not one region (shuffled, far apart, empty ends): range by range,
-        // the descriptors handed over through LDS -- one memory latency before
-        // the data, as in the per-range kernel (this path paid
-        // three and ran 1.12x k_segments<16,6> on a shuffled 1500-B batch)
-        if (has && mine) {
-            dat[2u * rr] = u32x4{(uint32_t)d.off, (uint32_t)(d.off >> 32), d.len, d.pre};
-            dat[2u * rr + 1u] = u32x4{d.src, d.dst, d.proto, 0u};
-        }
-        __syncthreads();
-        const uint32_t lanes_per = T / kw;
-        if (lanes_per >= 64)
-            pk_ranges<MODE, 64>(arena, descs, out, aux, first, kw, T, dat);
-        else if (lanes_per >= 32)
-            pk_ranges<MODE, 32, 3>(arena, descs, out, aux, first, kw, T, dat);
-        else if (lanes_per >= 16)
-            pk_ranges<MODE, 16>(arena, descs, out, aux, first, kw, T, dat);
-        else
-            pk_ranges<MODE, 8>(arena, descs, out, aux, first, kw, T, dat);
-        return;
-    }
-    bool ranges = false; // workgroup-uniform: a range outside the region sends it range by range
+    bool ranges = !span_ok; // workgroup-uniform: sum range by range instead
     const uint32_t span = span_ok ? (uint32_t)(rend - r0) : 0u;
     const uint32_t nch = span_ok ? (s0 + span + 15u) >> 4 : 0u;
     const uint32_t npass = (nch + CH - 1u) / CH;
@@ -783,10 +739,16 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
         v[u] = load16<true>(base + (c < nch ? c : (nch ? nch - 1u : 0u)));
     }
     issue_fence();
-    // every wave: whether each of its ranges lies in the region, and its
-    // start and end in bytes from the first chunk
+    // every wave: its share of the K descriptors (lane r: range 64w + r),
+    // whether each lies in the region, and its start and end in bytes from the
+    // first chunk
+    const uint32_t rr = w * 64u + lane;
+    const bool mine = rr < kw;
+    const bool has = w * 64u < kw; // wave-uniform
+    SegDesc d{0, 0, 0, 0, 0, 0};
     uint32_t xs = 0, xe = 0, q16 = 0;
     if (has) {
+        d = load_desc<MODE>(descs, first + rr, mine);
         // P wraps mod 2^32 across passes, so a difference is exact only for a
         // range whose word sum stays below 2^32: < 128 KiB (<= 65536 words)
         const bool inside = !mine || (d.off >= r0 && d.off + d.len <= rend && d.len < (1u << 17));

@@ -1394,6 +1394,19 @@ __global__ __launch_bounds__(256) void k_flat_plan(const uint8_t *__restrict__ a
         plan->bad = gen;
 }
 
+// A 16-B chunk through the scalar data cache (reads only): the load waits on
+// lgkmcnt, not on the vector loads issued before it, so a value a workgroup
+// needs right after its window arrives can be fetched beside the window.
+// The wait is inside: the wave stalls only until this load returns, while
+// its window's vector loads stay in flight.  p must be uniform and 4-B
+// aligned.
+__device__ __forceinline__ u32x4 sload16(const void *p)
+{
+    u32x4 v;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+
 // Byte `i` (0..15) of a chunk (selects on named dwords: no dynamic indexing)
 __device__ __forceinline__ uint32_t chunk_byte(u32x4 v, uint32_t i)
 {
@@ -1427,9 +1440,9 @@ __global__ __launch_bounds__(W * 64) void k_flat_ipv4(uint8_t *__restrict__ aren
         // not a stream: this workgroup's share of the packets, one by one
         const uint32_t lo = (uint32_t)((uint64_t)n * blk / gridDim.x);
         const uint32_t hi = (uint32_t)((uint64_t)n * (blk + 1u) / gridDim.x);
-        constexpr uint32_t G = 16, PER = T / G;
+        constexpr uint32_t G = 16, PER = T / G; // 2 loads per lane: the stream's register budget
         for (uint32_t p0 = lo; p0 < hi; p0 += PER) // workgroup-uniform
-            ipv4_packet<G, 4, IPM>(arena, pkts, p0 + t / G, hi, out, flags_out, verdict_out, opts);
+            ipv4_packet<G, 2, IPM>(arena, pkts, p0 + t / G, hi, out, flags_out, verdict_out, opts);
         return;
     }
     const uint64_t base = plan->base, send = plan->end;
@@ -1463,6 +1476,33 @@ __global__ __launch_bounds__(W * 64) void k_flat_ipv4(uint8_t *__restrict__ aren
     const uint32_t pf = wfirst[blk], pl = wfirst[blk + 1u];
     const uint32_t j0 = pf > 0 ? pf - 1u : 0u;
     const uint32_t m = pl - j0;
+    // The straddler's header lies before this window: its descriptor and first
+    // 96 bytes through the scalar cache now, while the window is in flight
+    // (fetched after the barrier they put a whole memory latency into every
+    // workgroup's tail: 687 -> 1169 us on configs[3], profiles/r04/flat/).
+    // (six named chunks, not an array: captured into the fetch lambda below,
+    // an array went to scratch memory)
+    u32x4 sh0 = u32x4(0u), sh1 = u32x4(0u), sh2 = u32x4(0u), sh3 = u32x4(0u), sh4 = u32x4(0u), sh5 = u32x4(0u);
+    if (pf > 0) { // workgroup-uniform
+        const u32x4 sd = sload16(pkts + (pf - 1u));
+        const uint64_t ss = a0 + ((uint64_t)sd.x | ((uint64_t)sd.y << 32));
+        const uint32_t sfl = sd.z < kFlatMaxFrame ? sd.z : kFlatMaxFrame;
+        if (sd.z >= 20 && ss + sfl > wlo) { // a header to parse, and bytes in this window
+            const uint64_t c0 = ss & ~15ull, se = ss + sfl; // the packet's own chunks only
+            const int64_t r0 = (int64_t)(c0 - a0);
+            sh0 = sload16(arena + r0);
+            if (c0 + 16u < se)
+                sh1 = sload16(arena + r0 + 16);
+            if (c0 + 32u < se)
+                sh2 = sload16(arena + r0 + 32);
+            if (c0 + 48u < se)
+                sh3 = sload16(arena + r0 + 48);
+            if (c0 + 64u < se)
+                sh4 = sload16(arena + r0 + 64);
+            if (c0 + 80u < se)
+                sh5 = sload16(arena + r0 + 80);
+        }
+    }
     // packet i of the window goes to wave i % W, lane i / W (spread over the SIMDs)
     const uint32_t i0 = lane * W + wv;
     u32x4 dv0 = u32x4(0u);
@@ -1532,10 +1572,13 @@ __global__ __launch_bounds__(W * 64) void k_flat_ipv4(uint8_t *__restrict__ aren
         const uint32_t s0 = (uint32_t)(s & 15u);
         const uint64_t hc = s >> 4; // the packet's first chunk (absolute)
         const uint32_t nchp = big_enough ? (frame_ld + s0 + 15u) >> 4 : 0u; // the packet's chunks
-        // chunk k of the packet: from the window's LDS copy, else from memory
+        // chunk k of the packet: from the window's LDS copy, the straddler's
+        // prefetched header, else from memory
         auto fetch = [=](uint32_t k) -> u32x4 {
             if (!part_of || k >= nchp)
                 return u32x4(0u);
+            if (straddler && k < 6u)
+                return k == 0 ? sh0 : k == 1 ? sh1 : k == 2 ? sh2 : k == 3 ? sh3 : k == 4 ? sh4 : sh5;
             const uint64_t g = hc + k;
             const uint64_t rel = g - (wlo >> 4);
             if (rel < CH)
@@ -1545,10 +1588,16 @@ __global__ __launch_bounds__(W * 64) void k_flat_ipv4(uint8_t *__restrict__ aren
         const u32x4 h0 = fetch(0), h1 = fetch(1);
         const u32x4 h2 = s0 > 12 ? fetch(2) : u32x4(0u);
         const Hdr5 hd = header_dwords(h0, h1, h2, s0);
-        const IpHdr ih = ip_parse<IPM>(hd, frame, big_enough, [=](uint32_t ihl4) {
-            const uint32_t o = s0 + ihl4, cw = o >> 4;
-            return header_dwords(fetch(cw), fetch(cw + 1u), u32x4(0u), o & 15u);
-        });
+        // rx: the TCP/UDP header's first 16 bytes, fetched before the parse (a
+        // fetch inside its callback kept the closure in scratch memory)
+        u32x4 wa = u32x4(0u), wb = u32x4(0u);
+        const uint32_t ol4 = s0 + ((hd.d0 & 0xFu) << 2);
+        if (IPM == IP_RX) {
+            wa = fetch(ol4 >> 4);
+            wb = fetch((ol4 >> 4) + 1u);
+        }
+        const IpHdr ih = ip_parse<IPM>(hd, frame, big_enough,
+                                       [=](uint32_t) { return header_dwords(wa, wb, u32x4(0u), ol4 & 15u); });
         // the L4 range's part in this window
         const uint64_t A = s + ih.hl, B = s + ih.end;
         const uint32_t xa = A <= wlo ? 0u : A >= whi ? WB : (uint32_t)(A - wlo);

@@ -213,6 +213,14 @@ static void print_engine(void)
            (unsigned long long)st.tx_frames, (unsigned long long)st.tx_batches,
            (unsigned long long)st.rx_frames, (unsigned long long)st.rx_batches,
            (unsigned long long)st.rx_ip_filled, (unsigned long long)st.rx_used);
+    // frames per batch (tx coalescing, net_csum_gpu.h): 1, 2-3, 4-7, 8-15, 16-31, >= 32
+    printf("batch sizes: tx [1 %llu | 2-3 %llu | 4-7 %llu | 8-15 %llu | 16-31 %llu | 32+ %llu], "
+           "rx [1 %llu | 2-3 %llu | 4-7 %llu | 8-15 %llu | 16-31 %llu | 32+ %llu], %llu flushes\n",
+           (unsigned long long)st.tx_hist[0], (unsigned long long)st.tx_hist[1], (unsigned long long)st.tx_hist[2],
+           (unsigned long long)st.tx_hist[3], (unsigned long long)st.tx_hist[4], (unsigned long long)st.tx_hist[5],
+           (unsigned long long)st.rx_hist[0], (unsigned long long)st.rx_hist[1], (unsigned long long)st.rx_hist[2],
+           (unsigned long long)st.rx_hist[3], (unsigned long long)st.rx_hist[4], (unsigned long long)st.rx_hist[5],
+           (unsigned long long)st.tx_flushes);
 #else
     printf("engine: none (the reference's own CPU checksum, configs[0])\n");
 #endif

@@ -605,6 +605,13 @@ static void print_stats(const char *when)
            (unsigned long long)st.tx_fail_batches, (unsigned long long)st.tx_dropped,
            (unsigned long long)st.rx_fail_batches, (unsigned long long)pcapd_arp_replies(),
            (unsigned long long)pcapd_filtered(), (unsigned long long)pcapd_inject_failures());
+    // frames per batch (tx coalescing, net_csum_gpu.h): 1, 2-3, 4-7, 8-15, 16-31, >= 32
+    printf("batch sizes %s: tx [1 %llu | 2-3 %llu | 4-7 %llu | 8-15 %llu | 16-31 %llu | 32+ %llu], "
+           "rx [1 %llu | 2-3 %llu | 4-7 %llu | 8-15 %llu | 16-31 %llu | 32+ %llu]\n", when,
+           (unsigned long long)st.tx_hist[0], (unsigned long long)st.tx_hist[1], (unsigned long long)st.tx_hist[2],
+           (unsigned long long)st.tx_hist[3], (unsigned long long)st.tx_hist[4], (unsigned long long)st.tx_hist[5],
+           (unsigned long long)st.rx_hist[0], (unsigned long long)st.rx_hist[1], (unsigned long long)st.rx_hist[2],
+           (unsigned long long)st.rx_hist[3], (unsigned long long)st.rx_hist[4], (unsigned long long)st.rx_hist[5]);
     fflush(stdout);
 }
 

@@ -84,6 +84,26 @@ int tcsum_probe_flat(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev
                      uint64_t total_bytes, int variant, int waves, int loads, uint32_t *out /*[dev]*/,
                      uint64_t out_words, uint8_t *flags /*[dev] or NULL*/, void *stream);
 
+/* The tx fill's design-independent floor: read every byte of arena[0,
+ * nbytes) once and write each packet's two 2-byte checksum fields at the
+ * addresses the fill writes, with no descriptors, parse or sums.
+ * tcsum_probe_txfloor_prepare (outside any measurement) derives them with
+ * the fill's field rules: side = 2n u32 scratch (values, then positions),
+ * fpos = 2n u64 field offsets from the arena (~0: none), ffirst =
+ * tcsum_probe_txfloor_windows(nbytes) + 1 u32 (first packet of each 16-KiB
+ * window; pkts in arena order).  tcsum_probe_txfloor: variant 0 = the stores
+ * in-stream (each window's workgroup writes its packets' fields after its
+ * loads), 1 = deferred (the plain read, then one dense scatter of side's
+ * values).  The fields are left junk. */
+uint32_t tcsum_probe_txfloor_windows(uint64_t nbytes);
+int tcsum_probe_txfloor_prepare(const void *arena /*[dev]*/, uint64_t nbytes, const tcsum_pkt_t *pkts /*[dev]*/,
+                                uint32_t n, uint64_t total_bytes_hint, uint32_t *side /*[dev]*/, uint64_t side_words,
+                                uint64_t *fpos /*[dev]*/, uint64_t fpos_words, uint32_t *ffirst /*[dev]*/,
+                                uint64_t ffirst_words, void *stream);
+int tcsum_probe_txfloor(void *arena /*[dev]*/, uint64_t nbytes, const uint64_t *fpos /*[dev]*/,
+                        const uint32_t *side /*[dev]*/, uint32_t n, const uint32_t *ffirst /*[dev]*/, int variant,
+                        uint32_t *sink /*[dev]*/, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -271,6 +271,95 @@ __global__ __launch_bounds__(256) void k_probe_desc(const uint8_t *__restrict__ 
         sink[0] = acc;
 }
 
+// ---------------------------------------------------------------- tx floor
+//
+// What any tx fill must do, in the cheapest form either side of the store
+// policy: read every byte of the batch once and write the same 2 x 2-byte
+// checksum fields per packet at the same addresses -- no descriptors, no
+// header parse, no sums (VERDICT r03 "next round" 2).  Positions come from a
+// prepare pass (k_floor_index over k_probe_ipv4<PM_TX>'s field rules),
+// outside the measurement: fpos[2i], fpos[2i + 1] = packet i's IPv4 / L4
+// field byte offsets from the arena (~0: none), ffirst[w] = the first packet
+// starting at or after window w (16 KiB windows, k_probe_read<4>'s
+// workgroup tile).
+constexpr uint32_t kFloorWB = 16384;
+constexpr uint64_t kFloorNone = ~0ull;
+
+__global__ __launch_bounds__(256) void k_floor_index(const tcsum_pkt_t *__restrict__ pkts, uint32_t n,
+                                                     const uint32_t *__restrict__ posv, uint64_t nbytes,
+                                                     uint64_t *__restrict__ fpos, uint32_t *__restrict__ ffirst,
+                                                     uint32_t nw)
+{
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t > n)
+        return;
+    // windows (window of packet t-1's start, window of t's start] begin at packet t
+    const uint64_t lo = t == 0 ? 0ull : pkts[t - 1].offset / kFloorWB + 1u;
+    uint64_t hi = nw;
+    if (t < n) {
+        const uint64_t off = pkts[t].offset;
+        hi = off / kFloorWB;
+        const uint32_t q = posv[t];
+        const uint64_t a = off + 10u, b = off + (q & 0xFFFFu);
+        fpos[2ull * t] = (q >> 16) && a + 2u <= nbytes ? a : kFloorNone;
+        fpos[2ull * t + 1u] = (q >> 16) && (q & 0xFFFFu) && b + 2u <= nbytes ? b : kFloorNone;
+    }
+    for (uint64_t w = lo; w <= hi && w <= nw; ++w)
+        ffirst[w] = t;
+}
+
+__device__ __forceinline__ void floor_store(uint8_t *arena, uint64_t nbytes, uint64_t a, uint32_t v)
+{
+    if (a < nbytes - 1u) { // kFloorNone fails it
+        arena[a] = (uint8_t)v;
+        arena[a + 1u] = (uint8_t)(v >> 8);
+    }
+}
+
+// (i) in-stream: workgroup w reads window w as k_probe_read<4> does, then its
+// threads write the fields of the packets that start in it, with values from
+// their own loads (the stores wait for the window, as a fill's would).
+__global__ __launch_bounds__(256) void k_floor_stream(const u32x4 *__restrict__ p, uint64_t nchunks,
+                                                      uint8_t *__restrict__ arena, uint64_t nbytes,
+                                                      const uint64_t *__restrict__ fpos,
+                                                      const uint32_t *__restrict__ ffirst, uint32_t n)
+{
+    constexpr int U = 4;
+    const uint32_t w = blockIdx.x;
+    const uint64_t base = ((w * 256ull + threadIdx.x) >> 6) * 64ull * U;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t f0 = ffirst[w], f1 = ffirst[w + 1u];
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t idx = base + u * 64ull + lane;
+        v[u] = load16<true>(p + (idx < nchunks ? idx : nchunks - 1));
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    const uint32_t hi = f1 < n ? f1 : n;
+    for (uint32_t i = f0 + threadIdx.x; i < hi; i += 256u) {
+        floor_store(arena, nbytes, fpos[2ull * i], acc);
+        floor_store(arena, nbytes, fpos[2ull * i + 1u], acc >> 16);
+    }
+}
+
+// (ii) deferred: the read (k_probe_read<4>) and then this dense scatter of
+// precomputed values.
+__global__ __launch_bounds__(256) void k_floor_scatter(uint8_t *__restrict__ arena, uint64_t nbytes,
+                                                       const uint64_t *__restrict__ fpos,
+                                                       const uint32_t *__restrict__ vals, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t v = vals[i];
+    floor_store(arena, nbytes, fpos[2ull * i], v);
+    floor_store(arena, nbytes, fpos[2ull * i + 1u], v >> 16);
+}
+
 // The product's route (libtcsum.so's router with its debug knobs applied).
 static Geometry route(uint64_t mean_len)
 {
@@ -356,8 +445,10 @@ static hipError_t launch_probe_read(const void *p, uint64_t nbytes, uint32_t *si
     return hipGetLastError();
 }
 
+// ext_side (PM_TX): the caller's 2n words for the values and positions; then
+// nothing is scattered (the tx floor's prepare pass)
 static hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t mean_len,
-                                    int mode, uint32_t *sink, hipStream_t stream)
+                                    int mode, uint32_t *sink, hipStream_t stream, uint32_t *ext_side = nullptr)
 {
     if (n == 0)
         return hipSuccess;
@@ -377,8 +468,8 @@ static hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, 
     const uint8_t *a = static_cast<const uint8_t *>(arena);
     const uint32_t xg = (uint32_t)g.xcd;
     // PM_TX: the deferred fill's scratch (values, positions)
-    uint32_t *side = nullptr;
-    if (mode == PM_TX) {
+    uint32_t *side = ext_side;
+    if (mode == PM_TX && !side) {
         const hipError_t e = hipMallocAsync(reinterpret_cast<void **>(&side), (size_t)n * 8u, stream);
         if (e != hipSuccess)
             return e;
@@ -401,7 +492,7 @@ static hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, 
     TCSUM_PI(16, 1) TCSUM_PI(16, 2) TCSUM_PI(16, 3) TCSUM_PI(16, 4) TCSUM_PI(16, 6) TCSUM_PI(16, 8)
     TCSUM_PI(32, 6) TCSUM_PI(64, 4) TCSUM_PI(64, 16)
 #undef TCSUM_PI
-    if (mode == PM_TX) {
+    if (mode == PM_TX && !ext_side) {
         if (e == hipSuccess) { // the product's scatter, on the probe's values and positions
             hipLaunchKernelGGL(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, const_cast<uint8_t *>(a),
                                pkts, n, vals, posv);
@@ -411,6 +502,44 @@ static hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, 
         e = e != hipSuccess ? e : f;
     }
     return e;
+}
+
+static uint32_t floor_windows(uint64_t nbytes) { return (uint32_t)((nbytes / 16u * 16u + kFloorWB - 1u) / kFloorWB); }
+
+static hipError_t launch_floor_prepare(const void *arena, uint64_t nbytes, const tcsum_pkt_t *pkts, uint32_t n,
+                                       uint64_t mean_len, uint32_t *vals, uint32_t *posv, uint64_t *fpos,
+                                       uint32_t *ffirst, hipStream_t stream)
+{
+    if (posv != vals + n) // k_probe_ipv4's side layout: values, then positions
+        return hipErrorInvalidValue;
+    hipError_t e = launch_probe_ipv4(arena, pkts, n, mean_len, PM_TX, vals, stream, vals);
+    if (e != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(k_floor_index, dim3((n + 256u) / 256u), dim3(256), 0, stream, pkts, n, posv, nbytes, fpos,
+                       ffirst, floor_windows(nbytes));
+    return hipGetLastError();
+}
+
+static hipError_t launch_floor(void *arena, uint64_t nbytes, const uint64_t *fpos, const uint32_t *vals, uint32_t n,
+                               const uint32_t *ffirst, int variant, uint32_t *sink, hipStream_t stream)
+{
+    const uint64_t nchunks = nbytes / 16;
+    if (nchunks == 0 || n == 0)
+        return hipSuccess;
+    uint8_t *a = static_cast<uint8_t *>(arena);
+    const u32x4 *q = static_cast<const u32x4 *>(arena);
+    if (variant == 0) {
+        hipLaunchKernelGGL(k_floor_stream, dim3(floor_windows(nbytes)), dim3(256), 0, stream, q, nchunks, a, nbytes,
+                           fpos, ffirst, n);
+        return hipGetLastError();
+    }
+    if (variant != 1)
+        return hipErrorInvalidValue;
+    hipError_t e = launch_probe_read(arena, nbytes, sink, stream);
+    if (e != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(k_floor_scatter, dim3((n + 255u) / 256u), dim3(256), 0, stream, a, nbytes, fpos, vals, n);
+    return hipGetLastError();
 }
 
 static hipError_t launch_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, uint64_t seed,
@@ -548,6 +677,28 @@ int tcsum_probe_flat(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uin
     return rc_of(tcsum::launch_probe_flat(const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts, n,
                                           total_bytes, variant, waves, loads, out, flags,
                                           static_cast<hipStream_t>(stream)));
+}
+
+uint32_t tcsum_probe_txfloor_windows(uint64_t nbytes) { return tcsum::floor_windows(nbytes); }
+
+int tcsum_probe_txfloor_prepare(const void *arena, uint64_t nbytes, const tcsum_pkt_t *pkts, uint32_t n,
+                                uint64_t total_bytes_hint, uint32_t *side, uint64_t side_words, uint64_t *fpos,
+                                uint64_t fpos_words, uint32_t *ffirst, uint64_t ffirst_words, void *stream)
+{
+    if (!arena || !pkts || !side || !fpos || !ffirst || (reinterpret_cast<uintptr_t>(arena) & 15u) ||
+        side_words < 2ull * n || fpos_words < 2ull * n || ffirst_words < tcsum::floor_windows(nbytes) + 1ull)
+        return TCSUM_ERR_PARAM;
+    return rc_of(tcsum::launch_floor_prepare(arena, nbytes, pkts, n, mean_of(total_bytes_hint, n), side, side + n,
+                                             fpos, ffirst, static_cast<hipStream_t>(stream)));
+}
+
+int tcsum_probe_txfloor(void *arena, uint64_t nbytes, const uint64_t *fpos, const uint32_t *side, uint32_t n,
+                        const uint32_t *ffirst, int variant, uint32_t *sink, void *stream)
+{
+    if (!arena || !fpos || !side || !ffirst || !sink || (reinterpret_cast<uintptr_t>(arena) & 15u) || nbytes < 2)
+        return TCSUM_ERR_PARAM;
+    return rc_of(tcsum::launch_floor(arena, nbytes, fpos, side, n, ffirst, variant, sink,
+                                     static_cast<hipStream_t>(stream)));
 }
 
 int tcsum_probe_tile(const void *p, uint64_t nbytes, int lanes, int loads, int dep, uint32_t *sink, void *stream)

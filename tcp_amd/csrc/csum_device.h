@@ -1483,7 +1483,7 @@ __global__ __launch_bounds__(W * 64) void k_flat_ipv4(uint8_t *__restrict__ aren
     // (six named chunks, not an array: captured into the fetch lambda below,
     // an array went to scratch memory)
     u32x4 sh0 = u32x4(0u), sh1 = u32x4(0u), sh2 = u32x4(0u), sh3 = u32x4(0u), sh4 = u32x4(0u), sh5 = u32x4(0u);
-    if (pf > 0) { // workgroup-uniform
+    if (pf > 0 && wv == 0) { // wave-uniform: wave 0 takes the packets
         const u32x4 sd = sload16(pkts + (pf - 1u));
         const uint64_t ss = a0 + ((uint64_t)sd.x | ((uint64_t)sd.y << 32));
         const uint32_t sfl = sd.z < kFlatMaxFrame ? sd.z : kFlatMaxFrame;
@@ -1503,10 +1503,14 @@ __global__ __launch_bounds__(W * 64) void k_flat_ipv4(uint8_t *__restrict__ aren
                 sh5 = sload16(arena + r0 + 80);
         }
     }
-    // packet i of the window goes to wave i % W, lane i / W (spread over the SIMDs)
-    const uint32_t i0 = lane * W + wv;
+    // packet i of the window goes to lane i % 64 of wave 0: the packet phase
+    // is instruction-bound, not load-bound (one pass of it per wave per
+    // window), so the other waves leave after the scans
+    // (profiles/r04/flat/: packets spread over all W waves cost 4x the issue
+    // slots and ran at 2x the stream's time)
+    const uint32_t i0 = lane;
     u32x4 dv0 = u32x4(0u);
-    if (i0 < m)
+    if (wv == 0 && i0 < m)
         dv0 = *reinterpret_cast<const u32x4 *>(pkts + j0 + i0);
 
     // chunk sums, scans over each 32-lane half, the chunks and prefixes into LDS
@@ -1533,7 +1537,9 @@ __global__ __launch_bounds__(W * 64) void k_flat_ipv4(uint8_t *__restrict__ aren
             out[0] = 1u;
         return;
     }
-    // every wave: the sub-ranges' exclusive prefixes (lane k: sub-range k)
+    if (wv != 0)
+        return;
+    // the sub-ranges' exclusive prefixes (lane k: sub-range k)
     const uint32_t st = lane < 2u * W ? ex[lane * SR] : 0u;
     const uint32_t si = scan32(st);
     const uint32_t sx = si - st;
@@ -1552,9 +1558,9 @@ __global__ __launch_bounds__(W * 64) void k_flat_ipv4(uint8_t *__restrict__ aren
         return e;
     };
     const uint64_t whi = wlo + WB;
-    const uint32_t rounds = (m + T - 1u) / T; // workgroup-uniform
+    const uint32_t rounds = (m + 63u) / 64u; // wave-uniform
     for (uint32_t r = 0; r < rounds; ++r) {
-        const uint32_t i = r * T + i0;
+        const uint32_t i = r * 64u + i0;
         const bool act = i < m;
         const u32x4 dv = r == 0 ? dv0 : (act ? *reinterpret_cast<const u32x4 *>(pkts + j0 + i) : u32x4(0u));
         const uint32_t j = j0 + i;

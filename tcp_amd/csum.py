@@ -387,6 +387,32 @@ def probe_ipv4(arena, pkts, n: int, total_bytes: int, rx: bool = False, sink=Non
     return sink
 
 
+def txfloor_prepare(arena, nbytes: int, pkts, n: int, total_bytes: int, stream=None) -> dict:
+    """tcsum_probe_txfloor_prepare: the tx fill's field addresses and
+    16-KiB-window index, for probe_txfloor (outside any measurement)."""
+    torch = _torch()
+    dev = arena.device
+    nw = int(_lib.bench_lib().tcsum_probe_txfloor_windows(nbytes))
+    h = dict(arena=arena, nbytes=nbytes, n=n, side=torch.zeros(2 * max(n, 1), dtype=torch.uint32, device=dev),
+             fpos=torch.zeros(2 * max(n, 1), dtype=torch.int64, device=dev),
+             ffirst=torch.zeros(nw + 1, dtype=torch.uint32, device=dev),
+             sink=torch.zeros(1, dtype=torch.uint32, device=dev))
+    _lib.check(_lib.bench_lib().tcsum_probe_txfloor_prepare(
+        arena.data_ptr(), nbytes, pkts.data_ptr(), n, total_bytes, h["side"].data_ptr(), h["side"].numel(),
+        h["fpos"].data_ptr(), h["fpos"].numel(), h["ffirst"].data_ptr(), h["ffirst"].numel(), _stream_ptr(stream)),
+        "tcsum_probe_txfloor_prepare")
+    return h
+
+
+def probe_txfloor(h: dict, deferred: bool = False, stream=None):
+    """tcsum_probe_txfloor: one read of the batch's bytes plus the fill's
+    field writes, in-stream (deferred=False) or as one dense scatter."""
+    _lib.check(_lib.bench_lib().tcsum_probe_txfloor(
+        h["arena"].data_ptr(), h["nbytes"], h["fpos"].data_ptr(), h["side"].data_ptr(), h["n"],
+        h["ffirst"].data_ptr(), 1 if deferred else 0, h["sink"].data_ptr(), _stream_ptr(stream)),
+        "tcsum_probe_txfloor")
+
+
 def pick_geometry(mean_len: int):
     g, u = ctypes.c_int(), ctypes.c_int()
     _lib.lib().tcsum_pick_geometry(mean_len, ctypes.byref(g), ctypes.byref(u))

@@ -98,7 +98,7 @@ def _headers(rng, host, offs, lens, valid=0.85):
         h = host[o: o + 20]
         ihl = 5 if rng.random() < 0.8 else int(rng.integers(5, 16))
         h[0] = (0x40 | ihl) if rng.random() < valid else int(rng.integers(0, 256))
-        tl = ln if rng.random() < 0.8 else int(rng.integers(0, 70000)) & 0xFFFF
+        tl = (ln if rng.random() < 0.8 else int(rng.integers(0, 70000))) & 0xFFFF  # a 16-bit field
         h[2], h[3] = tl >> 8, tl & 0xFF
         if rng.random() < 0.85:
             h[6], h[7] = 0, 0

@@ -31,6 +31,18 @@ extern "C" {
  *   "sync_block"      1: drop-in calls block in hipStreamSynchronize
  *   "e2e_trace"       1: tcsum_host_batch_peso prints phase times on stderr
  *   "e2e_chunk_mb"    tcsum_host_batch_peso's copy chunk size
+ *   "server_max"      largest host-queue batch the queue server takes (65536)
+ *   "server_trace"    1: the queue server prints its phase stamps when stopped
+ *   "server_idle_ms"  the resident servers stop after this long idle (10)
+ *   "server_wgs"      queue server workgroups (64)
+ *   "hostq_dma_kb"    host-queue batches spanning this much go through the
+ *                     copy engine (262144)
+ *   "hostq_dma_keep_mb" device arena kept between host-queue calls (256)
+ *   "copy_threads"    host threads of a parallel gather / scatter (16; the
+ *                     worker pool is sized once, at first use)
+ * Only TCSUM_DEVICE and TCSUM_CALL_SERVER are read from the environment
+ * (deployment choices for an unmodified drop-in stack); nothing there changes
+ * a route or a tuning.
  * Returns TCSUM_OK, or TCSUM_ERR_PARAM for an unknown key. */
 int tcsum_debug_set(const char *key, int64_t value);
 

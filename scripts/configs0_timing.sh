@@ -1,27 +1,35 @@
 #!/bin/bash
 # configs[0] on the box: the loop echo with the reference's CPU checksum
-# (loop_echo_cpu) and with the GPU batches (loop_echo), the same process
-# layout, three runs each, plus the reference's own app/echo UDP server; and
-# the pcap driver over the test double (pcap_wire), phase lines kept.
+# (loop_echo_cpu) and with the GPU batches (loop_echo) -- tx coalescing on
+# (the default: frames held until the work thread is idle), off
+# (NET_CSUM_COALESCE=0: one fill per netif_out), and on with the resident
+# queue server (NET_CSUM_QUEUE_SERVER=1) -- the same process layout, three
+# runs each, plus the reference's own app/echo UDP server; and the pcap
+# driver over the test double (pcap_wire), phase lines and batch sizes kept.
 # Usage: scripts/configs0_timing.sh OUTDIR
 set -u
-out=${1:-gpurun_out/r03}
+out=${1:-gpurun_out/r04}
 mkdir -p "$out"
 B=integration/_build
 : > "$out/configs0_timing.txt"
+keep="^timing|echoed intact|^engine|^batch sizes"
+run() { # label env... exe args...
+  local label=$1; shift
+  echo "== $label" >> "$out/configs0_timing.txt"
+  timeout -k 10 120 env "$@" > "$out/run.raw" 2>&1 || { echo "$label failed rc=$?"; tail -20 "$out/run.raw"; exit 1; }
+  grep -E "$keep" "$out/run.raw" >> "$out/configs0_timing.txt"
+}
 for rep in 1 2 3; do
-  for exe in loop_echo_cpu loop_echo; do
-    echo "== $exe rep $rep (--rounds 2000 --tcp-bytes 1048576)" >> "$out/configs0_timing.txt"
-    timeout -k 10 120 $B/$exe --rounds 2000 --tcp-bytes 1048576 > "$out/$exe.raw" 2>&1 || { echo "$exe failed rc=$?"; tail -20 "$out/$exe.raw"; exit 1; }
-    grep -E "^timing|echoed intact|^engine" "$out/$exe.raw" >> "$out/configs0_timing.txt"
-    echo "== $exe rep $rep, reference app/echo/udp_echo_server.c (--ref-udp-server --udp-only --rounds 2000)" >> "$out/configs0_timing.txt"
-    timeout -k 10 120 $B/$exe --ref-udp-server --udp-only --rounds 2000 > "$out/$exe.raw" 2>&1 || { echo "$exe ref failed rc=$?"; tail -20 "$out/$exe.raw"; exit 1; }
-    grep -E "^timing|echoed intact|^engine" "$out/$exe.raw" >> "$out/configs0_timing.txt"
-  done
+  run "loop_echo_cpu rep $rep" X=0 $B/loop_echo_cpu --rounds 2000 --tcp-bytes 1048576
+  run "loop_echo_cpu rep $rep, reference udp_echo_server" X=0 $B/loop_echo_cpu --ref-udp-server --udp-only --rounds 2000
+  run "loop_echo coalesce rep $rep" X=0 $B/loop_echo --rounds 2000 --tcp-bytes 1048576
+  run "loop_echo coalesce rep $rep, reference udp_echo_server" X=0 $B/loop_echo --ref-udp-server --udp-only --rounds 2000
+  run "loop_echo no-coalesce rep $rep" NET_CSUM_COALESCE=0 $B/loop_echo --rounds 2000 --tcp-bytes 1048576
+  run "loop_echo coalesce+queue-server rep $rep" NET_CSUM_QUEUE_SERVER=1 $B/loop_echo --rounds 2000 --tcp-bytes 1048576
 done
-rm -f "$out"/*.raw
+rm -f "$out"/run.raw
 timeout -k 10 200 $B/pcap_wire tests/golden > "$out/pcap_wire.raw" 2>&1
 rc=$?
-grep -o "phase [a-z_]*: .*\|pcap netif.*\|^engine.*\|pcap_wire: .*" "$out/pcap_wire.raw" > "$out/pcap_wire_gpu.txt"
+grep -o "phase [a-z_]*: .*\|pcap netif.*\|^engine.*\|^batch sizes.*\|pcap_wire: .*" "$out/pcap_wire.raw" > "$out/pcap_wire_gpu.txt"
 rm -f "$out/pcap_wire.raw"
 exit $rc

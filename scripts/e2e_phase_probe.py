@@ -1,6 +1,6 @@
 """Where the end-to-end host batch loses to a plain H2D copy (configs[1]):
 the copy of the same bytes, the descriptors' own copy, the fixed cost of a
-small call, and one traced call (TCSUM_E2E_TRACE: host-side phase times).
+small call, and one traced call (debug knob e2e_trace: host-side phase times).
 Measurement script, not product code; run it under rocprofv3
 --memory-copy-trace --kernel-trace for the device side."""
 import ctypes
@@ -60,7 +60,7 @@ print(f"host_batch_peso (full)           {dt * 1e3:8.3f} ms  {b.total_bytes / dt
 small = b.descs[:4096]
 dt = timed(lambda: tc.host_batch_peso(host, small), 20)
 print(f"host_batch_peso (4096 segments)  {dt * 1e3:8.3f} ms  (fixed cost of a call)", flush=True)
-os.environ["TCSUM_E2E_TRACE"] = "1"
+tc.debug_set("e2e_trace", 1)
 print("traced full call (host-side phases on stderr):", flush=True)
 tc.host_batch_peso(host, b.descs)
 L.tcsum_host_free(pd)

@@ -37,9 +37,9 @@ print(f"plain H2D copy (one shot)        {b.alloc_bytes / dt / GIB:7.2f} GiB/s",
 
 for mb in (None, 32, 64, 128, 256, 384, 512):
     if mb is None:  # the library's own choice (a quarter of the batch, >= 64 MiB)
-        os.environ.pop("TCSUM_E2E_CHUNK_MB", None)
+        tc.debug_set("e2e_chunk_mb", -1)
     else:
-        os.environ["TCSUM_E2E_CHUNK_MB"] = str(mb)
+        tc.debug_set("e2e_chunk_mb", mb)
     out = tc.host_batch_peso(host, b.descs)
     t0 = time.perf_counter()
     for _ in range(5):

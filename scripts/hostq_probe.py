@@ -40,4 +40,4 @@ for n in sizes:
                   f"  ({b.total_bytes} B)", flush=True)
     ha.free()
 if os.environ.get("TCSUM_PROBE_SERVER") == "1":
-    tc.queue_server(False)  # TCSUM_SERVER_TRACE=1: prints the grid's phase timings
+    tc.queue_server(False)  # debug knob server_trace=1: prints the grid's phase timings

@@ -12,6 +12,7 @@ Layouts (all ~1.5 GB, device-resident):
   ragged     packed, lengths uniform in 64..2936 B (mean 1500)
   small / big / tiny / s200 / j9000 / k16   packed, 576 / 4000 / 64 / 200 / 9000 / 16384 B each
   mixedlen   packed, lengths uniform in 64..9000 B
+  shufNAME   any of the above with the descriptor order permuted (shufsmall, shufragged, ...)
 """
 import os
 import sys
@@ -36,6 +37,9 @@ NAMES = sys.argv[1].split(",") if len(sys.argv) > 1 and "=" not in sys.argv[1] e
 
 
 def layout(name):
+    if name.startswith("shuf") and name != "shuffled":
+        d, span = layout(name[4:])
+        return d[rng.permutation(d.size)], span
     if name in FIXED:
         L = FIXED[name]
         lens = np.full(TOTAL // L, L, np.uint32)

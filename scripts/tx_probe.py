@@ -1,6 +1,6 @@
 """Where does tx fill time go?  Interleaved rounds in one process: ipv4 sums,
 tx fill (stores deferred to k_tx_scatter: the default for this size), tx fill
-with the stores in the kernel (TCSUM_TX_SPLIT=0), tx offload (the same kernel
+with the stores in the kernel (debug knob tx_split=0), tx offload (the same kernel
 without the stores), rx verify.  Both fill forms must leave the same bytes.
 (Round 2 also had a variant re-reading the field lines with the default cache
 policy before the stores: no gain, profiles/r02/tx_probe_rx_fast.txt.)"""
@@ -29,11 +29,8 @@ def tx():
 
 
 def tx_fused():
-    os.environ["TCSUM_TX_SPLIT"] = "0"
-    try:
+    with tc.debug(tx_split=0):
         tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
-    finally:
-        del os.environ["TCSUM_TX_SPLIT"]
 
 
 outo = torch.empty(b.n, dtype=torch.uint32, device="cuda")

@@ -19,7 +19,7 @@ for n in (131072, 1 << 20):
     arena, descs = workload.materialize(b)
     res = {}
     for split in ("0", "1"):
-        os.environ["TCSUM_TX_SPLIT"] = split
+        tc.debug_set("tx_split", int(split))
         for _ in range(3):
             tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
         torch.cuda.synchronize()
@@ -30,7 +30,7 @@ for n in (131072, 1 << 20):
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         res[split] = np.median(ts) * 1e6
-    del os.environ["TCSUM_TX_SPLIT"]
+    tc.debug_set("tx_split", -1)
     print(f"n {n:8d}: fused {res['0']:8.1f} us   deferred {res['1']:8.1f} us per synchronized call", flush=True)
     del arena, descs
     torch.cuda.empty_cache()

@@ -428,6 +428,10 @@ static const struct {
     {"flat", tcsum::KNOB_FLAT},           {"tx_split", tcsum::KNOB_TX_SPLIT},
     {"args_launch", tcsum::KNOB_ARGS_LAUNCH}, {"sync_block", tcsum::KNOB_SYNC_BLOCK},
     {"e2e_trace", tcsum::KNOB_E2E_TRACE}, {"e2e_chunk_mb", tcsum::KNOB_E2E_CHUNK_MB},
+    {"server_max", tcsum::KNOB_SERVER_MAX}, {"server_trace", tcsum::KNOB_SERVER_TRACE},
+    {"server_idle_ms", tcsum::KNOB_SERVER_IDLE_MS}, {"server_wgs", tcsum::KNOB_SERVER_WGS},
+    {"hostq_dma_kb", tcsum::KNOB_HOSTQ_DMA_KB}, {"hostq_dma_keep_mb", tcsum::KNOB_HOSTQ_DMA_KEEP_MB},
+    {"copy_threads", tcsum::KNOB_COPY_THREADS},
 };
 
 static int knob_of(const char *key)
@@ -1101,17 +1105,14 @@ class HostPool {
 };
 
 extern "C++" {
-// Host threads a parallel pass may use: TCSUM_COPY_THREADS (default 16, the
-// box's CPU share), at most the machine's.
+// Host threads a parallel pass may use: 16 (the box's CPU share; debug knob
+// copy_threads), at most the machine's.
 unsigned host_threads()
 {
-    static const unsigned cap = [] {
-        const char *s = getenv("TCSUM_COPY_THREADS");
-        const int v = s ? atoi(s) : 16;
-        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        return std::max(1u, std::min(hw, (unsigned)(v > 0 ? v : 1)));
-    }();
-    return cap;
+    static const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int64_t k = tcsum::knob(tcsum::KNOB_COPY_THREADS);
+    const unsigned v = k > 0 ? (unsigned)std::min<int64_t>(k, 4096) : 16u;
+    return std::max(1u, std::min(hw, v));
 }
 
 // The one pool of the process (every parallel_for instantiation shares it).
@@ -1168,15 +1169,16 @@ constexpr uint64_t kTxWindow = 78;
 
 // ---- queue server (k_server, csum_kernels.hip) ----
 
-int env_int(const char *name, int dflt)
+// a debug knob's value, or the default while it is unset (-1)
+int knob_or(tcsum::Knob k, int dflt)
 {
-    const char *s = getenv(name);
-    return s && *s ? atoi(s) : dflt;
+    const int64_t v = tcsum::knob(k);
+    return v >= 0 ? (int)v : dflt;
 }
 
 // Largest host-queue batch handed to the server (bigger ones are bandwidth
 // work: a launch per batch costs nothing there).
-uint32_t srv_max_packets() { return (uint32_t)env_int("TCSUM_SERVER_MAX", 65536); }
+uint32_t srv_max_packets() { return (uint32_t)knob_or(tcsum::KNOB_SERVER_MAX, 65536); }
 
 int srv_setup(Ctx &c)
 {
@@ -1192,7 +1194,7 @@ int srv_setup(Ctx &c)
         return TCSUM_ERR_MEM;
     }
     memset(c.srv_h, 0, sizeof(tcsum::SrvHost));
-    if (env_int("TCSUM_SERVER_TRACE", 0)) { // phase stamps, printed by srv_stop (measurement only)
+    if (knob_or(tcsum::KNOB_SERVER_TRACE, 0)) { // phase stamps, printed by srv_stop (measurement only)
         uint64_t *t = nullptr, *td = nullptr;
         if (hipHostMalloc(reinterpret_cast<void **>(&t), 256 * 8 * sizeof(uint64_t), hipHostMallocCoherent) ==
                 hipSuccess &&
@@ -1234,8 +1236,8 @@ void reap_at_exit();
 int srv_launch(Ctx &c, uint32_t last)
 {
     reap_at_exit();
-    const uint64_t idle_ticks = 100000ull * (uint64_t)std::max(1, env_int("TCSUM_SERVER_IDLE_MS", 10)); // 100 MHz
-    if (tcsum::launch_server(c.srv_hd, c.srv_d, last, idle_ticks, std::max(1, env_int("TCSUM_SERVER_WGS", 64)),
+    const uint64_t idle_ticks = 100000ull * (uint64_t)std::max(1, knob_or(tcsum::KNOB_SERVER_IDLE_MS, 10)); // 100 MHz
+    if (tcsum::launch_server(c.srv_hd, c.srv_d, last, idle_ticks, std::max(1, knob_or(tcsum::KNOB_SERVER_WGS, 64)),
                              c.srv_stream) != hipSuccess)
         return TCSUM_ERR_SYS;
     c.srv_running = true;
@@ -1351,7 +1353,7 @@ int cs_setup(Ctx &c)
 void cs_launch(Ctx &c, uint32_t last)
 {
     reap_at_exit();
-    const uint64_t idle_ticks = 100000ull * (uint64_t)std::max(1, env_int("TCSUM_SERVER_IDLE_MS", 10)); // 100 MHz
+    const uint64_t idle_ticks = 100000ull * (uint64_t)std::max(1, knob_or(tcsum::KNOB_SERVER_IDLE_MS, 10)); // 100 MHz
     const hipError_t e = tcsum::launch_call_server(c.cs_hd, c.cs_stage_d, last, idle_ticks, c.cs_stream);
     if (e != hipSuccess)
         die("call server launch", e);
@@ -1621,7 +1623,7 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     // pinned memory by the host threads just before its copy (the staging of
     // piece k+1 overlaps the copy of piece k) instead of being read in place
     // from the staging by the kernel.
-    const uint64_t dma_min = (uint64_t)env_int("TCSUM_HOSTQ_DMA_KB", 256 << 10) << 10;
+    const uint64_t dma_min = (uint64_t)knob_or(tcsum::KNOB_HOSTQ_DMA_KB, 256 << 10) << 10;
     const uint64_t alo = lo & ~uint64_t(15), ahi = std::min<uint64_t>(arena_bytes, (hi + 15) & ~uint64_t(15));
     // A tx fill takes it too: the packets are read from the HBM copy and the
     // fields stored straight into the frames in host memory (or the staging)
@@ -1701,7 +1703,7 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
         // the HBM copy of the span is cached for the next batch only up to
         // TCSUM_HOSTQ_DMA_KEEP_MB (default 256): a one-off multi-GiB verify
         // does not keep its span allocated for the life of the process
-        if (c.d_arena_cap > ((size_t)env_int("TCSUM_HOSTQ_DMA_KEEP_MB", 256) << 20)) {
+        if (c.d_arena_cap > ((size_t)knob_or(tcsum::KNOB_HOSTQ_DMA_KEEP_MB, 256) << 20)) {
             (void)hipFree(c.d_arena);
             c.d_arena = nullptr;
             c.d_arena_cap = 0;

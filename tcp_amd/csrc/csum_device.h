@@ -838,16 +838,25 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
         if (pass + 1u < npass)
             __syncthreads(); // the next pass overwrites dat / ex / subtot
     }
-    if (ranges) { // G lanes per range: the widest power of two that gives every range a group
-        const uint32_t lanes_per = T / kw;
-        if (lanes_per >= 64)
-            pk_ranges<MODE, 64>(arena, descs, out, aux, first, kw, T);
-        else if (lanes_per >= 32)
-            pk_ranges<MODE, 32, 3>(arena, descs, out, aux, first, kw, T);
-        else if (lanes_per >= 16)
-            pk_ranges<MODE, 16>(arena, descs, out, aux, first, kw, T);
+    if (ranges) {
+        // G lanes x UL loads per range, so that one pass covers a range of the
+        // mean length K implies (K ranges fill one 12-KiB pass: K = 8 at 1500
+        // B) -- the per-range kernel's load depth (k_segments<16,6> at 1500
+        // B); groups past kw idle (their waves leave at once).  The widest-
+        // group form (32 lanes x 3 loads at 1500 B: half the loads in flight
+        // per wave) ran shuffled 1500-B batches 1.12x slower than
+        // k_segments<16,6> (profiles/r03/packed/ab_pk_layouts_default.txt).
+        static_assert(CH == 768 && T == 256, "thresholds for the 4-wave x 3-load pass");
+        if (kw <= 4)
+            pk_ranges<MODE, 64, 4>(arena, descs, out, aux, first, kw, T); // >= 3 KiB: 4 KiB per pass
+        else if (kw <= 7)
+            pk_ranges<MODE, 32, 6>(arena, descs, out, aux, first, kw, T); // 1.5-2.4 KiB: 3 KiB
+        else if (kw <= 16)
+            pk_ranges<MODE, 16, 6>(arena, descs, out, aux, first, kw, T); // 0.77-1.5 KiB: 1.5 KiB
+        else if (kw <= 32)
+            pk_ranges<MODE, 8, 6>(arena, descs, out, aux, first, kw, T); // 384-722 B: 768 B
         else
-            pk_ranges<MODE, 8>(arena, descs, out, aux, first, kw, T);
+            pk_ranges<MODE, 4, 4>(arena, descs, out, aux, first, kw, T); // < 372 B: 256 B, 1-4 rounds
         return;
     }
     if (mine)

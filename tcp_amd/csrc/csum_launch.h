@@ -38,6 +38,13 @@ enum Knob : int {
     KNOB_SYNC_BLOCK, // 1: drop-in calls block in hipStreamSynchronize instead of spinning
     KNOB_E2E_TRACE,  // 1: tcsum_host_batch_peso prints phase stamps
     KNOB_E2E_CHUNK_MB, // tcsum_host_batch_peso chunk size
+    KNOB_SERVER_MAX,   // largest host-queue batch handed to the queue server (65536)
+    KNOB_SERVER_TRACE, // 1: the queue server prints its phase stamps when stopped
+    KNOB_SERVER_IDLE_MS, // resident servers stop after this long without a job (10)
+    KNOB_SERVER_WGS,   // queue server workgroups (64)
+    KNOB_HOSTQ_DMA_KB, // host-queue batches from this span on go through the copy engine (262144)
+    KNOB_HOSTQ_DMA_KEEP_MB, // device arena kept between host-queue calls up to this size (256)
+    KNOB_COPY_THREADS, // host threads of a parallel gather / scatter pass (16)
     KNOB_COUNT
 };
 int64_t knob(Knob k);

@@ -19,3 +19,19 @@ def oracle():
 
     pyoracle.build()
     return pyoracle
+
+
+@pytest.fixture
+def dbg():
+    """Set libtcsum debug knobs (include/tcsum_debug.h) for one test:
+    dbg(server_idle_ms=50, ...); every knob it touched is unset after."""
+    import tcp_amd
+    touched = []
+
+    def set_(**kv):
+        for k, v in kv.items():
+            tcp_amd.debug_set(k, int(v))
+            touched.append(k)
+    yield set_
+    for k in touched:
+        tcp_amd.debug_set(k, -1)

@@ -108,6 +108,15 @@ def test_environment_does_not_route(libpath):
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr
 
 
+def test_product_reads_only_deployment_variables(libpath):
+    """The only environment names in libtcsum.so are the two deployment
+    choices a drop-in stack cannot make in code (device, call server); every
+    tuning and route is a debug knob (include/tcsum_debug.h)."""
+    import re
+    names = set(re.findall(rb"TCSUM_[A-Z_0-9]+", open(libpath, "rb").read()))
+    assert names <= {b"TCSUM_DEVICE", b"TCSUM_CALL_SERVER"}, names
+
+
 def test_debug_knobs(libpath):
     import tcp_amd as tc
     assert tc.debug_get("lanes") == -1 and tc.debug_get("no_such_knob") == -2

@@ -19,8 +19,8 @@ tc = P.tc
 
 
 @pytest.fixture
-def served(tc, monkeypatch):
-    monkeypatch.setenv("TCSUM_SERVER_IDLE_MS", "50")
+def served(tc, dbg):
+    dbg(server_idle_ms="50")
     tc.call_server(True)
     yield
     tc.call_server(False)
@@ -42,9 +42,9 @@ def test_served_checksum_peso_golden(tc, served):
     P.test_checksum_peso_golden(tc)
 
 
-def test_served_idle_out_and_relaunch(tc, monkeypatch):
+def test_served_idle_out_and_relaunch(tc, dbg):
     """The wave leaves after 2 ms without a call; the next call relaunches it."""
-    monkeypatch.setenv("TCSUM_SERVER_IDLE_MS", "2")
+    dbg(server_idle_ms="2")
     tc.call_server(True)
     try:
         hdr = bytes.fromhex("450000730000400040110000c0a80001c0a800c7")

@@ -204,7 +204,7 @@ def test_host_multi_device_golden(tc, oracle, devices, where, shift):
 
 
 @pytest.mark.parametrize("where", ["pinned", "pageable"])
-def test_host_tx_fill_copy_engine_path(tc, oracle, monkeypatch, where):
+def test_host_tx_fill_copy_engine_path(tc, oracle, dbg, where):
     """A large tx fill in offset order through the copy engine: packets read
     from their HBM copy, the fields stored into the frames in host memory (or
     the pageable batch's staging) by k_tx_scatter -- every byte equals the
@@ -218,7 +218,7 @@ def test_host_tx_fill_copy_engine_path(tc, oracle, monkeypatch, where):
     ha = tc.HostArena(unfilled.size) if where == "pinned" else None
     try:
         for dma_kb in ("1", "0"):  # copy-engine path, then the in-place one
-            monkeypatch.setenv("TCSUM_HOSTQ_DMA_KB", dma_kb)
+            dbg(hostq_dma_kb=dma_kb)
             if ha is not None:
                 ha.array[:] = unfilled
                 arg, host = ha, ha.array
@@ -235,14 +235,14 @@ def test_host_tx_fill_copy_engine_path(tc, oracle, monkeypatch, where):
 
 @pytest.mark.parametrize("where", ["pinned", "pageable"])
 @pytest.mark.parametrize("mode", ["sums", "rx"])
-def test_host_pinned_copy_engine_path(tc, oracle, monkeypatch, mode, where):
+def test_host_pinned_copy_engine_path(tc, oracle, dbg, mode, where):
     """Large read-only batches in offset order go through the copy engine into
     HBM in pieces growing from 64 MiB (pageable ones staged piece by piece into
     pinned memory first; TCSUM_HOSTQ_DMA_KB lowered so a test-sized batch
     takes that path): same results as the in-place path and as the oracle;
     the reference's fixtures too."""
     from tcp_amd import workload
-    monkeypatch.setenv("TCSUM_HOSTQ_DMA_KB", "1")
+    dbg(hostq_dma_kb="1")
     cases, pool = G.ipv4_rx_cases() if mode == "rx" else G.ipv4_cases()
     arg, view, keep = host_copy(tc, pool, where, 5)
     pk = G.pkt_descs(cases, tc.PKT_DTYPE)
@@ -267,14 +267,14 @@ def test_host_pinned_copy_engine_path(tc, oracle, monkeypatch, mode, where):
             arg = host
         if mode == "rx":
             v_dma, o_dma, f_dma = tc.host_batch_ipv4_rx_verify(arg, b.descs)
-            monkeypatch.setenv("TCSUM_HOSTQ_DMA_KB", "0")
+            dbg(hostq_dma_kb="0")
             v_in, o_in, f_in = tc.host_batch_ipv4_rx_verify(arg, b.descs)
             ev, ef = oracle.batch_ipv4_rx_verify(host, b.descs, nthreads=8)
             np.testing.assert_array_equal(v_dma, ev)
             np.testing.assert_array_equal(v_dma, v_in)
         else:
             o_dma, f_dma = tc.host_batch_ipv4(arg, b.descs)
-            monkeypatch.setenv("TCSUM_HOSTQ_DMA_KB", "0")
+            dbg(hostq_dma_kb="0")
             o_in, f_in = tc.host_batch_ipv4(arg, b.descs)
             eo, ef = oracle.batch_ipv4(host, b.descs, nthreads=8)
             np.testing.assert_array_equal(o_dma, eo)
@@ -287,12 +287,12 @@ def test_host_pinned_copy_engine_path(tc, oracle, monkeypatch, mode, where):
 
 
 @pytest.mark.parametrize("mode", ["sums", "rx"])
-def test_host_sparse_batch_and_release(tc, oracle, mode, monkeypatch):
+def test_host_sparse_batch_and_release(tc, oracle, mode, dbg):
     """A few frames spread over a large pinned pool (the packets cover far
     less than 3/4 of their span): the copy-engine path is not taken (it would
     move the whole span), results equal the oracle; tcsum_release frees the
     cached buffers and the next call allocates them again."""
-    monkeypatch.setenv("TCSUM_HOSTQ_DMA_KB", "1")
+    dbg(hostq_dma_kb="1")
     cases, pool = G.ipv4_rx_cases()
     take = cases[:64]
     stride = 1 << 20  # one frame per MiB: 64 frames over a 64 MiB pool
@@ -334,7 +334,7 @@ def _semi_valid_ipv4(rng, arena, offs, lens):
 
 
 @pytest.mark.parametrize("seed", range(32))
-def test_host_paths_fuzz(tc, oracle, monkeypatch, seed):
+def test_host_paths_fuzz(tc, oracle, dbg, seed):
     """Seeded fuzz over the host-memory batch paths: sizes from one frame to
     tens of thousands, packed / gapped / shuffled / sparse layouts, pinned /
     registered / pageable memory, the copy-engine threshold off, forced or
@@ -344,8 +344,8 @@ def test_host_paths_fuzz(tc, oracle, monkeypatch, seed):
     n = int(rng.choice([1, 7, 50, 1000, 20000, 60000]))
     layout = rng.choice(["packed", "gaps", "shuffled", "sparse"])
     where = str(rng.choice(["pinned", "registered", "pageable"]))
-    monkeypatch.setenv("TCSUM_HOSTQ_DMA_KB", str(rng.choice(["0", "1", "262144"])))
-    monkeypatch.setenv("TCSUM_E2E_CHUNK_MB", str(rng.choice(["1", "8", "64"])))
+    dbg(hostq_dma_kb=str(rng.choice(["0", "1", "262144"])))
+    dbg(e2e_chunk_mb=str(rng.choice(["1", "8", "64"])))
     lens = rng.integers(0, 3000, n) if rng.random() < 0.5 else rng.integers(20, 9001, n)
     gap = {"gaps": rng.integers(0, 64, n),
            "sparse": rng.integers(0, (1 << 16) if n <= 1000 else 4096, n)}.get(layout, np.zeros(n, np.int64))

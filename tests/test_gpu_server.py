@@ -26,10 +26,10 @@ def tc():
 
 
 @pytest.fixture
-def server(tc, monkeypatch):
+def server(tc, dbg):
     def start(wgs=64, idle_ms=10):
-        monkeypatch.setenv("TCSUM_SERVER_WGS", str(wgs))
-        monkeypatch.setenv("TCSUM_SERVER_IDLE_MS", str(idle_ms))
+        dbg(server_wgs=str(wgs))
+        dbg(server_idle_ms=str(idle_ms))
         tc.queue_server(True)
     yield start
     tc.queue_server(False)

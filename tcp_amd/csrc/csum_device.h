@@ -1440,7 +1440,12 @@ __global__ __launch_bounds__(W * 64) void k_flat_ipv4(uint8_t *__restrict__ aren
 {
     static_assert(2 * W <= 32, "the sub-range totals are scanned by 32 lanes");
     constexpr uint32_t T = W * 64u, CH = T * U, SR = 32u * U, WB = 16u * CH;
-    __shared__ u32x4 dat[CH];   // the window's chunks (headers, boundary bytes)
+    // the window's chunks (headers, boundary bytes), then kHalo chunks past
+    // its end (the headers of packets that start in its last bytes), then the
+    // straddler's first kHalo chunks: every chunk a packet's parse reads is
+    // one LDS read (max. chunk 5: s0 + IHL*4 + the L4 field's 2 bytes <= 92)
+    constexpr uint32_t kHalo = 6;
+    __shared__ u32x4 dat[CH + 2 * kHalo];
     __shared__ uint32_t ex[CH]; // per chunk: its sub-range's word sum before it; slot 0 of a sub-range: its total
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
@@ -1463,13 +1468,21 @@ __global__ __launch_bounds__(W * 64) void k_flat_ipv4(uint8_t *__restrict__ aren
     // bytes belong to no packet)
     const int64_t rel0 = (int64_t)(wlo - a0); // from the arena pointer: global_load, not flat_load
     const u32x4 *wbase = reinterpret_cast<const u32x4 *>(arena + rel0);
-    const uint32_t nchw = send - wlo >= WB ? CH : (uint32_t)((send - wlo + 15u) >> 4);
+    const uint64_t nchx = (send - wlo + 15u) >> 4; // chunks to the stream's end
+    const uint32_t nchw = nchx >= CH ? CH : (uint32_t)nchx;
     const uint32_t sub = t >> 5, l = t & 31u, hf = (t >> 5) & 1u;
     u32x4 v[U];
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
         const uint32_t c = sub * SR + u * 32u + l;
         v[u] = load16<true>(wbase + (c < nchw ? c : nchw - 1u));
+    }
+    // the halo: wave 0's first lanes, default policy (the next window's
+    // workgroup streams the same line at about the same time, on the same XCD)
+    u32x4 hv = u32x4(0u);
+    if (wv == 0 && lane < kHalo) {
+        const uint64_t c = CH + lane;
+        hv = load16<false>(wbase + (c < nchx ? c : nchx - 1u));
     }
     issue_fence();
     if constexpr (PROBE == 1) {
@@ -1540,6 +1553,11 @@ __global__ __launch_bounds__(W * 64) void k_flat_ipv4(uint8_t *__restrict__ aren
         if (l == 0)
             ex[sub * SR] = a; // the sub-range's total (its first chunk's prefix is 0)
     }
+    if (wv == 0 && lane < 2u * kHalo) { // the halo and the straddler's chunks
+        const uint32_t k = lane >= kHalo ? lane - kHalo : lane;
+        const u32x4 sk = k == 0 ? sh0 : k == 1 ? sh1 : k == 2 ? sh2 : k == 3 ? sh3 : k == 4 ? sh4 : sh5;
+        dat[CH + lane] = lane < kHalo ? hv : sk;
+    }
     __syncthreads();
     if constexpr (PROBE == 2) {
         if (ex[(t * 37u) % CH] == 0x9E3779B9u && dv0.x == 1u)
@@ -1587,18 +1605,11 @@ __global__ __launch_bounds__(W * 64) void k_flat_ipv4(uint8_t *__restrict__ aren
         const uint32_t s0 = (uint32_t)(s & 15u);
         const uint64_t hc = s >> 4; // the packet's first chunk (absolute)
         const uint32_t nchp = big_enough ? (frame_ld + s0 + 15u) >> 4 : 0u; // the packet's chunks
-        // chunk k of the packet: from the window's LDS copy, the straddler's
-        // prefetched header, else from memory
+        // chunk k (< kHalo) of the packet: an owner's from the window's copy
+        // (and the halo), the straddler's from its prefetched header
+        const uint32_t hb = straddler ? CH + kHalo : owner ? (uint32_t)(hc - (wlo >> 4)) : 0u;
         auto fetch = [=](uint32_t k) -> u32x4 {
-            if (!part_of || k >= nchp)
-                return u32x4(0u);
-            if (straddler && k < 6u)
-                return k == 0 ? sh0 : k == 1 ? sh1 : k == 2 ? sh2 : k == 3 ? sh3 : k == 4 ? sh4 : sh5;
-            const uint64_t g = hc + k;
-            const uint64_t rel = g - (wlo >> 4);
-            if (rel < CH)
-                return dat[rel];
-            return load16<false>(reinterpret_cast<const u32x4 *>(arena + (int64_t)((g << 4) - a0)));
+            return part_of && k < nchp ? dat[hb + k] : u32x4(0u);
         };
         const u32x4 h0 = fetch(0), h1 = fetch(1);
         const u32x4 h2 = s0 > 12 ? fetch(2) : u32x4(0u);

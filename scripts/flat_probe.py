@@ -4,7 +4,12 @@ interleaved rounds, median us per launch): the product's per-packet kernel
 (tcsum_probe_flat: 1 = plan + window loads, 2 = + LDS prefix scans, 3 = all
 but the cross-window combine, 0 = the full stream's sums).
 
-  python scripts/flat_probe.py [config] [shapes, e.g. 4x3,16x4]
+  python scripts/flat_probe.py [config] [shapes, e.g. 4x3,16x4] [variants, e.g. 0,1] [extra]
+
+extra: also the packet-agnostic ceiling on the same arena (its bytes cut into
+64-KiB checksum_peso ranges: the TSO kernel, k_segments_wgx<16,32,4>), the
+product's tile-shaped read probes, and k_ipv4 in its other compiled shapes
+(debug lanes x loads).
 """
 import os
 import sys
@@ -18,6 +23,8 @@ from tcp_amd import _lib, workload  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "mixed"
 shapes = [tuple(map(int, s.split("x"))) for s in (sys.argv[2] if len(sys.argv) > 2 else "4x3,8x3,8x4,16x4,16x2").split(",")]
+variants = [int(v) for v in (sys.argv[3] if len(sys.argv) > 3 else "0,1,2,3").split(",")]
+extra = len(sys.argv) > 4 and sys.argv[4] == "extra"
 b = workload.make_batch(cfg)
 arena, descs = workload.materialize(b)
 n = b.n
@@ -49,10 +56,30 @@ def probe(variant, w, u):
 kinds = {"k_ipv4 (product default)": product, "flat 4x3 (product, knob)": product_flat,
          "plain read probe": lambda: tc.probe_read(arena, b.arena_bytes, sink)}
 for w, u in shapes:
-    for v in (0, 1, 2, 3):
+    for v in variants:
         kinds[f"flat {w}x{u} v{v}"] = probe(v, w, u)
+if extra:
+    from tcp_amd.csum import PESO_DTYPE
+    L64 = 65536
+    n64 = b.arena_bytes // L64
+    p64 = np.zeros(n64, PESO_DTYPE)
+    p64["offset"] = np.arange(n64, dtype=np.uint64) * np.uint64(L64)
+    p64["len"] = L64
+    p64["protocol"] = 6
+    d64 = tc.descs_to_device(p64)
+    o64 = torch.empty(n64, dtype=torch.uint16, device="cuda")
+    kinds["64-KiB ranges (wgx<16,32,4>)"] = lambda: tc.batch_peso(arena, d64, n64, n64 * L64, out=o64)
+    for g, u, dep in ((32, 4, True), (32, 6, True), (64, 4, False), (256, 4, False)):
+        kinds[f"tile {g}x{u}{' dep' if dep else ''}"] = (
+            lambda g=g, u=u, dep=dep: tc.probe_tile(arena, b.arena_bytes, g, u, sink, dep=dep))
+    for g, u in ((64, 4), (16, 8), (64, 16)):
+        def shaped(g=g, u=u):
+            with tc.debug(lanes=g, loads=u):
+                tc.batch_ipv4(arena, descs, n, b.total_bytes, out=out, want_flags=False)
+        kinds[f"k_ipv4 {g}x{u} (knob)"] = shaped
 # the variants that compute real sums must equal the product's
-for name in ["flat 4x3 (product, knob)"] + [f"flat {w}x{u} v0" for w, u in shapes]:
+for name in ["flat 4x3 (product, knob)"] + [f"flat {w}x{u} v0" for w, u in shapes if 0 in variants] + \
+        [k for k in kinds if k.startswith("k_ipv4 ") and "knob" in k]:
     out.zero_()
     kinds[name]()
     torch.cuda.synchronize()

@@ -671,18 +671,15 @@ __device__ __forceinline__ void desc_span(const void *__restrict__ descs, uint32
 }
 
 // The per-range path for a workgroup whose ranges are not one region:
-// groups of G lanes x UL loads, range t / G first (its descriptor `d0`,
-// loaded by the caller), then every T / G-th.
-template <int MODE, int G, int UL>
+// groups of G lanes, G the widest power of two with one group per range.
+template <int MODE, int G, int UL = 4>
 __device__ __forceinline__ void pk_ranges(const uint8_t *__restrict__ arena, const void *__restrict__ descs,
                                           uint16_t *__restrict__ out, uint32_t aux, uint32_t first, uint32_t kw,
-                                          uint32_t T, SegDesc d0)
+                                          uint32_t T)
 {
     const uint32_t t = threadIdx.x, gl = t & (G - 1u);
-    SegDesc e = d0;
     for (uint32_t r = t / G; r < kw; r += T / G) {
-        if (r != t / G)
-            e = load_desc<MODE>(descs, first + r, true);
+        const SegDesc e = load_desc<MODE>(descs, first + r, true);
         uint32_t q = 0;
         uint32_t acc = sum_range<G, UL, false>(arena, e.off, e.len, gl, [&] {
             if constexpr (MODE == MODE_PESO)
@@ -691,29 +688,6 @@ __device__ __forceinline__ void pk_ranges(const uint8_t *__restrict__ arena, con
         acc = group_sum<G>(acc);
         if (gl == 0)
             out[first + r] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + e.off), e, aux, q);
-    }
-}
-
-// G lanes per range for a workgroup of kw ranges: the widest power of two
-// that gives every range a group (1500 B: K = 8, 32 lanes x 3 loads, one
-// pass).  The per-range kernel's deeper 6-load groups did not fit beside the
-// stream's registers (spills at 64 VGPRs).
-__device__ __forceinline__ uint32_t pk_group(uint32_t kw)
-{
-    return kw <= 4 ? 64u : kw <= 8 ? 32u : kw <= 16 ? 16u : kw <= 32 ? 8u : 4u;
-}
-
-template <int MODE>
-__device__ __forceinline__ void pk_ranges_any(const uint8_t *__restrict__ arena, const void *__restrict__ descs,
-                                              uint16_t *__restrict__ out, uint32_t aux, uint32_t first, uint32_t kw,
-                                              uint32_t T, SegDesc d0)
-{
-    switch (pk_group(kw)) { // workgroup-uniform
-    case 64: pk_ranges<MODE, 64, 4>(arena, descs, out, aux, first, kw, T, d0); break;
-    case 32: pk_ranges<MODE, 32, 3>(arena, descs, out, aux, first, kw, T, d0); break;
-    case 16: pk_ranges<MODE, 16, 4>(arena, descs, out, aux, first, kw, T, d0); break;
-    case 8: pk_ranges<MODE, 8, 4>(arena, descs, out, aux, first, kw, T, d0); break;
-    default: pk_ranges<MODE, 4, 4>(arena, descs, out, aux, first, kw, T, d0); break; // 33..256 ranges: up to 4 rounds
     }
 }
 
@@ -742,14 +716,6 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     // (fetching the two descriptors with vector loads instead cut the read
     // traffic from 1.0165x to 1.0018x the algorithmic bytes but ran 11 %
     // slower, profiles/r03/packed/ab_vdesc_w8.txt)
-    // the range-by-range path's first descriptor, loaded beside the two
-    // scalar ones that decide between the paths: a batch not in arena order
-    // then waits on one descriptor latency, as the per-range kernel does
-    // (loaded after the decision it ran shuffled 1500-B batches 1.17x slower
-    // than k_segments<16,6>, profiles/r04/packed/)
-    static_assert(T == 256, "pk_group's thresholds are for 256-thread workgroups");
-    const uint32_t rg = t / pk_group(kw);
-    const SegDesc fd = load_desc<MODE>(descs, first + (rg < kw ? rg : 0u), true);
     desc_span<MODE>(descs, first, r0, len0);
     desc_span<MODE>(descs, first + kw - 1u, offl, lenl);
     const uint64_t rend = offl + lenl;
@@ -760,12 +726,7 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     // safe to load before the ranges are known to lie inside it
     const bool span_ok = len0 != 0 && lenl != 0 && rend > r0 &&
                          rend - r0 <= (uint64_t)kPkMaxPasses * CH * 16u - s0;
-    if (!span_ok) { // workgroup-uniform: not one region, sum range by range
-        if constexpr (!PROBE) // (the probe's `out` is a one-word sink)
-            pk_ranges_any<MODE>(arena, descs, out, aux, first, kw, T, fd);
-        return;
-    }
-    bool ranges = false; // a range outside the region (found after the first pass)
+    bool ranges = !span_ok; // workgroup-uniform: sum range by range instead
     const uint32_t span = span_ok ? (uint32_t)(rend - r0) : 0u;
     const uint32_t nch = span_ok ? (s0 + span + 15u) >> 4 : 0u;
     const uint32_t npass = (nch + CH - 1u) / CH;
@@ -877,9 +838,16 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
         if (pass + 1u < npass)
             __syncthreads(); // the next pass overwrites dat / ex / subtot
     }
-    if (ranges) { // the rare late case: reload the first descriptors
-        const SegDesc d0 = load_desc<MODE>(descs, first + (rg < kw ? rg : 0u), true);
-        pk_ranges_any<MODE>(arena, descs, out, aux, first, kw, T, d0);
+    if (ranges) { // G lanes per range: the widest power of two that gives every range a group
+        const uint32_t lanes_per = T / kw;
+        if (lanes_per >= 64)
+            pk_ranges<MODE, 64>(arena, descs, out, aux, first, kw, T);
+        else if (lanes_per >= 32)
+            pk_ranges<MODE, 32, 3>(arena, descs, out, aux, first, kw, T);
+        else if (lanes_per >= 16)
+            pk_ranges<MODE, 16>(arena, descs, out, aux, first, kw, T);
+        else
+            pk_ranges<MODE, 8>(arena, descs, out, aux, first, kw, T);
         return;
     }
     if (mine)

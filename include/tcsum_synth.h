@@ -95,6 +95,12 @@ int tcsum_probe_flat(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev
  * in-stream (each window's workgroup writes its packets' fields after its
  * loads), 1 = deferred (the plain read, then one dense scatter of side's
  * values).  The fields are left junk. */
+/* tcsum_batch_ipv4's sums (out[i] as it stores them) by k_ipv4<32, 6> in
+ * wg = 256 / 512 / 1024-thread workgroups, or (occ8 = 1, wg = 256) held to
+ * 64 VGPRs: launch forms the route does not take, for measurement. */
+int tcsum_probe_ipv4_shape(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n, int wg, int occ8,
+                           uint32_t *out /*[dev]*/, void *stream);
+
 uint32_t tcsum_probe_txfloor_windows(uint64_t nbytes);
 int tcsum_probe_txfloor_prepare(const void *arena /*[dev]*/, uint64_t nbytes, const tcsum_pkt_t *pkts /*[dev]*/,
                                 uint32_t n, uint64_t total_bytes_hint, uint32_t *side /*[dev]*/, uint64_t side_words,

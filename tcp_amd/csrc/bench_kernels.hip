@@ -620,6 +620,34 @@ static hipError_t launch_probe_flat(uint8_t *arena, const tcsum_pkt_t *pkts, uin
     return hipErrorInvalidValue;
 }
 
+// k_ipv4's sums kernel in other launch forms (measurement): 32 lanes x 6
+// loads as the route, in 256- / 512- / 1024-thread workgroups, or held to 64
+// VGPRs (k_ipv4_o8: 8 waves per SIMD; the route's build takes 66, i.e. 7)
+static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n, int wg, int occ8,
+                                    uint32_t *out, hipStream_t stream)
+{
+    if (n == 0)
+        return hipSuccess;
+    const uint32_t xg = (uint32_t)route(1500).xcd;
+    const uint32_t per = (uint32_t)wg / 32u;
+    const dim3 grid((n + per - 1u) / per);
+    if (occ8 && wg == 256)
+        hipLaunchKernelGGL((k_ipv4_o8<32, 6, IP_SUMS>), grid, dim3(256), 0, stream, arena, pkts, n, out,
+                           (uint8_t *)nullptr, (int8_t *)nullptr, 0u, xg);
+    else if (!occ8 && wg == 256)
+        hipLaunchKernelGGL((k_ipv4<32, 6, IP_SUMS, 256>), grid, dim3(256), 0, stream, arena, pkts, n, out,
+                           (uint8_t *)nullptr, (int8_t *)nullptr, 0u, xg);
+    else if (!occ8 && wg == 512)
+        hipLaunchKernelGGL((k_ipv4<32, 6, IP_SUMS, 512>), grid, dim3(512), 0, stream, arena, pkts, n, out,
+                           (uint8_t *)nullptr, (int8_t *)nullptr, 0u, xg);
+    else if (!occ8 && wg == 1024)
+        hipLaunchKernelGGL((k_ipv4<32, 6, IP_SUMS, 1024>), grid, dim3(1024), 0, stream, arena, pkts, n, out,
+                           (uint8_t *)nullptr, (int8_t *)nullptr, 0u, xg);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 } // namespace tcsum
 
 // ===================================================================== ABI
@@ -704,6 +732,15 @@ int tcsum_probe_txfloor(void *arena, uint64_t nbytes, const uint64_t *fpos, cons
         return TCSUM_ERR_PARAM;
     return rc_of(tcsum::launch_floor(arena, nbytes, fpos, side, n, ffirst, variant, sink,
                                      static_cast<hipStream_t>(stream)));
+}
+
+int tcsum_probe_ipv4_shape(void *arena, const tcsum_pkt_t *pkts, uint32_t n, int wg, int occ8, uint32_t *out,
+                           void *stream)
+{
+    if (!arena || !pkts || !out)
+        return TCSUM_ERR_PARAM;
+    return rc_of(tcsum::launch_ipv4_shape(static_cast<uint8_t *>(arena), pkts, n, wg, occ8, out,
+                                          static_cast<hipStream_t>(stream)));
 }
 
 int tcsum_probe_tile(const void *p, uint64_t nbytes, int lanes, int loads, int dep, uint32_t *sink, void *stream)

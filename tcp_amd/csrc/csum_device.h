@@ -1274,6 +1274,17 @@ __global__ __launch_bounds__(T) void k_ipv4(uint8_t *__restrict__ arena, const t
                            opts); // no 32-bit wrap for any n
 }
 
+// k_ipv4 held to 64 VGPRs (8 waves per SIMD; the sums form takes 66, i.e. 7):
+// measurement (libtcsum_bench.so, tcsum_probe_ipv4_shape)
+template <int G, int U, int IPM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_ipv4_o8(
+    uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts, uint32_t n, uint32_t *__restrict__ out,
+    uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out, uint32_t opts, uint32_t xg)
+{
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    ipv4_packet<G, U, IPM>(arena, pkts, blk * (256u / G) + threadIdx.x / G, n, out, flags_out, verdict_out, opts);
+}
+
 // The deferred tx stores (IP_OPT_DEFER): one lane per packet writes the values
 // k_ipv4 left in `csums` at the positions it left in `pos` (bit 16: the IPv4
 // header field; low 16 bits: the L4 field's offset, 0 for none).  All the

@@ -95,11 +95,13 @@ int tcsum_probe_flat(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev
  * in-stream (each window's workgroup writes its packets' fields after its
  * loads), 1 = deferred (the plain read, then one dense scatter of side's
  * values).  The fields are left junk. */
-/* tcsum_batch_ipv4's sums (out[i] as it stores them) by k_ipv4<32, 6> in
- * wg = 256 / 512 / 1024-thread workgroups, or (occ8 = 1, wg = 256) held to
- * 64 VGPRs: launch forms the route does not take, for measurement. */
-int tcsum_probe_ipv4_shape(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n, int wg, int occ8,
-                           uint32_t *out /*[dev]*/, void *stream);
+/* An IPv4 batch in launch forms the route does not take (measurement): mode 0
+ * = tcsum_batch_ipv4's sums by k_ipv4<32, 6> (out), mode 2 = rx verify by
+ * k_ipv4<16, 6> (verdict, and the sums into out), in wg = 256 / 512 / 1024
+ * thread workgroups (rx: 256 / 1024), or with wg = 256 held to occ waves per
+ * SIMD (sums: 8; rx: 7 or 8; 0 = as built).  Others: TCSUM_ERR_PARAM. */
+int tcsum_probe_ipv4_shape(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n, int mode, int wg,
+                           int occ, uint32_t *out /*[dev]*/, int8_t *verdict /*[dev] or NULL*/, void *stream);
 
 uint32_t tcsum_probe_txfloor_windows(uint64_t nbytes);
 int tcsum_probe_txfloor_prepare(const void *arena /*[dev]*/, uint64_t nbytes, const tcsum_pkt_t *pkts /*[dev]*/,

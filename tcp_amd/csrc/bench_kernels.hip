@@ -620,32 +620,37 @@ static hipError_t launch_probe_flat(uint8_t *arena, const tcsum_pkt_t *pkts, uin
     return hipErrorInvalidValue;
 }
 
-// k_ipv4's sums kernel in other launch forms (measurement): 32 lanes x 6
-// loads as the route, in 256- / 512- / 1024-thread workgroups, or held to 64
-// VGPRs (k_ipv4_o8: 8 waves per SIMD; the route's build takes 66, i.e. 7)
-static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n, int wg, int occ8,
-                                    uint32_t *out, hipStream_t stream)
+// k_ipv4 in other launch forms (measurement): the route's shape for the mode
+// (sums 32 x 6, rx 16 x 6) in 256- / 512- / 1024-thread workgroups, or held to
+// `occ` waves per SIMD (the route's builds: sums 66 VGPRs = 7 waves, rx 74 = 6)
+static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n, int mode, int wg, int occ,
+                                    uint32_t *out, int8_t *verdict, hipStream_t stream)
 {
     if (n == 0)
         return hipSuccess;
     const uint32_t xg = (uint32_t)route(1500).xcd;
-    const uint32_t per = (uint32_t)wg / 32u;
-    const dim3 grid((n + per - 1u) / per);
-    if (occ8 && wg == 256)
-        hipLaunchKernelGGL((k_ipv4_o8<32, 6, IP_SUMS>), grid, dim3(256), 0, stream, arena, pkts, n, out,
-                           (uint8_t *)nullptr, (int8_t *)nullptr, 0u, xg);
-    else if (!occ8 && wg == 256)
-        hipLaunchKernelGGL((k_ipv4<32, 6, IP_SUMS, 256>), grid, dim3(256), 0, stream, arena, pkts, n, out,
-                           (uint8_t *)nullptr, (int8_t *)nullptr, 0u, xg);
-    else if (!occ8 && wg == 512)
-        hipLaunchKernelGGL((k_ipv4<32, 6, IP_SUMS, 512>), grid, dim3(512), 0, stream, arena, pkts, n, out,
-                           (uint8_t *)nullptr, (int8_t *)nullptr, 0u, xg);
-    else if (!occ8 && wg == 1024)
-        hipLaunchKernelGGL((k_ipv4<32, 6, IP_SUMS, 1024>), grid, dim3(1024), 0, stream, arena, pkts, n, out,
-                           (uint8_t *)nullptr, (int8_t *)nullptr, 0u, xg);
-    else
+    const uint32_t G = mode == IP_RX ? 16u : 32u;
+    if (wg != 256 && wg != 512 && wg != 1024)
         return hipErrorInvalidValue;
+    const uint32_t per = (uint32_t)wg / G;
+    const dim3 grid((n + per - 1u) / per), blk((uint32_t)wg);
+    uint8_t *fl = nullptr;
+#define TCSUM_SH(KERN)                                                                                   \
+    hipLaunchKernelGGL(KERN, grid, blk, 0, stream, arena, pkts, n, out, fl, verdict, 0u, xg);            \
     return hipGetLastError();
+    if (mode == IP_SUMS) {
+        if (occ == 0 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256>)) }
+        if (occ == 0 && wg == 512) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 512>)) }
+        if (occ == 0 && wg == 1024) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 1024>)) }
+        if (occ == 8 && wg == 256) { TCSUM_SH((k_ipv4_occ<32, 6, IP_SUMS, 8>)) }
+    } else if (mode == IP_RX && verdict) {
+        if (occ == 0 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256>)) }
+        if (occ == 0 && wg == 1024) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 1024>)) }
+        if (occ == 7 && wg == 256) { TCSUM_SH((k_ipv4_occ<16, 6, IP_RX, 7>)) }
+        if (occ == 8 && wg == 256) { TCSUM_SH((k_ipv4_occ<16, 6, IP_RX, 8>)) }
+    }
+#undef TCSUM_SH
+    return hipErrorInvalidValue;
 }
 
 } // namespace tcsum
@@ -734,12 +739,12 @@ int tcsum_probe_txfloor(void *arena, uint64_t nbytes, const uint64_t *fpos, cons
                                      static_cast<hipStream_t>(stream)));
 }
 
-int tcsum_probe_ipv4_shape(void *arena, const tcsum_pkt_t *pkts, uint32_t n, int wg, int occ8, uint32_t *out,
-                           void *stream)
+int tcsum_probe_ipv4_shape(void *arena, const tcsum_pkt_t *pkts, uint32_t n, int mode, int wg, int occ, uint32_t *out,
+                           int8_t *verdict, void *stream)
 {
-    if (!arena || !pkts || !out)
+    if (!arena || !pkts || !out || (mode == 2 && !verdict))
         return TCSUM_ERR_PARAM;
-    return rc_of(tcsum::launch_ipv4_shape(static_cast<uint8_t *>(arena), pkts, n, wg, occ8, out,
+    return rc_of(tcsum::launch_ipv4_shape(static_cast<uint8_t *>(arena), pkts, n, mode, wg, occ, out, verdict,
                                           static_cast<hipStream_t>(stream)));
 }
 

@@ -1274,10 +1274,10 @@ __global__ __launch_bounds__(T) void k_ipv4(uint8_t *__restrict__ arena, const t
                            opts); // no 32-bit wrap for any n
 }
 
-// k_ipv4 held to 64 VGPRs (8 waves per SIMD; the sums form takes 66, i.e. 7):
-// measurement (libtcsum_bench.so, tcsum_probe_ipv4_shape)
-template <int G, int U, int IPM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_ipv4_o8(
+// k_ipv4 held to OCC waves per SIMD (the sums form takes 66 VGPRs, i.e. 7
+// waves; rx 74, 6): measurement (libtcsum_bench.so, tcsum_probe_ipv4_shape)
+template <int G, int U, int IPM, int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void k_ipv4_occ(
     uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts, uint32_t n, uint32_t *__restrict__ out,
     uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out, uint32_t opts, uint32_t xg)
 {

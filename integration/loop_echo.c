@@ -195,8 +195,36 @@ static int tcp_echo(void)
         got += (int)k;
     }
     const double dt = now_s() - t0;
-    if (memcmp(in, out, (size_t)TCP_BYTES) != 0)
-        return fprintf(stderr, "tcp: echoed bytes differ\n"), 1;
+    if (memcmp(in, out, (size_t)TCP_BYTES) != 0) {
+        /* where, and how: the reference's TCP occasionally hands a stretch of
+         * the stream back out of place (CPU build too, no GPU involved) */
+        int first = -1, ndiff = 0, last = -1;
+        for (int i = 0; i < TCP_BYTES; i++)
+            if (in[i] != out[i]) {
+                if (first < 0)
+                    first = i;
+                last = i;
+                ndiff++;
+            }
+        int shift = 0; /* the received bytes at `first` found at out[first + d], |d| <= 64 KiB */
+        for (int d = -65536; d <= 65536 && !shift; d++)
+            if (d && first + d >= 0 && first + d + 64 <= TCP_BYTES && first + 64 <= TCP_BYTES &&
+                memcmp(in + first, out + first + d, 64) == 0)
+                shift = d;
+        fprintf(stderr, "tcp: got  ");
+        for (int i = first; i < first + 16; i++)
+            fprintf(stderr, " %02x", in[i]);
+        fprintf(stderr, "\ntcp: sent ");
+        for (int i = first; i < first + 16; i++)
+            fprintf(stderr, " %02x", out[i]);
+        fprintf(stderr, "\n");
+        fprintf(stderr, "tcp: echoed bytes differ: %d bytes differ in [%d, %d]; the bytes at %d are the "
+                        "sent stream's at offset %+d (0: not found)\n", ndiff, first, last, first, shift);
+        /* the transfer itself completed: its time still says what the path costs */
+        printf("timing tcp: %d bytes each way, %.3f s: %.3f MB/s (echo corrupted by the reference's TCP)\n",
+               TCP_BYTES, dt, TCP_BYTES / dt / 1e6);
+        return 1;
+    }
     close(s);
     printf("tcp: %d bytes echoed intact\n", TCP_BYTES);
     printf("timing tcp: %d bytes each way, %.3f s: %.3f MB/s\n", TCP_BYTES, dt, TCP_BYTES / dt / 1e6);

@@ -14,10 +14,17 @@ B=integration/_build
 : > "$out/configs0_timing.txt"
 keep="^timing|echoed intact|^engine|^batch sizes"
 run() { # label env... exe args...
+  # rc 1 = the echo's own check failed (the reference's TCP occasionally hands
+  # back a segment's header in place of its data, CPU build too: DESIGN.md §2);
+  # the run's lines are kept and the next one starts.  Anything else (a
+  # crash, a time-out) ends the script.
   local label=$1; shift
   echo "== $label" >> "$out/configs0_timing.txt"
-  timeout -k 10 120 env "$@" > "$out/run.raw" 2>&1 || { echo "$label failed rc=$?"; tail -20 "$out/run.raw"; exit 1; }
-  grep -E "$keep" "$out/run.raw" >> "$out/configs0_timing.txt"
+  timeout -k 10 120 env "$@" > "$out/run.raw" 2>&1
+  local rc=$?
+  grep -E "$keep|^tcp: echoed bytes differ|^tcp: (got|sent) " "$out/run.raw" >> "$out/configs0_timing.txt"
+  if [ $rc -eq 1 ]; then echo "   (rc 1: echo check failed)" >> "$out/configs0_timing.txt"; return 0; fi
+  [ $rc -eq 0 ] || { echo "$label failed rc=$rc"; tail -20 "$out/run.raw"; exit $rc; }
 }
 for rep in 1 2 3; do
   run "loop_echo_cpu rep $rep" X=0 $B/loop_echo_cpu --rounds 2000 --tcp-bytes 1048576

@@ -58,6 +58,7 @@ sys_mutex_t sys_mutex_create(void)
 #define UDP_PORT 7
 #define TCP_PORT 8
 static int UDP_ROUNDS = 200, UDP_MAX = 1400, TCP_BYTES = 64 * 1024;
+#define TCP_INFLIGHT 2100 /* below the reference's 4-KiB window (TCP_RBUF / TCP_SBUF, net_cfg.h) */
 
 static double now_s(void)
 {
@@ -182,7 +183,11 @@ static int tcp_echo(void)
     int sent = 0, got = 0;
     const double t0 = now_s();
     while (got < TCP_BYTES) {
-        if (sent < TCP_BYTES) {
+        /* at most TCP_INFLIGHT bytes sent and not yet echoed: with more, the
+         * client can block in send() on a peer whose own send() waits for the
+         * client to read -- both windows at 0, which the reference's TCP only
+         * leaves by its retransmission timer (seconds per stall) */
+        if (sent < TCP_BYTES && sent - got < TCP_INFLIGHT) {
             int chunk = TCP_BYTES - sent < 700 ? TCP_BYTES - sent : 700;
             ssize_t k = send(s, out + sent, (size_t)chunk, 0);
             if (k <= 0)

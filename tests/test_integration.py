@@ -28,11 +28,42 @@ def test_patch_applies_and_links():
 def test_loop_echo_cpu_reference():
     """configs[0] as the reference runs it (its CPU checksum), over loopback."""
     exe = os.path.join(BUILD, "loop_echo_cpu")
-    if not os.path.exists(exe):
-        subprocess.run(["make", "-C", INTEG, "all"], check=True, capture_output=True, timeout=280)
+    subprocess.run(["make", "-C", INTEG, exe], check=True, capture_output=True, timeout=280)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "udp: 200 datagrams" in r.stdout and "tcp: 65536 bytes echoed intact" in r.stdout
+
+
+def _batch_hist(out: str):
+    """loop_echo's tx batch-size histogram: counts of 1, 2-3, 4-7, ... frames."""
+    line = next(ln for ln in out.splitlines() if ln.startswith("batch sizes"))
+    tx = line.split("tx [", 1)[1].split("]", 1)[0]
+    return [int(part.split()[-1]) for part in tx.split("|")]
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="needs /root/reference (build container)")
+@pytest.mark.timeout(300)
+def test_loop_echo_coalescing_cpu_double():
+    """configs[0] through the patched stack's own glue (net_csum_gpu.c: frames
+    held until the work thread is idle, one fill per flush) with the oracle
+    behind the engine's entry points: 1 MiB over TCP echoed intact, no
+    retransmission stall, and batches of more than one frame; with
+    NET_CSUM_COALESCE=0 every batch is one frame, as in round 3."""
+    exe = os.path.join(BUILD, "loop_echo_dbl")
+    subprocess.run(["make", "-C", INTEG, exe], check=True, capture_output=True, timeout=280)
+    for _ in range(3):
+        r = subprocess.run([exe, "--rounds", "100", "--tcp-bytes", "1048576"], capture_output=True, text=True,
+                           timeout=90)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        assert "tcp: 1048576 bytes echoed intact" in r.stdout
+        assert "tcp rexmit" not in r.stdout + r.stderr
+        h = _batch_hist(r.stdout)
+        assert sum(h[1:]) > 0, h  # frames did leave together
+    r = subprocess.run([exe, "--rounds", "100", "--tcp-bytes", "262144"], capture_output=True, text=True,
+                       timeout=90, env=dict(os.environ, NET_CSUM_COALESCE="0"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    h = _batch_hist(r.stdout)
+    assert h[0] > 0 and sum(h[1:]) == 0, h
 
 
 @pytest.mark.gpu

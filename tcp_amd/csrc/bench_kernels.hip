@@ -7,6 +7,7 @@
 #include "tcsum_debug.h"
 #include "tcsum_synth.h"
 
+#include <atomic>
 #include <stdlib.h>
 #include <string.h>
 
@@ -588,8 +589,8 @@ static hipError_t flat_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n
     uint32_t *wfirst = reinterpret_cast<uint32_t *>(scr + sizeof(FlatPlan));
     unsigned long long *slot =
         reinterpret_cast<unsigned long long *>(scr + sizeof(FlatPlan) + ((4 * (nw + 1) + 7) & ~size_t(7)));
-    static uint32_t gen = 0x80000000u; // apart from the product's
-    ++gen;
+    static std::atomic<uint32_t> g_gen{0x80000000u}; // apart from the product's
+    const uint32_t gen = g_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
     const uint64_t pthreads = (uint64_t)n + 1u > nw ? (uint64_t)n + 1u : nw;
     hipLaunchKernelGGL((k_flat_plan<WB>), dim3((uint32_t)((pthreads + 255u) / 256u)), dim3(256), 0, stream, arena, pkts,
                        n, (uint32_t)nw, plan, wfirst, slot, gen);

@@ -103,6 +103,15 @@ int tcsum_probe_flat(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev
 int tcsum_probe_ipv4_shape(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n, int mode, int wg,
                            int occ, uint32_t *out /*[dev]*/, int8_t *verdict /*[dev] or NULL*/, void *stream);
 
+/* The byte-window stream's load phase alone (measurement): waves x loads in
+ * {16x4, 8x4, 4x3}, one window per workgroup, XOR-folded into sink; dep = what
+ * the loads wait for: 0 nothing, 1 one shared scalar word, 2 two dependent
+ * shared 16-B loads (word[0..3], all 0), 3 a 24-B descriptor per
+ * workgroup (descs: ndescs >= the grid's count, offsets < 2^63). */
+int tcsum_probe_window(const void *p /*[dev]*/, uint64_t nbytes, int waves, int loads, int dep,
+                       const uint64_t *word /*[dev]*/, const void *descs /*[dev]*/, uint64_t ndescs,
+                       uint32_t *sink /*[dev]*/, void *stream);
+
 uint32_t tcsum_probe_txfloor_windows(uint64_t nbytes);
 int tcsum_probe_txfloor_prepare(const void *arena /*[dev]*/, uint64_t nbytes, const tcsum_pkt_t *pkts /*[dev]*/,
                                 uint32_t n, uint64_t total_bytes_hint, uint32_t *side /*[dev]*/, uint64_t side_words,

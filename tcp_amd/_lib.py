@@ -78,6 +78,7 @@ BENCH_SIGNATURES = {
     "tcsum_probe_ipv4": (_I, [_V, _V, _U32, _U64, _I, _V, _V]),
     "tcsum_probe_flat": (_I, [_V, _V, _U32, _U64, _I, _I, _I, _V, _U64, _V, _V]),
     "tcsum_probe_ipv4_shape": (_I, [_V, _V, _U32, _I, _I, _I, _V, _V, _V]),
+    "tcsum_probe_window": (_I, [_V, _U64, _I, _I, _I, _V, _V, _U64, _V, _V]),
     "tcsum_probe_txfloor_windows": (_U32, [_U64]),
     "tcsum_probe_txfloor_prepare": (_I, [_V, _U64, _V, _U32, _U64, _V, _U64, _V, _U64, _V, _U64, _V]),
     "tcsum_probe_txfloor": (_I, [_V, _U64, _V, _V, _U32, _V, _I, _V, _V]),

@@ -366,6 +366,86 @@ __global__ __launch_bounds__(256) void k_floor_scatter(uint8_t *__restrict__ are
     floor_store(arena, nbytes, fpos[2ull * i + 1u], v >> 16);
 }
 
+static Geometry route(uint64_t mean_len);
+
+// ---------------------------------------------------------------- window read
+//
+// The byte-window stream's load phase alone, with the prologue varied: W
+// waves x 64 lanes x U nontemporal 16-B loads per workgroup over one window
+// (half-wave sub-ranges, k_flat_ipv4's and the TSO kernel's map), XCD-grouped
+// order, XOR-folded into a sink.  DEP = what the window's loads wait for:
+// 0 nothing (base and size are kernel arguments), 1 one scalar load of a
+// word every workgroup shares (k_flat_ipv4's plan, a scalar-cache hit),
+// 2 two dependent ones (the plan's `bad`, then base / end, as k_flat_ipv4
+// compiles), 3 a 24-B descriptor of the workgroup's own (k_segments_wgx's
+// range descriptor: a scalar load that misses).  Measurement only.
+template <int W, int U, int DEP>
+__global__ __launch_bounds__(W * 64) void k_probe_window(const u32x4 *__restrict__ p, uint64_t nchunks,
+                                                         const uint64_t *__restrict__ shared_word,
+                                                         const uint8_t *__restrict__ descs,
+                                                         uint32_t *__restrict__ sink, uint32_t xg)
+{
+    constexpr uint32_t CH = W * 64u * U, SR = 32u * U;
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    uint64_t c0 = (uint64_t)blk * CH;
+    if constexpr (DEP == 1) {
+        c0 += *shared_word; // 0
+    } else if constexpr (DEP == 2) {
+        // two scalar loads, the second's address behind the first's value
+        const u32x4 a = sload16(shared_word);
+        const u32x4 b2 = sload16(shared_word + 2 + (a.x & 1u));
+        c0 += b2.x;
+    } else if constexpr (DEP == 3) {
+        c0 += *reinterpret_cast<const uint64_t *>(descs + 24ull * blk) >> 63; // 0: offsets < 2^63
+    }
+    const uint32_t t = threadIdx.x, sub = t >> 5, l = t & 31u;
+    u32x4 v[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+        const uint64_t c = c0 + sub * SR + u * 32u + l;
+        v[u] = load16<true>(p + (c < nchunks ? c : nchunks - 1u));
+    }
+    u32x4 z = v[0];
+#pragma unroll
+    for (uint32_t u = 1; u < U; ++u)
+        z ^= v[u];
+    if ((z.x ^ z.y ^ z.z ^ z.w) == 0x9E3779B9u)
+        sink[0] = z.x;
+}
+
+template <int W, int U>
+static hipError_t window_read(const u32x4 *p, uint64_t nchunks, int dep, const uint64_t *word, const uint8_t *descs,
+                              uint32_t *sink, hipStream_t stream)
+{
+    constexpr uint32_t CH = W * 64u * U;
+    const dim3 grid((uint32_t)((nchunks + CH - 1u) / CH));
+    const uint32_t xg = (uint32_t)route(1500).xcd;
+    switch (dep) {
+    case 0: hipLaunchKernelGGL((k_probe_window<W, U, 0>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
+    case 1: hipLaunchKernelGGL((k_probe_window<W, U, 1>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
+    case 2: hipLaunchKernelGGL((k_probe_window<W, U, 2>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
+    case 3: hipLaunchKernelGGL((k_probe_window<W, U, 3>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+static hipError_t launch_probe_window(const void *p, uint64_t nbytes, int waves, int loads, int dep,
+                                      const uint64_t *word, const uint8_t *descs, uint32_t *sink, hipStream_t stream)
+{
+    const uint64_t nchunks = nbytes / 16;
+    if (nchunks == 0)
+        return hipSuccess;
+    const u32x4 *q = static_cast<const u32x4 *>(p);
+    if (waves == 16 && loads == 4)
+        return window_read<16, 4>(q, nchunks, dep, word, descs, sink, stream);
+    if (waves == 8 && loads == 4)
+        return window_read<8, 4>(q, nchunks, dep, word, descs, sink, stream);
+    if (waves == 4 && loads == 3)
+        return window_read<4, 3>(q, nchunks, dep, word, descs, sink, stream);
+    return hipErrorInvalidValue;
+}
+
 // The product's route (libtcsum.so's router with its debug knobs applied).
 static Geometry route(uint64_t mean_len)
 {
@@ -679,6 +759,22 @@ int tcsum_synth_ipv4(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t 
     if (n && (!arena || !pkts))
         return TCSUM_ERR_PARAM;
     return rc_of(tcsum::launch_synth_ipv4(arena, pkts, n, seed, static_cast<hipStream_t>(stream)));
+}
+
+int tcsum_probe_window(const void *p, uint64_t nbytes, int waves, int loads, int dep, const uint64_t *word,
+                       const void *descs, uint64_t ndescs, uint32_t *sink, void *stream)
+{
+    // dep 1 / 2 read word[0..3] (all 0); dep 3 reads one 24-B descriptor per
+    // workgroup: descs must hold the grid's count
+    if (!p || !sink || (reinterpret_cast<uintptr_t>(p) & 15u) || ((dep == 1 || dep == 2) && !word))
+        return TCSUM_ERR_PARAM;
+    if (dep == 3) {
+        const uint64_t ch = (uint64_t)waves * 64u * (uint64_t)loads;
+        if (!descs || ch == 0 || ndescs < (nbytes / 16 + ch - 1) / ch)
+            return TCSUM_ERR_PARAM;
+    }
+    return rc_of(tcsum::launch_probe_window(p, nbytes, waves, loads, dep, word, static_cast<const uint8_t *>(descs),
+                                            sink, static_cast<hipStream_t>(stream)));
 }
 
 int tcsum_probe_read(const void *p, uint64_t nbytes, uint32_t *sink, void *stream)

@@ -10,4 +10,5 @@ scripts/gpu_steps.sh \
   "configs0:400:scripts/configs0_timing.sh $out" \
   "suite:600:python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $out/pytest_gpu.log 2>&1" \
   "smoke:200:python -u -c 'import __graft_entry__ as g; g.smoke()' > $out/smoke.log 2>&1" \
-  "profile:700:scripts/profile_round.sh $out"
+  "profile:700:scripts/profile_round.sh $out" \
+  "window:300:python -u scripts/window_probe.py > $out/window_probe.txt 2>&1"

@@ -455,17 +455,20 @@ static void *time_thread(void *arg)
         CPU_SET(j->cpu, &set);
         (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
     }
-    uint64_t lo = UINT64_MAX, hi = 0;
+    uint64_t lo = UINT64_MAX, hi = 0, own = 0;
     for (uint32_t i = j->lo; i < j->hi; i++) {
         const orc_peso_t *d = j->segs + i;
         if (d->offset < lo)
             lo = d->offset;
         if (d->offset + d->len > hi)
             hi = d->offset + d->len;
+        own += d->len;
     }
     uint8_t *local = NULL;
     const uint8_t *src = j->arena;
-    if (hi > lo) {
+    /* a slice whose segments are spread over much more than their own bytes
+     * (descriptors in no particular order) reads the shared sample instead */
+    if (hi > lo && hi - lo <= 2 * own + (1u << 20)) {
         local = (uint8_t *)malloc(hi - lo + 64);
         if (local) {
             memcpy(local, j->arena + lo, hi - lo);
@@ -503,13 +506,20 @@ double orc_time_peso(orc_peso_fn fn, const uint8_t *arena, const orc_peso_t *seg
     tjob_t jobs[256];
     pthread_barrier_t bar;
     pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
-    const long ncpu = sysconf(_SC_NPROCESSORS_ONLN);
+    /* the CPUs this process may run on, in order: thread t on the t-th */
+    int allowed[1024], nallowed = 0;
+    cpu_set_t mask;
+    CPU_ZERO(&mask);
+    if (sched_getaffinity(0, sizeof(mask), &mask) == 0)
+        for (int c = 0; c < CPU_SETSIZE && nallowed < 1024; c++)
+            if (CPU_ISSET(c, &mask))
+                allowed[nallowed++] = c;
     for (int t = 0; t < nthreads; t++) {
         jobs[t] = (tjob_t){fn, arena, segs,
                            (uint32_t)((uint64_t)n * t / nthreads),
                            (uint32_t)((uint64_t)n * (t + 1) / nthreads),
                            min_seconds, &bar, 0, 0, 0.0,
-                           nthreads > 1 && ncpu >= nthreads ? t : -1};
+                           nthreads > 1 && nallowed >= nthreads ? allowed[t] : -1};
         pthread_create(&th[t], NULL, time_thread, &jobs[t]);
     }
     double rate = 0.0, max_secs = 0.0;

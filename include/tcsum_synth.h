@@ -107,7 +107,10 @@ int tcsum_probe_ipv4_shape(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev
  * {16x4, 8x4, 4x3}, one window per workgroup, XOR-folded into sink; dep = what
  * the loads wait for: 0 nothing, 1 one shared scalar word, 2 two dependent
  * shared 16-B loads (word[0..3], all 0), 3 a 24-B descriptor per
- * workgroup (descs: ndescs >= the grid's count, offsets < 2^63). */
+ * workgroup (descs: ndescs >= the grid's count, offsets < 2^63); 4 the
+ * window's chunks shifted 16 B past its boundary, 5 default-policy loads of
+ * its first and last chunk beside them, 6 both, 7 both behind the descriptor
+ * (k_segments_wgx's own pattern). */
 int tcsum_probe_window(const void *p /*[dev]*/, uint64_t nbytes, int waves, int loads, int dep,
                        const uint64_t *word /*[dev]*/, const void *descs /*[dev]*/, uint64_t ndescs,
                        uint32_t *sink /*[dev]*/, void *stream);

@@ -60,9 +60,12 @@ kinds = {"k_ipv4 (product)": lambda: tc.batch_ipv4(arena, descs, n, b.total_byte
          "64-KiB ranges, its load probe": lambda: tc.probe_segments(arena, d64, n64, n64 * L64, sink),
          "plain read probe": lambda: tc.probe_read(arena, nbytes, sink),
          "flat 16x4 v1 (plan pass + loads)": flat_v1(16, 4)}
-for w, u in ((16, 4), (8, 4), (4, 3)):
-    for dep in (0, 1, 2, 3):
-        kinds[f"window {w}x{u} dep{dep}"] = window(w, u, dep)
+NAMES = {0: "nothing first", 1: "1 shared scalar word first", 2: "2 dependent shared words first",
+         3: "own descriptor first", 4: "shifted 16 B", 5: "+ default-policy edge chunks",
+         6: "shifted 16 B + edge chunks", 7: "shifted + edges + own descriptor (wgx's pattern)"}
+for w, u, deps in ((16, 4, range(8)), (8, 4, (0, 4, 6)), (4, 3, (0, 4, 6))):
+    for dep in deps:
+        kinds[f"window {w}x{u}: {NAMES[dep]}"] = window(w, u, dep)
 times = {k: [] for k in kinds}
 for k, fn in kinds.items():
     fn()
@@ -81,4 +84,4 @@ base = np.median(times["k_ipv4 (product)"])
 print(f"# mixed arena: {nbytes} B; median of 7 rounds x 10 launches, interleaved; of 8 TB/s on the arena's bytes")
 for k, t in times.items():
     m = np.median(t)
-    print(f"{k:42s} {m*1e3:9.1f} us  {m/base:6.3f}x  {nbytes / (m*1e-3) / 8e12:6.4f}", flush=True)
+    print(f"{k:62s} {m*1e3:9.1f} us  {m/base:6.3f}x  {nbytes / (m*1e-3) / 8e12:6.4f}", flush=True)

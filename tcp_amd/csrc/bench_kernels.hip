@@ -379,7 +379,11 @@ static Geometry route(uint64_t mean_len);
 // 2 two dependent ones (the plan's `bad`, then base / end, as k_flat_ipv4
 // compiles), 3 a 24-B descriptor of the workgroup's own (k_segments_wgx's
 // range descriptor: a scalar load that misses).  Measurement only.
-template <int W, int U, int DEP>
+// SH: the window's chunks start SH chunks after its boundary (k_segments_wgx's
+// interior starts 16 B into its range); EDGE: lanes 0 and 1 also load the
+// window's first and last chunk with the default cache policy (wgx's edge
+// chunks).
+template <int W, int U, int DEP, int SH = 0, bool EDGE = false>
 __global__ __launch_bounds__(W * 64) void k_probe_window(const u32x4 *__restrict__ p, uint64_t nchunks,
                                                          const uint64_t *__restrict__ shared_word,
                                                          const uint8_t *__restrict__ descs,
@@ -399,13 +403,18 @@ __global__ __launch_bounds__(W * 64) void k_probe_window(const u32x4 *__restrict
         c0 += *reinterpret_cast<const uint64_t *>(descs + 24ull * blk) >> 63; // 0: offsets < 2^63
     }
     const uint32_t t = threadIdx.x, sub = t >> 5, l = t & 31u;
+    u32x4 ev = u32x4(0u);
+    if constexpr (EDGE) {
+        const uint64_t c = c0 + (t == 0 ? 0u : CH - 1u);
+        ev = load16<false>(p + (c < nchunks ? c : nchunks - 1u));
+    }
     u32x4 v[U];
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
-        const uint64_t c = c0 + sub * SR + u * 32u + l;
+        const uint64_t c = c0 + SH + sub * SR + u * 32u + l;
         v[u] = load16<true>(p + (c < nchunks ? c : nchunks - 1u));
     }
-    u32x4 z = v[0];
+    u32x4 z = v[0] ^ ev;
 #pragma unroll
     for (uint32_t u = 1; u < U; ++u)
         z ^= v[u];
@@ -425,6 +434,10 @@ static hipError_t window_read(const u32x4 *p, uint64_t nchunks, int dep, const u
     case 1: hipLaunchKernelGGL((k_probe_window<W, U, 1>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
     case 2: hipLaunchKernelGGL((k_probe_window<W, U, 2>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
     case 3: hipLaunchKernelGGL((k_probe_window<W, U, 3>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
+    case 4: hipLaunchKernelGGL((k_probe_window<W, U, 0, 1, false>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
+    case 5: hipLaunchKernelGGL((k_probe_window<W, U, 0, 0, true>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
+    case 6: hipLaunchKernelGGL((k_probe_window<W, U, 0, 1, true>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
+    case 7: hipLaunchKernelGGL((k_probe_window<W, U, 3, 1, true>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -768,7 +781,7 @@ int tcsum_probe_window(const void *p, uint64_t nbytes, int waves, int loads, int
     // workgroup: descs must hold the grid's count
     if (!p || !sink || (reinterpret_cast<uintptr_t>(p) & 15u) || ((dep == 1 || dep == 2) && !word))
         return TCSUM_ERR_PARAM;
-    if (dep == 3) {
+    if (dep == 3 || dep == 7) {
         const uint64_t ch = (uint64_t)waves * 64u * (uint64_t)loads;
         if (!descs || ch == 0 || ndescs < (nbytes / 16 + ch - 1) / ch)
             return TCSUM_ERR_PARAM;

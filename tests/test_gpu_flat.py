@@ -283,3 +283,43 @@ def test_flat_full_mixed_config(tc, torch, oracle, config):
     np.testing.assert_array_equal(v, ev)
     np.testing.assert_array_equal(flags.cpu().numpy(), ef)
     assert (v[bad] == -13).mean() > 0.99
+
+
+@pytest.mark.parametrize("layout", ["packed", "shuffled"])
+@pytest.mark.parametrize("flat_knob", [-1, 1])
+def test_ipv4_layout_hints_give_the_same_results(tc, torch, oracle, layout, flat_knob):
+    """tcsum_batch's layout hint on every IPv4 operation (sums, rx verify, tx
+    offload, tx fill) changes only the kernel, never a result -- with the
+    byte-window stream off (the route) and on, and when an ORDERED promise is
+    false (a shuffled batch)."""
+    tc.debug_set("flat", flat_knob)
+    rng = np.random.default_rng(300 + (layout == "shuffled"))
+    lens = rng.integers(20, 9000, 3000).astype(np.int64)
+    offs = _stream(lens, 7)
+    host = _arena(rng, int(offs[-1] + lens[-1]) + 512)
+    _headers(rng, host, offs, lens, valid=0.9)
+    pk = _pk(tc, offs, lens)
+    if layout == "shuffled":
+        pk = pk[rng.permutation(pk.size)]
+    n, total = pk.size, int(lens.sum())
+    exp, efl = oracle.batch_ipv4(host, pk, nthreads=8)
+    ev, evfl = oracle.batch_ipv4_rx_verify(host, pk, nthreads=8)
+    want = host.copy()
+    oracle.batch_ipv4_tx_fill(want, pk, nthreads=8)
+    d = tc.descs_to_device(pk)
+    for lay in (tc.LAYOUT_UNKNOWN, tc.LAYOUT_ORDERED, tc.LAYOUT_SHUFFLED):
+        arena = to_dev(torch, host)
+        fl = torch.empty(n, dtype=torch.uint8, device="cuda")
+        out, _, _ = tc.batch(tc.OP_IPV4, arena, d, n, flags=fl, total_bytes=total, layout=lay)
+        np.testing.assert_array_equal(out.cpu().numpy(), exp)
+        np.testing.assert_array_equal(fl.cpu().numpy(), efl)
+        rout = torch.empty(n, dtype=torch.uint32, device="cuda")
+        _, _, v = tc.batch(tc.OP_IPV4_RX_VERIFY, arena, d, n, out=rout, total_bytes=total, layout=lay)
+        np.testing.assert_array_equal(v.cpu().numpy(), ev)
+        np.testing.assert_array_equal(rout.cpu().numpy(), exp)
+        tout, tfl, _ = tc.batch(tc.OP_IPV4_TX_OFFLOAD, arena, d, n, total_bytes=total, layout=lay)
+        filled = host.copy()
+        tc.tx_apply_batch(filled, pk, tout.cpu().numpy(), tfl.cpu().numpy())
+        np.testing.assert_array_equal(filled, want)
+        tc.batch(tc.OP_IPV4_TX_FILL, arena, d, n, total_bytes=total, layout=lay)
+        np.testing.assert_array_equal(arena.cpu().numpy()[: host.size], want)

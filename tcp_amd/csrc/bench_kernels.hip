@@ -414,6 +414,9 @@ __global__ __launch_bounds__(W * 64) void k_probe_window(const u32x4 *__restrict
         const uint64_t c = c0 + SH + sub * SR + u * 32u + l;
         v[u] = load16<true>(p + (c < nchunks ? c : nchunks - 1u));
     }
+    // every load in flight before the first wait (without it the 16x4 form
+    // issued two loads, waited, then two more: half the bytes in flight)
+    issue_fence();
     u32x4 z = v[0] ^ ev;
 #pragma unroll
     for (uint32_t u = 1; u < U; ++u)

@@ -99,7 +99,9 @@ int tcsum_probe_flat(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev
  * = tcsum_batch_ipv4's sums by k_ipv4<32, 6> (out), mode 2 = rx verify by
  * k_ipv4<16, 6> (verdict, and the sums into out), in wg = 256 / 512 / 1024
  * thread workgroups (rx: 256 / 1024), or with wg = 256 held to occ waves per
- * SIMD (sums: 8; rx: 7 or 8; 0 = as built).  Others: TCSUM_ERR_PARAM. */
+ * SIMD (sums: 8; rx: 7 or 8; 0 = as built), or (occ = 100 + s, wg = 256)
+ * with its data pass starting s bytes past a 128-B line instead of on one
+ * (sums: s = 16, 64; rx: 16).  Others: TCSUM_ERR_PARAM. */
 int tcsum_probe_ipv4_shape(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n, int mode, int wg,
                            int occ, uint32_t *out /*[dev]*/, int8_t *verdict /*[dev] or NULL*/, void *stream);
 

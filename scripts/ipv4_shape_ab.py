@@ -18,7 +18,8 @@ import tcp_amd as tc  # noqa: E402
 from tcp_amd import _lib, workload  # noqa: E402
 
 B = _lib.bench_lib()
-for cfg in (sys.argv[1:] or ["mixed", "mixed_aligned", "mixed_rx"]):
+SKEW_ONLY = "--skew" in sys.argv
+for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mixed_aligned", "mixed_rx"]):
     b = workload.make_batch(cfg)
     arena, descs = workload.materialize(b)
     n = b.n
@@ -46,12 +47,17 @@ for cfg in (sys.argv[1:] or ["mixed", "mixed_aligned", "mixed_rx"]):
         return f
 
     kinds = {"product (256 threads)": product, "256 threads, same kernel (probe lib)": shape(256, 0)}
-    if rx:
+    if SKEW_ONLY:
+        kinds.update({"data pass 16 B past the line": shape(256, 116)})
+        if not rx:
+            kinds["data pass 64 B past the line"] = shape(256, 164)
+    elif rx:
         kinds.update({"1024 threads": shape(1024, 0), "<= 72 VGPRs (7 waves/SIMD)": shape(256, 7),
-                      "<= 64 VGPRs (8 waves/SIMD)": shape(256, 8)})
+                      "<= 64 VGPRs (8 waves/SIMD)": shape(256, 8), "data pass 16 B past the line": shape(256, 116)})
     else:
         kinds.update({"512 threads": shape(512, 0), "1024 threads": shape(1024, 0),
-                      "<= 64 VGPRs (8 waves/SIMD)": shape(256, 8)})
+                      "<= 64 VGPRs (8 waves/SIMD)": shape(256, 8), "data pass 16 B past the line": shape(256, 116),
+                      "data pass 64 B past the line": shape(256, 164)})
     bufs = {k: (torch.empty(n, dtype=torch.uint32, device="cuda"), torch.empty(n, dtype=torch.int8, device="cuda"))
             for k in kinds}
     for k, fn in kinds.items():

@@ -740,11 +740,14 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 0 && wg == 512) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 512>)) }
         if (occ == 0 && wg == 1024) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 1024>)) }
         if (occ == 8 && wg == 256) { TCSUM_SH((k_ipv4_occ<32, 6, IP_SUMS, 8>)) }
+        if (occ == 100 + 16 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 16>)) } // data pass skewed 16 B
+        if (occ == 100 + 64 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 64>)) }
     } else if (mode == IP_RX && verdict) {
         if (occ == 0 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256>)) }
         if (occ == 0 && wg == 1024) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 1024>)) }
         if (occ == 7 && wg == 256) { TCSUM_SH((k_ipv4_occ<16, 6, IP_RX, 7>)) }
         if (occ == 8 && wg == 256) { TCSUM_SH((k_ipv4_occ<16, 6, IP_RX, 8>)) }
+        if (occ == 100 + 16 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256, 16>)) }
     }
 #undef TCSUM_SH
     return hipErrorInvalidValue;

@@ -876,7 +876,7 @@ constexpr uint32_t IP_OPT_NO_STORE = 1u; // IP_TX: compute the fill's values, le
 // IP_TX, deferred stores (launch_ipv4 mode 4): the values go to `out` and each
 // packet's store positions to a side array (through the verdict pointer, which
 // tx never uses); k_tx_scatter then writes them into the packets in a second,
-// short launch (tx fill)
+// short launch (DESIGN.md Â§6, tx fill)
 constexpr uint32_t IP_OPT_DEFER = 2u;
 // launch_ipv4 mode 3: IP_TX kernels with IP_OPT_NO_STORE
 constexpr int IP_TX_OFFLOAD = 3;
@@ -1115,7 +1115,10 @@ __device__ __forceinline__ void ip_finish(const IpHdr &ih, uint32_t fl, bool big
 // Packet `pk` (one per G-lane group; pk >= n: a dead group that reads
 // descriptor 0 and writes nothing).  Every lane of the wave must call it: the
 // group reduction crosses lanes.
-template <int G, int U, int IPM>
+// SKEW (measurement): the data pass starts SKEW bytes past the packet's
+// 128-B line instead of on it, for packets that start that far in (0: the
+// route)
+template <int G, int U, int IPM, int SKEW = 0>
 __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                             uint32_t pk, uint32_t n, uint32_t *__restrict__ out,
                                             uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
@@ -1166,7 +1169,10 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     // the time the next pass, a memory latency later, wants the other half).
     // Chunks of that line before the packet are loaded (same line, same page)
     // but fall outside every byte range below.
-    const uint32_t sl = (uint32_t)(start & 127u);
+    // (SKEW: only for packets that start at least SKEW bytes into their line,
+    // so the pass never begins before the packet's own line)
+    const uint32_t s127 = (uint32_t)(start & 127u);
+    const uint32_t sl = SKEW && s127 >= (uint32_t)SKEW ? s127 - (uint32_t)SKEW : s127;
     const uint32_t dch = big_enough ? (frame_ld + sl + 15) >> 4 : 0u;
     const u32x4 *dbase = dch ? reinterpret_cast<const u32x4 *>(pp - sl) : &g_zero_chunk;
     const uint32_t dlast = dch ? dch - 1u : 0u;
@@ -1263,14 +1269,14 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
                        verdict_out, opts);
 }
 
-template <int G, int U, int IPM, int T = 256>
+template <int G, int U, int IPM, int T = 256, int SKEW = 0>
 __global__ __launch_bounds__(T) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                             uint32_t n, uint32_t *__restrict__ out,
                                             uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
                                             uint32_t opts, uint32_t xg)
 {
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
-    ipv4_packet<G, U, IPM>(arena, pkts, blk * (uint32_t)(T / G) + threadIdx.x / G, n, out, flags_out, verdict_out,
+    ipv4_packet<G, U, IPM, SKEW>(arena, pkts, blk * (uint32_t)(T / G) + threadIdx.x / G, n, out, flags_out, verdict_out,
                            opts); // no 32-bit wrap for any n
 }
 

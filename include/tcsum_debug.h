@@ -46,7 +46,10 @@ extern "C" {
  * Returns TCSUM_OK, or TCSUM_ERR_PARAM for an unknown key. */
 int tcsum_debug_set(const char *key, int64_t value);
 
-/* The knob's value (-1 = the router's choice; -2 = unknown key). */
+/* The knob's value (-1 = the router's choice; -2 = unknown key).  Two
+ * read-only keys: "scratch_reserved" (bytes the tx fill's scratch pool holds on
+ * the calling thread's device) and "last_sys_error" (the last TCSUM_ERR_SYS
+ * of tcsum_host_batch_peso: step * 1000 + the hipError_t; 0 = none). */
 int64_t tcsum_debug_get(const char *key);
 
 /* The route a batch call would take for a mean range length, with the knobs

@@ -152,4 +152,8 @@ def pcap_lib() -> ctypes.CDLL:
 
 def check(rc: int, what: str) -> None:
     if rc != OK:
-        raise RuntimeError(f"{what} failed with net_err_t {rc}")
+        extra = ""
+        if rc == ERR_SYS and what.startswith("tcsum_host_batch_peso"):
+            v = lib().tcsum_debug_get(b"last_sys_error")  # step * 1000 + hipError_t
+            extra = f" (step {v // 1000}, hipError_t {v % 1000})"
+        raise RuntimeError(f"{what} failed with net_err_t {rc}{extra}")

@@ -452,8 +452,20 @@ int tcsum_debug_set(const char *key, int64_t value)
     return TCSUM_OK;
 }
 
+// The last TCSUM_ERR_SYS of tcsum_host_batch_peso: step * 1000 + the HIP
+// error code (tcsum_debug_get "last_sys_error"; 0 = none yet).
+static std::atomic<int64_t> g_last_sys{0};
+static int note_sys(int step, hipError_t e)
+{
+    g_last_sys.store((int64_t)step * 1000 + (int64_t)e, std::memory_order_relaxed);
+    (void)hipGetLastError();
+    return TCSUM_ERR_SYS;
+}
+
 int64_t tcsum_debug_get(const char *key)
 {
+    if (key && strcmp(key, "last_sys_error") == 0)
+        return g_last_sys.load(std::memory_order_relaxed);
     if (key && strcmp(key, "scratch_reserved") == 0) { // the calling thread's current device
         int dev = 0;
         return hipGetDevice(&dev) == hipSuccess ? (int64_t)tcsum::scratch_reserved(dev) : -2;
@@ -754,9 +766,9 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     std::lock_guard<std::mutex> lk(c.mu);
     int rc = ctx_init(c, device);
     if (rc != TCSUM_OK)
-        return rc;
-    if (hipSetDevice(device) != hipSuccess)
-        return TCSUM_ERR_SYS;
+        return rc == TCSUM_ERR_SYS ? note_sys(12, hipSuccess) : rc;
+    if (const hipError_t e = hipSetDevice(device); e != hipSuccess)
+        return note_sys(1, e);
     const uint8_t *h = static_cast<const uint8_t *>(host_arena);
     hipStream_t cs = c.hs[0], ks = c.hs[1];
     // device buffers (grow-only) hold only the spans the segments touch (a
@@ -791,13 +803,14 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         (void)hipStreamSynchronize(cs);
         return code;
     };
+    auto fail_sys = [&](int step, hipError_t e) { return fail(note_sys(step, e)); };
     uint8_t *lead_base = nullptr;
     if (early) {
         if (!grow(c.d_lead, c.d_lead_cap, span_bytes(lead)))
             return TCSUM_ERR_MEM;
         lead_base = c.d_lead - (lead.lo & ~uint64_t(15));
-        if (copy_bytes(lead_base, lead) != hipSuccess)
-            return fail(TCSUM_ERR_SYS);
+        if (const hipError_t e = copy_bytes(lead_base, lead); e != hipSuccess)
+            return fail_sys(2, e);
         stamp("lead copy");
     }
     // the rest of the descriptors, in parallel
@@ -865,8 +878,8 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     if (!c.q_desc.reserve(sizeof(tcsum_seg_t) * n) || (stage_out && !c.q_res.reserve(sizeof(uint16_t) * n + 64)))
         return fail(TCSUM_ERR_MEM);
     uint16_t *hout = stage_out ? reinterpret_cast<uint16_t *>(c.q_res.h) : out;
-    if (!early && copy_bytes(ch[0].base, ch[0].sp) != hipSuccess) // its bytes cross while the host stages
-        return fail(TCSUM_ERR_SYS);
+    if (const hipError_t e = early ? hipSuccess : copy_bytes(ch[0].base, ch[0].sp); e != hipSuccess)
+        return fail_sys(3, e); // its bytes cross while the host stages
     tcsum_seg_t *hseg = reinterpret_cast<tcsum_seg_t *>(c.q_desc.h);
     parallel_for(n, size_t(1) << 16, [&](size_t b, size_t e) {
         for (size_t i = b; i < e; ++i) {
@@ -884,15 +897,18 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
             hseg[i].pre_sum = (uint32_t)q;
         }
     });
-    if (hipMemcpyAsync(c.d_descs, hseg, sizeof(tcsum_seg_t) * n, hipMemcpyHostToDevice, cs) != hipSuccess)
-        return fail(TCSUM_ERR_SYS);
+    if (const hipError_t e = hipMemcpyAsync(c.d_descs, hseg, sizeof(tcsum_seg_t) * n, hipMemcpyHostToDevice, cs);
+        e != hipSuccess)
+        return fail_sys(4, e);
     stamp("descs staged");
     for (size_t k = 0; k < ch.size(); ++k) {
-        if (k && copy_bytes(ch[k].base, ch[k].sp) != hipSuccess)
-            return fail(TCSUM_ERR_SYS);
+        if (const hipError_t e = k ? copy_bytes(ch[k].base, ch[k].sp) : hipSuccess; e != hipSuccess)
+            return fail_sys(5, e);
         hipEvent_t ev = c.hev[k % kHostEvents];
-        if (hipEventRecord(ev, cs) != hipSuccess || hipStreamWaitEvent(ks, ev, 0) != hipSuccess)
-            return fail(TCSUM_ERR_SYS);
+        if (const hipError_t e = hipEventRecord(ev, cs); e != hipSuccess)
+            return fail_sys(6, e);
+        if (const hipError_t e = hipStreamWaitEvent(ks, ev, 0); e != hipSuccess)
+            return fail_sys(7, e);
         const uint32_t i0 = ch[k].b0 * kSpanBlock;
         const uint32_t i1 = (uint32_t)std::min<uint64_t>(n, (uint64_t)ch[k].b1 * kSpanBlock);
         if (i1 <= i0)
@@ -901,13 +917,16 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
                                                     tcsum::pick_geometry(mean_of(ch[k].sp.bytes, i1 - i0)),
                                                     ch[k].base, c.d_descs + i0, i1 - i0, c.d_out + i0, 1u, ks);
         if (e != hipSuccess)
-            return fail(TCSUM_ERR_SYS);
+            return fail_sys(8, e);
     }
-    if (hipMemcpyAsync(hout, c.d_out, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, ks) != hipSuccess)
-        return fail(TCSUM_ERR_SYS);
+    if (const hipError_t e = hipMemcpyAsync(hout, c.d_out, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, ks);
+        e != hipSuccess)
+        return fail_sys(9, e);
     stamp("all issued");
-    if (hipStreamSynchronize(ks) != hipSuccess || hipStreamSynchronize(cs) != hipSuccess)
-        return TCSUM_ERR_SYS;
+    if (const hipError_t e = hipStreamSynchronize(ks); e != hipSuccess)
+        return fail_sys(10, e);
+    if (const hipError_t e = hipStreamSynchronize(cs); e != hipSuccess)
+        return note_sys(11, e);
     stamp("synced");
     if (hout != out)
         memcpy(out, hout, sizeof(uint16_t) * n);

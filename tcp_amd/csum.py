@@ -180,9 +180,10 @@ def batch_ipv4_rx_verify(arena, pkts, n: int, total_bytes: int = 0, verdict=None
 def host_batch_peso(host_arena: np.ndarray, segs: np.ndarray, device: int = 0) -> np.ndarray:
     """End-to-end: host arena -> H2D -> kernel -> D2H (tcsum_host_batch_peso)."""
     assert segs.dtype == PESO_DTYPE
+    segs = np.ascontiguousarray(segs)  # held for the call: a temporary's buffer could be freed before it
     out = np.zeros(segs.size, np.uint16)
     rc = _lib.lib().tcsum_host_batch_peso(device, host_arena.ctypes.data, host_arena.nbytes,
-                                          np.ascontiguousarray(segs).ctypes.data, segs.size, out.ctypes.data)
+                                          segs.ctypes.data, segs.size, out.ctypes.data)
     _lib.check(rc, "tcsum_host_batch_peso")
     return out
 
@@ -191,9 +192,10 @@ def host_batch_peso_multi(host_arena: np.ndarray, segs: np.ndarray, devices) -> 
     """tcsum_host_batch_peso_multi: one host batch sharded by bytes over `devices`."""
     assert segs.dtype == PESO_DTYPE
     devs = np.ascontiguousarray(np.asarray(list(devices), dtype=np.int32))
+    segs = np.ascontiguousarray(segs)
     out = np.zeros(segs.size, np.uint16)
     rc = _lib.lib().tcsum_host_batch_peso_multi(devs.ctypes.data, devs.size, host_arena.ctypes.data,
-                                                host_arena.nbytes, np.ascontiguousarray(segs).ctypes.data,
+                                                host_arena.nbytes, segs.ctypes.data,
                                                 segs.size, out.ctypes.data)
     _lib.check(rc, "tcsum_host_batch_peso_multi")
     return out

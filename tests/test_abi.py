@@ -125,6 +125,9 @@ def test_debug_knobs(libpath):
     assert tc.route(1500)["lanes"] == 16 and tc.debug_get("lanes") == -1
     from tcp_amd import _lib
     assert _lib.lib().tcsum_debug_set(b"no_such_knob", 1) == _lib.ERR_PARAM
+    # read-only: no system failure yet in this process, and not settable
+    assert tc.debug_get("last_sys_error") == 0
+    assert _lib.lib().tcsum_debug_set(b"last_sys_error", 1) == _lib.ERR_PARAM
 
 
 def test_capture_helper_is_a_library_of_its_own(libpath):

@@ -40,8 +40,6 @@ extern "C" {
  *   "hostq_dma_keep_mb" device arena kept between host-queue calls (256)
  *   "copy_threads"    host threads of a parallel gather / scatter (16; the
  *                     worker pool is sized once, at first use)
- *   "page_stage"      0: tcsum_host_batch_peso hands a pageable arena to the
- *                     runtime's copy instead of its own two pinned slots
  * Only TCSUM_DEVICE and TCSUM_CALL_SERVER are read from the environment
  * (deployment choices for an unmodified drop-in stack); nothing there changes
  * a route or a tuning.

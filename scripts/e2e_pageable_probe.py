@@ -1,8 +1,6 @@
 """tcsum_host_batch_peso on configs[1] from a pinned arena (tcsum_host_alloc)
-and from a pageable numpy array, same bytes, one process; the pageable
-arena through the library's two pinned slots (page_stage default) and handed
-to the runtime's pageable copy (page_stage=0).  Measurement script, not
-product code."""
+and from a pageable numpy array, same bytes, one process.  Measurement
+script, not product code."""
 import os
 import sys
 import time
@@ -23,9 +21,7 @@ ha.array[:] = arena[: b.alloc_bytes].cpu().numpy()
 page = np.array(ha.array)
 del arena, descs
 torch.cuda.empty_cache()
-legs = (("pinned", ha.array, -1), ("pageable", page, -1), ("page_rt", page, 0))
-for name, host, stage in legs + legs:
-    tc.debug_set("page_stage", stage)
+for name, host in (("pinned", ha.array), ("pageable", page), ("pinned", ha.array), ("pageable", page)):
     out = tc.host_batch_peso(host, b.descs)
     t0 = time.perf_counter()
     for _ in range(3):
@@ -33,4 +29,3 @@ for name, host, stage in legs + legs:
     dt = (time.perf_counter() - t0) / 3
     print(f"host_batch_peso {name:9s} {dt * 1e3:8.2f} ms  {b.total_bytes / dt / GIB:6.2f} GiB/s  "
           f"match={bool((out == want).all())}", flush=True)
-tc.debug_set("page_stage", -1)

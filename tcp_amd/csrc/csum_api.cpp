@@ -100,10 +100,6 @@ struct Ctx {
     // host-queue batches: pinned, fine-grained descriptors / results / a copy
     // of a pageable arena, all read and written by the kernel over PCIe
     Pinned q_desc, q_res, q_arena;
-    // tcsum_host_batch_peso from pageable memory: two pinned slots the bytes
-    // pass through on their way to the copy engine, and each slot's copy-done event
-    Pinned q_page[2];
-    hipEvent_t pev[2] = {};
     // queue server (tcsum_queue_server): a resident grid serving host-queue
     // jobs posted through pinned memory, instead of a launch + wait per job
     bool srv_on = false;      // enabled for this device
@@ -175,9 +171,6 @@ int ctx_init(Ctx &c, int dev)
         if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
             return TCSUM_ERR_SYS;
     for (auto &e : c.hev)
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
-            return TCSUM_ERR_SYS;
-    for (auto &e : c.pev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
             return TCSUM_ERR_SYS;
     if (hipHostMalloc(&c.desc, 64, hipHostMallocCoherent) != hipSuccess ||
@@ -438,7 +431,7 @@ static const struct {
     {"server_max", tcsum::KNOB_SERVER_MAX}, {"server_trace", tcsum::KNOB_SERVER_TRACE},
     {"server_idle_ms", tcsum::KNOB_SERVER_IDLE_MS}, {"server_wgs", tcsum::KNOB_SERVER_WGS},
     {"hostq_dma_kb", tcsum::KNOB_HOSTQ_DMA_KB}, {"hostq_dma_keep_mb", tcsum::KNOB_HOSTQ_DMA_KEEP_MB},
-    {"copy_threads", tcsum::KNOB_COPY_THREADS}, {"page_stage", tcsum::KNOB_PAGE_STAGE},
+    {"copy_threads", tcsum::KNOB_COPY_THREADS},
 };
 
 static int knob_of(const char *key)
@@ -796,41 +789,11 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     auto span_bytes = [](const HostSpan &sp) {
         return sp.hi > sp.lo ? (((sp.hi - (sp.lo & ~uint64_t(15))) + 15) & ~uint64_t(15)) + 16 : 16;
     };
-    // Pageable caller memory goes through the context's two pinned slots: the
-    // workers copy a slice into one while the copy engine drains the other, so
-    // every DMA reads memory the library owns (the runtime's own pageable path
-    // pins or stages the caller's pages per call).
-    const bool pageable = tcsum::knob(tcsum::KNOB_PAGE_STAGE) != 0 && mapped_host(host_arena) == nullptr;
-    constexpr uint64_t kPageSlot = 32ull << 20;
-    bool slot_busy[2] = {false, false};
-    int slot_turn = 0;
-    auto copy_staged = [&](uint8_t *dst, const uint8_t *src, uint64_t bytes) -> hipError_t {
-        for (uint64_t o = 0; o < bytes; o += kPageSlot) {
-            const int s = slot_turn;
-            slot_turn ^= 1;
-            if (slot_busy[s])
-                if (const hipError_t e = hipEventSynchronize(c.pev[s]); e != hipSuccess)
-                    return e;
-            const uint64_t len = std::min(kPageSlot, bytes - o);
-            if (!c.q_page[s].reserve(kPageSlot))
-                return hipErrorOutOfMemory;
-            par_memcpy(c.q_page[s].h, src + o, len);
-            if (const hipError_t e = hipMemcpyAsync(dst + o, c.q_page[s].h, len, hipMemcpyHostToDevice, cs);
-                e != hipSuccess)
-                return e;
-            if (const hipError_t e = hipEventRecord(c.pev[s], cs); e != hipSuccess)
-                return e;
-            slot_busy[s] = true;
-        }
-        return hipSuccess;
-    };
     // copy a span to `dbase` (the device address arena offset 0 has there)
     auto copy_bytes = [&](uint8_t *dbase, const HostSpan &sp) {
         if (sp.hi <= sp.lo)
             return hipSuccess;
         const uint64_t lo = sp.lo & ~uint64_t(15), hi = std::min(arena_bytes, (sp.hi + 15) & ~uint64_t(15));
-        if (pageable)
-            return copy_staged(dbase + lo, h + lo, hi - lo);
         return hipMemcpyAsync(dbase + lo, h + lo, hi - lo, hipMemcpyHostToDevice, cs);
     };
     // once a copy is queued, an error return first drains both streams: no
@@ -1555,7 +1518,7 @@ int release_ctx(Ctx &c, int dev)
     c.d_descs = nullptr;
     c.d_out = nullptr;
     c.d_arena_cap = c.d_descs_cap = c.d_out_cap = 0;
-    for (Pinned *q : {&c.q_desc, &c.q_res, &c.q_arena, &c.q_page[0], &c.q_page[1]}) {
+    for (Pinned *q : {&c.q_desc, &c.q_res, &c.q_arena}) {
         if (q->h)
             (void)hipHostFree(q->h);
         q->h = q->d = nullptr;

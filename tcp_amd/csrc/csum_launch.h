@@ -45,7 +45,6 @@ enum Knob : int {
     KNOB_HOSTQ_DMA_KB, // host-queue batches from this span on go through the copy engine (262144)
     KNOB_HOSTQ_DMA_KEEP_MB, // device arena kept between host-queue calls up to this size (256)
     KNOB_COPY_THREADS, // host threads of a parallel gather / scatter pass (16)
-    KNOB_PAGE_STAGE, // 0: tcsum_host_batch_peso hands pageable memory to the runtime's copy (1)
     KNOB_COUNT
 };
 int64_t knob(Knob k);

@@ -773,19 +773,14 @@ def test_huge_ipv4_batch_index_math(tc, torch, oracle, geometry):
     np.testing.assert_array_equal(vflags[tidx].cpu().numpy(), evf)
 
 
-@pytest.mark.parametrize("page_stage", [None, 0])
 @pytest.mark.parametrize("order,chunk_mb", [("permuted", None), ("offset", None), ("offset", "1")])
-def test_host_batch_end_to_end(tc, oracle, knobs, order, chunk_mb, page_stage):
+def test_host_batch_end_to_end(tc, oracle, knobs, order, chunk_mb):
     """Pageable host arena -> H2D -> kernel -> D2H matches the device-resident
     path: descriptors in any order (one span copy) and in offset order (the
-    chunk pipeline; 1 MiB chunks = one per 4096-segment block, 11 chunks);
-    the arena's bytes through the library's two pinned slots (default) or
-    handed to the runtime's pageable copy (page_stage=0)."""
+    chunk pipeline; 1 MiB chunks = one per 4096-segment block, 11 chunks)."""
     from tcp_amd import workload
     if chunk_mb:
         knobs(e2e_chunk_mb=int(chunk_mb))
-    if page_stage is not None:
-        knobs(page_stage=page_stage)
     b = workload.make_batch("mtu", n=43000)
     host = oracle.synth_fill(b.byte_base, b.alloc_bytes, b.seed)
     rng = np.random.default_rng(3)
@@ -794,9 +789,8 @@ def test_host_batch_end_to_end(tc, oracle, knobs, order, chunk_mb, page_stage):
     np.testing.assert_array_equal(out, oracle.batch_peso(host, d, nthreads=8))
 
 
-@pytest.mark.parametrize("page_stage", [None, 0])
 @pytest.mark.parametrize("case", ["late_low", "rest_empty", "lead_sparse", "chunks"])
-def test_host_batch_lead_and_rest(tc, oracle, knobs, case, page_stage):
+def test_host_batch_lead_and_rest(tc, oracle, knobs, case):
     """The host batch's lead (its first 64 MiB of segments, copied before the
     rest of the descriptors are read, into a buffer of its own when dense)
     and the rest: a later segment back inside / below the lead's span, a rest
@@ -814,8 +808,6 @@ def test_host_batch_lead_and_rest(tc, oracle, knobs, case, page_stage):
         d = d[::2].copy()  # every other 1500-B slot: the lead's span is 2x its bytes
     else:
         knobs(e2e_chunk_mb=8)
-    if page_stage is not None:
-        knobs(page_stage=page_stage)
     out = tc.host_batch_peso(host, d)
     np.testing.assert_array_equal(out, oracle.batch_peso(host, d, nthreads=8))
 

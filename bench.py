@@ -326,6 +326,25 @@ def is_step_kernel(name: str) -> bool:
     return "k_segments" in name or "k_ipv4<" in name or "k_tx_scatter" in name or "k_flat_" in name
 
 
+def step_counter(files, counter: str):
+    """One step's value of `counter` from rocprofv3 counter-collection CSVs:
+    per step kernel the median over its launches, summed over the kernels a
+    step launches (tx fill: k_ipv4 + k_tx_scatter).  Only kernels launched
+    every step count: rx's setup runs one tx fill (a k_ipv4 of another shape +
+    k_tx_scatter) that is no part of its step.  None without a step kernel."""
+    per = {}  # kernel name -> values
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                name = row.get("Kernel_Name", "")
+                if is_step_kernel(name) and row.get("Counter_Name", counter) == counter:
+                    per.setdefault(name.split("(")[0], []).append(float(row["Counter_Value"]))
+    if not per:
+        return None
+    top = max(len(v) for v in per.values())
+    return sum(sorted(v)[len(v) // 2] for v in per.values() if len(v) == top)
+
+
 def pmc_traffic(config: str):
     """HBM bytes per launch from rocprofv3 counters, in separate passes
     (FETCH_SIZE, then WRITE_SIZE), run as a child before this process touches
@@ -351,17 +370,11 @@ def pmc_traffic(config: str):
             os.makedirs(keep, exist_ok=True)
             for i, f in enumerate(files):
                 shutil.copy(f, os.path.join(keep, f"pmc_{counter.lower()}_{config}{'_%d' % i if i else ''}.csv"))
-        per = {}  # kernel name -> values; a step is one launch of each (tx fill: k_ipv4 + k_tx_scatter)
-        for f in files:
-            with open(f) as fh:
-                for row in csv.DictReader(fh):
-                    name = row.get("Kernel_Name", "")
-                    if is_step_kernel(name) and row.get("Counter_Name", counter) == counter:
-                        per.setdefault(name.split("(")[0], []).append(float(row["Counter_Value"]))
+        v = step_counter(files, counter)
         shutil.rmtree(d, ignore_errors=True)
-        if not per:
+        if v is None:
             return None, f"no {counter} rows for the checksum kernel", None
-        vals[counter] = sum(sorted(v)[len(v) // 2] for v in per.values())
+        vals[counter] = v
     raw = {k: v * 1024 for k, v in vals.items()}  # KiB -> bytes, as the counters report them
     if PMC_CALIB is None:
         traffic = raw["FETCH_SIZE"] * 2 + raw["WRITE_SIZE"]

@@ -112,6 +112,28 @@ def test_calibrated_traffic_accounting():
         assert abs(t5 - nominal - 0.05 * reads) < 1e-6 * nominal
 
 
+def test_step_counter_counts_only_kernels_of_every_step(tmp_path):
+    """A step's counter value: the median launch of each kernel the step runs,
+    summed (the deferred tx fill's two kernels); a setup kernel launched once
+    (rx's preparing tx fill, the synthetic fill) is no part of it -- round 4's
+    rx line first counted it and reported 2x its traffic."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    def csv_of(rows):
+        f = tmp_path / f"c{len(list(tmp_path.iterdir()))}.csv"
+        f.write_text("Kernel_Name,Counter_Name,Counter_Value\n" +
+                     "".join(f'"{k}(args)",FETCH_SIZE,{v}\n' for k, v in rows))
+        return str(f)
+
+    rx = [("void tcsum::k_ipv4<32, 6, 1, 256, 0>", 200.0), ("tcsum::k_tx_scatter", 50.0),
+          ("tcsum::k_synth_fill", 999.0)] + [("void tcsum::k_ipv4<16, 6, 2, 256, 0>", 100.0 + i) for i in range(7)]
+    assert bench.step_counter([csv_of(rx)], "FETCH_SIZE") == 103.0
+    tx = [("void tcsum::k_ipv4<32, 6, 1, 256, 0>", 100.0)] * 7 + [("tcsum::k_tx_scatter", 10.0)] * 7
+    assert bench.step_counter([csv_of(tx)], "FETCH_SIZE") == 110.0
+    assert bench.step_counter([csv_of([("tcsum::k_synth_fill", 1.0)])], "FETCH_SIZE") is None
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("world", [4, 8])
 def test_launcher_rehearsal_many_ranks(world):

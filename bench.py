@@ -55,9 +55,11 @@ def parse():
     ap.add_argument("--config", default="mtu", help="headline workload (mtu|tso|mixed|mixed_aligned)")
     ap.add_argument("--secondary", default="tso,mixed,mixed_aligned,mixed_tx,mixed_txo,mixed_rx",
                     help="extra configs measured at N=1")
-    ap.add_argument("--settle-ms", type=float, default=30.0,
+    ap.add_argument("--settle-ms", type=float, default=300.0,
                     help="untimed: the warm-up also lasts at least this long (GPU clocks out of idle "
-                         "whatever W is; 0 = exactly W launches)")
+                         "whatever W is; 0 = exactly W launches).  300: with 30 one box read the headline "
+                         "at 0.908 against 0.935 with 300 in the same call, and the secondary configs "
+                         "1-2.5 %% low (profiles/r04/gap/)")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")

@@ -12,6 +12,8 @@
 
 #include <stdint.h>
 
+#include "tcsum.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -48,9 +50,31 @@ int tcsum_debug_set(const char *key, int64_t value);
 
 /* The knob's value (-1 = the router's choice; -2 = unknown key).  Two
  * read-only keys: "scratch_reserved" (bytes the tx fill's scratch pool holds on
- * the calling thread's device) and "last_sys_error" (the last TCSUM_ERR_SYS
- * of tcsum_host_batch_peso: step * 1000 + the hipError_t; 0 = none). */
+ * the calling thread's device) and "last_sys_error": the last HIP call that
+ * failed under any TCSUM_ERR_SYS / TCSUM_ERR_MEM return of the library, as
+ * step * 1000 + its hipError_t (0 = none yet).  Steps:
+ *    1-16  tcsum_host_batch_peso (1 set device, 2-5 copies, 6-7 events,
+ *          8 launch, 9 results copy, 10-11 stream syncs, 13-16 allocations)
+ *   20-25  device context init (any entry point that creates it)
+ *   31-37  host-queue IPv4 batches (31 set device, 32-33 pinned staging,
+ *          34-35 copy-engine pieces, 36 launch, 37 wait)
+ *   40-49  queue / call server set-up, launch, stop
+ *   50-52  tcsum_release;  60-61 tcsum_host_register / unregister
+ *   70     a device-resident batch call's launch */
 int64_t tcsum_debug_get(const char *key);
+
+/* The plan tcsum_host_batch_peso makes for a batch of n segments in an
+ * arena of arena_bytes, without touching a device (host arithmetic only):
+ * the copies and kernel launches it would queue, in queue order, as rows of
+ * five u64 -- {0, buffer, host lo, host hi, buffer offset of lo} for a copy
+ * of host bytes [lo, hi) into device buffer 0 (the lead's) or 1 (the
+ * arena's), {1, buffer, i0, i1, arena offset of the buffer's byte 0} for a
+ * kernel over segments [i0, i1) reading that buffer -- at most max_rows of
+ * them written; buf_bytes[0..1]: the two buffers' sizes (0: unused).  Uses
+ * the "e2e_chunk_mb" knob like the call.  Returns the row count, or
+ * TCSUM_ERR_PARAM (a segment outside the arena, as the call would). */
+int64_t tcsum_debug_plan_host_peso(const tcsum_peso_t *segs, uint32_t n, uint64_t arena_bytes, uint64_t *rows,
+                                   uint32_t max_rows, uint64_t *buf_bytes);
 
 /* The route a batch call would take for a mean range length, with the knobs
  * applied: out[0] lanes, out[1] loads, out[2] xcd, out[3] packed K (0 = off),

@@ -65,6 +65,7 @@ SIGNATURES = {
     "tcsum_debug_set": (_I, [ctypes.c_char_p, ctypes.c_int64]),
     "tcsum_debug_get": (ctypes.c_int64, [ctypes.c_char_p]),
     "tcsum_debug_route": (None, [_U64, ctypes.POINTER(ctypes.c_int32)]),
+    "tcsum_debug_plan_host_peso": (ctypes.c_int64, [_V, _U32, _U64, _V, _U32, _V]),
 }
 
 # tcsum_synth.h: libtcsum_bench.so (synthetic batches, load probes)
@@ -153,7 +154,7 @@ def pcap_lib() -> ctypes.CDLL:
 def check(rc: int, what: str) -> None:
     if rc != OK:
         extra = ""
-        if rc == ERR_SYS and what.startswith("tcsum_host_batch_peso"):
-            v = lib().tcsum_debug_get(b"last_sys_error")  # step * 1000 + hipError_t
-            extra = f" (step {v // 1000}, hipError_t {v % 1000})"
+        if rc in (ERR_SYS, ERR_MEM):
+            v = lib().tcsum_debug_get(b"last_sys_error")  # step * 1000 + hipError_t (tcsum_debug.h)
+            extra = f" (last failed HIP call: step {v // 1000}, hipError_t {v % 1000})"
         raise RuntimeError(f"{what} failed with net_err_t {rc}{extra}")

@@ -13,6 +13,22 @@
 
 namespace tcsum {
 
+// The first failed launch status of this thread since the last take (each
+// launch reports its own status through launch(), csum_device.h, never the
+// thread's last-error slot).
+static thread_local hipError_t t_launch_rc = hipSuccess;
+static void note_launch(hipError_t e)
+{
+    if (t_launch_rc == hipSuccess)
+        t_launch_rc = e;
+}
+static hipError_t take_launch_rc()
+{
+    const hipError_t e = t_launch_rc;
+    t_launch_rc = hipSuccess;
+    return e;
+}
+
 // k_ipv4's loads and nothing else (measurement: tcsum_probe_ipv4): the 16-B
 // descriptor, the two or three default-policy header chunks (four for rx),
 // the line-aligned nontemporal data pass -- same lanes, same clamping, same
@@ -433,17 +449,17 @@ static hipError_t window_read(const u32x4 *p, uint64_t nchunks, int dep, const u
     const dim3 grid((uint32_t)((nchunks + CH - 1u) / CH));
     const uint32_t xg = (uint32_t)route(1500).xcd;
     switch (dep) {
-    case 0: hipLaunchKernelGGL((k_probe_window<W, U, 0>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
-    case 1: hipLaunchKernelGGL((k_probe_window<W, U, 1>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
-    case 2: hipLaunchKernelGGL((k_probe_window<W, U, 2>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
-    case 3: hipLaunchKernelGGL((k_probe_window<W, U, 3>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
-    case 4: hipLaunchKernelGGL((k_probe_window<W, U, 0, 1, false>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
-    case 5: hipLaunchKernelGGL((k_probe_window<W, U, 0, 0, true>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
-    case 6: hipLaunchKernelGGL((k_probe_window<W, U, 0, 1, true>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
-    case 7: hipLaunchKernelGGL((k_probe_window<W, U, 3, 1, true>), grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg); break;
+    case 0: note_launch(launch(k_probe_window<W, U, 0>, grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg)); break;
+    case 1: note_launch(launch(k_probe_window<W, U, 1>, grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg)); break;
+    case 2: note_launch(launch(k_probe_window<W, U, 2>, grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg)); break;
+    case 3: note_launch(launch(k_probe_window<W, U, 3>, grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg)); break;
+    case 4: note_launch(launch(k_probe_window<W, U, 0, 1, false>, grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg)); break;
+    case 5: note_launch(launch(k_probe_window<W, U, 0, 0, true>, grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg)); break;
+    case 6: note_launch(launch(k_probe_window<W, U, 0, 1, true>, grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg)); break;
+    case 7: note_launch(launch(k_probe_window<W, U, 3, 1, true>, grid, dim3(W * 64), 0, stream, p, nchunks, word, descs, sink, xg)); break;
     default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
+    return take_launch_rc();
 }
 
 static hipError_t launch_probe_window(const void *p, uint64_t nbytes, int waves, int loads, int dep,
@@ -483,26 +499,26 @@ static hipError_t launch_probe_desc(const void *arena, const void *descs, uint32
                                                                           : kPkMaxRanges * kPkWaves;
         if ((n + K - 1) / K >= (1u << 24))
             return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_segments_pk<MODE_PESO, kPkWaves, kPkLoads, true>), dim3((n + K - 1) / K),
+        note_launch(launch(k_segments_pk<MODE_PESO, kPkWaves, kPkLoads, true>, dim3((n + K - 1) / K),
                            dim3(kPkWaves * 64), 0, stream, a, descs, n, reinterpret_cast<uint16_t *>(sink), 0u, xg,
-                           K);
-        return hipGetLastError();
+                           K));
+        return take_launch_rc();
     }
     if (g.lanes == 1024 && g.loads == 4) { // k_segments_wgx<16, 32, 4>'s loads
         if (n >= (1u << 22))
             return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_segments_wgx<16, 32, 4, MODE_PESO, true>), dim3(n), dim3(1024), 0, stream, a, descs, n,
-                           reinterpret_cast<uint16_t *>(sink), 0u, xg);
-        return hipGetLastError();
+        note_launch(launch(k_segments_wgx<16, 32, 4, MODE_PESO, true>, dim3(n), dim3(1024), 0, stream, a, descs, n,
+                           reinterpret_cast<uint16_t *>(sink), 0u, xg));
+        return take_launch_rc();
     }
 #define TCSUM_PD(GG, UU)                                                                                     \
     if (g.lanes == GG && g.loads == UU) {                                                                    \
         const uint32_t per_block = GG == 256 ? 1u : 256u / GG;                                               \
         if ((n + per_block - 1) / per_block >= (1u << 24))                                                   \
             return hipErrorInvalidValue;                                                                     \
-        hipLaunchKernelGGL((k_probe_desc<GG, UU>), dim3((n + per_block - 1) / per_block), dim3(256), 0, stream, a, \
-                           descs, n, sink, xg);                                                              \
-        return hipGetLastError();                                                                            \
+        note_launch(launch(k_probe_desc<GG, UU>, dim3((n + per_block - 1) / per_block), dim3(256), 0, stream, a, \
+                           descs, n, sink, xg));                                                              \
+        return take_launch_rc();                                                                            \
     }
     TCSUM_PD(4, 1) TCSUM_PD(4, 2) TCSUM_PD(8, 4) TCSUM_PD(16, 3) TCSUM_PD(16, 4) TCSUM_PD(16, 6) TCSUM_PD(16, 8)
     TCSUM_PD(32, 6) TCSUM_PD(256, 16)
@@ -522,10 +538,10 @@ static hipError_t launch_probe_tile(const void *p, uint64_t nbytes, int G, int U
 #define TCSUM_PT(GG, UU)                                                                         \
     if (G == GG && U == UU) {                                                                  \
         if (dep)                                                                               \
-            hipLaunchKernelGGL((k_probe_tile<GG, UU, true>), grid, dim3(256), 0, stream, q, nchunks, sink, xg); \
+            note_launch(launch(k_probe_tile<GG, UU, true>, grid, dim3(256), 0, stream, q, nchunks, sink, xg)); \
         else                                                                                   \
-            hipLaunchKernelGGL((k_probe_tile<GG, UU, false>), grid, dim3(256), 0, stream, q, nchunks, sink, xg); \
-        return hipGetLastError();                                                              \
+            note_launch(launch(k_probe_tile<GG, UU, false>, grid, dim3(256), 0, stream, q, nchunks, sink, xg)); \
+        return take_launch_rc();                                                              \
     }
     TCSUM_PT(16, 4) TCSUM_PT(16, 6) TCSUM_PT(16, 8) TCSUM_PT(32, 4) TCSUM_PT(32, 6) TCSUM_PT(32, 8)
     TCSUM_PT(64, 4) TCSUM_PT(64, 8) TCSUM_PT(256, 4) TCSUM_PT(256, 8) TCSUM_PT(256, 16)
@@ -543,8 +559,8 @@ static hipError_t launch_probe_read(const void *p, uint64_t nbytes, uint32_t *si
         return hipSuccess;
     const uint64_t per_block = 4ull * 64 * 4;
     const dim3 grid((uint32_t)((nchunks + per_block - 1) / per_block));
-    hipLaunchKernelGGL(k_probe_read<4>, grid, dim3(256), 0, stream, static_cast<const u32x4 *>(p), nchunks, sink, 1u);
-    return hipGetLastError();
+    note_launch(launch(k_probe_read<4>, grid, dim3(256), 0, stream, static_cast<const u32x4 *>(p), nchunks, sink, 1u));
+    return take_launch_rc();
 }
 
 // ext_side (PM_TX): the caller's 2n words for the values and positions; then
@@ -581,24 +597,24 @@ static hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, 
 #define TCSUM_PI(GG, UU)                                                                                     \
     if (e == hipErrorInvalidValue && g.lanes == GG && g.loads == UU) {                                       \
         if (mode == PM_RX)                                                                                   \
-            hipLaunchKernelGGL((k_probe_ipv4<GG, UU, PM_RX>), dim3((uint32_t)blocks), dim3(256), 0, stream, a,   \
-                               pkts, n, sink, xg, vals, posv);                                              \
+            note_launch(launch(k_probe_ipv4<GG, UU, PM_RX>, dim3((uint32_t)blocks), dim3(256), 0, stream, a,   \
+                               pkts, n, sink, xg, vals, posv));                                              \
         else if (mode == PM_TX)                                                                              \
-            hipLaunchKernelGGL((k_probe_ipv4<GG, UU, PM_TX>), dim3((uint32_t)blocks), dim3(256), 0, stream, a,   \
-                               pkts, n, sink, xg, vals, posv);                                              \
+            note_launch(launch(k_probe_ipv4<GG, UU, PM_TX>, dim3((uint32_t)blocks), dim3(256), 0, stream, a,   \
+                               pkts, n, sink, xg, vals, posv));                                              \
         else                                                                                                 \
-            hipLaunchKernelGGL((k_probe_ipv4<GG, UU, PM_SUMS>), dim3((uint32_t)blocks), dim3(256), 0, stream, a, \
-                               pkts, n, sink, xg, vals, posv);                                              \
-        e = hipGetLastError();                                                                               \
+            note_launch(launch(k_probe_ipv4<GG, UU, PM_SUMS>, dim3((uint32_t)blocks), dim3(256), 0, stream, a, \
+                               pkts, n, sink, xg, vals, posv));                                              \
+        e = take_launch_rc();                                                                               \
     }
     TCSUM_PI(16, 1) TCSUM_PI(16, 2) TCSUM_PI(16, 3) TCSUM_PI(16, 4) TCSUM_PI(16, 6) TCSUM_PI(16, 8)
     TCSUM_PI(32, 6) TCSUM_PI(64, 4) TCSUM_PI(64, 16)
 #undef TCSUM_PI
     if (mode == PM_TX && !ext_side) {
         if (e == hipSuccess) { // the product's scatter, on the probe's values and positions
-            hipLaunchKernelGGL(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, const_cast<uint8_t *>(a),
-                               pkts, n, vals, posv);
-            e = hipGetLastError();
+            note_launch(launch(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, const_cast<uint8_t *>(a),
+                               pkts, n, vals, posv));
+            e = take_launch_rc();
         }
         const hipError_t f = hipFreeAsync(side, stream);
         e = e != hipSuccess ? e : f;
@@ -617,9 +633,9 @@ static hipError_t launch_floor_prepare(const void *arena, uint64_t nbytes, const
     hipError_t e = launch_probe_ipv4(arena, pkts, n, mean_len, PM_TX, vals, stream, vals);
     if (e != hipSuccess)
         return e;
-    hipLaunchKernelGGL(k_floor_index, dim3((n + 256u) / 256u), dim3(256), 0, stream, pkts, n, posv, nbytes, fpos,
-                       ffirst, floor_windows(nbytes));
-    return hipGetLastError();
+    note_launch(launch(k_floor_index, dim3((n + 256u) / 256u), dim3(256), 0, stream, pkts, n, posv, nbytes, fpos,
+                       ffirst, floor_windows(nbytes)));
+    return take_launch_rc();
 }
 
 static hipError_t launch_floor(void *arena, uint64_t nbytes, const uint64_t *fpos, const uint32_t *vals, uint32_t n,
@@ -631,17 +647,17 @@ static hipError_t launch_floor(void *arena, uint64_t nbytes, const uint64_t *fpo
     uint8_t *a = static_cast<uint8_t *>(arena);
     const u32x4 *q = static_cast<const u32x4 *>(arena);
     if (variant == 0) {
-        hipLaunchKernelGGL(k_floor_stream, dim3(floor_windows(nbytes)), dim3(256), 0, stream, q, nchunks, a, nbytes,
-                           fpos, ffirst, n, sink);
-        return hipGetLastError();
+        note_launch(launch(k_floor_stream, dim3(floor_windows(nbytes)), dim3(256), 0, stream, q, nchunks, a, nbytes,
+                           fpos, ffirst, n, sink));
+        return take_launch_rc();
     }
     if (variant != 1)
         return hipErrorInvalidValue;
     hipError_t e = launch_probe_read(arena, nbytes, sink, stream);
     if (e != hipSuccess)
         return e;
-    hipLaunchKernelGGL(k_floor_scatter, dim3((n + 255u) / 256u), dim3(256), 0, stream, a, nbytes, fpos, vals, n);
-    return hipGetLastError();
+    note_launch(launch(k_floor_scatter, dim3((n + 255u) / 256u), dim3(256), 0, stream, a, nbytes, fpos, vals, n));
+    return take_launch_rc();
 }
 
 static hipError_t launch_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_base, uint64_t seed,
@@ -653,9 +669,9 @@ static hipError_t launch_synth_fill(void *arena, uint64_t nbytes, uint64_t byte_
     uint64_t blocks = (units + 255) / 256;
     if (blocks > 65536)
         blocks = 65536;
-    hipLaunchKernelGGL(k_synth_fill, dim3((uint32_t)blocks), dim3(256), 0, stream,
-                       static_cast<uint8_t *>(arena), nbytes, byte_base / 8, seed);
-    return hipGetLastError();
+    note_launch(launch(k_synth_fill, dim3((uint32_t)blocks), dim3(256), 0, stream,
+                       static_cast<uint8_t *>(arena), nbytes, byte_base / 8, seed));
+    return take_launch_rc();
 }
 
 static hipError_t launch_synth_ipv4(void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t seed,
@@ -663,9 +679,9 @@ static hipError_t launch_synth_ipv4(void *arena, const tcsum_pkt_t *pkts, uint32
 {
     if (n == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(k_synth_ipv4, dim3((n + 255) / 256), dim3(256), 0, stream,
-                       static_cast<uint8_t *>(arena), pkts, n, seed);
-    return hipGetLastError();
+    note_launch(launch(k_synth_ipv4, dim3((n + 255) / 256), dim3(256), 0, stream,
+                       static_cast<uint8_t *>(arena), pkts, n, seed));
+    return take_launch_rc();
 }
 
 // The byte-window stream in other workgroup shapes and as load probes
@@ -688,11 +704,11 @@ static hipError_t flat_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n
     static std::atomic<uint32_t> g_gen{0x80000000u}; // apart from the product's
     const uint32_t gen = g_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
     const uint64_t pthreads = (uint64_t)n + 1u > nw ? (uint64_t)n + 1u : nw;
-    hipLaunchKernelGGL((k_flat_plan<WB>), dim3((uint32_t)((pthreads + 255u) / 256u)), dim3(256), 0, stream, arena, pkts,
-                       n, (uint32_t)nw, plan, wfirst, slot, gen);
-    hipLaunchKernelGGL((k_flat_ipv4<IP_SUMS, W, U, PROBE>), dim3((uint32_t)nw), dim3(W * 64), 0, stream, arena, pkts, n,
-                       out, flags, (int8_t *)nullptr, 0u, 64u, plan, wfirst, slot, gen);
-    e = hipGetLastError();
+    note_launch(launch(k_flat_plan<WB>, dim3((uint32_t)((pthreads + 255u) / 256u)), dim3(256), 0, stream, arena, pkts,
+                       n, (uint32_t)nw, plan, wfirst, slot, gen));
+    note_launch(launch(k_flat_ipv4<IP_SUMS, W, U, PROBE>, dim3((uint32_t)nw), dim3(W * 64), 0, stream, arena, pkts, n,
+                       out, flags, (int8_t *)nullptr, 0u, 64u, plan, wfirst, slot, gen));
+    e = take_launch_rc();
     const hipError_t f = hipFreeAsync(scr, stream);
     return e != hipSuccess ? e : f;
 }
@@ -733,8 +749,8 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
     const dim3 grid((n + per - 1u) / per), blk((uint32_t)wg);
     uint8_t *fl = nullptr;
 #define TCSUM_SH(KERN)                                                                                   \
-    hipLaunchKernelGGL(KERN, grid, blk, 0, stream, arena, pkts, n, out, fl, verdict, 0u, xg);            \
-    return hipGetLastError();
+    note_launch(launch(KERN, grid, blk, 0, stream, arena, pkts, n, out, fl, verdict, 0u, xg));            \
+    return take_launch_rc();
     if (mode == IP_SUMS) {
         if (occ == 0 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256>)) }
         if (occ == 0 && wg == 512) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 512>)) }

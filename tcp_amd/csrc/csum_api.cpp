@@ -51,10 +51,10 @@ struct Pinned {
     uint8_t *h = nullptr;
     uint8_t *d = nullptr;
     size_t cap = 0;
-    bool reserve(size_t bytes)
+    hipError_t reserve(size_t bytes)
     {
         if (bytes <= cap)
-            return true;
+            return hipSuccess;
         size_t c = 1 << 16;
         while (c < bytes)
             c <<= 1;
@@ -62,12 +62,18 @@ struct Pinned {
             (void)hipHostFree(h);
         h = d = nullptr;
         cap = 0;
-        if (hipHostMalloc(reinterpret_cast<void **>(&h), c, hipHostMallocCoherent) != hipSuccess)
-            return false;
-        if (hipHostGetDevicePointer(reinterpret_cast<void **>(&d), h, 0) != hipSuccess)
-            return false;
+        hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&h), c, hipHostMallocCoherent);
+        if (e != hipSuccess) {
+            h = nullptr;
+            return e;
+        }
+        if ((e = hipHostGetDevicePointer(reinterpret_cast<void **>(&d), h, 0)) != hipSuccess) {
+            (void)hipHostFree(h);
+            h = d = nullptr;
+            return e;
+        }
         cap = c;
-        return true;
+        return hipSuccess;
     }
 };
 
@@ -145,6 +151,38 @@ int g_default_dev = -1;
     abort();
 }
 
+// The last failed HIP call of a batch, init or release path:
+// step * 1000 + the hipError_t (tcsum_debug_get "last_sys_error"; 0 = none
+// yet).  Steps: include/tcsum_debug.h.  Returns `rc`.
+std::atomic<int64_t> g_last_sys{0};
+int note_err(int step, hipError_t e, int rc)
+{
+    g_last_sys.store((int64_t)step * 1000 + (int64_t)e, std::memory_order_relaxed);
+    // the failed call's error is returned as rc: it must not also reach the
+    // caller's next hipGetLastError() as an error of the caller's own
+    if (e != hipSuccess && hipPeekAtLastError() == e)
+        (void)hipGetLastError();
+    return rc;
+}
+int note_sys(int step, hipError_t e) { return note_err(step, e, TCSUM_ERR_SYS); }
+int note_mem(int step, hipError_t e) { return note_err(step, e, TCSUM_ERR_MEM); }
+
+// hipStreamQuery for a poll: hipErrorNotReady is an answer there, not a
+// failure.  A runtime that also stores it in the calling thread's last-error
+// slot would hand it to the caller's next hipGetLastError() (PyTorch checks
+// every kernel launch of its own that way) as an error of the caller's; so a
+// NotReady this poll left in a slot that was clear before it is taken out
+// again.  (No launch of this library reads that slot: launch(),
+// csum_device.h, returns each launch's own status.)
+hipError_t poll_stream(hipStream_t s)
+{
+    const hipError_t before = hipPeekAtLastError();
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipErrorNotReady && before == hipSuccess && hipPeekAtLastError() == hipErrorNotReady)
+        (void)hipGetLastError();
+    return q;
+}
+
 bool is_gfx950(int dev)
 {
     hipDeviceProp_t p;
@@ -163,22 +201,29 @@ int ctx_init(Ctx &c, int dev)
         return TCSUM_ERR_NOT_SUPPORT;
     if (!is_gfx950(dev))
         return TCSUM_ERR_NOT_SUPPORT;
-    if (hipSetDevice(dev) != hipSuccess)
-        return TCSUM_ERR_SYS;
-    if (hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess)
-        return TCSUM_ERR_SYS;
+    hipError_t e = hipSetDevice(dev);
+    if (e != hipSuccess)
+        return note_sys(20, e);
+    // a failure part-way leaves what was made so far: the next call resumes
+    if (!c.stream && (e = hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking)) != hipSuccess)
+        return note_sys(21, e);
     for (auto &s : c.hs)
-        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
-            return TCSUM_ERR_SYS;
-    for (auto &e : c.hev)
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
-            return TCSUM_ERR_SYS;
-    if (hipHostMalloc(&c.desc, 64, hipHostMallocCoherent) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void **>(&c.result), 64, hipHostMallocCoherent) != hipSuccess)
-        return TCSUM_ERR_MEM;
-    if (hipHostGetDevicePointer(&c.d_desc, c.desc, 0) != hipSuccess ||
-        hipHostGetDevicePointer(reinterpret_cast<void **>(&c.d_result), c.result, 0) != hipSuccess)
-        return TCSUM_ERR_SYS;
+        if (!s && (e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess)
+            return note_sys(22, e);
+    for (auto &ev : c.hev)
+        if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess)
+            return note_sys(23, e);
+    if (!c.desc && (e = hipHostMalloc(&c.desc, 64, hipHostMallocCoherent)) != hipSuccess) {
+        c.desc = nullptr;
+        return note_mem(24, e);
+    }
+    if (!c.result && (e = hipHostMalloc(reinterpret_cast<void **>(&c.result), 64, hipHostMallocCoherent)) != hipSuccess) {
+        c.result = nullptr;
+        return note_mem(24, e);
+    }
+    if ((e = hipHostGetDevicePointer(&c.d_desc, c.desc, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c.d_result), c.result, 0)) != hipSuccess)
+        return note_sys(25, e);
     c.device = dev;
     c.ready = true;
     return TCSUM_OK;
@@ -260,7 +305,7 @@ hipError_t stream_wait(Ctx &c)
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned spins = 1; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq; ++spins) {
         if ((spins & 4095u) == 0) {
-            e = hipStreamQuery(c.stream);
+            e = poll_stream(c.stream);
             if (e != hipSuccess && e != hipErrorNotReady)
                 return e;
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
@@ -399,10 +444,9 @@ int tcsum_host_register(void *p, size_t bytes)
     if (!p || bytes == 0)
         return TCSUM_ERR_PARAM;
     // portable + mapped, like tcsum_host_alloc: every GPU of a *_multi batch maps it
-    if (hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) {
-        (void)hipGetLastError();
-        return TCSUM_ERR_SYS;
-    }
+    if (const hipError_t e = hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+        e != hipSuccess)
+        return note_sys(60, e);
     return TCSUM_OK;
 }
 
@@ -410,10 +454,8 @@ int tcsum_host_unregister(void *p)
 {
     if (!p)
         return TCSUM_ERR_PARAM;
-    if (hipHostUnregister(p) != hipSuccess) {
-        (void)hipGetLastError();
-        return TCSUM_ERR_SYS;
-    }
+    if (const hipError_t e = hipHostUnregister(p); e != hipSuccess)
+        return note_sys(61, e);
     return TCSUM_OK;
 }
 
@@ -452,16 +494,6 @@ int tcsum_debug_set(const char *key, int64_t value)
     return TCSUM_OK;
 }
 
-// The last TCSUM_ERR_SYS of tcsum_host_batch_peso: step * 1000 + the HIP
-// error code (tcsum_debug_get "last_sys_error"; 0 = none yet).
-static std::atomic<int64_t> g_last_sys{0};
-static int note_sys(int step, hipError_t e)
-{
-    g_last_sys.store((int64_t)step * 1000 + (int64_t)e, std::memory_order_relaxed);
-    (void)hipGetLastError();
-    return TCSUM_ERR_SYS;
-}
-
 int64_t tcsum_debug_get(const char *key)
 {
     if (key && strcmp(key, "last_sys_error") == 0)
@@ -489,7 +521,7 @@ void tcsum_debug_route(uint64_t mean_len, int32_t out[5])
 // hipErrorInvalidValue from a launcher: a shape or size it refuses
 static int rc_of(hipError_t e)
 {
-    return e == hipSuccess ? TCSUM_OK : e == hipErrorInvalidValue ? TCSUM_ERR_PARAM : TCSUM_ERR_SYS;
+    return e == hipSuccess ? TCSUM_OK : e == hipErrorInvalidValue ? note_err(70, e, TCSUM_ERR_PARAM) : note_sys(70, e);
 }
 
 static uint64_t mean_of(uint64_t total, uint32_t n) { return total && n ? total / n : 1500; }
@@ -519,7 +551,7 @@ int tcsum_batch(int op, void *arena, const void *descs, uint32_t n, void *out, u
         return TCSUM_OK;
     const uint64_t total = hint ? hint->total_bytes : 0;
     const uint32_t layout = hint ? hint->layout : TCSUM_LAYOUT_UNKNOWN;
-    if (!arena || !descs || layout > TCSUM_LAYOUT_SHUFFLED)
+    if (!arena || !descs || layout > TCSUM_LAYOUT_SHUFFLED || (hint && hint->rsv != 0))
         return TCSUM_ERR_PARAM;
     const Geometry g = route_for(total, n, layout);
     const hipStream_t st = static_cast<hipStream_t>(stream);
@@ -692,6 +724,147 @@ struct HostSpan {
         bad |= o.bad;
     }
 };
+
+extern "C++" { // (inside the extern "C" block: C++ linkage for these helpers)
+// ---- tcsum_host_batch_peso's plan: which bytes go where, which kernels
+// run on which descriptors.  Host arithmetic only (no HIP call), so the plan
+// of any batch can be checked without a device (tcsum_debug_plan_host_peso,
+// tests/test_abi.py): every copy inside the caller's arena and its device
+// buffer, every byte a kernel reads copied before it.
+
+constexpr uint32_t kSpanBlock = 4096; // segments per span block
+
+// The device buffer bytes a span needs: its 16-byte chunks from the one
+// holding lo, plus a 16-byte tail so the last aligned chunk is in bounds.
+uint64_t span_bytes(const HostSpan &sp)
+{
+    return sp.hi > sp.lo ? (((sp.hi - (sp.lo & ~uint64_t(15))) + 15) & ~uint64_t(15)) + 16 : 16;
+}
+
+// The host bytes [lo, hi) a span's copy moves (whole 16-byte chunks, cut at
+// the arena's end); empty when the span is.
+void span_copy(const HostSpan &sp, uint64_t arena_bytes, uint64_t &lo, uint64_t &hi)
+{
+    lo = hi = 0;
+    if (sp.hi <= sp.lo)
+        return;
+    lo = sp.lo & ~uint64_t(15);
+    hi = std::min(arena_bytes, (sp.hi + 15) & ~uint64_t(15));
+}
+
+struct PesoChunk {
+    uint32_t b0, b1; // span blocks [b0, b1)
+    HostSpan sp;
+    int buf;         // 0: the lead's buffer, 1: the arena buffer
+};
+
+struct PesoPlan {
+    uint32_t n = 0, nblk = 0;
+    uint32_t m = 0;      // blocks of the lead
+    bool early = false;  // the lead's copy starts before the rest is looked at
+    uint64_t target = 0; // chunk size in packet bytes
+    HostSpan lead, rest; // the lead's span; the span of the blocks after it (all of them if !early)
+    std::vector<HostSpan> blk;
+    std::vector<PesoChunk> ch;
+    uint32_t r0() const { return early ? m : 0u; }
+    // device buffer sizes and where arena offset 0 sits in each (offset of
+    // arena byte x in buffer b: x - base[b])
+    uint64_t lead_base() const { return lead.hi ? lead.lo & ~uint64_t(15) : 0; }
+    uint64_t rest_base() const { return rest.hi ? rest.lo & ~uint64_t(15) : 0; }
+};
+
+HostSpan span_of_block(const tcsum_peso_t *segs, uint32_t n, uint64_t arena_bytes, size_t k)
+{
+    HostSpan sp;
+    const uint32_t i1 = (uint32_t)std::min<uint64_t>(n, (k + 1) * (uint64_t)kSpanBlock);
+    for (uint32_t i = (uint32_t)k * kSpanBlock; i < i1; ++i) {
+        const uint64_t o = segs[i].offset, l = segs[i].len;
+        sp.bad |= o > arena_bytes || l > arena_bytes - o;
+        if (l) {
+            sp.lo = o < sp.lo ? o : sp.lo;
+            sp.hi = o + l > sp.hi ? o + l : sp.hi;
+            sp.bytes += l;
+        }
+    }
+    return sp;
+}
+
+// Stage 1, on the calling thread before anything else: the chunk size and
+// the lead -- the first blocks, up to 64 MiB of packet bytes.  When they are
+// dense (their span at most 1.25x their bytes) their copy starts at once,
+// into a buffer of their own, and the rest of the descriptors are looked at
+// while it runs (the whole pass first kept the link idle for 420-635 us of a
+// 29-ms batch).  false: a lead segment lies outside the arena.
+bool peso_plan_lead(PesoPlan &pl, const tcsum_peso_t *segs, uint32_t n, uint64_t arena_bytes)
+{
+    pl.n = n;
+    pl.nblk = (n + kSpanBlock - 1) / kSpanBlock;
+    pl.blk.assign(pl.nblk, HostSpan());
+    // Chunks of >= `target` packet bytes (whole span blocks).  All copies go
+    // in order on ONE copy stream, so the host link never idles between
+    // chunks and no two copies compete for it; each chunk's kernel waits on
+    // its copy's event on the kernel stream and runs under the next copy.
+    // Every copy costs ~18 us of link idle before it (rocprofv3
+    // --memory-copy-trace, profiles/r02/e2e_phase.txt), so chunks are large:
+    // a quarter of the batch, at least 64 MiB (debug knob "e2e_chunk_mb": fixed size).
+    const uint32_t step = std::max<uint32_t>(1, n / 64); // the batch's bytes, estimated from 64 segments
+    uint64_t sampled = 0, taken = 0;
+    for (uint32_t i = 0; i < n; i += step, ++taken)
+        sampled += segs[i].len;
+    const uint64_t total_hint = sampled / taken * (uint64_t)n;
+    pl.target = std::max<uint64_t>(64ull << 20, total_hint / 4);
+    if (const int64_t v = tcsum::knob(tcsum::KNOB_E2E_CHUNK_MB); v > 0)
+        pl.target = (uint64_t)v << 20;
+    const uint64_t lead_target = std::min<uint64_t>(pl.target, 64ull << 20);
+    pl.m = 0;
+    while (pl.m < pl.nblk && pl.lead.bytes < lead_target) {
+        pl.blk[pl.m] = span_of_block(segs, n, arena_bytes, pl.m);
+        pl.lead.merge(pl.blk[pl.m]);
+        ++pl.m;
+    }
+    if (pl.lead.bad)
+        return false;
+    pl.early = pl.m < pl.nblk && pl.lead.hi > pl.lead.lo && pl.lead.hi - pl.lead.lo <= pl.lead.bytes + pl.lead.bytes / 4;
+    return true;
+}
+
+// Stage 2 (while the lead's bytes cross): the other blocks' spans, in
+// parallel, and the chunks: [the lead], then the rest in `target`-byte
+// chunks.  false: a segment lies outside the arena.
+bool peso_plan_rest(PesoPlan &pl, const tcsum_peso_t *segs, uint64_t arena_bytes)
+{
+    const uint32_t m = pl.m, nblk = pl.nblk, r0 = pl.r0(), n = pl.n;
+    parallel_for(nblk - m, 16, [&](size_t b, size_t e) {
+        for (size_t k = m + b; k < m + e; ++k)
+            pl.blk[k] = span_of_block(segs, n, arena_bytes, k);
+    });
+    for (uint32_t k = r0; k < nblk; ++k)
+        pl.rest.merge(pl.blk[k]);
+    if (pl.rest.bad)
+        return false;
+    pl.ch.clear();
+    if (pl.early)
+        pl.ch.push_back({0u, m, pl.lead, 0});
+    const size_t first_rest = pl.ch.size();
+    for (uint32_t k = r0; k < nblk; ++k) {
+        if (pl.ch.size() == first_rest || pl.ch.back().sp.bytes >= pl.target)
+            pl.ch.push_back({k, k, HostSpan(), 1});
+        pl.ch.back().sp.merge(pl.blk[k]);
+        pl.ch.back().b1 = k + 1;
+    }
+    // segments in no particular order: every chunk's span covers most of the
+    // batch's, so copy the batch's span once and run one kernel on it
+    uint64_t spans = 0;
+    for (size_t k = first_rest; k < pl.ch.size(); ++k)
+        spans += pl.ch[k].sp.hi > pl.ch[k].sp.lo ? pl.ch[k].sp.hi - pl.ch[k].sp.lo : 0;
+    const uint64_t rest_span = pl.rest.hi > pl.rest.lo ? pl.rest.hi - pl.rest.lo : 0;
+    if (pl.ch.size() > first_rest + 1 && spans > rest_span + rest_span / 4) {
+        pl.ch.resize(first_rest);
+        pl.ch.push_back({r0, nblk, pl.rest, 1});
+    }
+    return true;
+}
+} // extern "C++"
 } // namespace
 
 int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_bytes,
@@ -709,92 +882,43 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     };
     if (!host_arena || !segs || !out || device < 0 || device >= kMaxDev)
         return TCSUM_ERR_PARAM;
-    // Per block of kSpanBlock segments: validity and the byte span [lo, hi)
-    // its segments touch.
-    constexpr uint32_t kSpanBlock = 4096;
-    const uint32_t nblk = (n + kSpanBlock - 1) / kSpanBlock;
-    std::vector<HostSpan> blk(nblk);
-    auto span_of = [&](size_t k) {
-        HostSpan sp;
-        const uint32_t i1 = (uint32_t)std::min<uint64_t>(n, (k + 1) * (uint64_t)kSpanBlock);
-        for (uint32_t i = (uint32_t)k * kSpanBlock; i < i1; ++i) {
-            const uint64_t o = segs[i].offset, l = segs[i].len;
-            sp.bad |= o > arena_bytes || l > arena_bytes - o;
-            if (l) {
-                sp.lo = o < sp.lo ? o : sp.lo;
-                sp.hi = o + l > sp.hi ? o + l : sp.hi;
-                sp.bytes += l;
-            }
-        }
-        return sp;
-    };
-    // Chunks of >= `target` packet bytes (whole span blocks).  All copies go
-    // in order on ONE copy stream, so the host link never idles between
-    // chunks and no two copies compete for it; each chunk's kernel waits on
-    // its copy's event on the kernel stream and runs under the next copy.
-    // Every copy costs ~18 us of link idle before it (rocprofv3
-    // --memory-copy-trace, profiles/r02/e2e_phase.txt), so chunks are large:
-    // a quarter of the batch, at least 64 MiB (debug knob "e2e_chunk_mb": fixed size).
-    const uint32_t step = std::max<uint32_t>(1, n / 64); // the batch's bytes, estimated from 64 segments
-    uint64_t sampled = 0, taken = 0;
-    for (uint32_t i = 0; i < n; i += step, ++taken)
-        sampled += segs[i].len;
-    const uint64_t total_hint = sampled / taken * (uint64_t)n;
-    uint64_t target = std::max<uint64_t>(64ull << 20, total_hint / 4);
-    if (const int64_t v = tcsum::knob(tcsum::KNOB_E2E_CHUNK_MB); v > 0)
-        target = (uint64_t)v << 20;
-    // The lead: the first blocks, up to 64 MiB of packet bytes, looked at on
-    // this thread before anything else.  When they are dense (their span at
-    // most 1.25x their bytes) their copy starts at once, into a buffer of
-    // their own, and the rest of the descriptors are looked at while it runs
-    // (the whole pass first kept the link idle for 420-635 us of a 29-ms
-    // batch).
-    const uint64_t lead_target = std::min<uint64_t>(target, 64ull << 20);
-    uint32_t m = 0;
-    HostSpan lead;
-    while (m < nblk && lead.bytes < lead_target) {
-        blk[m] = span_of(m);
-        lead.merge(blk[m]);
-        ++m;
-    }
-    if (lead.bad)
+    PesoPlan pl;
+    if (!peso_plan_lead(pl, segs, n, arena_bytes))
         return TCSUM_ERR_PARAM;
-    const bool early = m < nblk && lead.hi > lead.lo && lead.hi - lead.lo <= lead.bytes + lead.bytes / 4;
     stamp("lead");
 
     Ctx &c = g_ctx[device];
     std::lock_guard<std::mutex> lk(c.mu);
-    int rc = ctx_init(c, device);
+    int rc = ctx_init(c, device); // a failing HIP call is recorded there (steps 20-25)
     if (rc != TCSUM_OK)
-        return rc == TCSUM_ERR_SYS ? note_sys(12, hipSuccess) : rc;
+        return rc;
     if (const hipError_t e = hipSetDevice(device); e != hipSuccess)
         return note_sys(1, e);
     const uint8_t *h = static_cast<const uint8_t *>(host_arena);
     hipStream_t cs = c.hs[0], ks = c.hs[1];
     // device buffers (grow-only) hold only the spans the segments touch (a
-    // shard of a multi-device batch holds its own part only), plus a 16-byte
-    // tail so the last aligned chunk is in bounds
+    // shard of a multi-device batch holds its own part only)
     auto grow = [](uint8_t *&buf, size_t &cap, size_t need) {
         if (need <= cap)
-            return true;
+            return hipSuccess;
         if (buf)
             (void)hipFree(buf);
         buf = nullptr;
         cap = 0;
-        if (hipMalloc(reinterpret_cast<void **>(&buf), need) != hipSuccess)
-            return false;
+        const hipError_t e = hipMalloc(reinterpret_cast<void **>(&buf), need);
+        if (e != hipSuccess) {
+            buf = nullptr;
+            return e;
+        }
         cap = need;
-        return true;
+        return hipSuccess;
     };
-    auto span_bytes = [](const HostSpan &sp) {
-        return sp.hi > sp.lo ? (((sp.hi - (sp.lo & ~uint64_t(15))) + 15) & ~uint64_t(15)) + 16 : 16;
-    };
-    // copy a span to `dbase` (the device address arena offset 0 has there)
-    auto copy_bytes = [&](uint8_t *dbase, const HostSpan &sp) {
-        if (sp.hi <= sp.lo)
-            return hipSuccess;
-        const uint64_t lo = sp.lo & ~uint64_t(15), hi = std::min(arena_bytes, (sp.hi + 15) & ~uint64_t(15));
-        return hipMemcpyAsync(dbase + lo, h + lo, hi - lo, hipMemcpyHostToDevice, cs);
+    // copy a span into buffer `buf` of the plan
+    uint8_t *base[2] = {nullptr, nullptr}; // device address arena offset 0 has in each buffer
+    auto copy_span = [&](int buf, const HostSpan &sp) {
+        uint64_t lo, hi;
+        span_copy(sp, arena_bytes, lo, hi);
+        return hi > lo ? hipMemcpyAsync(base[buf] + lo, h + lo, hi - lo, hipMemcpyHostToDevice, cs) : hipSuccess;
     };
     // once a copy is queued, an error return first drains both streams: no
     // copy may still read the caller's memory after the call returns
@@ -804,31 +928,20 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         return code;
     };
     auto fail_sys = [&](int step, hipError_t e) { return fail(note_sys(step, e)); };
-    uint8_t *lead_base = nullptr;
-    if (early) {
-        if (!grow(c.d_lead, c.d_lead_cap, span_bytes(lead)))
-            return TCSUM_ERR_MEM;
-        lead_base = c.d_lead - (lead.lo & ~uint64_t(15));
-        if (const hipError_t e = copy_bytes(lead_base, lead); e != hipSuccess)
+    if (pl.early) {
+        if (const hipError_t e = grow(c.d_lead, c.d_lead_cap, span_bytes(pl.lead)); e != hipSuccess)
+            return note_mem(13, e);
+        base[0] = c.d_lead - pl.lead_base();
+        if (const hipError_t e = copy_span(0, pl.lead); e != hipSuccess)
             return fail_sys(2, e);
         stamp("lead copy");
     }
-    // the rest of the descriptors, in parallel
-    const uint32_t r0 = early ? m : 0u; // first block after the lead's copy
-    parallel_for(nblk - m, 16, [&](size_t b, size_t e) {
-        for (size_t k = m + b; k < m + e; ++k)
-            blk[k] = span_of(k);
-    });
-    HostSpan rest;
-    for (uint32_t k = r0; k < nblk; ++k)
-        rest.merge(blk[k]);
-    if (rest.bad)
+    if (!peso_plan_rest(pl, segs, arena_bytes))
         return fail(TCSUM_ERR_PARAM);
     stamp("span pass");
-    const uint64_t glo = rest.hi ? rest.lo & ~uint64_t(15) : 0;
-    if (!grow(c.d_arena, c.d_arena_cap, span_bytes(rest)))
-        return fail(TCSUM_ERR_MEM);
-    uint8_t *const dbase = c.d_arena - glo;
+    if (const hipError_t e = grow(c.d_arena, c.d_arena_cap, span_bytes(pl.rest)); e != hipSuccess)
+        return fail(note_mem(14, e));
+    base[1] = c.d_arena - pl.rest_base();
     if (n > c.d_descs_cap) {
         if (c.d_descs)
             (void)hipFree(c.d_descs);
@@ -837,37 +950,19 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         c.d_descs = nullptr;
         c.d_out = nullptr;
         c.d_descs_cap = c.d_out_cap = 0;
-        if (hipMalloc(reinterpret_cast<void **>(&c.d_descs), sizeof(tcsum_seg_t) * n) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&c.d_out), sizeof(uint16_t) * n) != hipSuccess)
-            return fail(TCSUM_ERR_MEM);
+        hipError_t e = hipMalloc(reinterpret_cast<void **>(&c.d_descs), sizeof(tcsum_seg_t) * n);
+        if (e == hipSuccess)
+            e = hipMalloc(reinterpret_cast<void **>(&c.d_out), sizeof(uint16_t) * n);
+        if (e != hipSuccess) {
+            if (c.d_descs)
+                (void)hipFree(c.d_descs); // both or neither: the caps below describe both
+            c.d_descs = nullptr;
+            c.d_out = nullptr;
+            return fail(note_mem(15, e));
+        }
         c.d_descs_cap = c.d_out_cap = n;
     }
-    // chunks: [the lead], then the rest in `target`-byte chunks
-    struct Chunk {
-        uint32_t b0, b1; // span blocks [b0, b1)
-        HostSpan sp;
-        uint8_t *base;
-    };
-    std::vector<Chunk> ch;
-    if (early)
-        ch.push_back({0u, m, lead, lead_base});
-    const size_t first_rest = ch.size();
-    for (uint32_t k = r0; k < nblk; ++k) {
-        if (ch.size() == first_rest || ch.back().sp.bytes >= target)
-            ch.push_back({k, k, HostSpan(), dbase});
-        ch.back().sp.merge(blk[k]);
-        ch.back().b1 = k + 1;
-    }
-    // segments in no particular order: every chunk's span covers most of the
-    // batch's, so copy the batch's span once and run one kernel on it
-    uint64_t spans = 0;
-    for (size_t k = first_rest; k < ch.size(); ++k)
-        spans += ch[k].sp.hi > ch[k].sp.lo ? ch[k].sp.hi - ch[k].sp.lo : 0;
-    const uint64_t rest_span = rest.hi > rest.lo ? rest.hi - rest.lo : 0;
-    if (ch.size() > first_rest + 1 && spans > rest_span + rest_span / 4) {
-        ch.resize(first_rest);
-        ch.push_back({r0, nblk, rest, dbase});
-    }
+    const std::vector<PesoChunk> &ch = pl.ch;
     // a hipMemcpyAsync from pageable memory is staged by the runtime per call
     // (~100 us per chunk), so descriptors and results go through pinned
     // staging.  The descriptors cross the link as tcsum_seg_t (16 B, not 24):
@@ -875,10 +970,12 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     // pseudo-header as pre_sum (tools.c:58-73), so the pseudo-header is folded
     // here, in the staging pass, and the kernels run as pktbuf_checksum16
     const bool stage_out = !mapped_host(out);
-    if (!c.q_desc.reserve(sizeof(tcsum_seg_t) * n) || (stage_out && !c.q_res.reserve(sizeof(uint16_t) * n + 64)))
-        return fail(TCSUM_ERR_MEM);
+    if (const hipError_t e = c.q_desc.reserve(sizeof(tcsum_seg_t) * n); e != hipSuccess)
+        return fail(note_mem(16, e));
+    if (const hipError_t e = stage_out ? c.q_res.reserve(sizeof(uint16_t) * n + 64) : hipSuccess; e != hipSuccess)
+        return fail(note_mem(16, e));
     uint16_t *hout = stage_out ? reinterpret_cast<uint16_t *>(c.q_res.h) : out;
-    if (const hipError_t e = early ? hipSuccess : copy_bytes(ch[0].base, ch[0].sp); e != hipSuccess)
+    if (const hipError_t e = pl.early ? hipSuccess : copy_span(ch[0].buf, ch[0].sp); e != hipSuccess)
         return fail_sys(3, e); // its bytes cross while the host stages
     tcsum_seg_t *hseg = reinterpret_cast<tcsum_seg_t *>(c.q_desc.h);
     parallel_for(n, size_t(1) << 16, [&](size_t b, size_t e) {
@@ -902,7 +999,7 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         return fail_sys(4, e);
     stamp("descs staged");
     for (size_t k = 0; k < ch.size(); ++k) {
-        if (const hipError_t e = k ? copy_bytes(ch[k].base, ch[k].sp) : hipSuccess; e != hipSuccess)
+        if (const hipError_t e = k ? copy_span(ch[k].buf, ch[k].sp) : hipSuccess; e != hipSuccess)
             return fail_sys(5, e);
         hipEvent_t ev = c.hev[k % kHostEvents];
         if (const hipError_t e = hipEventRecord(ev, cs); e != hipSuccess)
@@ -915,7 +1012,7 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
             continue;
         const hipError_t e = tcsum::launch_segments(tcsum::MODE_SEG,
                                                     tcsum::pick_geometry(mean_of(ch[k].sp.bytes, i1 - i0)),
-                                                    ch[k].base, c.d_descs + i0, i1 - i0, c.d_out + i0, 1u, ks);
+                                                    base[ch[k].buf], c.d_descs + i0, i1 - i0, c.d_out + i0, 1u, ks);
         if (e != hipSuccess)
             return fail_sys(8, e);
     }
@@ -932,6 +1029,39 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         memcpy(out, hout, sizeof(uint16_t) * n);
     stamp("done");
     return TCSUM_OK;
+}
+
+// The plan tcsum_host_batch_peso makes for a batch, as rows of 5 u64
+// (tcsum_debug.h): no device is touched.
+int64_t tcsum_debug_plan_host_peso(const tcsum_peso_t *segs, uint32_t n, uint64_t arena_bytes, uint64_t *rows,
+                                   uint32_t max_rows, uint64_t *buf_bytes)
+{
+    if (!segs || n == 0 || !buf_bytes || (max_rows && !rows))
+        return TCSUM_ERR_PARAM;
+    PesoPlan pl;
+    if (!peso_plan_lead(pl, segs, n, arena_bytes) || !peso_plan_rest(pl, segs, arena_bytes))
+        return TCSUM_ERR_PARAM;
+    buf_bytes[0] = pl.early ? span_bytes(pl.lead) : 0;
+    buf_bytes[1] = span_bytes(pl.rest);
+    const uint64_t bases[2] = {pl.lead_base(), pl.rest_base()};
+    uint32_t k = 0;
+    auto row = [&](uint64_t a, uint64_t b, uint64_t c, uint64_t d, uint64_t e) {
+        if (k < max_rows) {
+            uint64_t *r = rows + 5ull * k;
+            r[0] = a, r[1] = b, r[2] = c, r[3] = d, r[4] = e;
+        }
+        ++k;
+    };
+    for (const PesoChunk &c : pl.ch) { // in queue order: chunk k's copy, then its kernel
+        uint64_t lo, hi;
+        span_copy(c.sp, arena_bytes, lo, hi);
+        if (hi > lo) // copy: buffer, host [lo, hi), buffer offset of lo
+            row(0, (uint64_t)c.buf, lo, hi, lo - bases[c.buf]);
+        const uint32_t i0 = c.b0 * kSpanBlock, i1 = (uint32_t)std::min<uint64_t>(n, (uint64_t)c.b1 * kSpanBlock);
+        if (i1 > i0) // kernel: buffer, segments [i0, i1), the buffer's arena base
+            row(1, (uint64_t)c.buf, i0, i1, bases[c.buf]);
+    }
+    return (int64_t)k;
 }
 
 extern "C++" {
@@ -1203,14 +1333,17 @@ int srv_setup(Ctx &c)
 {
     if (c.srv_h)
         return TCSUM_OK;
-    if (hipStreamCreateWithFlags(&c.srv_stream, hipStreamNonBlocking) != hipSuccess)
-        return TCSUM_ERR_SYS;
-    if (hipHostMalloc(reinterpret_cast<void **>(&c.srv_h), sizeof(tcsum::SrvHost), hipHostMallocCoherent) !=
+    hipError_t e;
+    if (!c.srv_stream && (e = hipStreamCreateWithFlags(&c.srv_stream, hipStreamNonBlocking)) != hipSuccess) {
+        c.srv_stream = nullptr;
+        return note_sys(40, e);
+    }
+    if ((e = hipHostMalloc(reinterpret_cast<void **>(&c.srv_h), sizeof(tcsum::SrvHost), hipHostMallocCoherent)) !=
             hipSuccess ||
-        hipHostGetDevicePointer(reinterpret_cast<void **>(&c.srv_hd), c.srv_h, 0) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void **>(&c.srv_d), sizeof(tcsum::SrvCtl)) != hipSuccess) {
+        (e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c.srv_hd), c.srv_h, 0)) != hipSuccess ||
+        (e = hipMalloc(reinterpret_cast<void **>(&c.srv_d), sizeof(tcsum::SrvCtl))) != hipSuccess) {
         c.srv_h = nullptr;
-        return TCSUM_ERR_MEM;
+        return note_mem(41, e);
     }
     memset(c.srv_h, 0, sizeof(tcsum::SrvHost));
     if (knob_or(tcsum::KNOB_SERVER_TRACE, 0)) { // phase stamps, printed by srv_stop (measurement only)
@@ -1256,9 +1389,10 @@ int srv_launch(Ctx &c, uint32_t last)
 {
     reap_at_exit();
     const uint64_t idle_ticks = 100000ull * (uint64_t)std::max(1, knob_or(tcsum::KNOB_SERVER_IDLE_MS, 10)); // 100 MHz
-    if (tcsum::launch_server(c.srv_hd, c.srv_d, last, idle_ticks, std::max(1, knob_or(tcsum::KNOB_SERVER_WGS, 64)),
-                             c.srv_stream) != hipSuccess)
-        return TCSUM_ERR_SYS;
+    if (const hipError_t e = tcsum::launch_server(c.srv_hd, c.srv_d, last, idle_ticks,
+                                                  std::max(1, knob_or(tcsum::KNOB_SERVER_WGS, 64)), c.srv_stream);
+        e != hipSuccess)
+        return note_sys(42, e);
     c.srv_running = true;
     return TCSUM_OK;
 }
@@ -1273,11 +1407,11 @@ int srv_stop(Ctx &c)
     if (c.srv_running) {
         const auto t0 = std::chrono::steady_clock::now();
         for (;;) {
-            const hipError_t q = hipStreamQuery(c.srv_stream);
+            const hipError_t q = poll_stream(c.srv_stream);
             if (q == hipSuccess)
                 break;
             if (q != hipErrorNotReady || std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
-                rc = TCSUM_ERR_SYS;
+                rc = note_sys(43, q);
                 break;
             }
             std::this_thread::sleep_for(std::chrono::microseconds(100));
@@ -1324,11 +1458,11 @@ int srv_submit(Ctx &c, int op, uint8_t *d_arena, const tcsum_pkt_t *d_pkts, uint
             const auto now = std::chrono::steady_clock::now();
             if (now >= check) {
                 if (c.srv_running) {
-                    const hipError_t q = hipStreamQuery(c.srv_stream);
+                    const hipError_t q = poll_stream(c.srv_stream);
                     if (q == hipSuccess)
                         c.srv_running = false;
                     else if (q != hipErrorNotReady)
-                        return TCSUM_ERR_SYS;
+                        return note_sys(44, q);
                 }
                 if (!c.srv_running) {
                     if (__atomic_load_n(&h->done, __ATOMIC_ACQUIRE) == seq)
@@ -1337,7 +1471,7 @@ int srv_submit(Ctx &c, int op, uint8_t *d_arena, const tcsum_pkt_t *d_pkts, uint
                         return rc;
                 }
                 if (now - t0 > std::chrono::seconds(10))
-                    return TCSUM_ERR_SYS;
+                    return note_sys(45, hipErrorLaunchTimeOut);
                 check = now + std::chrono::microseconds(100);
             }
         }
@@ -1351,15 +1485,20 @@ int cs_setup(Ctx &c)
 {
     if (c.cs_h)
         return TCSUM_OK;
-    if (!c.cs_stream && hipStreamCreateWithFlags(&c.cs_stream, hipStreamNonBlocking) != hipSuccess)
-        return TCSUM_ERR_SYS;
+    hipError_t e;
+    if (!c.cs_stream && (e = hipStreamCreateWithFlags(&c.cs_stream, hipStreamNonBlocking)) != hipSuccess) {
+        c.cs_stream = nullptr;
+        return note_sys(49, e);
+    }
     tcsum::CallBox *h = nullptr, *hd = nullptr;
     uint8_t *st = nullptr, *std_ = nullptr;
-    if (hipHostMalloc(reinterpret_cast<void **>(&h), sizeof(tcsum::CallBox), hipHostMallocCoherent) != hipSuccess ||
-        hipHostGetDevicePointer(reinterpret_cast<void **>(&hd), h, 0) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void **>(&st), kCallStageMax + 64, hipHostMallocCoherent) != hipSuccess ||
-        hipHostGetDevicePointer(reinterpret_cast<void **>(&std_), st, 0) != hipSuccess)
-        return TCSUM_ERR_MEM;
+    if ((e = hipHostMalloc(reinterpret_cast<void **>(&h), sizeof(tcsum::CallBox), hipHostMallocCoherent)) !=
+            hipSuccess ||
+        (e = hipHostGetDevicePointer(reinterpret_cast<void **>(&hd), h, 0)) != hipSuccess ||
+        (e = hipHostMalloc(reinterpret_cast<void **>(&st), kCallStageMax + 64, hipHostMallocCoherent)) !=
+            hipSuccess ||
+        (e = hipHostGetDevicePointer(reinterpret_cast<void **>(&std_), st, 0)) != hipSuccess)
+        return note_mem(49, e);
     memset(h, 0, sizeof(tcsum::CallBox));
     memset(st, 0, kCallStageMax + 64);
     c.cs_stage = st;
@@ -1423,7 +1562,7 @@ uint32_t cs_post(Ctx &c, uint32_t ctl, uint32_t len, uint32_t pre, uint32_t src,
             const auto now = std::chrono::steady_clock::now();
             if (now >= check) {
                 if (c.cs_running) {
-                    const hipError_t q = hipStreamQuery(c.cs_stream);
+                    const hipError_t q = poll_stream(c.cs_stream);
                     if (q == hipSuccess)
                         c.cs_running = false;
                     else if (q != hipErrorNotReady)
@@ -1456,11 +1595,11 @@ int cs_stop(Ctx &c)
     c.cs_seq = seq;
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
-        const hipError_t q = hipStreamQuery(c.cs_stream);
+        const hipError_t q = poll_stream(c.cs_stream);
         if (q == hipSuccess)
             break;
         if (q != hipErrorNotReady || std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
-            return TCSUM_ERR_SYS;
+            return note_sys(46, q);
         std::this_thread::sleep_for(std::chrono::microseconds(100));
     }
     c.cs_running = false;
@@ -1490,20 +1629,41 @@ void reap_at_exit() { std::call_once(g_reap_once, [] { atexit(reap_servers); });
 // Give back every cached batch buffer of a device (tcsum_release): the HBM
 // copy of host spans and descriptors, and the pinned host-queue staging.  The
 // servers go first: their next job would name the freed buffers.
+// The calling thread's current device is restored on return (release may
+// run on a thread that works on another device).
+struct KeepDevice {
+    int dev = -1;
+    KeepDevice()
+    {
+        if (hipGetDevice(&dev) != hipSuccess)
+            dev = -1;
+    }
+    ~KeepDevice()
+    {
+        if (dev >= 0)
+            (void)hipSetDevice(dev);
+    }
+};
+
 int release_ctx(Ctx &c, int dev)
 {
     std::lock_guard<std::mutex> lk(c.mu);
+    const KeepDevice keep;
     if (!c.ready) {
         // no context (only device-resident batch calls on caller streams ran
-        // here): the tx fill's scratch pool may still hold memory
+        // here): the tx fill's scratch pool may still hold memory.  Its
+        // blocks are stream-ordered: the device is synchronized (tcsum.h)
         if (!tcsum::scratch_reserved(dev))
             return TCSUM_OK;
-        if (hipSetDevice(dev) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
-            return TCSUM_ERR_SYS;
-        return tcsum::scratch_trim(dev) == hipSuccess ? TCSUM_OK : TCSUM_ERR_SYS;
+        hipError_t e = hipSetDevice(dev);
+        if (e == hipSuccess)
+            e = hipDeviceSynchronize();
+        if (e == hipSuccess)
+            e = tcsum::scratch_trim(dev);
+        return e == hipSuccess ? TCSUM_OK : note_sys(50, e);
     }
-    if (hipSetDevice(c.device) != hipSuccess)
-        return TCSUM_ERR_SYS;
+    if (const hipError_t e = hipSetDevice(c.device); e != hipSuccess)
+        return note_sys(51, e);
     if ((c.srv_running && srv_stop(c) != TCSUM_OK) || (c.cs_running && cs_stop(c) != TCSUM_OK))
         return TCSUM_ERR_SYS;
     for (hipStream_t st : c.hs)
@@ -1527,8 +1687,8 @@ int release_ctx(Ctx &c, int dev)
     // the tx fill's pooled scratch (every stream of this context is idle;
     // a caller's own stream on this device must be too, tcsum.h)
     (void)hipDeviceSynchronize();
-    if (tcsum::scratch_trim(c.device) != hipSuccess)
-        return TCSUM_ERR_SYS;
+    if (const hipError_t e = tcsum::scratch_trim(c.device); e != hipSuccess)
+        return note_sys(52, e);
     return TCSUM_OK;
 }
 
@@ -1589,11 +1749,11 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     }
     Ctx &c = g_ctx[device];
     std::lock_guard<std::mutex> lk(c.mu);
-    int rc = ctx_init(c, device);
+    int rc = ctx_init(c, device); // a failing HIP call is recorded there (steps 20-25)
     if (rc != TCSUM_OK)
         return rc;
-    if (hipSetDevice(device) != hipSuccess)
-        return TCSUM_ERR_SYS;
+    if (const hipError_t se = hipSetDevice(device); se != hipSuccess)
+        return note_sys(31, se);
 
     uint8_t *d_arena = mapped_host(host_arena);
     const bool staged = d_arena == nullptr;
@@ -1601,12 +1761,14 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     if (staged) {
         if (hi <= lo)
             lo = hi = 0;
-        if (!c.q_arena.reserve(hi - lo + 2 * kPad))
-            return TCSUM_ERR_MEM;
+        if (const hipError_t me = c.q_arena.reserve(hi - lo + 2 * kPad); me != hipSuccess)
+            return note_mem(32, me);
         d_arena = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(c.q_arena.d) + kPad - lo);
     }
-    if (!c.q_desc.reserve(sizeof(tcsum_pkt_t) * n) || !c.q_res.reserve(6ull * n + 64))
-        return TCSUM_ERR_MEM;
+    if (const hipError_t me = c.q_desc.reserve(sizeof(tcsum_pkt_t) * n); me != hipSuccess)
+        return note_mem(33, me);
+    if (const hipError_t me = c.q_res.reserve(6ull * n + 64); me != hipSuccess)
+        return note_mem(33, me);
     par_memcpy(c.q_desc.h, reinterpret_cast<const uint8_t *>(pkts), sizeof(tcsum_pkt_t) * n);
     // results: out u32[n] | flags u8[n] | verdict i8[n]
     uint32_t *d_out = out ? reinterpret_cast<uint32_t *>(c.q_res.d) : nullptr;
@@ -1658,10 +1820,12 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
             (void)hipFree(c.d_arena);
         c.d_arena = nullptr;
         c.d_arena_cap = 0;
-        if (hipMalloc(reinterpret_cast<void **>(&c.d_arena), (size_t)(ahi - alo) + 32) == hipSuccess)
+        if (hipMalloc(reinterpret_cast<void **>(&c.d_arena), (size_t)(ahi - alo) + 32) == hipSuccess) {
             c.d_arena_cap = (size_t)(ahi - alo) + 32;
-        else
-            dma = false, (void)hipGetLastError();
+        } else {
+            c.d_arena = nullptr;
+            dma = false; // not an error: the in-place path needs no HBM copy
+        }
     }
     if (dma) {
         uint8_t *const dbase = c.d_arena + 16 - alo;
@@ -1727,8 +1891,10 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
             c.d_arena = nullptr;
             c.d_arena_cap = 0;
         }
-        if (e != hipSuccess || s1 != hipSuccess || s2 != hipSuccess)
-            return TCSUM_ERR_SYS;
+        if (e != hipSuccess)
+            return note_sys(34, e);
+        if (s1 != hipSuccess || s2 != hipSuccess)
+            return note_sys(35, s1 != hipSuccess ? s1 : s2);
         goto results;
     }
     if (!staged) {
@@ -1765,8 +1931,10 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     // on a failed launch the pieces already launched still read the arena
     // (and the staging the next call reuses): drain them before returning
     const hipError_t se = e == hipSuccess ? stream_wait(c) : hipStreamSynchronize(c.stream);
-    if (e != hipSuccess || se != hipSuccess)
-        return TCSUM_ERR_SYS;
+    if (e != hipSuccess)
+        return note_sys(36, e);
+    if (se != hipSuccess)
+        return note_sys(37, se);
     }
 results:
     if (out)
@@ -1886,8 +2054,8 @@ int tcsum_queue_server(int device, int enable)
     int rc = ctx_init(c, device);
     if (rc != TCSUM_OK)
         return rc;
-    if (hipSetDevice(device) != hipSuccess)
-        return TCSUM_ERR_SYS;
+    if (const hipError_t e = hipSetDevice(device); e != hipSuccess)
+        return note_sys(47, e);
     if (enable) {
         rc = srv_setup(c);
         if (rc == TCSUM_OK)
@@ -1907,8 +2075,8 @@ int tcsum_call_server(int device, int enable)
     int rc = ctx_init(c, device);
     if (rc != TCSUM_OK)
         return rc;
-    if (hipSetDevice(device) != hipSuccess)
-        return TCSUM_ERR_SYS;
+    if (const hipError_t e = hipSetDevice(device); e != hipSuccess)
+        return note_sys(48, e);
     if (enable) {
         rc = cs_setup(c);
         if (rc == TCSUM_OK)

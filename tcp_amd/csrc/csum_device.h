@@ -33,7 +33,32 @@
 
 #include "csum_launch.h"
 
+#include <tuple>
+#include <type_traits>
+
 namespace tcsum {
+
+// Launch kernel `k` and return the status of THIS launch: hipLaunchKernel's
+// own return value.  `k<<<...>>>(...); return hipGetLastError();` instead
+// reads the calling thread's last-error slot, which any earlier runtime call
+// on that thread may have left set -- a caller's own failed call, or a
+// hipStreamQuery that answered hipErrorNotReady -- and a launch that
+// succeeded was then reported as failed (round 4's intermittent
+// TCSUM_ERR_SYS from tcsum_host_batch_peso).  The arguments
+// are converted to the kernel's parameter types first, as a <<<>>> call
+// would convert them.
+template <typename... P, typename... A>
+inline hipError_t launch(void (*k)(P...), dim3 grid, dim3 block, size_t shmem, hipStream_t stream, A... a)
+{
+    static_assert(sizeof...(P) == sizeof...(A), "kernel argument count");
+    std::tuple<std::remove_cv_t<P>...> v{static_cast<std::remove_cv_t<P>>(a)...};
+    void *args[sizeof...(P)];
+    std::apply([&args](auto &...x) {
+        size_t i = 0;
+        ((args[i++] = static_cast<void *>(&x)), ...);
+    }, v);
+    return hipLaunchKernel(reinterpret_cast<const void *>(k), grid, block, args, shmem, stream);
+}
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 

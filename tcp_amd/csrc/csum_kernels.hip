@@ -349,20 +349,17 @@ static hipError_t seg_u(int G, int U, uint32_t xg, uint32_t n, const void *arena
     const uint8_t *a = static_cast<const uint8_t *>(arena);
 #define TCSUM_SEG(GG, UU)                                                                                     \
     if (G == GG && U == UU) {                                                                               \
-        hipLaunchKernelGGL((k_segments<GG, UU, MODE>), dim3((n + 256u / GG - 1) / (256u / GG)), dim3(256), 0, s, \
-                           a, descs, n, out, aux, xg);                                                      \
-        return hipGetLastError();                                                                           \
+        return launch(k_segments<GG, UU, MODE>, dim3((n + 256u / GG - 1) / (256u / GG)), dim3(256), 0, s, a,     \
+                      descs, n, out, aux, xg);                                                               \
     }
     TCSUM_SEG(4, 1) TCSUM_SEG(4, 2) TCSUM_SEG(8, 4) TCSUM_SEG(16, 3) TCSUM_SEG(16, 4) TCSUM_SEG(16, 6)
     TCSUM_SEG(16, 8) TCSUM_SEG(32, 6)
 #undef TCSUM_SEG
     if (G == 1024 && U == 4) { // one range per 16-wave workgroup, 2 KiB sub-ranges (TSO)
-        hipLaunchKernelGGL((k_segments_wgx<16, 32, 4, MODE>), dim3(n), dim3(1024), 0, s, a, descs, n, out, aux, xg);
-        return hipGetLastError();
+        return launch(k_segments_wgx<16, 32, 4, MODE>, dim3(n), dim3(1024), 0, s, a, descs, n, out, aux, xg);
     }
     if (G == 256 && U == 16) { // one range per workgroup
-        hipLaunchKernelGGL((k_segments_wg<16, MODE>), dim3(n), dim3(256), 0, s, a, descs, n, out, aux, xg);
-        return hipGetLastError();
+        return launch(k_segments_wg<16, MODE>, dim3(n), dim3(256), 0, s, a, descs, n, out, aux, xg);
     }
     return hipErrorInvalidValue;
 }
@@ -403,16 +400,12 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
         const uint8_t *a = static_cast<const uint8_t *>(arena);
         const dim3 gr((n + K - 1) / K), bl(kPkWaves * 64);
         if (mode == MODE_SEG)
-            hipLaunchKernelGGL((k_segments_pk<MODE_SEG>), gr, bl, 0, stream, a, descs, n, out, aux, (uint32_t)g.xcd, K);
-        else
-            hipLaunchKernelGGL((k_segments_pk<MODE_PESO>), gr, bl, 0, stream, a, descs, n, out, aux, (uint32_t)g.xcd,
-                               K);
-        return hipGetLastError();
+            return launch(k_segments_pk<MODE_SEG>, gr, bl, 0, stream, a, descs, n, out, aux, (uint32_t)g.xcd, K);
+        return launch(k_segments_pk<MODE_PESO>, gr, bl, 0, stream, a, descs, n, out, aux, (uint32_t)g.xcd, K);
     }
     if (mode == MODE_EXACT) {
-        hipLaunchKernelGGL((k_segments<64, 8, MODE_EXACT>), dim3((n + 3) / 4), dim3(256), 0, stream,
-                           static_cast<const uint8_t *>(arena), descs, n, out, aux, 1u);
-        return hipGetLastError();
+        return launch(k_segments<64, 8, MODE_EXACT>, dim3((n + 3) / 4), dim3(256), 0, stream,
+                      static_cast<const uint8_t *>(arena), descs, n, out, aux, 1u);
     }
     if (mode == MODE_SEG)
         return seg_u<MODE_SEG>(g.lanes, g.loads, (uint32_t)g.xcd, n, arena, descs, out, aux, stream);
@@ -428,9 +421,8 @@ static hipError_t ipv4_u(int G, int U, dim3 grid, uint8_t *arena, const tcsum_pk
 {
 #define TCSUM_IP(GG, UU)                                                                             \
     if (G == GG && U == UU) {                                                                      \
-        hipLaunchKernelGGL((k_ipv4<GG, UU, IPM>), grid, dim3(256), 0, s, arena, pkts, n, out, flags, \
-                           verdict, opts, xg);                                                     \
-        return hipGetLastError();                                                                  \
+        return launch(k_ipv4<GG, UU, IPM>, grid, dim3(256), 0, s, arena, pkts, n, out, flags, verdict, opts, \
+                      xg);                                                                           \
     }
     TCSUM_IP(16, 1) TCSUM_IP(16, 2) TCSUM_IP(16, 3) TCSUM_IP(16, 4) TCSUM_IP(16, 6) TCSUM_IP(16, 8)
     TCSUM_IP(32, 6) TCSUM_IP(64, 4) TCSUM_IP(64, 16)
@@ -509,8 +501,7 @@ static hipError_t tx_split_in(Geometry g, dim3 grid, uint32_t xg, uint8_t *arena
     hipError_t e = ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, vals, flags,
                                  reinterpret_cast<int8_t *>(side), IP_OPT_DEFER, xg, stream);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, store, pkts, n, vals, side);
-        e = hipGetLastError();
+        e = launch(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, store, pkts, n, vals, side);
     }
     return e;
 }
@@ -591,9 +582,8 @@ static hipError_t flat_u(uint32_t nw, uint32_t xg, uint8_t *arena, const tcsum_p
                          uint32_t *out, uint8_t *flags, int8_t *verdict, uint32_t opts, const FlatPlan *plan,
                          const uint32_t *wfirst, unsigned long long *slot, uint32_t gen, hipStream_t s)
 {
-    hipLaunchKernelGGL((k_flat_ipv4<IPM, kFlatWaves, kFlatLoads>), dim3(nw), dim3(kFlatWaves * 64), 0, s, arena, pkts,
-                       n, out, flags, verdict, opts, xg, plan, wfirst, slot, gen);
-    return hipGetLastError();
+    return launch(k_flat_ipv4<IPM, kFlatWaves, kFlatLoads>, dim3(nw), dim3(kFlatWaves * 64), 0, s, arena, pkts, n, out,
+                  flags, verdict, opts, xg, plan, wfirst, slot, gen);
 }
 
 // ip_mode as launch_ipv4 (0 sums, 1 tx fill, 2 rx, 3 tx offload, 4 tx fill
@@ -621,9 +611,8 @@ static hipError_t launch_ipv4_flat(int ip_mode, Geometry g, uint8_t *arena, cons
     if (gen == 0)
         gen = g_flat_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
     const uint64_t pthreads = (uint64_t)n + 1u > nw ? (uint64_t)n + 1u : nw;
-    hipLaunchKernelGGL((k_flat_plan<kFlatWB>), dim3((uint32_t)((pthreads + 255u) / 256u)), dim3(256), 0, stream, arena,
-                       pkts, n, (uint32_t)nw, plan, wfirst, slot, gen);
-    e = hipGetLastError();
+    e = launch(k_flat_plan<kFlatWB>, dim3((uint32_t)((pthreads + 255u) / 256u)), dim3(256), 0, stream, arena, pkts, n,
+               (uint32_t)nw, plan, wfirst, slot, gen);
     const uint32_t xg = (uint32_t)g.xcd, w = (uint32_t)nw;
     if (e == hipSuccess) {
         switch (ip_mode) {
@@ -636,9 +625,7 @@ static hipError_t launch_ipv4_flat(int ip_mode, Geometry g, uint8_t *arena, cons
             e = flat_u<IP_TX>(w, xg, arena, pkts, n, vals, flags, reinterpret_cast<int8_t *>(side), IP_OPT_DEFER,
                               plan, wfirst, slot, gen, stream);
             if (e == hipSuccess) {
-                hipLaunchKernelGGL(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, arena, pkts, n, vals,
-                                   side);
-                e = hipGetLastError();
+                e = launch(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, arena, pkts, n, vals, side);
             }
             break;
         }
@@ -714,9 +701,7 @@ hipError_t launch_server(SrvHost *h, SrvCtl *d, uint32_t last, uint64_t idle_tic
         return e;
     // 64 lanes x 16 loads per frame: a frame of up to 16 KiB is one pass -- one
     // PCIe round trip for its bytes (the server's frames live in host memory)
-    hipLaunchKernelGGL((k_server<64, 16>), dim3((uint32_t)(wgs > 0 ? wgs : 1)), dim3(256), 0, stream, h, d, last,
-                       idle_ticks);
-    return hipGetLastError();
+    return launch(k_server<64, 16>, dim3((uint32_t)(wgs > 0 ? wgs : 1)), dim3(256), 0, stream, h, d, last, idle_ticks);
 }
 
 // checksum16 on <= kCallInline bytes with the bytes in the kernel arguments
@@ -783,15 +768,12 @@ hipError_t launch_once(Mode mode, const uint8_t *stage, uint32_t off, uint32_t l
 {
     const uint32_t comp = complement ? 1u : 0u;
     if (mode == MODE_EXACT)
-        hipLaunchKernelGGL(k_once<MODE_EXACT>, dim3(1), dim3(64), 0, stream, stage, off, len, pre, src, dst, proto,
-                           comp, out);
-    else if (mode == MODE_PESO)
-        hipLaunchKernelGGL(k_once<MODE_PESO>, dim3(1), dim3(64), 0, stream, stage, off, len, pre, src, dst, proto,
-                           comp, out);
-    else
-        hipLaunchKernelGGL(k_once<MODE_SEG>, dim3(1), dim3(64), 0, stream, stage, off, len, pre, src, dst, proto,
-                           comp, out);
-    return hipGetLastError();
+        return launch(k_once<MODE_EXACT>, dim3(1), dim3(64), 0, stream, stage, off, len, pre, src, dst, proto, comp,
+                      out);
+    if (mode == MODE_PESO)
+        return launch(k_once<MODE_PESO>, dim3(1), dim3(64), 0, stream, stage, off, len, pre, src, dst, proto, comp,
+                      out);
+    return launch(k_once<MODE_SEG>, dim3(1), dim3(64), 0, stream, stage, off, len, pre, src, dst, proto, comp, out);
 }
 
 hipError_t launch_inline16(Mode mode, const void *bytes, uint32_t len, uint32_t odd, uint32_t pre, int complement,
@@ -803,19 +785,16 @@ hipError_t launch_inline16(Mode mode, const void *bytes, uint32_t len, uint32_t 
     if (len)
         memcpy(reinterpret_cast<uint8_t *>(w) + odd, bytes, len);
     if (mode == MODE_EXACT)
-        hipLaunchKernelGGL(k_inline16<MODE_EXACT>, dim3(1), dim3(64), 0, stream, w[0], w[1], w[2], w[3], w[4], w[5],
-                           odd, len, pre, complement ? 1u : 0u, out);
-    else
-        hipLaunchKernelGGL(k_inline16<MODE_SEG>, dim3(1), dim3(64), 0, stream, w[0], w[1], w[2], w[3], w[4], w[5],
-                           odd, len, pre, complement ? 1u : 0u, out);
-    return hipGetLastError();
+        return launch(k_inline16<MODE_EXACT>, dim3(1), dim3(64), 0, stream, w[0], w[1], w[2], w[3], w[4], w[5], odd,
+                      len, pre, complement ? 1u : 0u, out);
+    return launch(k_inline16<MODE_SEG>, dim3(1), dim3(64), 0, stream, w[0], w[1], w[2], w[3], w[4], w[5], odd, len,
+                  pre, complement ? 1u : 0u, out);
 }
 
 hipError_t launch_call_server(CallBox *box, const uint8_t *stage, uint32_t last, uint64_t idle_ticks,
                               hipStream_t stream)
 {
-    hipLaunchKernelGGL(k_call, dim3(1), dim3(64), 0, stream, box, stage, last, idle_ticks);
-    return hipGetLastError();
+    return launch(k_call, dim3(1), dim3(64), 0, stream, box, stage, last, idle_ticks);
 }
 
 } // namespace tcsum

@@ -1,0 +1,251 @@
+"""Round 4's intermittent TCSUM_ERR_SYS, made deterministic.
+
+Every launch of libtcsum.so used to judge itself by hipGetLastError(), the
+calling thread's last-error slot -- which other runtime calls on that thread
+(a hipStreamQuery answering NotReady, a caller's own failed call) may have
+left set.  Now each launch returns hipLaunchKernel's own status.  These tests
+leave the slot dirty on purpose -- a NotReady from a poll of a busy stream and
+a real error of the caller's (hipSetDevice past the last device) -- and then
+call every batch entry point: each must return OK with the oracle's results.
+They also check the other direction: a call that polls its own stream while
+the kernel runs must not leave a NotReady in a slot that was clear."""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HIP_NOT_READY = 600
+HIP_INVALID_DEVICE = 101
+
+
+@pytest.fixture(scope="module")
+def tc():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need an MI355X"
+    from tcp_amd import build
+    build.build()
+    import tcp_amd
+    tcp_amd.plat_init(0)
+    return tcp_amd
+
+
+@pytest.fixture(scope="module")
+def hip(tc):
+    """The HIP runtime this process runs on (torch's copy, same SONAME as the
+    one libtcsum.so is linked against: one runtime, one last-error slot)."""
+    h = ctypes.CDLL("libamdhip64.so.7")
+    for name in ("hipPeekAtLastError", "hipGetLastError", "hipGetDeviceCount"):
+        getattr(h, name).restype = ctypes.c_int
+    h.hipStreamQuery.restype = ctypes.c_int
+    h.hipStreamQuery.argtypes = [ctypes.c_void_p]
+    h.hipSetDevice.restype = ctypes.c_int
+    h.hipSetDevice.argtypes = [ctypes.c_int]
+    return h
+
+
+def _dirty_not_ready(hip):
+    """A hipStreamQuery that answers NotReady on this thread: a stream kept
+    busy by a sleeping kernel.  Returns what the slot then holds."""
+    import torch
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(50_000_000)  # ~tens of ms of a spinning wave
+    q = hip.hipStreamQuery(ctypes.c_void_p(s.cuda_stream))
+    assert q == HIP_NOT_READY, q
+    slot = hip.hipPeekAtLastError()
+    s.synchronize()
+    return slot
+
+
+def _dirty_invalid_device(hip):
+    """A failed call of the caller's own (an out-of-range device): the
+    runtime keeps its error in the slot until someone reads it."""
+    n = ctypes.c_int(0)
+    hip.hipGetDeviceCount(ctypes.byref(n))
+    r = hip.hipSetDevice(n.value)
+    hip.hipSetDevice(0)
+    return r
+
+
+DIRT = ["not_ready", "invalid_device"]
+
+
+def _dirty(hip, kind):
+    if kind == "not_ready":
+        _dirty_not_ready(hip)
+    else:
+        assert _dirty_invalid_device(hip) == HIP_INVALID_DEVICE
+
+
+def test_runtime_slot_semantics_recorded(hip, tc):
+    """What this runtime keeps in the slot after the two calls (recorded in
+    the test log; the library must be right either way)."""
+    nr = _dirty_not_ready(hip)
+    hip.hipGetLastError()
+    bad = _dirty_invalid_device(hip)
+    after_bad = hip.hipPeekAtLastError()
+    hip.hipGetLastError()
+    print(f"slot after NotReady query: {nr}; after invalid hipSetDevice ({bad}): {after_bad}")
+    assert after_bad in (0, HIP_INVALID_DEVICE)
+
+
+@pytest.fixture(scope="module")
+def mixed(tc, oracle):
+    """A small configs[3]-shaped IPv4 batch and a 1500-B peso batch, with
+    their oracle results (host copies)."""
+    import torch
+    from tcp_amd import workload
+    b = workload.make_batch("mixed", n=3000)
+    arena, descs = workload.materialize(b)
+    host = arena.cpu().numpy()
+    eo, ef = oracle.batch_ipv4(host, b.descs, nthreads=8)
+    p = workload.make_batch("mtu", n=5000)
+    parena, pdescs = workload.materialize(p)
+    phost = parena.cpu().numpy()
+    pe = oracle.batch_peso(phost, p.descs, nthreads=8)
+    torch.cuda.synchronize()
+    return dict(b=b, arena=arena, descs=descs, host=host, eo=eo, ef=ef,
+                p=p, parena=parena, pdescs=pdescs, phost=phost, pe=pe)
+
+
+@pytest.mark.parametrize("dirt", DIRT)
+def test_device_batches_with_a_dirty_slot(tc, hip, oracle, mixed, dirt):
+    import torch
+    m = mixed
+    b, p = m["b"], m["p"]
+    checks = []
+
+    def run(name, fn):
+        _dirty(hip, dirt)
+        checks.append((name, fn()))
+
+    run("peso packed", lambda: tc.batch_peso(m["parena"], m["pdescs"], p.n, p.total_bytes))
+    run("peso per-range", lambda: tc.batch(tc.OP_PESO, m["parena"], m["pdescs"], p.n, total_bytes=p.total_bytes,
+                                          layout=tc.LAYOUT_SHUFFLED)[0])
+    run("ipv4 sums", lambda: tc.batch_ipv4(m["arena"], m["descs"], b.n, b.total_bytes)[0])
+    run("ipv4 offload", lambda: tc.batch_ipv4_tx_offload(m["arena"], m["descs"], b.n, b.total_bytes)[0])
+    run("ipv4 rx", lambda: tc.batch_ipv4_rx_verify(m["arena"], m["descs"], b.n, b.total_bytes)[0])
+    for name, got in checks:
+        got = got.cpu().numpy()
+        if name.startswith("peso"):
+            np.testing.assert_array_equal(got, m["pe"], err_msg=name)
+        elif name == "ipv4 sums":
+            np.testing.assert_array_equal(got, m["eo"], err_msg=name)
+    rx = checks[-1][1].cpu().numpy()
+    ev, _ = oracle.batch_ipv4_rx_verify(m["host"], b.descs, nthreads=8)
+    np.testing.assert_array_equal(rx, ev)
+    # the tx fill (both forms) on a copy: bytes equal the oracle's fill
+    want = m["host"].copy()
+    oracle.batch_ipv4_tx_fill(want, b.descs, nthreads=8)
+    for split in (0, 1):
+        a = m["arena"].clone()
+        with tc.debug(tx_split=split):
+            _dirty(hip, dirt)
+            tc.batch_ipv4_tx_fill(a, m["descs"], b.n, b.total_bytes)
+        np.testing.assert_array_equal(a.cpu().numpy(), want, err_msg=f"tx fill split={split}")
+    a = m["arena"].clone()
+    scratch = torch.empty(8 * b.n, dtype=torch.uint8, device="cuda")
+    _dirty(hip, dirt)
+    tc.batch_ipv4_tx_fill(a, m["descs"], b.n, b.total_bytes, scratch=scratch)
+    np.testing.assert_array_equal(a.cpu().numpy(), want, err_msg="tx fill scratch")
+    hip.hipGetLastError()
+
+
+@pytest.mark.parametrize("dirt", DIRT)
+@pytest.mark.parametrize("where", ["pinned", "pageable"])
+def test_host_batches_with_a_dirty_slot(tc, hip, oracle, mixed, dirt, where):
+    m = mixed
+    b, p = m["b"], m["p"]
+    if where == "pinned":
+        ha = tc.HostArena(m["host"].size)
+        ha.array[:] = m["host"]
+        arg, view = ha, ha.array
+    else:
+        arg = view = m["host"].copy()
+    try:
+        for dma_kb in (0, 1):  # in place (the kernel polls) / through the copy engine
+            with tc.debug(hostq_dma_kb=dma_kb):
+                _dirty(hip, dirt)
+                out, fl = tc.host_batch_ipv4(arg, b.descs)
+                np.testing.assert_array_equal(out, m["eo"])
+                np.testing.assert_array_equal(fl, m["ef"])
+                _dirty(hip, dirt)
+                v, _, _ = tc.host_batch_ipv4_rx_verify(arg, b.descs)
+                ev, _ = oracle.batch_ipv4_rx_verify(m["host"], b.descs, nthreads=8)
+                np.testing.assert_array_equal(v, ev)
+        _dirty(hip, dirt)
+        got = tc.host_batch_peso(m["phost"], p.descs)
+        np.testing.assert_array_equal(got, m["pe"])
+        want = m["host"].copy()
+        oracle.batch_ipv4_tx_fill(want, b.descs, nthreads=8)
+        _dirty(hip, dirt)
+        tc.host_batch_ipv4_tx_fill(arg, b.descs)
+        np.testing.assert_array_equal(np.array(view[: want.size]), want)
+    finally:
+        hip.hipGetLastError()
+        if where == "pinned":
+            ha.free()
+
+
+def test_a_poll_leaves_no_not_ready_behind(tc, hip, oracle):
+    """A host batch read in place over PCIe runs long enough for the
+    library's wait to poll its stream while it is busy; with a clear slot
+    before the call the slot is clear after it (a NotReady left there would
+    reach the caller's next hipGetLastError, e.g. PyTorch's launch check)."""
+    from tcp_amd import workload
+    b = workload.make_batch("mixed", n=20000)  # ~90 MB: milliseconds over PCIe
+    rng = np.random.default_rng(5)
+    ha = tc.HostArena(b.alloc_bytes)
+    try:
+        ha.array[:] = rng.integers(0, 256, ha.array.size, dtype=np.uint8)
+        with tc.debug(hostq_dma_kb=0, server_max=0):
+            for _ in range(3):
+                hip.hipGetLastError()
+                assert hip.hipPeekAtLastError() == 0
+                out, _ = tc.host_batch_ipv4(ha, b.descs)
+                assert hip.hipPeekAtLastError() == 0
+        eo, _ = oracle.batch_ipv4(ha.array, b.descs, nthreads=8)
+        np.testing.assert_array_equal(out, eo)
+    finally:
+        ha.free()
+
+
+def test_dropin_symbols_with_a_dirty_slot(tc):
+    """The three drop-in symbols abort on a failed launch (they have no error
+    channel): a child process leaves the slot dirty before each and must
+    finish with the reference's KAT values."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = r"""
+import ctypes, sys
+sys.path.insert(0, %r)
+import torch, tcp_amd as tc
+from tcp_amd.pktbuf import PktBuf, IpAddr
+hip = ctypes.CDLL("libamdhip64.so.7")
+hip.hipStreamQuery.argtypes = [ctypes.c_void_p]
+def dirty():
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(20_000_000)
+    assert hip.hipStreamQuery(ctypes.c_void_p(s.cuda_stream)) == 600
+    s.synchronize()
+    n = ctypes.c_int(0); hip.hipGetDeviceCount(ctypes.byref(n)); hip.hipSetDevice(n.value); hip.hipSetDevice(0)
+h = bytes.fromhex("450000730000400040110000c0a80001c0a800c7")
+b = bytes((i * 7 + 3) & 0xFF for i in range(999))
+for args_launch in (1, 0):
+    tc.debug_set("args_launch", args_launch)
+    dirty(); assert tc.checksum16(0, h, 20, 0, 1) == 0x61B8
+    dirty(); assert tc.checksum16(0, b, 999, 0, 1) == 0x8EE9
+    pb = PktBuf([b[i:i + 127] for i in range(0, 999, 127)])
+    dirty(); assert tc.pktbuf_checksum16(pb, 999, 0, 1) == 0x8EE9
+    pb = PktBuf([b[i:i + 127] for i in range(0, 999, 127)])
+    dst, src = IpAddr.v4(bytes([192, 168, 74, 3])), IpAddr.v4(bytes([192, 168, 74, 2]))
+    dirty(); assert tc.checksum_peso(pb, dst, src, 6) == 0x4AD0
+print("ok")
+""" % root
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.returncode, r.stdout[-1000:], r.stderr[-3000:])

@@ -76,6 +76,18 @@ def parse():
     return ap.parse_args()
 
 
+def algorithmic_split(batch):
+    """(bytes read, bytes written) of algorithmic_bytes: every packet byte and
+    its descriptor read; the result (or, tx fill, the 2 x 2-byte checksum
+    fields written into the packet) written."""
+    desc = 24 if batch.kind == "peso" else 16
+    if batch.kind == "peso":
+        wr = 2
+    else:
+        wr = {"sums": 4, "tx": 4, "rx": 1, "txo": 4 + 1}[batch.op]
+    return batch.total_bytes + desc * batch.n, wr * batch.n
+
+
 def algorithmic_bytes(batch) -> int:
     """Bytes one launch must move: every packet byte once, its descriptor, its result.
 
@@ -378,12 +390,39 @@ def pmc_traffic(config: str):
             return None, f"no {counter} rows for the checksum kernel", None
         vals[counter] = v
     raw = {k: v * 1024 for k, v in vals.items()}  # KiB -> bytes, as the counters report them
+    from tcp_amd import workload
+    batch = workload.make_batch(config)
     if PMC_CALIB is None:
         traffic = raw["FETCH_SIZE"] * 2 + raw["WRITE_SIZE"]
-        return traffic, None, {"raw": raw, "method": "blanket x2 on FETCH_SIZE (uncalibrated)"}
-    from tcp_amd import workload
-    traffic, detail = calibrated_traffic(access_classes(workload.make_batch(config)), raw)
-    return traffic, None, {"per_counter": detail, "method": "per access class (scripts/pmc_calib.py)"}
+        return traffic, None, {"raw": raw, "method": "blanket x2 on FETCH_SIZE (uncalibrated)",
+                               "raw_bytes": raw_traffic(batch, raw)}
+    traffic, detail = calibrated_traffic(access_classes(batch), raw)
+    return traffic, None, {"per_counter": detail, "method": "per access class (scripts/pmc_calib.py)",
+                           "raw_bytes": raw_traffic(batch, raw)}
+
+
+def raw_traffic(batch, raw: dict) -> dict:
+    """The counters with the guide's gfx950 corrections only (MI355X_MICROARCH.md,
+    HBM / rocprofv3: FETCH_SIZE x 2, WRITE_SIZE as is), in bytes per step, and
+    each over the algorithmic bytes of its direction.  Unlike the calibrated
+    `traffic`, nothing here is divided by what an access class costs on its
+    own, so write amplification (a lone 2-byte field costing a 32-B or 64-B
+    write) and re-fetched lines show as they are."""
+    rd, wr = algorithmic_split(batch)
+    fetch = raw["FETCH_SIZE"] * 2
+    write = raw["WRITE_SIZE"]
+    # the bytes the step's kernels store by design (the deferred tx fill also
+    # writes 8 B of scratch per packet): amplification over those is the
+    # hardware's, over the algorithmic writes the design's and the hardware's
+    cls = access_classes(batch)
+    nominal_wr = sum(v for (_, c), v in cls.items() if c == "WRITE_SIZE")
+    return {"fetch_bytes": round(fetch), "write_bytes": round(write), "total_bytes": round(fetch + write),
+            "algorithmic_read_bytes": rd, "algorithmic_write_bytes": wr, "step_store_bytes": nominal_wr,
+            "fetch_vs_algorithmic_read": round(fetch / rd, 4) if rd else None,
+            "write_vs_algorithmic_write": round(write / wr, 4) if wr else None,
+            "write_vs_step_stores": round(write / nominal_wr, 4) if nominal_wr else None,
+            "total_vs_algorithmic": round((fetch + write) / (rd + wr), 4),
+            "method": "FETCH_SIZE x 2 + WRITE_SIZE (KiB x 1024), the guide's corrections only"}
 
 
 def calibrated_traffic(classes: dict, raw: dict):
@@ -643,15 +682,33 @@ def e2e_multi_child(config: str, ndev: int, timeout_s: float = 240.0):
     return json.loads(lines[-1])
 
 
+def shard_report(shards: list, identity) -> dict:
+    """Per shard of a multi-device host batch (tcsum_debug_shards): the
+    device that took it, named as the device-resident line names its ranks'
+    GPUs, and that shard's own packets, bytes, wall time and rate, plus the
+    spread of the shard times -- a slow host link or GPU then shows as its
+    own entry instead of a lower aggregate."""
+    rows = [{"device": identity(s["device"]), "packets": s["count"], "bytes": s["bytes"], "rc": s["rc"],
+             "ms": round(s["ms"], 3),
+             "gib_s": round(s["bytes"] / (s["ms"] * 1e-3) / GIB, 2) if s["ms"] > 0 else None} for s in shards]
+    ms = [r["ms"] for r in rows if r["packets"]] or [0.0]
+    return {"shards": rows, "devices": [r["device"] for r in rows],
+            "shard_ms_spread": {"min": min(ms), "max": max(ms), "max_over_min": round(max(ms) / max(1e-9, min(ms)), 4)}}
+
+
 def e2e_multi_main(config: str) -> None:
     """The child: the batch generated on GPU 0, copied to pinned host memory,
     then checksummed from there by every GPU (one shard each) and checked
-    against the device-resident results."""
+    against the device-resident results; the same for configs[3]'s frames
+    through the host-queue rx verify.  Every shard's device and time is
+    reported."""
     import ctypes
     import numpy as np
     import torch
     import tcp_amd as tc
     from tcp_amd import _lib, workload
+    devs = list(range(torch.cuda.device_count()))
+    ident = lambda d: device_identity(torch, d)  # noqa: E731
     b = workload.make_batch(config)
     arena, descs = workload.materialize(b)
     want = tc.batch_peso(arena, descs, b.n, b.total_bytes).cpu().numpy()
@@ -659,22 +716,46 @@ def e2e_multi_main(config: str) -> None:
     p = L.tcsum_host_alloc(b.alloc_bytes)
     if not p:
         raise MemoryError("tcsum_host_alloc")
+    res = {"gpus": len(devs)}
     try:
         host = np.ctypeslib.as_array((ctypes.c_uint8 * b.alloc_bytes).from_address(p))
         host[:] = arena[: b.alloc_bytes].cpu().numpy()
-        del arena
+        del arena, descs
         torch.cuda.empty_cache()
-        devs = list(range(torch.cuda.device_count()))
         out = tc.host_batch_peso_multi(host, b.descs, devs)
         reps = 3
         t0 = time.perf_counter()
         for _ in range(reps):
             out = tc.host_batch_peso_multi(host, b.descs, devs)
         dt = (time.perf_counter() - t0) / reps
-        print(json.dumps({"gpus": len(devs), "gib_s": round(b.total_bytes / dt / GIB, 2),
-                          "matches_device_resident": bool((out == want).all())}), flush=True)
+        res.update({"gib_s": round(b.total_bytes / dt / GIB, 2), "matches_device_resident": bool((out == want).all())})
+        res.update(shard_report(tc.last_shards(), ident))  # the last repetition's shards
     finally:
         L.tcsum_host_free(p)
+    try:  # the receive path's host-queue batch over the same devices
+        rb = workload.make_batch("mixed_rx")
+        arena, descs = workload.materialize(rb)
+        wv, _ = tc.batch_ipv4_rx_verify(arena, descs, rb.n, rb.total_bytes, want_flags=False)
+        wv = wv.cpu().numpy()
+        ha = tc.HostArena(arena.numel())
+        try:
+            ha.array[:] = arena.cpu().numpy()
+            del arena, descs
+            torch.cuda.empty_cache()
+            v, _, _ = tc.host_batch_ipv4_rx_verify(ha, rb.descs, devices=devs)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                v, _, _ = tc.host_batch_ipv4_rx_verify(ha, rb.descs, devices=devs)
+            dt = (time.perf_counter() - t0) / reps
+            q = {"frames": rb.n, "gib_s": round(rb.total_bytes / dt / GIB, 2),
+                 "matches_device_resident": bool((v == wv).all())}
+            q.update(shard_report(tc.last_shards(), ident))
+            res["host_queue_rx"] = q
+        finally:
+            ha.free()
+    except Exception as e:  # reported, never fatal
+        res["host_queue_rx"] = {"error": repr(e)}
+    print(json.dumps(res), flush=True)
 
 
 def legacy_latency(tc):
@@ -803,6 +884,7 @@ def rehearsal(args, rank, world) -> None:
     dt = time.perf_counter() - t0
     D.barrier(dist)
     t = D.max_over_ranks(dist, dt)
+    multi = rehearse_multi_device(b, data, world) if rank == 0 else None
     # the same post-timing checks as the GPU run: which device each rank used
     # (here: its CPU process) and the stand-in re-run against its timed result
     bad = int(int(data.astype(np.uint64).sum()) != s)
@@ -820,10 +902,32 @@ def rehearsal(args, rank, world) -> None:
                           "ms_per_step_spread": {"min": round(min(r["ms_per_step"] for r in ranks), 4),
                                                  "max": round(max(r["ms_per_step"] for r in ranks), 4)},
                           "self_check": {"segments_per_rank": 1,
-                                         "mismatches": sum(r["self_check"]["mismatches"] for r in ranks)}}),
+                                         "mismatches": sum(r["self_check"]["mismatches"] for r in ranks)},
+                          "e2e": {"multi_device": multi}}),
               flush=True)
     D.barrier(dist)
     dist.destroy_process_group()
+
+
+def rehearse_multi_device(b, data, ndev: int) -> dict:
+    """e2e.multi_device's report on CPU: rank 0's batch cut into ndev shards
+    by bytes (tcsum_host_batch_peso_multi's split, workload.shard_bounds), a
+    numpy sum over each shard's bytes standing in for its device's host batch,
+    reported through the same shard_report as the GPU child."""
+    import numpy as np
+    from tcp_amd import workload
+    cut = workload.shard_bounds(b.descs["len"], ndev)
+    shards = []
+    for d in range(ndev):
+        i0, i1 = int(cut[d]), int(cut[d + 1])
+        lo = int(b.descs["offset"][i0]) if i1 > i0 else 0
+        hi = int(b.descs["offset"][i1 - 1] + b.descs["len"][i1 - 1]) if i1 > i0 else 0
+        t0 = time.perf_counter()
+        data[lo:hi].sum(dtype=np.uint64)
+        shards.append({"device": d, "rc": 0, "first": i0, "count": i1 - i0,
+                       "bytes": int(b.descs["len"][i0:i1].sum()), "ms": (time.perf_counter() - t0) * 1e3})
+    ident = lambda d: {"ordinal": d, "pci": None, "uuid": f"cpu-stand-in-{d}", "name": "cpu (rehearsal)"}  # noqa: E731
+    return dict(shard_report(shards, ident), gpus=ndev, rehearsal=True)
 
 
 def main():
@@ -899,6 +1003,7 @@ def main():
         roof["traffic_note"] = pmc_note
     else:
         roof["traffic_vs_algorithmic"] = round(traffic / algorithmic_bytes(b), 4)
+        roof["traffic_raw"] = pmc_detail.pop("raw_bytes", None)
         roof["traffic_accounting"] = pmc_detail
     if trace is None:
         roof["rocprof_frac"] = None

@@ -113,11 +113,12 @@ typedef struct tcsum_hint {
 
 /* Every device-resident batch in one call, with the caller's layout hint
  * (hint NULL: total unknown, layout UNKNOWN -- exactly the named calls).
- * Results are the same whatever the hint, except that ORDERED promises what
- * the kernels then rely on: a batch that breaks the promise is still summed
- * exactly (the stream kernels check it) but may take a slower path.
- * SHUFFLED skips the stream kernels, which a batch in no particular order
- * would only leave again.  arena is written only by TCSUM_OP_IPV4_TX_FILL. */
+ * Results are the same whatever the hint.  ORDERED is routed as UNKNOWN
+ * today (the stream kernels check the order per workgroup either way; a
+ * batch that breaks the promise is still summed exactly).  SHUFFLED skips
+ * the stream kernels, which a batch in no particular order would only leave
+ * again.  hint->rsv must be 0 (TCSUM_ERR_PARAM otherwise).  arena is written
+ * only by TCSUM_OP_IPV4_TX_FILL. */
 int tcsum_batch(int op, void *arena /*[dev]*/, const void *descs /*[dev]*/, uint32_t n, void *out /*[dev]*/,
                 uint8_t *flags /*[dev] or NULL*/, int8_t *verdict /*[dev] or NULL*/, const tcsum_hint_t *hint /*[host]*/,
                 void *stream);
@@ -157,8 +158,8 @@ int tcsum_batch_ipv4(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev
  *   ICMP checksum (L4 + 2)                  icmpv4.c:45-58
  * L4 fields are left alone for fragments and short L4s; nothing is written
  * for SHORT / BAD_* packets.  out (ip | l4 << 16) and flags may be NULL.
- * From 131,072 packets on (TCSUM_TX_SPLIT=0/1 forces either form) the stores
- * are deferred: one launch computes every packet's values and field
+ * From 131,072 packets on the stores are deferred (tests and measurement
+ * force either form with tcsum_debug_set("tx_split", 0 / 1), tcsum_debug.h): one launch computes every packet's values and field
  * positions into stream-ordered scratch (4-8 B per packet, from a memory
  * pool the library keeps per device, up to 1 GiB retained between calls;
  * freed on the stream), a second short launch writes all the fields.  Same
@@ -302,12 +303,12 @@ int tcsum_host_batch_ipv4_rx_verify_multi(const int *devices, int ndev, const vo
 
 /* Queue server for small host-queue batches (the stack's <= 50-frame netif
  * queues, NETIF_INQ_SIZE net_cfg.h:39): with enable != 0, the
- * tcsum_host_batch_ipv4* calls on `device` with n <= $TCSUM_SERVER_MAX
- * (default 65536) frames are served by a resident grid that polls pinned
- * memory for the next job, instead of one kernel launch and one stream sync
- * per call (same results, same arguments).  The grid leaves by itself after
- * $TCSUM_SERVER_IDLE_MS (default 10) without a job and is relaunched by the
- * next call; while it is up, a device-wide synchronisation
+ * tcsum_host_batch_ipv4* calls on `device` with n <= 65,536 frames are
+ * served by a resident grid that polls pinned memory for the next job,
+ * instead of one kernel launch and one stream sync per call (same results,
+ * same arguments).  The grid leaves by itself after 10 ms without a job and
+ * is relaunched by the next call (both limits: tcsum_debug_set "server_max"
+ * / "server_idle_ms", tcsum_debug.h; nothing in the environment sets them); while it is up, a device-wide synchronisation
  * (hipDeviceSynchronize) waits for it to leave.  enable == 0 stops it (bounded
  * wait).  Returns TCSUM_OK, TCSUM_ERR_NOT_SUPPORT without a gfx950 device. */
 int tcsum_queue_server(int device, int enable);
@@ -318,8 +319,8 @@ int tcsum_queue_server(int device, int enable);
  * served by one resident wave that polls a pinned job box, instead of one
  * kernel launch and one stream sync per call (same results, same side
  * effects).  Ranges over 64 KiB still take the launch path.  The wave leaves
- * by itself after $TCSUM_SERVER_IDLE_MS (default 10) without a call and the
- * next call relaunches it; while it is up, a device-wide synchronisation
+ * by itself after 10 ms without a call ("server_idle_ms", tcsum_debug.h) and
+ * the next call relaunches it; while it is up, a device-wide synchronisation
  * waits for it to leave.  $TCSUM_CALL_SERVER=1 turns it on at the first
  * legacy call without a code change.  enable == 0 stops it (bounded wait).
  * Returns TCSUM_OK, TCSUM_ERR_NOT_SUPPORT without a gfx950 device. */
@@ -355,8 +356,8 @@ int tcsum_host_unregister(void *p);
  * memory the tx fill's scratch pool keeps (up to 1 GiB); a running queue /
  * call server is stopped first and the device is synchronized, so no work of
  * the caller's may still be queued on it.  The next call allocates again.
- * (The copy-engine path keeps at most $TCSUM_HOSTQ_DMA_KEEP_MB, default 256,
- * between calls by itself.)  Returns TCSUM_OK, TCSUM_ERR_PARAM, or
+ * (The copy-engine path keeps at most 256 MiB between calls by itself;
+ * "hostq_dma_keep_mb", tcsum_debug.h.)  Returns TCSUM_OK, TCSUM_ERR_PARAM, or
  * TCSUM_ERR_SYS. */
 int tcsum_release(int device);
 
@@ -365,7 +366,7 @@ int tcsum_device_count(void);
 
 /* Kernel geometry the batch calls choose for a mean length: lanes per packet
  * (G) and 16-byte loads in flight per lane (U).  Exposed for tests/tuning;
- * TCSUM_G / TCSUM_U in the environment override the choice. */
+ * tcsum_debug_set("lanes" / "loads") overrides the choice (tcsum_debug.h). */
 void tcsum_pick_geometry(uint64_t mean_len, int *lanes_per_packet, int *loads_per_lane);
 
 /* Library identification string. */

@@ -76,6 +76,22 @@ int64_t tcsum_debug_get(const char *key);
 int64_t tcsum_debug_plan_host_peso(const tcsum_peso_t *segs, uint32_t n, uint64_t arena_bytes, uint64_t *rows,
                                    uint32_t max_rows, uint64_t *buf_bytes);
 
+/* One shard of a multi-device host batch (tcsum_host_batch_peso_multi,
+ * tcsum_host_batch_ipv4*_multi). */
+typedef struct tcsum_shard_stat {
+    int32_t device;  /* the devices[] entry that took it */
+    int32_t rc;      /* its return code */
+    uint32_t first;  /* descriptors [first, first + count) */
+    uint32_t count;
+    uint64_t bytes;  /* the shard's packet bytes */
+    double ms;       /* wall time of the shard's call on its host thread */
+} tcsum_shard_stat_t;
+
+/* The shards of the last multi-device host batch of this process (any
+ * thread), in devices[] order: up to max written to out; returns how many
+ * there were (0 before the first). */
+int tcsum_debug_shards(tcsum_shard_stat_t *out, int max);
+
 /* The route a batch call would take for a mean range length, with the knobs
  * applied: out[0] lanes, out[1] loads, out[2] xcd, out[3] packed K (0 = off),
  * out[4] flat (0/1).  libtcsum_bench.so's probes follow it. */

@@ -115,7 +115,7 @@ struct Ctx {
     tcsum::SrvHost *srv_hd = nullptr; // ... and the device's address of it
     tcsum::SrvCtl *srv_d = nullptr;
     uint32_t srv_seq = 0; // last job posted (0 = none)
-    uint64_t *srv_trace = nullptr; // TCSUM_SERVER_TRACE stamps (host address)
+    uint64_t *srv_trace = nullptr; // debug knob "server_trace": phase stamps (host address)
     // call server (tcsum_call_server): one resident wave serving the three
     // synchronous drop-in symbols, instead of a launch + wait per call
     bool cs_on = false;      // enabled for this device
@@ -134,7 +134,7 @@ constexpr size_t kCallStageMax = 1u << 16;
 
 // Launch-path drop-in calls up to this many bytes pass their descriptor (and
 // up to kCallInline bytes) in the kernel arguments: one wave, one pass
-// (k_once / k_inline16).  TCSUM_ARGS_LAUNCH=0: the descriptor in pinned
+// (k_once / k_inline16).  Debug knob "args_launch" = 0: the descriptor in pinned
 // memory, as before (debug knob "args_launch", include/tcsum_debug.h; read per
 // call so one process can run both, tests/test_gpu_parity.py).
 constexpr size_t kOnceMax = 16u << 10;
@@ -1113,6 +1113,52 @@ std::vector<uint32_t> byte_shards(const D *descs, uint32_t n, int ndev)
     return cut;
 }
 
+// Per shard of the last multi-device host batch (tcsum_debug_shards): which
+// device took which descriptors, how many bytes, its return code and its
+// wall time -- so a slow host link or GPU shows on its own.
+std::mutex g_shards_mu;
+std::vector<tcsum_shard_stat_t> g_shards;
+
+// Run `one(device, i0, i1)` on contiguous shards of descs[0, n) balanced by
+// bytes, one host thread per entry of devices[] (the calling thread when
+// there is one), and record every shard.  Returns the first failing shard's
+// code.
+template <class D, class F>
+int run_shards(const int *devices, int ndev, const D *descs, uint32_t n, F &&one)
+{
+    const std::vector<uint32_t> cut = ndev > 1 ? byte_shards(descs, n, ndev) : std::vector<uint32_t>{0u, n};
+    std::vector<tcsum_shard_stat_t> st((size_t)ndev);
+    auto shard = [&](int d) {
+        tcsum_shard_stat_t &s = st[d];
+        const auto t0 = std::chrono::steady_clock::now();
+        if (s.count)
+            s.rc = one(devices[d], cut[d], cut[d + 1]);
+        s.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        for (uint32_t i = cut[d]; i < cut[d + 1]; ++i)
+            s.bytes += descs[i].len;
+    };
+    for (int d = 0; d < ndev; ++d)
+        st[d] = tcsum_shard_stat_t{devices[d], TCSUM_OK, cut[d], cut[d + 1] - cut[d], 0u, 0.0};
+    if (ndev == 1) {
+        shard(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int d = 0; d < ndev; ++d)
+            if (cut[d + 1] > cut[d])
+                th.emplace_back([&shard, d] { shard(d); });
+        for (auto &t : th)
+            t.join();
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_shards_mu);
+        g_shards = st;
+    }
+    for (const auto &s : st)
+        if (s.rc != TCSUM_OK)
+            return s.rc;
+    return TCSUM_OK;
+}
+
 }
 
 // One host batch over several GPUs: contiguous shards balanced by bytes
@@ -1128,23 +1174,18 @@ int tcsum_host_batch_peso_multi(const int *devices, int ndev, const void *host_a
     for (int d = 0; d < ndev; ++d)
         if (devices[d] < 0 || devices[d] >= kMaxDev)
             return TCSUM_ERR_PARAM;
-    if (ndev == 1)
-        return tcsum_host_batch_peso(devices[0], host_arena, arena_bytes, segs, n, out);
-    const std::vector<uint32_t> cut = byte_shards(segs, n, ndev);
-    std::vector<int> rc((size_t)ndev, TCSUM_OK);
-    std::vector<std::thread> th;
-    for (int d = 0; d < ndev; ++d)
-        if (cut[d + 1] > cut[d])
-            th.emplace_back([&, d] {
-                rc[d] = tcsum_host_batch_peso(devices[d], host_arena, arena_bytes, segs + cut[d], cut[d + 1] - cut[d],
-                                              out + cut[d]);
-            });
-    for (auto &t : th)
-        t.join();
-    for (int r : rc)
-        if (r != TCSUM_OK)
-            return r;
-    return TCSUM_OK;
+    return run_shards(devices, ndev, segs, n, [&](int dev, uint32_t i0, uint32_t i1) {
+        return tcsum_host_batch_peso(dev, host_arena, arena_bytes, segs + i0, i1 - i0, out + i0);
+    });
+}
+
+int tcsum_debug_shards(tcsum_shard_stat_t *out, int max)
+{
+    std::lock_guard<std::mutex> lk(g_shards_mu);
+    const int k = (int)g_shards.size();
+    for (int i = 0; i < k && i < max && out; ++i)
+        out[i] = g_shards[i];
+    return k;
 }
 
 // ------------------------------------------------------ host-queue batches
@@ -1359,7 +1400,7 @@ int srv_setup(Ctx &c)
     return TCSUM_OK;
 }
 
-// Mean phase durations over the traced jobs (TCSUM_SERVER_TRACE=1), in us.
+// Mean phase durations over the traced jobs (debug knob "server_trace" = 1), in us.
 void srv_print_trace(const Ctx &c)
 {
     const uint64_t *t = c.srv_trace;
@@ -1795,7 +1836,7 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     // own PCIe reads: pieces copied in order on
     // one copy stream into HBM, each piece's kernel behind its copy's event
     // (tcsum_host_batch_peso's pipeline): 50.7 against 49.3 GiB/s for 1M
-    // mixed frames (profiles/r01/hostq_dma.txt).  TCSUM_HOSTQ_DMA_KB: the
+    // mixed frames (profiles/r01/hostq_dma.txt).  Debug knob "hostq_dma_kb": the
     // span from which it is used (0 = never).  Only for DENSE batches -- the
     // packets cover at least 3/4 of their span: a few frames spread over a big
     // pinned pool would otherwise move gigabytes to sum kilobytes, where the
@@ -1884,7 +1925,7 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
         }
         const hipError_t s1 = hipStreamSynchronize(ks), s2 = hipStreamSynchronize(cs);
         // the HBM copy of the span is cached for the next batch only up to
-        // TCSUM_HOSTQ_DMA_KEEP_MB (default 256): a one-off multi-GiB verify
+        // debug knob "hostq_dma_keep_mb" (default 256): a one-off multi-GiB verify
         // does not keep its span allocated for the life of the process
         if (c.d_arena_cap > ((size_t)knob_or(tcsum::KNOB_HOSTQ_DMA_KEEP_MB, 256) << 20)) {
             (void)hipFree(c.d_arena);
@@ -1998,25 +2039,10 @@ static int host_ipv4_multi(int ip_mode, const int *devices, int ndev, uint8_t *h
     for (int d = 0; d < ndev; ++d)
         if (devices[d] < 0 || devices[d] >= kMaxDev)
             return TCSUM_ERR_PARAM;
-    if (ndev == 1)
-        return host_ipv4(ip_mode, devices[0], host_arena, arena_bytes, pkts, n, verdict, out, flags);
-    const std::vector<uint32_t> cut = byte_shards(pkts, n, ndev);
-    std::vector<int> rc((size_t)ndev, TCSUM_OK);
-    std::vector<std::thread> th;
-    for (int d = 0; d < ndev; ++d)
-        if (cut[d + 1] > cut[d])
-            th.emplace_back([&, d] {
-                const uint32_t i0 = cut[d];
-                rc[d] = host_ipv4(ip_mode, devices[d], host_arena, arena_bytes, pkts + i0, cut[d + 1] - i0,
-                                  verdict ? verdict + i0 : nullptr, out ? out + i0 : nullptr,
-                                  flags ? flags + i0 : nullptr);
-            });
-    for (auto &t : th)
-        t.join();
-    for (int r : rc)
-        if (r != TCSUM_OK)
-            return r;
-    return TCSUM_OK;
+    return run_shards(devices, ndev, pkts, n, [&](int dev, uint32_t i0, uint32_t i1) {
+        return host_ipv4(ip_mode, dev, host_arena, arena_bytes, pkts + i0, i1 - i0, verdict ? verdict + i0 : nullptr,
+                         out ? out + i0 : nullptr, flags ? flags + i0 : nullptr);
+    });
 }
 
 int tcsum_host_batch_ipv4_multi(const int *devices, int ndev, const void *host_arena, uint64_t arena_bytes,

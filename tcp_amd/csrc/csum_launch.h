@@ -87,7 +87,7 @@ struct SrvHost {
     uint32_t op;   // IP_SUMS / IP_TX / IP_RX
     uint32_t n;    // packets
     uint64_t ptr[5]; // device-visible: arena, pkts, out, flags, verdict (0 = none)
-    uint64_t trace;  // device-visible u64[256 * 8] of phase stamps, or 0 (TCSUM_SERVER_TRACE)
+    uint64_t trace;  // device-visible u64[256 * 8] of phase stamps, or 0 (debug knob "server_trace")
     uint32_t pad[2];
     alignas(64) uint32_t done; // device: last completed job
 };

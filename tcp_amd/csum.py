@@ -439,6 +439,20 @@ def debug_get(key: str) -> int:
     return int(_lib.lib().tcsum_debug_get(key.encode()))
 
 
+SHARD_DTYPE = np.dtype([("device", "<i4"), ("rc", "<i4"), ("first", "<u4"), ("count", "<u4"), ("bytes", "<u8"),
+                        ("ms", "<f8")])
+
+
+def last_shards() -> list:
+    """Per shard of the last multi-device host batch (tcsum_debug_shards):
+    device, rc, first, count, bytes, ms."""
+    L = _lib.lib()
+    k = L.tcsum_debug_shards(None, 0)
+    st = np.zeros(max(k, 1), SHARD_DTYPE)
+    k = L.tcsum_debug_shards(st.ctypes.data, st.size)
+    return [{f: st[f][i].item() for f in SHARD_DTYPE.names} for i in range(k)]
+
+
 class debug:
     """Context manager: `with tc.debug(lanes=16, loads=6): ...` sets the knobs
     and restores their previous values on exit."""

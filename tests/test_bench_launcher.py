@@ -43,6 +43,20 @@ def test_launcher_world2_rehearsal():
     assert len(line["ranks_ms_per_step"]) == 2 and all(t > 0 for t in line["ranks_ms_per_step"])
     sp = line["ms_per_step_spread"]
     assert sp["min"] == min(line["ranks_ms_per_step"]) and sp["max"] == max(line["ranks_ms_per_step"])
+    check_multi_device(line, 2)
+
+
+def check_multi_device(line, world):
+    """e2e.multi_device names every shard's device and times it on its own
+    (VERDICT r04 item 7), the way the device-resident line names ranks."""
+    m = line["e2e"]["multi_device"]
+    assert m["gpus"] == world and len(m["shards"]) == world == len(m["devices"])
+    assert [s["device"]["ordinal"] for s in m["shards"]] == list(range(world))
+    assert all(set(s["device"]) >= {"ordinal", "pci", "uuid", "name"} for s in m["shards"])
+    assert all(s["ms"] > 0 and s["gib_s"] > 0 and s["rc"] == 0 for s in m["shards"])
+    assert sum(s["packets"] for s in m["shards"]) == line["ranks"][0]["packets"]
+    sp = m["shard_ms_spread"]
+    assert sp["max"] >= sp["min"] > 0 and sp["max_over_min"] >= 1.0
 
 
 def test_shared_gpu_is_refused():
@@ -112,6 +126,30 @@ def test_calibrated_traffic_accounting():
         assert abs(t5 - nominal - 0.05 * reads) < 1e-6 * nominal
 
 
+def test_raw_traffic_shows_write_amplification():
+    """traffic_raw: the guide's corrections only, each
+    counter over the algorithmic bytes of its direction.  Counters as round
+    4's mixed_tx line read them (FETCH x2 ~ algorithmic reads, 65.96 MB of
+    writes) give WRITE ~5.2x the 12 B per packet the deferred fill stores,
+    ~15.7x the 4 B of checksum fields, and total ~1.02x;
+    the headline's descriptors fetched twice show as FETCH ~1.016x."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from tcp_amd import workload
+    tx = workload.make_batch("mixed_tx")
+    rd, wr = bench.algorithmic_split(tx)
+    assert wr == 4 * tx.n and rd + wr == bench.algorithmic_bytes(tx)
+    r = bench.raw_traffic(tx, {"FETCH_SIZE": rd / 2 * 1.0004, "WRITE_SIZE": 65.96e6})
+    assert 5.0 < r["write_vs_step_stores"] < 5.4  # over the 12 B the deferred fill stores per packet
+    assert 15.0 < r["write_vs_algorithmic_write"] < 16.5  # over the 4 B of checksum fields
+    assert 1.01 < r["total_vs_algorithmic"] < 1.03
+    mtu = workload.make_batch("mtu")
+    rd, wr = bench.algorithmic_split(mtu)
+    r = bench.raw_traffic(mtu, {"FETCH_SIZE": (rd + 24 * mtu.n) / 2, "WRITE_SIZE": wr})
+    assert abs(r["fetch_vs_algorithmic_read"] - 1.0 - 24 * mtu.n / rd) < 1e-3
+    assert r["write_vs_algorithmic_write"] == 1.0
+
+
 def test_step_counter_counts_only_kernels_of_every_step(tmp_path):
     """A step's counter value: the median launch of each kernel the step runs,
     summed (the deferred tx fill's two kernels); a setup kernel launched once
@@ -154,3 +192,4 @@ def test_launcher_rehearsal_many_ranks(world):
     assert line["self_check"]["mismatches"] == 0
     assert len(line["ranks_ms_per_step"]) == world and line["ms_per_step_spread"]["max"] >= \
         line["ms_per_step_spread"]["min"] > 0
+    check_multi_device(line, world)

@@ -182,6 +182,8 @@ def test_host_multi_device_golden(tc, oracle, devices, where, shift):
     cases, pool = G.ipv4_cases()
     arg, view, keep = host_copy(tc, pool, where, shift)
     out, flags = tc.host_batch_ipv4(arg, G.pkt_descs(cases, tc.PKT_DTYPE), devices=devices)
+    sh = tc.last_shards()  # one record per devices[] entry, covering every packet once
+    assert [s["device"] for s in sh] == list(devices) and sum(s["count"] for s in sh) == len(cases)
     np.testing.assert_array_equal(out & 0xFFFF, cases["ip"])
     np.testing.assert_array_equal(out >> 16, cases["l4"])
     np.testing.assert_array_equal(flags, cases["flags"])

@@ -875,6 +875,12 @@ def test_host_batch_multi_device(tc, oracle, devices):
     p["protocol"] = rng.choice([6, 17], n)
     out = tc.host_batch_peso_multi(host, p, devices)
     np.testing.assert_array_equal(out, oracle.batch_peso(host, p, nthreads=8))
+    # every shard recorded: its device, its contiguous descriptors, its bytes and time
+    sh = tc.last_shards()
+    assert [s["device"] for s in sh] == list(devices) and all(s["rc"] == 0 for s in sh)
+    assert [s["first"] for s in sh] == list(np.cumsum([0] + [s["count"] for s in sh[:-1]]))
+    assert sum(s["count"] for s in sh) == n and sum(s["bytes"] for s in sh) == int(p["len"].sum())
+    assert all(s["ms"] > 0 for s in sh if s["count"])
     few = p[:2].copy()
     few["offset"] = [host.size - 100, 5]  # the span is not in offset order
     few["len"] = [100, 51]

@@ -19,6 +19,8 @@ extern "C" {
 #endif
 
 /* Set a knob; value -1 gives the choice back to the router.  Keys:
+ *   "pf_dist"         descriptor prefetch distance of the stream / packet
+ *                     kernels, in workgroups (0 = off)
  *   "lanes", "loads"  per-range kernel shape (lanes per range x 16-B loads per
  *                     lane): one of the shapes the router picks -- 4x1, 4x2,
  *                     8x4, 16x3, 16x4, 16x6, 16x8, 32x6, 256x16, 1024x4 (IPv4
@@ -27,7 +29,6 @@ extern "C" {
  *   "xcd"             workgroups per XCD run (1 = dispatch order)
  *   "packed"          0 / 1: checksum_peso / pktbuf_checksum16 batches on the
  *                     packed-stream kernel (k_segments_pk) off / on
- *   "flat"            0 / 1: the byte-window stream (k_flat_*) off / on
  *   "tx_split"        0 / 1: the tx fill's stores in the kernel / deferred
  *   "args_launch"     0: drop-in calls pass their descriptor in pinned memory
  *   "sync_block"      1: drop-in calls block in hipStreamSynchronize
@@ -94,7 +95,8 @@ int tcsum_debug_shards(tcsum_shard_stat_t *out, int max);
 
 /* The route a batch call would take for a mean range length, with the knobs
  * applied: out[0] lanes, out[1] loads, out[2] xcd, out[3] packed K (0 = off),
- * out[4] flat (0/1).  libtcsum_bench.so's probes follow it. */
+ * out[4] reserved (0; round 4's byte-window stream is libtcsum_bench.so's
+ * tcsum_flat_ipv4 since round 5).  libtcsum_bench.so's probes follow it. */
 void tcsum_debug_route(uint64_t mean_len, int32_t out[5]);
 
 #ifdef __cplusplus

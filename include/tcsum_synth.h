@@ -84,6 +84,20 @@ int tcsum_probe_flat(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev
                      uint64_t total_bytes, int variant, int waves, int loads, uint32_t *out /*[dev]*/,
                      uint64_t out_words, uint8_t *flags /*[dev] or NULL*/, void *stream);
 
+/* The byte-window stream (k_flat_plan + k_flat_ipv4, 4 waves x 3 loads: 12-KiB
+ * windows) in every IPv4 mode -- round 4's candidate for configs[3], exact
+ * but slower than the route (k_ipv4), kept here for A/Bs and its parity tests
+ * (tests/test_gpu_flat.py).  mode: 0 sums (out required, flags or NULL), 1 tx
+ * fill in place, 2 rx verify (verdict required), 3 tx offload (out and flags
+ * required), 4 tx fill with deferred stores -- the arguments of the matching
+ * tcsum_batch_ipv4* call.  total_bytes (the sum of the lengths) sizes the
+ * windows; a batch that is not a stream (descriptors out of arena order,
+ * overlaps, a span the total does not cover) is summed packet by packet in
+ * the same launch.  Allocates its plan with hipMallocAsync on the stream. */
+int tcsum_flat_ipv4(int mode, void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n,
+                    uint64_t total_bytes, uint32_t *out /*[dev] or NULL*/, uint8_t *flags /*[dev] or NULL*/,
+                    int8_t *verdict /*[dev] or NULL*/, void *stream);
+
 /* The tx fill's design-independent floor: read every byte of arena[0,
  * nbytes) once and write each packet's two 2-byte checksum fields at the
  * addresses the fill writes, with no descriptors, parse or sums.

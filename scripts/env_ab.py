@@ -44,7 +44,7 @@ def run():
 
 
 OLD = {"TCSUM_G": "lanes", "TCSUM_U": "loads", "TCSUM_XCD": "xcd", "TCSUM_PACKED": "packed",
-       "TCSUM_TX_SPLIT": "tx_split", "TCSUM_FLAT": "flat"}
+       "TCSUM_TX_SPLIT": "tx_split"}
 
 
 def with_env(env, fn):

@@ -39,9 +39,8 @@ def product():
     tc.batch_ipv4(arena, descs, n, b.total_bytes, out=out, want_flags=False)
 
 
-def product_flat():
-    with tc.debug(flat=1):
-        tc.batch_ipv4(arena, descs, n, b.total_bytes, out=out, want_flags=False)
+def product_flat():  # round 4's route candidate, libtcsum_bench.so since round 5
+    tc.flat_ipv4(0, arena, descs, n, b.total_bytes, out=out)
 
 
 def probe(variant, w, u):
@@ -53,7 +52,7 @@ def probe(variant, w, u):
     return f
 
 
-kinds = {"k_ipv4 (product default)": product, "flat 4x3 (product, knob)": product_flat,
+kinds = {"k_ipv4 (product default)": product, "flat 4x3 (tcsum_flat_ipv4)": product_flat,
          "plain read probe": lambda: tc.probe_read(arena, b.arena_bytes, sink)}
 for w, u in shapes:
     for v in variants:

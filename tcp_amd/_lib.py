@@ -79,6 +79,7 @@ BENCH_SIGNATURES = {
     "tcsum_probe_segments": (_I, [_V, _V, _U32, _U64, _V, _V]),
     "tcsum_probe_ipv4": (_I, [_V, _V, _U32, _U64, _I, _V, _V]),
     "tcsum_probe_flat": (_I, [_V, _V, _U32, _U64, _I, _I, _I, _V, _U64, _V, _V]),
+    "tcsum_flat_ipv4": (_I, [_I, _V, _V, _U32, _U64, _V, _V, _V, _V]),
     "tcsum_probe_ipv4_shape": (_I, [_V, _V, _U32, _I, _I, _I, _V, _V, _V]),
     "tcsum_probe_window": (_I, [_V, _U64, _I, _I, _I, _V, _V, _U64, _V, _V]),
     "tcsum_probe_txfloor_windows": (_U32, [_U64]),

@@ -483,7 +483,7 @@ static Geometry route(uint64_t mean_len)
 {
     int32_t r[5];
     tcsum_debug_route(mean_len, r);
-    return Geometry{r[0], r[1], r[2], r[3], r[4]};
+    return Geometry{r[0], r[1], r[2], r[3]};
 }
 
 static hipError_t launch_probe_desc(const void *arena, const void *descs, uint32_t n, uint64_t mean_len,
@@ -733,6 +733,91 @@ static hipError_t launch_probe_flat(uint8_t *arena, const tcsum_pkt_t *pkts, uin
     return hipErrorInvalidValue;
 }
 
+// ---- the byte-window stream in every IPv4 mode (tcsum_flat_ipv4): round 4's
+// candidate for configs[3], exact but 1.45-2x slower than k_ipv4 (DESIGN.md
+// §6, Round 4), so it left libtcsum.so in round 5 and lives here for A/Bs
+// and its parity tests.
+
+constexpr int kFlatWaves = 4, kFlatLoads = 3; // a 12-KiB window per 4-wave workgroup
+constexpr uint32_t kFlatWB = 16u * 64u * kFlatWaves * kFlatLoads;
+static std::atomic<uint32_t> g_flat_gen{0x40000000u}; // apart from flat_shape's
+
+// Windows the grid needs for a batch of n packets whose bytes sum to
+// total_bytes, allowing 16 B of padding per packet (16-B aligned starts) and
+// the first packet's 128-B line; a batch whose span is larger is found by
+// k_flat_plan and summed packet by packet.
+static uint64_t flat_windows(uint64_t total_bytes, uint32_t n)
+{
+    return (total_bytes + 16ull * n + 256u + kFlatWB - 1u) / kFlatWB;
+}
+
+template <int IPM>
+static hipError_t flat_u(uint32_t nw, uint32_t xg, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
+                         uint32_t *out, uint8_t *flags, int8_t *verdict, uint32_t opts, const FlatPlan *plan,
+                         const uint32_t *wfirst, unsigned long long *slot, uint32_t gen, hipStream_t s)
+{
+    return launch(k_flat_ipv4<IPM, kFlatWaves, kFlatLoads>, dim3(nw), dim3(kFlatWaves * 64), 0, s, arena, pkts, n, out,
+                  flags, verdict, opts, xg, plan, wfirst, slot, gen);
+}
+
+// ip_mode as launch_ipv4 (0 sums, 1 tx fill, 2 rx, 3 tx offload, 4 tx fill
+// with its stores deferred to k_tx_scatter).
+static hipError_t launch_ipv4_flat(int ip_mode, uint32_t xg, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
+                                   uint64_t total_bytes, uint32_t *out, uint8_t *flags, int8_t *verdict,
+                                   hipStream_t stream)
+{
+    const uint64_t nw = flat_windows(total_bytes, n);
+    if (nw == 0 || nw >= (1ull << 31))
+        return hipErrorInvalidValue;
+    // scratch: the plan, wfirst[nw + 1], slot[nw]; the deferred fill's 8 B per packet
+    const size_t plan_bytes = sizeof(FlatPlan) + ((4 * (nw + 1) + 7) & ~size_t(7)) + 8 * nw;
+    const bool defer = ip_mode == IP_TX_SPLIT;
+    const size_t side_bytes = defer ? (size_t)n * (out ? 4u : 8u) : 0u;
+    uint8_t *scr = nullptr;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void **>(&scr), plan_bytes + side_bytes, stream);
+    if (e != hipSuccess)
+        return e;
+    FlatPlan *plan = reinterpret_cast<FlatPlan *>(scr);
+    uint32_t *wfirst = reinterpret_cast<uint32_t *>(scr + sizeof(FlatPlan));
+    unsigned long long *slot =
+        reinterpret_cast<unsigned long long *>(scr + sizeof(FlatPlan) + ((4 * (nw + 1) + 7) & ~size_t(7)));
+    uint32_t gen = g_flat_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
+    if (gen == 0)
+        gen = g_flat_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
+    const uint64_t pthreads = (uint64_t)n + 1u > nw ? (uint64_t)n + 1u : nw;
+    e = launch(k_flat_plan<kFlatWB>, dim3((uint32_t)((pthreads + 255u) / 256u)), dim3(256), 0, stream, arena, pkts, n,
+               (uint32_t)nw, plan, wfirst, slot, gen);
+    const uint32_t w = (uint32_t)nw;
+    if (e == hipSuccess) {
+        switch (ip_mode) {
+        case IP_TX:
+            e = flat_u<IP_TX>(w, xg, arena, pkts, n, out, flags, verdict, 0u, plan, wfirst, slot, gen, stream);
+            break;
+        case IP_TX_SPLIT: {
+            uint32_t *side = reinterpret_cast<uint32_t *>(scr + plan_bytes);
+            uint32_t *vals = out ? out : side + n;
+            e = flat_u<IP_TX>(w, xg, arena, pkts, n, vals, flags, reinterpret_cast<int8_t *>(side), IP_OPT_DEFER,
+                              plan, wfirst, slot, gen, stream);
+            if (e == hipSuccess) {
+                e = launch(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, arena, pkts, n, vals, side);
+            }
+            break;
+        }
+        case IP_TX_OFFLOAD:
+            e = flat_u<IP_TX>(w, xg, arena, pkts, n, out, flags, verdict, IP_OPT_NO_STORE, plan, wfirst, slot, gen,
+                              stream);
+            break;
+        case IP_RX:
+            e = flat_u<IP_RX>(w, xg, arena, pkts, n, out, flags, verdict, 0u, plan, wfirst, slot, gen, stream);
+            break;
+        default:
+            e = flat_u<IP_SUMS>(w, xg, arena, pkts, n, out, flags, verdict, 0u, plan, wfirst, slot, gen, stream);
+        }
+    }
+    const hipError_t f = hipFreeAsync(scr, stream);
+    return e != hipSuccess ? e : f;
+}
+
 // k_ipv4 in other launch forms (measurement): the route's shape for the mode
 // (sums 32 x 6, rx 16 x 6) in 256- / 512- / 1024-thread workgroups, or held to
 // `occ` waves per SIMD (the route's builds: sums 66 VGPRs = 7 waves, rx 74 = 6)
@@ -847,6 +932,18 @@ int tcsum_probe_flat(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uin
     return rc_of(tcsum::launch_probe_flat(const_cast<uint8_t *>(static_cast<const uint8_t *>(arena)), pkts, n,
                                           total_bytes, variant, waves, loads, out, flags,
                                           static_cast<hipStream_t>(stream)));
+}
+
+int tcsum_flat_ipv4(int mode, void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t total_bytes, uint32_t *out,
+                    uint8_t *flags, int8_t *verdict, void *stream)
+{
+    if (n == 0)
+        return TCSUM_OK;
+    if (!arena || !pkts || !total_bytes || mode < 0 || mode > 4 || (mode == tcsum::IP_RX && !verdict) ||
+        (mode == tcsum::IP_TX_OFFLOAD && (!out || !flags)) || (mode == tcsum::IP_SUMS && !out))
+        return TCSUM_ERR_PARAM;
+    return rc_of(tcsum::launch_ipv4_flat(mode, (uint32_t)tcsum::route(1500).xcd, static_cast<uint8_t *>(arena), pkts,
+                                         n, total_bytes, out, flags, verdict, static_cast<hipStream_t>(stream)));
 }
 
 uint32_t tcsum_probe_txfloor_windows(uint64_t nbytes) { return tcsum::floor_windows(nbytes); }

@@ -467,13 +467,13 @@ static const struct {
 } kKnobs[] = {
     {"lanes", tcsum::KNOB_LANES},         {"loads", tcsum::KNOB_LOADS},
     {"xcd", tcsum::KNOB_XCD},             {"packed", tcsum::KNOB_PACKED},
-    {"flat", tcsum::KNOB_FLAT},           {"tx_split", tcsum::KNOB_TX_SPLIT},
+    {"tx_split", tcsum::KNOB_TX_SPLIT},
     {"args_launch", tcsum::KNOB_ARGS_LAUNCH}, {"sync_block", tcsum::KNOB_SYNC_BLOCK},
     {"e2e_trace", tcsum::KNOB_E2E_TRACE}, {"e2e_chunk_mb", tcsum::KNOB_E2E_CHUNK_MB},
     {"server_max", tcsum::KNOB_SERVER_MAX}, {"server_trace", tcsum::KNOB_SERVER_TRACE},
     {"server_idle_ms", tcsum::KNOB_SERVER_IDLE_MS}, {"server_wgs", tcsum::KNOB_SERVER_WGS},
     {"hostq_dma_kb", tcsum::KNOB_HOSTQ_DMA_KB}, {"hostq_dma_keep_mb", tcsum::KNOB_HOSTQ_DMA_KEEP_MB},
-    {"copy_threads", tcsum::KNOB_COPY_THREADS},
+    {"copy_threads", tcsum::KNOB_COPY_THREADS}, {"pf_dist", tcsum::KNOB_PF_DIST},
 };
 
 static int knob_of(const char *key)
@@ -514,7 +514,7 @@ void tcsum_debug_route(uint64_t mean_len, int32_t out[5])
         out[1] = g.loads;
         out[2] = g.xcd;
         out[3] = g.packed;
-        out[4] = g.flat;
+        out[4] = 0; // reserved (round 4's byte-window stream: libtcsum_bench.so)
     }
 }
 
@@ -530,17 +530,13 @@ static uint64_t mean_of(uint64_t total, uint32_t n) { return total && n ? total 
 static constexpr uint32_t kTxSplitMin = 131072;
 
 // The route for a batch and what its caller knows of the layout
-// (tcsum_hint_t): SHUFFLED skips the stream kernels, which would find out
-// per workgroup; a debug knob set to 1 keeps its kernel on regardless.
+// (tcsum_hint_t): SHUFFLED skips the stream kernel, which would find out
+// per workgroup; the debug knob "packed" set to 1 keeps it on regardless.
 static Geometry route_for(uint64_t total, uint32_t n, uint32_t layout)
 {
     Geometry g = tcsum::pick_geometry(mean_of(total, n));
-    if (layout == TCSUM_LAYOUT_SHUFFLED) {
-        if (tcsum::knob(tcsum::KNOB_PACKED) != 1)
-            g.packed = 0;
-        if (tcsum::knob(tcsum::KNOB_FLAT) != 1)
-            g.flat = 0;
-    }
+    if (layout == TCSUM_LAYOUT_SHUFFLED && tcsum::knob(tcsum::KNOB_PACKED) != 1)
+        g.packed = 0;
     return g;
 }
 
@@ -569,7 +565,7 @@ int tcsum_batch(int op, void *arena, const void *descs, uint32_t n, void *out, u
     case TCSUM_OP_IPV4:
         if (!out)
             return TCSUM_ERR_PARAM;
-        return rc_of(tcsum::launch_ipv4(0, g, a, pk, n, static_cast<uint32_t *>(out), flags, nullptr, st, total));
+        return rc_of(tcsum::launch_ipv4(0, g, a, pk, n, static_cast<uint32_t *>(out), flags, nullptr, st));
     case TCSUM_OP_IPV4_TX_FILL: {
         // Large batches: every packet's values and store positions first, then
         // all the field stores in one short second launch (mode 4) -- 4-6 %
@@ -583,19 +579,18 @@ int tcsum_batch(int op, void *arena, const void *descs, uint32_t n, void *out, u
         hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
         if (split && hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone)
             split = false;
-        return rc_of(tcsum::launch_ipv4(split ? 4 : 1, g, a, pk, n, static_cast<uint32_t *>(out), flags, nullptr, st,
-                                        total));
+        return rc_of(tcsum::launch_ipv4(split ? 4 : 1, g, a, pk, n, static_cast<uint32_t *>(out), flags, nullptr, st));
     }
     case TCSUM_OP_IPV4_TX_OFFLOAD:
         if (!out || !flags)
             return TCSUM_ERR_PARAM;
         // the kernel never writes the arena in this mode
-        return rc_of(tcsum::launch_ipv4(3, g, a, pk, n, static_cast<uint32_t *>(out), flags, nullptr, st, total));
+        return rc_of(tcsum::launch_ipv4(3, g, a, pk, n, static_cast<uint32_t *>(out), flags, nullptr, st));
     case TCSUM_OP_IPV4_RX_VERIFY:
         if (!verdict)
             return TCSUM_ERR_PARAM;
         // the kernel never writes the arena in this mode
-        return rc_of(tcsum::launch_ipv4(2, g, a, pk, n, static_cast<uint32_t *>(out), flags, verdict, st, total));
+        return rc_of(tcsum::launch_ipv4(2, g, a, pk, n, static_cast<uint32_t *>(out), flags, verdict, st));
     default:
         return TCSUM_ERR_PARAM;
     }
@@ -2149,7 +2144,7 @@ uint16_t checksum16(int offset, void *buf, uint16_t len, uint32_t pre_sum, int c
     d->offset = par;
     d->len = len;
     d->pre_sum = pre_sum;
-    const hipError_t e = tcsum::launch_segments(tcsum::MODE_EXACT, Geometry{64, 8, 1, 0, 0} /* unused for MODE_EXACT */, c.d_stage, c.d_desc,
+    const hipError_t e = tcsum::launch_segments(tcsum::MODE_EXACT, Geometry{64, 8, 1, 0} /* unused for MODE_EXACT */, c.d_stage, c.d_desc,
                                                 1, c.d_result, (complement ? 1u : 0u) | (par << 1), c.stream);
     run_sync(c, e);
     return *c.result;

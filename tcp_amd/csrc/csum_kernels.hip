@@ -284,7 +284,7 @@ Geometry pick_geometry(uint64_t mean_len)
 {
     // xcd: 64 workgroups per XCD run (scripts/xcd_tune.py, profiles/r01/xcd_tune.txt:
     // 2-4 % on every config, flat from 32 to 512)
-    Geometry g{32, 4, 64, 0, 0};
+    Geometry g{32, 4, 64, 0};
     const uint64_t chunks = mean_len / 16 + 1;
     const uint64_t interior = chunks > 2 ? chunks - 2 : 0;
     if (chunks >= 3072) {
@@ -327,8 +327,6 @@ Geometry pick_geometry(uint64_t mean_len)
     // ragged 64..2936 B 0.96, with 0..63-B gaps 1.00; with K < 3 (mean > ~4
     // KiB) it lost (9000 B 1.04, ragged 64..9000 B 1.20).  A forced per-range
     // geometry (debug lanes / loads) keeps it off unless debug "packed" = 1.
-    const int64_t kf = knob(KNOB_FLAT);
-    g.flat = kf > 0 ? 1 : 0; // IPv4 batches: the byte-window stream (measured before it becomes a default)
     const bool forced = kl >= 0 || ku >= 0;
     if ((kp >= 0 ? kp != 0 : !forced) && mean_len > 0) {
         const uint64_t pass = 16ull * 64u * kPkWaves * kPkLoads;
@@ -338,6 +336,14 @@ Geometry pick_geometry(uint64_t mean_len)
             g.packed = (int)(k > kmax ? kmax : k);
     }
     return g;
+}
+
+// Descriptor prefetch distance in workgroups (debug knob "pf_dist"; 0 = off),
+// passed to the stream / packet kernels in the high bits of aux / opts.
+static uint32_t pf_dist()
+{
+    const int64_t v = knob(KNOB_PF_DIST);
+    return v > 0 ? (uint32_t)(v < (1 << 23) ? v : (1 << 23) - 1) : 0u;
 }
 
 // The shapes the router can pick for the per-range kernels (and only those:
@@ -356,7 +362,8 @@ static hipError_t seg_u(int G, int U, uint32_t xg, uint32_t n, const void *arena
     TCSUM_SEG(16, 8) TCSUM_SEG(32, 6)
 #undef TCSUM_SEG
     if (G == 1024 && U == 4) { // one range per 16-wave workgroup, 2 KiB sub-ranges (TSO)
-        return launch(k_segments_wgx<16, 32, 4, MODE>, dim3(n), dim3(1024), 0, s, a, descs, n, out, aux, xg);
+        return launch(k_segments_wgx<16, 32, 4, MODE>, dim3(n), dim3(1024), 0, s, a, descs, n, out,
+                      aux | (pf_dist() << 8), xg);
     }
     if (G == 256 && U == 16) { // one range per workgroup
         return launch(k_segments_wg<16, MODE>, dim3(n), dim3(256), 0, s, a, descs, n, out, aux, xg);
@@ -399,9 +406,10 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
                                                                           : kPkMaxRanges * kPkWaves;
         const uint8_t *a = static_cast<const uint8_t *>(arena);
         const dim3 gr((n + K - 1) / K), bl(kPkWaves * 64);
+        const uint32_t ax = aux | (pf_dist() << 8);
         if (mode == MODE_SEG)
-            return launch(k_segments_pk<MODE_SEG>, gr, bl, 0, stream, a, descs, n, out, aux, (uint32_t)g.xcd, K);
-        return launch(k_segments_pk<MODE_PESO>, gr, bl, 0, stream, a, descs, n, out, aux, (uint32_t)g.xcd, K);
+            return launch(k_segments_pk<MODE_SEG>, gr, bl, 0, stream, a, descs, n, out, ax, (uint32_t)g.xcd, K);
+        return launch(k_segments_pk<MODE_PESO>, gr, bl, 0, stream, a, descs, n, out, ax, (uint32_t)g.xcd, K);
     }
     if (mode == MODE_EXACT) {
         return launch(k_segments<64, 8, MODE_EXACT>, dim3((n + 3) / 4), dim3(256), 0, stream,
@@ -421,8 +429,8 @@ static hipError_t ipv4_u(int G, int U, dim3 grid, uint8_t *arena, const tcsum_pk
 {
 #define TCSUM_IP(GG, UU)                                                                             \
     if (G == GG && U == UU) {                                                                      \
-        return launch(k_ipv4<GG, UU, IPM>, grid, dim3(256), 0, s, arena, pkts, n, out, flags, verdict, opts, \
-                      xg);                                                                           \
+        return launch(k_ipv4<GG, UU, IPM>, grid, dim3(256), 0, s, arena, pkts, n, out, flags, verdict,       \
+                      opts | (pf_dist() << 8), xg);                                                  \
     }
     TCSUM_IP(16, 1) TCSUM_IP(16, 2) TCSUM_IP(16, 3) TCSUM_IP(16, 4) TCSUM_IP(16, 6) TCSUM_IP(16, 8)
     TCSUM_IP(32, 6) TCSUM_IP(64, 4) TCSUM_IP(64, 16)
@@ -562,100 +570,11 @@ hipError_t launch_ipv4_tx_to(Geometry g, uint8_t *arena, uint8_t *store, const t
                     out, flags, stream);
 }
 
-// ---- byte-window stream (k_flat_plan + k_flat_ipv4), csum_device.h
-
-constexpr int kFlatWaves = 4, kFlatLoads = 3; // a 12-KiB window per 4-wave workgroup
-constexpr uint32_t kFlatWB = 16u * 64u * kFlatWaves * kFlatLoads;
-static std::atomic<uint32_t> g_flat_gen{0};
-
-// Windows the grid needs for a batch of n packets whose bytes sum to
-// total_bytes, allowing 16 B of padding per packet (16-B aligned starts) and
-// the first packet's 128-B line; a batch whose span is larger is found by
-// k_flat_plan and summed packet by packet.
-static uint64_t flat_windows(uint64_t total_bytes, uint32_t n)
-{
-    return (total_bytes + 16ull * n + 256u + kFlatWB - 1u) / kFlatWB;
-}
-
-template <int IPM>
-static hipError_t flat_u(uint32_t nw, uint32_t xg, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
-                         uint32_t *out, uint8_t *flags, int8_t *verdict, uint32_t opts, const FlatPlan *plan,
-                         const uint32_t *wfirst, unsigned long long *slot, uint32_t gen, hipStream_t s)
-{
-    return launch(k_flat_ipv4<IPM, kFlatWaves, kFlatLoads>, dim3(nw), dim3(kFlatWaves * 64), 0, s, arena, pkts, n, out,
-                  flags, verdict, opts, xg, plan, wfirst, slot, gen);
-}
-
-// ip_mode as launch_ipv4 (0 sums, 1 tx fill, 2 rx, 3 tx offload, 4 tx fill
-// with its stores deferred to k_tx_scatter).
-static hipError_t launch_ipv4_flat(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
-                                   uint64_t total_bytes, uint32_t *out, uint8_t *flags, int8_t *verdict,
-                                   hipStream_t stream)
-{
-    const uint64_t nw = flat_windows(total_bytes, n);
-    if (nw == 0 || nw >= (1ull << 31))
-        return hipErrorInvalidValue;
-    // scratch: the plan, wfirst[nw + 1], slot[nw]; the deferred fill's 8 B per packet
-    const size_t plan_bytes = sizeof(FlatPlan) + ((4 * (nw + 1) + 7) & ~size_t(7)) + 8 * nw;
-    const bool defer = ip_mode == IP_TX_SPLIT;
-    const size_t side_bytes = defer ? (size_t)n * (out ? 4u : 8u) : 0u;
-    uint8_t *scr = nullptr;
-    hipError_t e = scratch_alloc(reinterpret_cast<void **>(&scr), plan_bytes + side_bytes, stream);
-    if (e != hipSuccess)
-        return e;
-    FlatPlan *plan = reinterpret_cast<FlatPlan *>(scr);
-    uint32_t *wfirst = reinterpret_cast<uint32_t *>(scr + sizeof(FlatPlan));
-    unsigned long long *slot =
-        reinterpret_cast<unsigned long long *>(scr + sizeof(FlatPlan) + ((4 * (nw + 1) + 7) & ~size_t(7)));
-    uint32_t gen = g_flat_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
-    if (gen == 0)
-        gen = g_flat_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
-    const uint64_t pthreads = (uint64_t)n + 1u > nw ? (uint64_t)n + 1u : nw;
-    e = launch(k_flat_plan<kFlatWB>, dim3((uint32_t)((pthreads + 255u) / 256u)), dim3(256), 0, stream, arena, pkts, n,
-               (uint32_t)nw, plan, wfirst, slot, gen);
-    const uint32_t xg = (uint32_t)g.xcd, w = (uint32_t)nw;
-    if (e == hipSuccess) {
-        switch (ip_mode) {
-        case IP_TX:
-            e = flat_u<IP_TX>(w, xg, arena, pkts, n, out, flags, verdict, 0u, plan, wfirst, slot, gen, stream);
-            break;
-        case IP_TX_SPLIT: {
-            uint32_t *side = reinterpret_cast<uint32_t *>(scr + plan_bytes);
-            uint32_t *vals = out ? out : side + n;
-            e = flat_u<IP_TX>(w, xg, arena, pkts, n, vals, flags, reinterpret_cast<int8_t *>(side), IP_OPT_DEFER,
-                              plan, wfirst, slot, gen, stream);
-            if (e == hipSuccess) {
-                e = launch(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, arena, pkts, n, vals, side);
-            }
-            break;
-        }
-        case IP_TX_OFFLOAD:
-            e = flat_u<IP_TX>(w, xg, arena, pkts, n, out, flags, verdict, IP_OPT_NO_STORE, plan, wfirst, slot, gen,
-                              stream);
-            break;
-        case IP_RX:
-            e = flat_u<IP_RX>(w, xg, arena, pkts, n, out, flags, verdict, 0u, plan, wfirst, slot, gen, stream);
-            break;
-        default:
-            e = flat_u<IP_SUMS>(w, xg, arena, pkts, n, out, flags, verdict, 0u, plan, wfirst, slot, gen, stream);
-        }
-    }
-    const hipError_t f = hipFreeAsync(scr, stream);
-    return e != hipSuccess ? e : f;
-}
-
 hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
-                       uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream, uint64_t total_bytes)
+                       uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream)
 {
     if (n == 0)
         return hipSuccess;
-    // the byte-window stream: a batch whose byte count is known, outside
-    // hipGraph capture (its plan lives in stream-ordered scratch)
-    if (g.flat && total_bytes) {
-        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(stream, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone)
-            return launch_ipv4_flat(ip_mode, g, arena, pkts, n, total_bytes, out, flags, verdict, stream);
-    }
     if (g.lanes < 16)
         g.lanes = 16;
     if (g.lanes > 64) // k_ipv4 keeps a packet inside one wave (no workgroup-per-packet form)

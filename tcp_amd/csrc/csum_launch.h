@@ -22,7 +22,6 @@ struct Geometry {
     int xcd;    // consecutive workgroups kept on one XCD (1: dispatch order)
     int packed; // K > 0: checksum_peso / pktbuf_checksum16 batches as a packed
                 // stream, K consecutive ranges per 4-wave workgroup (k_segments_pk)
-    int flat;   // 1: byte-window stream (k_flat_*): fixed byte windows per workgroup
 };
 
 // Test and measurement overrides (include/tcsum_debug.h): -1 = the router's
@@ -32,7 +31,7 @@ enum Knob : int {
     KNOB_LOADS,      // per-range loads per lane (U)
     KNOB_XCD,        // XCD run length
     KNOB_PACKED,     // 0 / 1: k_segments_pk off / on
-    KNOB_FLAT,       // 0 / 1: the byte-window stream off / on
+    KNOB_RESERVED_4, // round 4's "flat" (the byte-window stream, now libtcsum_bench.so's tcsum_flat_ipv4)
     KNOB_TX_SPLIT,   // 0 / 1: tx fill stores in the kernel / deferred to k_tx_scatter
     KNOB_ARGS_LAUNCH, // 0: drop-in launch path with its descriptor in pinned memory
     KNOB_SYNC_BLOCK, // 1: drop-in calls block in hipStreamSynchronize instead of spinning
@@ -45,6 +44,7 @@ enum Knob : int {
     KNOB_HOSTQ_DMA_KB, // host-queue batches from this span on go through the copy engine (262144)
     KNOB_HOSTQ_DMA_KEEP_MB, // device arena kept between host-queue calls up to this size (256)
     KNOB_COPY_THREADS, // host threads of a parallel gather / scatter pass (16)
+    KNOB_PF_DIST,      // descriptor prefetch distance of the stream / packet kernels, in workgroups
     KNOB_COUNT
 };
 int64_t knob(Knob k);
@@ -59,10 +59,8 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
 // ip_mode: 0 sums, 1 tx fill (writes into arena), 2 rx verify (verdict required),
 //          3 tx offload (the tx fill's values into out only; out required),
 //          4 tx fill with its stores deferred to a second launch (k_tx_scatter)
-// total_bytes (the batch's byte count, 0 = unknown) lets g.flat take the
-// byte-window stream (k_flat_plan + k_flat_ipv4).
 hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
-                       uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream, uint64_t total_bytes = 0);
+                       uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream);
 
 // The tx fill (deferred stores) reading `arena` and storing the fields into
 // `store` (the same packets at another device-visible address).

@@ -423,10 +423,20 @@ def pick_geometry(mean_len: int):
 
 def route(mean_len: int) -> dict:
     """The route the batch calls take for a mean range length (debug knobs
-    applied): lanes, loads, xcd, packed K (0 = off), flat (tcsum_debug_route)."""
+    applied): lanes, loads, xcd, packed K (0 = off) (tcsum_debug_route)."""
     r = (ctypes.c_int32 * 5)()
     _lib.lib().tcsum_debug_route(mean_len, r)
-    return dict(zip(("lanes", "loads", "xcd", "packed", "flat"), list(r)))
+    return dict(zip(("lanes", "loads", "xcd", "packed"), list(r)[:4]))
+
+
+def flat_ipv4(mode: int, arena, pkts, n: int, total_bytes: int, out=None, flags=None, verdict=None, stream=None):
+    """The byte-window stream (libtcsum_bench.so's tcsum_flat_ipv4, measurement
+    and tests only): mode 0 sums, 1 tx fill, 2 rx verify, 3 tx offload, 4 tx
+    fill with deferred stores; device tensors, as the tcsum_batch_ipv4* calls."""
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    rc = _lib.bench_lib().tcsum_flat_ipv4(mode, arena.data_ptr(), pkts.data_ptr(), n, total_bytes, ptr(out),
+                                          ptr(flags), ptr(verdict), _stream_ptr(stream))
+    _lib.check(rc, "tcsum_flat_ipv4")
 
 
 def debug_set(key: str, value: int) -> None:

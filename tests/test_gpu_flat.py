@@ -1,5 +1,6 @@
 """k_flat_ipv4 -- the byte-window stream for IPv4 batches (plan + stream,
-csum_device.h) -- against the reference's fixtures and the oracle (the CPU
+csum_device.h; libtcsum_bench.so's tcsum_flat_ipv4 since round 5, when it
+left the product's route) -- against the reference's fixtures and the oracle (the CPU
 restatement of net/src/tools.c:24-75 / pktbuf.c:646-670 and of the receive
 gates of ipv4.c / tcp_in.c / udp.c / icmpv4.c, pinned to the reference's
 own outputs).
@@ -31,7 +32,7 @@ def torch():
 
 
 @pytest.fixture(scope="module")
-def tc(torch):
+def prod(torch):
     from tcp_amd import build
     build.build()
     import tcp_amd
@@ -39,13 +40,53 @@ def tc(torch):
     return tcp_amd
 
 
-@pytest.fixture(autouse=True)
-def flat(tc):
-    tc.debug_set("flat", 1)
-    assert tc.route(4500)["flat"] == 1
-    yield
-    tc.debug_set("flat", -1)
-    tc.debug_set("tx_split", -1)
+class FlatStream:
+    """The tcsum_batch_ipv4* calls the tests below make, run by the
+    byte-window stream (libtcsum_bench.so's tcsum_flat_ipv4: round 5 took it
+    out of libtcsum.so's route); every other attribute is tcp_amd's."""
+
+    def __init__(self, tc, torch):
+        self._tc, self._torch, self._split = tc, torch, 1
+
+    def __getattr__(self, name):
+        return getattr(self._tc, name)
+
+    def debug_set(self, key, value):
+        if key == "tx_split":  # the fill's two forms: stores in the kernel / deferred
+            self._split = 1 if value == -1 else int(value)
+        else:
+            self._tc.debug_set(key, value)
+
+    def _t(self, n, dt):
+        return self._torch.empty(n, dtype=dt, device="cuda")
+
+    def batch_ipv4(self, arena, d, n, total, out=None, flags=None, want_flags=True):
+        out = self._t(n, self._torch.uint32) if out is None else out
+        flags = self._t(n, self._torch.uint8) if flags is None and want_flags else flags
+        self._tc.flat_ipv4(0, arena, d, n, total, out=out, flags=flags)
+        return out, flags
+
+    def batch_ipv4_rx_verify(self, arena, d, n, total, verdict=None, out=None, flags=None, want_flags=True):
+        verdict = self._t(n, self._torch.int8) if verdict is None else verdict
+        flags = self._t(n, self._torch.uint8) if flags is None and want_flags else flags
+        self._tc.flat_ipv4(2, arena, d, n, total, out=out, flags=flags, verdict=verdict)
+        return verdict, flags
+
+    def batch_ipv4_tx_offload(self, arena, d, n, total, out=None, flags=None):
+        out = self._t(n, self._torch.uint32) if out is None else out
+        flags = self._t(n, self._torch.uint8) if flags is None else flags
+        self._tc.flat_ipv4(3, arena, d, n, total, out=out, flags=flags)
+        return out, flags
+
+    def batch_ipv4_tx_fill(self, arena, d, n, total, out=None, flags=None, want_flags=True):
+        flags = self._t(n, self._torch.uint8) if flags is None and want_flags else flags
+        self._tc.flat_ipv4(4 if self._split else 1, arena, d, n, total, out=out, flags=flags)
+        return flags
+
+
+@pytest.fixture(scope="module")
+def tc(prod, torch):
+    return FlatStream(prod, torch)
 
 
 def to_dev(torch, a: np.ndarray, pad: int = 256):
@@ -286,13 +327,11 @@ def test_flat_full_mixed_config(tc, torch, oracle, config):
 
 
 @pytest.mark.parametrize("layout", ["packed", "shuffled"])
-@pytest.mark.parametrize("flat_knob", [-1, 1])
-def test_ipv4_layout_hints_give_the_same_results(tc, torch, oracle, layout, flat_knob):
+def test_ipv4_layout_hints_give_the_same_results(prod, torch, oracle, layout):
     """tcsum_batch's layout hint on every IPv4 operation (sums, rx verify, tx
-    offload, tx fill) changes only the kernel, never a result -- with the
-    byte-window stream off (the route) and on, and when an ORDERED promise is
-    false (a shuffled batch)."""
-    tc.debug_set("flat", flat_knob)
+    offload, tx fill) changes only the kernel, never a result -- also when an
+    ORDERED promise is false (a shuffled batch)."""
+    tc = prod
     rng = np.random.default_rng(300 + (layout == "shuffled"))
     lens = rng.integers(20, 9000, 3000).astype(np.int64)
     offs = _stream(lens, 7)

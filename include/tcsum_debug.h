@@ -70,7 +70,8 @@ int64_t tcsum_debug_get(const char *key);
  * five u64 -- {0, buffer, host lo, host hi, buffer offset of lo} for a copy
  * of host bytes [lo, hi) into device buffer 0 (the lead's) or 1 (the
  * arena's), {1, buffer, i0, i1, arena offset of the buffer's byte 0} for a
- * kernel over segments [i0, i1) reading that buffer -- at most max_rows of
+ * kernel over segments [i0, i1) reading that buffer ({2, ...}: the same, the
+ * segments out of offset order, so the per-range kernel) -- at most max_rows of
  * them written; buf_bytes[0..1]: the two buffers' sizes (0: unused).  Uses
  * the "e2e_chunk_mb" knob like the call.  Returns the row count, or
  * TCSUM_ERR_PARAM (a segment outside the arena, as the call would). */

@@ -708,15 +708,23 @@ void parallel_for(size_t n, size_t min_per, F &&f);
 }
 
 // Byte span [lo, hi) and byte count of a run of segments.
+// `ordered`: the non-empty segments' offsets never decrease (first / last:
+// the first and last such offset); merged in segment order.
 struct HostSpan {
     uint64_t lo = UINT64_MAX, hi = 0, bytes = 0;
-    bool bad = false;
+    uint64_t first = UINT64_MAX, last = 0;
+    bool bad = false, ordered = true;
     void merge(const HostSpan &o)
     {
         lo = o.lo < lo ? o.lo : lo;
         hi = o.hi > hi ? o.hi : hi;
         bytes += o.bytes;
         bad |= o.bad;
+        if (o.first != UINT64_MAX) {
+            ordered = ordered && o.ordered && (first == UINT64_MAX || o.first >= last);
+            first = first == UINT64_MAX ? o.first : first;
+            last = o.last;
+        }
     }
 };
 
@@ -779,6 +787,9 @@ HostSpan span_of_block(const tcsum_peso_t *segs, uint32_t n, uint64_t arena_byte
             sp.lo = o < sp.lo ? o : sp.lo;
             sp.hi = o + l > sp.hi ? o + l : sp.hi;
             sp.bytes += l;
+            sp.ordered &= sp.first == UINT64_MAX || o >= sp.last;
+            sp.first = sp.first == UINT64_MAX ? o : sp.first;
+            sp.last = o;
         }
     }
     return sp;
@@ -1005,9 +1016,14 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         const uint32_t i1 = (uint32_t)std::min<uint64_t>(n, (uint64_t)ch[k].b1 * kSpanBlock);
         if (i1 <= i0)
             continue;
-        const hipError_t e = tcsum::launch_segments(tcsum::MODE_SEG,
-                                                    tcsum::pick_geometry(mean_of(ch[k].sp.bytes, i1 - i0)),
-                                                    base[ch[k].buf], c.d_descs + i0, i1 - i0, c.d_out + i0, 1u, ks);
+        // the host saw the order: segments out of offset order go straight to
+        // the per-range kernel (tcsum_batch's SHUFFLED), not the packed stream,
+        // whose workgroups would each find out and sum range by range
+        tcsum::Geometry g = tcsum::pick_geometry(mean_of(ch[k].sp.bytes, i1 - i0));
+        if (!ch[k].sp.ordered && tcsum::knob(tcsum::KNOB_PACKED) != 1)
+            g.packed = 0;
+        const hipError_t e = tcsum::launch_segments(tcsum::MODE_SEG, g, base[ch[k].buf], c.d_descs + i0, i1 - i0,
+                                                    c.d_out + i0, 1u, ks);
         if (e != hipSuccess)
             return fail_sys(8, e);
     }
@@ -1053,8 +1069,8 @@ int64_t tcsum_debug_plan_host_peso(const tcsum_peso_t *segs, uint32_t n, uint64_
         if (hi > lo) // copy: buffer, host [lo, hi), buffer offset of lo
             row(0, (uint64_t)c.buf, lo, hi, lo - bases[c.buf]);
         const uint32_t i0 = c.b0 * kSpanBlock, i1 = (uint32_t)std::min<uint64_t>(n, (uint64_t)c.b1 * kSpanBlock);
-        if (i1 > i0) // kernel: buffer, segments [i0, i1), the buffer's arena base
-            row(1, (uint64_t)c.buf, i0, i1, bases[c.buf]);
+        if (i1 > i0) // kernel (2: the segments are out of offset order), buffer, segments [i0, i1), arena base
+            row(c.sp.ordered ? 1 : 2, (uint64_t)c.buf, i0, i1, bases[c.buf]);
     }
     return (int64_t)k;
 }

@@ -743,6 +743,24 @@ __device__ __forceinline__ void pk_ranges(const uint8_t *__restrict__ arena, con
 
 constexpr uint32_t kPkMaxPasses = 64; // longer regions go range by range
 
+// A workgroup of k_segments_pk whose kw ranges are not one region: G lanes
+// per range, G the widest power of two that gives every range a group.
+template <int MODE>
+__device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, const void *__restrict__ descs,
+                                            uint16_t *__restrict__ out, uint32_t aux, uint32_t first, uint32_t kw,
+                                            uint32_t T)
+{
+    const uint32_t lanes_per = T / kw;
+    if (lanes_per >= 64)
+        pk_ranges<MODE, 64>(arena, descs, out, aux, first, kw, T);
+    else if (lanes_per >= 32)
+        pk_ranges<MODE, 32, 3>(arena, descs, out, aux, first, kw, T);
+    else if (lanes_per >= 16)
+        pk_ranges<MODE, 16>(arena, descs, out, aux, first, kw, T);
+    else
+        pk_ranges<MODE, 8>(arena, descs, out, aux, first, kw, T);
+}
+
 
 template <int MODE, int W = kPkWaves, int U = kPkLoads, bool PROBE = false>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) void k_segments_pk(
@@ -769,6 +787,10 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     // slower, profiles/r03/packed/ab_vdesc_w8.txt)
     desc_span<MODE>(descs, first, r0, len0);
     desc_span<MODE>(descs, first + kw - 1u, offl, lenl);
+    uint32_t pf = 0;
+    if (const uint32_t pfd = aux >> 8; pfd != 0u && w == 0) // wave-uniform
+        pf = prefetch_descs(descs, (uint64_t)(blk + pfd) * K, n, MODE == MODE_PESO ? 24u : 16u,
+                            (K * (MODE == MODE_PESO ? 24u : 16u) + 127u) / 128u + 1u, lane);
     const uint64_t rend = offl + lenl;
     const uint8_t *p = arena + r0;
     const uint32_t s0 = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
@@ -777,6 +799,17 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     // safe to load before the ranges are known to lie inside it
     const bool span_ok = len0 != 0 && lenl != 0 && rend > r0 &&
                          rend - r0 <= (uint64_t)kPkMaxPasses * CH * 16u - s0;
+    if (!PROBE && !span_ok) {
+        // workgroup-uniform, known from the two scalar descriptors: range by
+        // range at once (a shuffled batch's usual case), before any stream
+        // load or the region check's own descriptor loads -- so its ranges'
+        // descriptors (lines the scalar loads just brought in) and then their
+        // bytes are the only waits
+        pk_fallback<MODE>(arena, descs, out, aux, first, kw, T);
+        if (pf == 0x9E3779B9u && K == 0u) // never: keeps the prefetch load alive
+            out[0] = (uint16_t)pf;
+        return;
+    }
     bool ranges = !span_ok; // workgroup-uniform: sum range by range instead
     const uint32_t span = span_ok ? (uint32_t)(rend - r0) : 0u;
     const uint32_t nch = span_ok ? (s0 + span + 15u) >> 4 : 0u;
@@ -790,10 +823,6 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
         v[u] = load16<true>(base + (c < nch ? c : (nch ? nch - 1u : 0u)));
     }
     issue_fence();
-    uint32_t pf = 0;
-    if (const uint32_t pfd = aux >> 8; pfd != 0u && w == 0) // wave-uniform
-        pf = prefetch_descs(descs, (uint64_t)(blk + pfd) * K, n, MODE == MODE_PESO ? 24u : 16u,
-                            (K * (MODE == MODE_PESO ? 24u : 16u) + 127u) / 128u + 1u, lane);
     // every wave: its share of the K descriptors (lane r: range 64w + r),
     // whether each lies in the region, and its start and end in bytes from the
     // first chunk
@@ -893,16 +922,8 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
         if (pass + 1u < npass)
             __syncthreads(); // the next pass overwrites dat / ex / subtot
     }
-    if (ranges) { // G lanes per range: the widest power of two that gives every range a group
-        const uint32_t lanes_per = T / kw;
-        if (lanes_per >= 64)
-            pk_ranges<MODE, 64>(arena, descs, out, aux, first, kw, T);
-        else if (lanes_per >= 32)
-            pk_ranges<MODE, 32, 3>(arena, descs, out, aux, first, kw, T);
-        else if (lanes_per >= 16)
-            pk_ranges<MODE, 16>(arena, descs, out, aux, first, kw, T);
-        else
-            pk_ranges<MODE, 8>(arena, descs, out, aux, first, kw, T);
+    if (ranges) { // a range outside the region, found by the descriptor check
+        pk_fallback<MODE>(arena, descs, out, aux, first, kw, T);
         return;
     }
     if (mine)

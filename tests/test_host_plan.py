@@ -44,6 +44,9 @@ def check_plan(segs: np.ndarray, arena_bytes: int):
             copied[buf].append((a, b, c))
             continue
         # kernel on segments [a, b) of buffer `buf` whose byte 0 is arena offset c
+        # (kind 2: out of offset order, so the per-range kernel, not the packed stream)
+        o_all = off[a:b][ln[a:b] > 0]
+        assert (kind == 1) == bool((np.diff(o_all) >= 0).all()), (kind, a, b)
         assert a == next_i and b > a, (a, b, next_i)
         next_i = b
         covered[a:b] += 1
@@ -107,7 +110,7 @@ def test_seed26_plan(chunk_knob):
     assert segs.size == 1000 and chunk_mb == 8
     chunk_knob(chunk_mb)
     rows, bufs = check_plan(segs, arena_bytes)
-    assert rows[:, 0].tolist() == [0, 1] and bufs[0] == 0
+    assert rows[:, 0].tolist() == [0, 1] and bufs[0] == 0  # in order: the packed stream
 
 
 @pytest.mark.parametrize("shape", ["lead_then_far", "shuffled_big", "sparse_tail", "zeros", "one_byte_end",

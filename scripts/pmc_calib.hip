@@ -78,6 +78,32 @@ __global__ __launch_bounds__(256) void k_desc(const uint8_t *__restrict__ d, uin
     sink_it(x, sink);
 }
 
+// k_segments_pk's descriptor pattern (K = 8 ranges of 24 B per 4-wave
+// workgroup): every wave scalar-loads the first and the last descriptor's
+// offset and length (desc_span: a workgroup-uniform index, so s_load), and
+// lanes 0..7 of wave 0 then vector-load all eight (load_desc).  SCALAR_ONLY:
+// the scalar loads alone; VECTOR_ONLY: the vector loads alone.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_pkdesc(const uint8_t *__restrict__ d, uint32_t n, uint32_t *sink)
+{
+    constexpr uint32_t K = 8;
+    const uint32_t first = blockIdx.x * K;
+    uint32_t x = 0;
+    if (MODE != 2) { // scalar: offset (8 B) and length (4 B) of the first and last descriptor
+        const uint8_t *a = d + 24ull * first, *b = d + 24ull * (first + K - 1u);
+        const uint2 oa = *reinterpret_cast<const uint2 *>(a), ob = *reinterpret_cast<const uint2 *>(b);
+        x ^= oa.x ^ oa.y ^ ob.x ^ ob.y ^ *reinterpret_cast<const uint32_t *>(a + 8) ^
+             *reinterpret_cast<const uint32_t *>(b + 8);
+    }
+    if (MODE != 1 && threadIdx.x < K) { // vector: lane r loads descriptor first + r (16 + 8 B)
+        const uint8_t *r = d + 24ull * (first + threadIdx.x);
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(r);
+        const uint2 w = *reinterpret_cast<const uint2 *>(r + 16);
+        x ^= v.x ^ v.y ^ v.z ^ v.w ^ w.x ^ w.y;
+    }
+    sink_it(x, sink);
+}
+
 // one default-policy 16-B chunk per packet (the edge / header chunks)
 __global__ __launch_bounds__(256) void k_sparse16(const uint8_t *__restrict__ a, uint32_t n, uint64_t stride,
                                                   uint32_t *sink)
@@ -176,6 +202,12 @@ int main()
         flush_l2();
         hipLaunchKernelGGL(k_desc<24>, dim3(kPkts / 16), dim3(256), 0, 0, desc, kPkts, sink);
         flush_l2();
+        hipLaunchKernelGGL(k_pkdesc<0>, dim3(kPkts / 8), dim3(256), 0, 0, desc, kPkts, sink);
+        flush_l2();
+        hipLaunchKernelGGL(k_pkdesc<1>, dim3(kPkts / 8), dim3(256), 0, 0, desc, kPkts, sink);
+        flush_l2();
+        hipLaunchKernelGGL(k_pkdesc<2>, dim3(kPkts / 8), dim3(256), 0, 0, desc, kPkts, sink);
+        flush_l2();
         hipLaunchKernelGGL(k_sparse16, dim3(pblocks), dim3(256), 0, 0, pkts, kPkts, (uint64_t)1500, sink);
         flush_l2();
         hipLaunchKernelGGL(k_sparse16, dim3(pblocks), dim3(256), 0, 0, pkts, kPkts, kStride, sink);
@@ -204,6 +236,10 @@ int main()
     note("k_stream<false>", "streaming read, 16 B/lane, default policy", (double)stream_bytes, 0);
     note("k_desc<16>", "16-B descriptor per 16-lane group", 16.0 * kPkts, 0);
     note("k_desc<24>", "24-B descriptor (16 + 8 B loads) per 16-lane group", 24.0 * kPkts, 0);
+    note("k_pkdesc<0>", "k_segments_pk's descriptors: scalar first/last + vector all (24 B x 8 per workgroup)",
+         24.0 * kPkts, 0);
+    note("k_pkdesc<1>", "the same, scalar first/last only (algorithmic: every descriptor line)", 24.0 * kPkts, 0);
+    note("k_pkdesc<2>", "the same, vector loads only", 24.0 * kPkts, 0);
     note("k_sparse16@1500", "one default-policy 16-B chunk per packet, stride 1500", 16.0 * kPkts, 0);
     note("k_sparse16@4532", "one default-policy 16-B chunk per packet, stride 4532", 16.0 * kPkts, 0);
     note("k_load<unsigned int, 4>", "dense u32 load per lane", 4.0 * kPkts, 0);

@@ -233,6 +233,7 @@ def test_batch_argument_errors_without_device(libpath):
     v = ctypes.c_void_p(64)
     assert L.tcsum_batch(99, v, v, 4, v, None, None, ctypes.byref(h), None) == _lib.ERR_PARAM  # no such op
     assert L.tcsum_batch(2, v, v, 4, v, None, None, ctypes.byref(Hint(0, 7, 0)), None) == _lib.ERR_PARAM  # layout
+    assert L.tcsum_batch(2, v, v, 4, v, None, None, ctypes.byref(Hint(0, 1, 5)), None) == _lib.ERR_PARAM  # rsv != 0
     assert L.tcsum_batch(2, v, v, 4, None, None, None, ctypes.byref(h), None) == _lib.ERR_PARAM  # no out
     assert L.tcsum_batch(6, v, v, 4, v, None, None, ctypes.byref(h), None) == _lib.ERR_PARAM  # rx: no verdict
     assert L.tcsum_batch(2, v, v, 0, None, None, None, None, None) == _lib.OK

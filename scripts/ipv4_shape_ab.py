@@ -19,6 +19,7 @@ from tcp_amd import _lib, workload  # noqa: E402
 
 B = _lib.bench_lib()
 SKEW_ONLY = "--skew" in sys.argv
+DB_ONLY = "--db" in sys.argv  # two data passes in flight, with and without the descriptor prefetch
 for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mixed_aligned", "mixed_rx"]):
     b = workload.make_batch(cfg)
     arena, descs = workload.materialize(b)
@@ -47,7 +48,18 @@ for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mi
         return f
 
     kinds = {"product (256 threads)": product, "256 threads, same kernel (probe lib)": shape(256, 0)}
-    if SKEW_ONLY:
+
+    def with_pf(f, pf):
+        def g(o, v):
+            with tc.debug(pf_dist=pf):
+                f(o, v)
+        return g
+
+    if DB_ONLY:
+        kinds.update({"two passes in flight": shape(256, 200),
+                      "product, pf_dist 2048": with_pf(product, 2048),
+                      "two passes in flight, pf_dist 2048": with_pf(shape(256, 200), 2048)})
+    elif SKEW_ONLY:
         kinds.update({"data pass 16 B past the line": shape(256, 116)})
         if not rx:
             kinds["data pass 64 B past the line"] = shape(256, 164)

@@ -833,8 +833,11 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
     const uint32_t per = (uint32_t)wg / G;
     const dim3 grid((n + per - 1u) / per), blk((uint32_t)wg);
     uint8_t *fl = nullptr;
+    // the product's descriptor prefetch distance (debug knob "pf_dist") rides in opts
+    const int64_t pfk = tcsum_debug_get("pf_dist");
+    const uint32_t opts = pfk > 0 ? (uint32_t)pfk << 8 : 0u;
 #define TCSUM_SH(KERN)                                                                                   \
-    note_launch(launch(KERN, grid, blk, 0, stream, arena, pkts, n, out, fl, verdict, 0u, xg));            \
+    note_launch(launch(KERN, grid, blk, 0, stream, arena, pkts, n, out, fl, verdict, opts, xg));          \
     return take_launch_rc();
     if (mode == IP_SUMS) {
         if (occ == 0 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256>)) }
@@ -842,6 +845,7 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 0 && wg == 1024) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 1024>)) }
         if (occ == 8 && wg == 256) { TCSUM_SH((k_ipv4_occ<32, 6, IP_SUMS, 8>)) }
         if (occ == 100 + 16 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 16>)) } // data pass skewed 16 B
+        if (occ == 200 && wg == 256) { TCSUM_SH((k_ipv4_db<32, 6, IP_SUMS>)) } // two passes in flight
         if (occ == 100 + 64 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 64>)) }
     } else if (mode == IP_RX && verdict) {
         if (occ == 0 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256>)) }
@@ -849,6 +853,7 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 7 && wg == 256) { TCSUM_SH((k_ipv4_occ<16, 6, IP_RX, 7>)) }
         if (occ == 8 && wg == 256) { TCSUM_SH((k_ipv4_occ<16, 6, IP_RX, 8>)) }
         if (occ == 100 + 16 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256, 16>)) }
+        if (occ == 200 && wg == 256) { TCSUM_SH((k_ipv4_db<16, 6, IP_RX>)) } // two passes in flight
     }
 #undef TCSUM_SH
     return hipErrorInvalidValue;

@@ -1196,7 +1196,9 @@ __device__ __forceinline__ void ip_finish(const IpHdr &ih, uint32_t fl, bool big
 // SKEW (measurement): the data pass starts SKEW bytes past the packet's
 // 128-B line instead of on it, for packets that start that far in (0: the
 // route)
-template <int G, int U, int IPM, int SKEW = 0>
+// DB (measurement): each later pass's loads are issued before the previous
+// pass is summed (two passes in flight per lane group, more registers).
+template <int G, int U, int IPM, int SKEW = 0, bool DB = false>
 __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                             uint32_t pk, uint32_t n, uint32_t *__restrict__ out,
                                             uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
@@ -1326,16 +1328,37 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
         acc_h += ph; // header <= 60 bytes: no overflow
         acc_l = fold_step(acc_l + pl);
     };
-    if (dch)
-        pass(v, 0u);
-    for (uint32_t b0 = G * U; b0 < dch; b0 += G * U) {
-        u32x4 w[U];
+    if constexpr (DB) {
+        u32x4 nx[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t idx = b0 + u * G + gl;
-            w[u] = load16<true>(dbase + (idx < dch ? idx : dlast));
+            const uint32_t idx = G * U + u * G + gl;
+            nx[u] = load16<true>(dbase + (idx < dch ? idx : dlast));
         }
-        pass(w, b0);
+        if (dch)
+            pass(v, 0u);
+        for (uint32_t b0 = G * U; b0 < dch; b0 += G * U) {
+            u32x4 cur[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                cur[u] = nx[u];
+                const uint32_t idx = b0 + G * U + u * G + gl;
+                nx[u] = load16<true>(dbase + (idx < dch ? idx : dlast));
+            }
+            pass(cur, b0);
+        }
+    } else {
+        if (dch)
+            pass(v, 0u);
+        for (uint32_t b0 = G * U; b0 < dch; b0 += G * U) {
+            u32x4 w[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t idx = b0 + u * G + gl;
+                w[u] = load16<true>(dbase + (idx < dch ? idx : dlast));
+            }
+            pass(w, b0);
+        }
     }
     acc_h = group_sum<G>(acc_h);
     acc_l = group_sum<G>(acc_l);
@@ -1362,6 +1385,18 @@ __global__ __launch_bounds__(T) void k_ipv4(uint8_t *__restrict__ arena, const t
                            opts); // no 32-bit wrap for any n
     if (pf == 0x9E3779B9u && n == 0u) // never: keeps the prefetch load alive
         out[0] = pf;
+}
+
+// k_ipv4 with two data passes in flight per lane group (measurement)
+template <int G, int U, int IPM>
+__global__ __launch_bounds__(256) void k_ipv4_db(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
+                                                 uint32_t n, uint32_t *__restrict__ out,
+                                                 uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
+                                                 uint32_t opts, uint32_t xg)
+{
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    ipv4_packet<G, U, IPM, 0, true>(arena, pkts, blk * (256u / G) + threadIdx.x / G, n, out, flags_out, verdict_out,
+                                    opts);
 }
 
 // k_ipv4 held to OCC waves per SIMD (the sums form takes 66 VGPRs, i.e. 7

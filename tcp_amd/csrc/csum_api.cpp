@@ -59,7 +59,7 @@ struct Pinned {
         while (c < bytes)
             c <<= 1;
         if (h)
-            (void)hipHostFree(h);
+            (void)tcsum::quiet(hipHostFree(h));
         h = d = nullptr;
         cap = 0;
         hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&h), c, hipHostMallocCoherent);
@@ -68,7 +68,7 @@ struct Pinned {
             return e;
         }
         if ((e = hipHostGetDevicePointer(reinterpret_cast<void **>(&d), h, 0)) != hipSuccess) {
-            (void)hipHostFree(h);
+            (void)tcsum::quiet(hipHostFree(h));
             h = d = nullptr;
             return e;
         }
@@ -160,33 +160,31 @@ int note_err(int step, hipError_t e, int rc)
     g_last_sys.store((int64_t)step * 1000 + (int64_t)e, std::memory_order_relaxed);
     // the failed call's error is returned as rc: it must not also reach the
     // caller's next hipGetLastError() as an error of the caller's own
-    if (e != hipSuccess && hipPeekAtLastError() == e)
-        (void)hipGetLastError();
+    (void)tcsum::quiet(e);
     return rc;
 }
 int note_sys(int step, hipError_t e) { return note_err(step, e, TCSUM_ERR_SYS); }
 int note_mem(int step, hipError_t e) { return note_err(step, e, TCSUM_ERR_MEM); }
 
 // hipStreamQuery for a poll: hipErrorNotReady is an answer there, not a
-// failure.  A runtime that also stores it in the calling thread's last-error
-// slot would hand it to the caller's next hipGetLastError() (PyTorch checks
-// every kernel launch of its own that way) as an error of the caller's; so a
-// NotReady this poll left in a slot that was clear before it is taken out
-// again.  (No launch of this library reads that slot: launch(),
-// csum_device.h, returns each launch's own status.)
+// failure.  ROCm 7.2's runtime does not store it in the calling thread's
+// last-error slot (scripts/lasterror_probe.hip, profiles/r05/); a runtime
+// that did would hand it to the caller's next hipGetLastError() (PyTorch
+// checks every kernel launch that way), so a NotReady this poll left in a
+// slot that was clear before it is taken out again.
 hipError_t poll_stream(hipStream_t s)
 {
     const hipError_t before = hipPeekAtLastError();
     const hipError_t q = hipStreamQuery(s);
-    if (q == hipErrorNotReady && before == hipSuccess && hipPeekAtLastError() == hipErrorNotReady)
-        (void)hipGetLastError();
+    if (q == hipErrorNotReady && before == hipSuccess)
+        (void)tcsum::quiet(q);
     return q;
 }
 
 bool is_gfx950(int dev)
 {
     hipDeviceProp_t p;
-    if (hipGetDeviceProperties(&p, dev) != hipSuccess)
+    if (tcsum::quiet(hipGetDeviceProperties(&p, dev)) != hipSuccess)
         return false;
     return strncmp(p.gcnArchName, "gfx950", 6) == 0;
 }
@@ -197,7 +195,7 @@ int ctx_init(Ctx &c, int dev)
     if (c.ready)
         return TCSUM_OK;
     int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || dev < 0 || dev >= count)
+    if (tcsum::quiet(hipGetDeviceCount(&count)) != hipSuccess || dev < 0 || dev >= count)
         return TCSUM_ERR_NOT_SUPPORT;
     if (!is_gfx950(dev))
         return TCSUM_ERR_NOT_SUPPORT;
@@ -272,7 +270,7 @@ void ensure_stage(Ctx &c, size_t bytes)
     while (cap < bytes)
         cap <<= 1;
     if (c.stage)
-        (void)hipHostFree(c.stage);
+        (void)tcsum::quiet(hipHostFree(c.stage));
     c.stage = nullptr;
     c.stage_cap = 0;
     hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&c.stage), cap, hipHostMallocCoherent);
@@ -394,7 +392,7 @@ const char *tcsum_version(void) { return "tcsum 0.1 (gfx950, hand-written HIP)";
 int tcsum_device_count(void)
 {
     int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess)
+    if (tcsum::quiet(hipGetDeviceCount(&count)) != hipSuccess)
         return 0;
     int ok = 0;
     for (int d = 0; d < count; ++d)
@@ -436,7 +434,7 @@ void *tcsum_host_alloc(size_t bytes)
 void tcsum_host_free(void *p)
 {
     if (p)
-        (void)hipHostFree(p);
+        (void)tcsum::quiet(hipHostFree(p));
 }
 
 int tcsum_host_register(void *p, size_t bytes)
@@ -500,7 +498,7 @@ int64_t tcsum_debug_get(const char *key)
         return g_last_sys.load(std::memory_order_relaxed);
     if (key && strcmp(key, "scratch_reserved") == 0) { // the calling thread's current device
         int dev = 0;
-        return hipGetDevice(&dev) == hipSuccess ? (int64_t)tcsum::scratch_reserved(dev) : -2;
+        return tcsum::quiet(hipGetDevice(&dev)) == hipSuccess ? (int64_t)tcsum::scratch_reserved(dev) : -2;
     }
     const int k = knob_of(key);
     return k < 0 ? -2 : tcsum::knob((tcsum::Knob)k);
@@ -577,7 +575,7 @@ int tcsum_batch(int op, void *arena, const void *descs, uint32_t n, void *out, u
         const int64_t ks = tcsum::knob(tcsum::KNOB_TX_SPLIT);
         bool split = ks >= 0 ? ks != 0 : n >= kTxSplitMin;
         hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-        if (split && hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone)
+        if (split && tcsum::quiet(hipStreamIsCapturing(st, &cap)) == hipSuccess && cap != hipStreamCaptureStatusNone)
             split = false;
         return rc_of(tcsum::launch_ipv4(split ? 4 : 1, g, a, pk, n, static_cast<uint32_t *>(out), flags, nullptr, st));
     }
@@ -908,7 +906,7 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         if (need <= cap)
             return hipSuccess;
         if (buf)
-            (void)hipFree(buf);
+            (void)tcsum::quiet(hipFree(buf));
         buf = nullptr;
         cap = 0;
         const hipError_t e = hipMalloc(reinterpret_cast<void **>(&buf), need);
@@ -929,8 +927,8 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     // once a copy is queued, an error return first drains both streams: no
     // copy may still read the caller's memory after the call returns
     auto fail = [&](int code) {
-        (void)hipStreamSynchronize(ks);
-        (void)hipStreamSynchronize(cs);
+        (void)tcsum::quiet(hipStreamSynchronize(ks));
+        (void)tcsum::quiet(hipStreamSynchronize(cs));
         return code;
     };
     auto fail_sys = [&](int step, hipError_t e) { return fail(note_sys(step, e)); };
@@ -950,9 +948,9 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     base[1] = c.d_arena - pl.rest_base();
     if (n > c.d_descs_cap) {
         if (c.d_descs)
-            (void)hipFree(c.d_descs);
+            (void)tcsum::quiet(hipFree(c.d_descs));
         if (c.d_out)
-            (void)hipFree(c.d_out);
+            (void)tcsum::quiet(hipFree(c.d_out));
         c.d_descs = nullptr;
         c.d_out = nullptr;
         c.d_descs_cap = c.d_out_cap = 0;
@@ -961,7 +959,7 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
             e = hipMalloc(reinterpret_cast<void **>(&c.d_out), sizeof(uint16_t) * n);
         if (e != hipSuccess) {
             if (c.d_descs)
-                (void)hipFree(c.d_descs); // both or neither: the caps below describe both
+                (void)tcsum::quiet(hipFree(c.d_descs)); // both or neither: the caps below describe both
             c.d_descs = nullptr;
             c.d_out = nullptr;
             return fail(note_mem(15, e));
@@ -1208,17 +1206,13 @@ namespace {
 uint8_t *mapped_host(const void *p)
 {
     hipPointerAttribute_t a{};
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-        (void)hipGetLastError();
+    if (tcsum::quiet(hipPointerGetAttributes(&a, p)) != hipSuccess) // unknown to the runtime: pageable
         return nullptr;
-    }
     if (a.type != hipMemoryTypeHost)
         return nullptr;
     void *d = nullptr;
-    if (hipHostGetDevicePointer(&d, const_cast<void *>(p), 0) != hipSuccess) {
-        (void)hipGetLastError();
+    if (tcsum::quiet(hipHostGetDevicePointer(&d, const_cast<void *>(p), 0)) != hipSuccess)
         return nullptr;
-    }
     return static_cast<uint8_t *>(d);
 }
 
@@ -1687,13 +1681,13 @@ struct KeepDevice {
     int dev = -1;
     KeepDevice()
     {
-        if (hipGetDevice(&dev) != hipSuccess)
+        if (tcsum::quiet(hipGetDevice(&dev)) != hipSuccess)
             dev = -1;
     }
     ~KeepDevice()
     {
         if (dev >= 0)
-            (void)hipSetDevice(dev);
+            (void)tcsum::quiet(hipSetDevice(dev));
     }
 };
 
@@ -1719,11 +1713,11 @@ int release_ctx(Ctx &c, int dev)
     if ((c.srv_running && srv_stop(c) != TCSUM_OK) || (c.cs_running && cs_stop(c) != TCSUM_OK))
         return TCSUM_ERR_SYS;
     for (hipStream_t st : c.hs)
-        (void)hipStreamSynchronize(st);
-    (void)hipStreamSynchronize(c.stream);
+        (void)tcsum::quiet(hipStreamSynchronize(st));
+    (void)tcsum::quiet(hipStreamSynchronize(c.stream));
     for (void *p : {(void *)c.d_arena, (void *)c.d_lead, (void *)c.d_descs, (void *)c.d_out})
         if (p)
-            (void)hipFree(p);
+            (void)tcsum::quiet(hipFree(p));
     c.d_arena = nullptr;
     c.d_lead = nullptr;
     c.d_lead_cap = 0;
@@ -1732,13 +1726,13 @@ int release_ctx(Ctx &c, int dev)
     c.d_arena_cap = c.d_descs_cap = c.d_out_cap = 0;
     for (Pinned *q : {&c.q_desc, &c.q_res, &c.q_arena}) {
         if (q->h)
-            (void)hipHostFree(q->h);
+            (void)tcsum::quiet(hipHostFree(q->h));
         q->h = q->d = nullptr;
         q->cap = 0;
     }
     // the tx fill's pooled scratch (every stream of this context is idle;
     // a caller's own stream on this device must be too, tcsum.h)
-    (void)hipDeviceSynchronize();
+    (void)tcsum::quiet(hipDeviceSynchronize());
     if (const hipError_t e = tcsum::scratch_trim(c.device); e != hipSuccess)
         return note_sys(52, e);
     return TCSUM_OK;
@@ -1869,10 +1863,10 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
     if (dma && (size_t)(ahi - alo) + 32 > c.d_arena_cap) {
         // no room in HBM for the span: the in-place path below needs none
         if (c.d_arena)
-            (void)hipFree(c.d_arena);
+            (void)tcsum::quiet(hipFree(c.d_arena));
         c.d_arena = nullptr;
         c.d_arena_cap = 0;
-        if (hipMalloc(reinterpret_cast<void **>(&c.d_arena), (size_t)(ahi - alo) + 32) == hipSuccess) {
+        if (tcsum::quiet(hipMalloc(reinterpret_cast<void **>(&c.d_arena), (size_t)(ahi - alo) + 32)) == hipSuccess) {
             c.d_arena_cap = (size_t)(ahi - alo) + 32;
         } else {
             c.d_arena = nullptr;
@@ -1939,7 +1933,7 @@ int host_ipv4(int ip_mode, int device, uint8_t *host_arena, uint64_t arena_bytes
         // debug knob "hostq_dma_keep_mb" (default 256): a one-off multi-GiB verify
         // does not keep its span allocated for the life of the process
         if (c.d_arena_cap > ((size_t)knob_or(tcsum::KNOB_HOSTQ_DMA_KEEP_MB, 256) << 20)) {
-            (void)hipFree(c.d_arena);
+            (void)tcsum::quiet(hipFree(c.d_arena));
             c.d_arena = nullptr;
             c.d_arena_cap = 0;
         }

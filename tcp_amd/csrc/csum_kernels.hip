@@ -462,9 +462,9 @@ static hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t stream)
             props.allocType = hipMemAllocationTypePinned;
             props.location.type = hipMemLocationTypeDevice;
             props.location.id = dev;
-            if (hipMemPoolCreate(&g_scratch_pools[dev], &props) == hipSuccess) {
+            if (quiet(hipMemPoolCreate(&g_scratch_pools[dev], &props)) == hipSuccess) {
                 uint64_t keep = 1ull << 30;
-                (void)hipMemPoolSetAttribute(g_scratch_pools[dev], hipMemPoolAttrReleaseThreshold, &keep);
+                (void)quiet(hipMemPoolSetAttribute(g_scratch_pools[dev], hipMemPoolAttrReleaseThreshold, &keep));
             } else {
                 g_scratch_pools[dev] = nullptr;
             }
@@ -481,7 +481,7 @@ uint64_t scratch_reserved(int dev)
     std::lock_guard<std::mutex> lk(g_scratch_mu);
     uint64_t v = 0;
     if (dev >= 0 && dev < 64 && g_scratch_pools[dev])
-        (void)hipMemPoolGetAttribute(g_scratch_pools[dev], hipMemPoolAttrReservedMemCurrent, &v);
+        (void)quiet(hipMemPoolGetAttribute(g_scratch_pools[dev], hipMemPoolAttrReservedMemCurrent, &v));
     return v;
 }
 

@@ -9,6 +9,20 @@
 
 namespace tcsum {
 
+// A failed runtime call whose failure this library handles itself (a
+// cleanup free, a fallback): its error must not stay in the calling thread's
+// last-error slot, where the caller's next hipGetLastError() -- PyTorch
+// checks every kernel launch that way -- would take it for its own.  The slot
+// is cleared only when it holds this call's error, so an error of the
+// caller's stays for the caller.  (No launch of the library reads the slot:
+// launch(), csum_device.h, returns each launch's own status.)
+inline hipError_t quiet(hipError_t e)
+{
+    if (e != hipSuccess && hipPeekAtLastError() == e)
+        (void)hipGetLastError();
+    return e;
+}
+
 // What a segment kernel computes per range (see csum_kernels.hip).
 enum Mode : int {
     MODE_SEG = 0,   // pktbuf_checksum16: u16 pre_sum, optional complement

@@ -1,14 +1,16 @@
 """Round 4's intermittent TCSUM_ERR_SYS, made deterministic.
 
 Every launch of libtcsum.so used to judge itself by hipGetLastError(), the
-calling thread's last-error slot -- which other runtime calls on that thread
-(a hipStreamQuery answering NotReady, a caller's own failed call) may have
-left set.  Now each launch returns hipLaunchKernel's own status.  These tests
-leave the slot dirty on purpose -- a NotReady from a poll of a busy stream and
-a real error of the caller's (hipSetDevice past the last device) -- and then
-call every batch entry point: each must return OK with the oracle's results.
-They also check the other direction: a call that polls its own stream while
-the kernel runs must not leave a NotReady in a slot that was clear."""
+calling thread's last-error slot -- which holds the first failed runtime
+call on that thread since the slot was last read: a caller's own, or one the
+library itself ignored.  Now each launch returns hipLaunchKernel's own status.
+These tests leave the slot dirty on purpose -- a real error of the caller's
+(hipSetDevice past the last device; ROCm 7.2 keeps it until it is read) and a
+NotReady from a poll of a busy stream (which this runtime does not keep) --
+and then call every batch entry point: each must return OK with the oracle's
+results, and leave the caller's error where it was (the library neither
+consumes nor replaces it).  They also check the other direction: a call that
+polls its own stream while the kernel runs leaves a clear slot clear."""
 import ctypes
 import os
 import subprocess
@@ -76,10 +78,19 @@ DIRT = ["not_ready", "invalid_device"]
 
 
 def _dirty(hip, kind):
+    """Dirty the slot; returns what it must still hold after a library call."""
+    hip.hipGetLastError()
     if kind == "not_ready":
-        _dirty_not_ready(hip)
-    else:
-        assert _dirty_invalid_device(hip) == HIP_INVALID_DEVICE
+        return _dirty_not_ready(hip)
+    assert _dirty_invalid_device(hip) == HIP_INVALID_DEVICE
+    return HIP_INVALID_DEVICE
+
+
+def _after(hip, expect):
+    """The library left the caller's slot as it found it; then clear it (a
+    pending error would reach PyTorch's next launch check)."""
+    slot = hip.hipGetLastError()
+    assert slot == expect, (slot, expect)
 
 
 def test_runtime_slot_semantics_recorded(hip, tc):
@@ -121,8 +132,9 @@ def test_device_batches_with_a_dirty_slot(tc, hip, oracle, mixed, dirt):
     checks = []
 
     def run(name, fn):
-        _dirty(hip, dirt)
+        expect = _dirty(hip, dirt)
         checks.append((name, fn()))
+        _after(hip, expect)
 
     run("peso packed", lambda: tc.batch_peso(m["parena"], m["pdescs"], p.n, p.total_bytes))
     run("peso per-range", lambda: tc.batch(tc.OP_PESO, m["parena"], m["pdescs"], p.n, total_bytes=p.total_bytes,
@@ -144,16 +156,19 @@ def test_device_batches_with_a_dirty_slot(tc, hip, oracle, mixed, dirt):
     oracle.batch_ipv4_tx_fill(want, b.descs, nthreads=8)
     for split in (0, 1):
         a = m["arena"].clone()
+        fl = torch.empty(b.n, dtype=torch.uint8, device="cuda")
         with tc.debug(tx_split=split):
-            _dirty(hip, dirt)
-            tc.batch_ipv4_tx_fill(a, m["descs"], b.n, b.total_bytes)
+            expect = _dirty(hip, dirt)
+            tc.batch_ipv4_tx_fill(a, m["descs"], b.n, b.total_bytes, flags=fl)
+            _after(hip, expect)
         np.testing.assert_array_equal(a.cpu().numpy(), want, err_msg=f"tx fill split={split}")
     a = m["arena"].clone()
     scratch = torch.empty(8 * b.n, dtype=torch.uint8, device="cuda")
-    _dirty(hip, dirt)
-    tc.batch_ipv4_tx_fill(a, m["descs"], b.n, b.total_bytes, scratch=scratch)
+    fl = torch.empty(b.n, dtype=torch.uint8, device="cuda")
+    expect = _dirty(hip, dirt)
+    tc.batch_ipv4_tx_fill(a, m["descs"], b.n, b.total_bytes, scratch=scratch, flags=fl)
+    _after(hip, expect)
     np.testing.assert_array_equal(a.cpu().numpy(), want, err_msg="tx fill scratch")
-    hip.hipGetLastError()
 
 
 @pytest.mark.parametrize("dirt", DIRT)
@@ -170,21 +185,25 @@ def test_host_batches_with_a_dirty_slot(tc, hip, oracle, mixed, dirt, where):
     try:
         for dma_kb in (0, 1):  # in place (the kernel polls) / through the copy engine
             with tc.debug(hostq_dma_kb=dma_kb):
-                _dirty(hip, dirt)
+                expect = _dirty(hip, dirt)
                 out, fl = tc.host_batch_ipv4(arg, b.descs)
+                _after(hip, expect)
                 np.testing.assert_array_equal(out, m["eo"])
                 np.testing.assert_array_equal(fl, m["ef"])
-                _dirty(hip, dirt)
+                expect = _dirty(hip, dirt)
                 v, _, _ = tc.host_batch_ipv4_rx_verify(arg, b.descs)
+                _after(hip, expect)
                 ev, _ = oracle.batch_ipv4_rx_verify(m["host"], b.descs, nthreads=8)
                 np.testing.assert_array_equal(v, ev)
-        _dirty(hip, dirt)
+        expect = _dirty(hip, dirt)
         got = tc.host_batch_peso(m["phost"], p.descs)
+        _after(hip, expect)
         np.testing.assert_array_equal(got, m["pe"])
         want = m["host"].copy()
         oracle.batch_ipv4_tx_fill(want, b.descs, nthreads=8)
-        _dirty(hip, dirt)
+        expect = _dirty(hip, dirt)
         tc.host_batch_ipv4_tx_fill(arg, b.descs)
+        _after(hip, expect)
         np.testing.assert_array_equal(np.array(view[: want.size]), want)
     finally:
         hip.hipGetLastError()
@@ -228,12 +247,14 @@ from tcp_amd.pktbuf import PktBuf, IpAddr
 hip = ctypes.CDLL("libamdhip64.so.7")
 hip.hipStreamQuery.argtypes = [ctypes.c_void_p]
 def dirty():
+    hip.hipGetLastError()  # the last call's pending error: torch's own launch checks below would report it
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
         torch.cuda._sleep(20_000_000)
     assert hip.hipStreamQuery(ctypes.c_void_p(s.cuda_stream)) == 600
     s.synchronize()
     n = ctypes.c_int(0); hip.hipGetDeviceCount(ctypes.byref(n)); hip.hipSetDevice(n.value); hip.hipSetDevice(0)
+    assert hip.hipPeekAtLastError() == 101  # the caller's error, pending through the drop-in call
 h = bytes.fromhex("450000730000400040110000c0a80001c0a800c7")
 b = bytes((i * 7 + 3) & 0xFF for i in range(999))
 for args_launch in (1, 0):
@@ -245,6 +266,7 @@ for args_launch in (1, 0):
     pb = PktBuf([b[i:i + 127] for i in range(0, 999, 127)])
     dst, src = IpAddr.v4(bytes([192, 168, 74, 3])), IpAddr.v4(bytes([192, 168, 74, 2]))
     dirty(); assert tc.checksum_peso(pb, dst, src, 6) == 0x4AD0
+hip.hipGetLastError()
 print("ok")
 """ % root
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)

@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--trace-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--e2e-multi-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-trace", action="store_true", help="skip the rocprofv3 kernel-trace child")
+    ap.add_argument("--knob", action="append", default=[], metavar="KEY=VALUE",
+                    help="measurement only: a libtcsum debug knob (include/tcsum_debug.h) set for the whole run, "
+                         "its PMC and trace children included; the line records it")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="rehearse the N-rank launcher, rendezvous, barrier and max-over-ranks timing on CPU "
                          "(gloo, a numpy stand-in for the kernel; no GPU, no GPU numbers)")
@@ -163,6 +166,7 @@ def launch(tc, batch, arena, descs, out, flags=None):
 
 
 SETTLE_MS = 30.0  # set from --settle-ms in main()
+KNOBS: list = []  # --knob KEY=VALUE (measurement), passed on to the profiler children
 
 
 def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None, probes=True):
@@ -372,7 +376,7 @@ def pmc_traffic(config: str):
         d = tempfile.mkdtemp(prefix=f"tcsum_pmc_{counter}_")
         cmd = [prof, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
                sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", config,
-               "--steps", "3", "--warmup", "1"]
+               "--steps", "3", "--warmup", "1"] + [f"--knob={k}" for k in KNOBS]
         try:
             subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
                            env=dict(os.environ, TMPDIR=d))
@@ -451,7 +455,8 @@ def rocprof_trace(config: str, steps: int, warmup: int, settle_ms: float):
     d = tempfile.mkdtemp(prefix="tcsum_trace_")
     cmd = [prof, "--kernel-trace", "--stats", "--output-format", "csv", "-d", d, "-o", "trace", "--",
            sys.executable, os.path.abspath(__file__), "--pmc-child", "--trace-child", "--config", config,
-           "--steps", str(steps), "--warmup", str(warmup), "--settle-ms", str(settle_ms)]
+           "--steps", str(steps), "--warmup", str(warmup), "--settle-ms", str(settle_ms)] + \
+        [f"--knob={k}" for k in KNOBS]
     try:
         res = subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                              env=dict(os.environ, TMPDIR=d), text=True)
@@ -932,6 +937,7 @@ def rehearse_multi_device(b, data, ndev: int) -> dict:
 
 def main():
     args = parse()
+    KNOBS.extend(args.knob)
     if args.e2e_multi_child:
         e2e_multi_main(args.config)
         return
@@ -960,6 +966,9 @@ def main():
     build.build()
     import tcp_amd as tc
     from tcp_amd import workload
+    for kv in KNOBS:
+        k, v = kv.split("=", 1)
+        tc.debug_set(k, int(v))
 
     # one process per GPU; TCSUM_DIST_BACKEND=gloo rehearses N ranks on fewer
     # GPUs (ranks share devices round-robin; RCCL refuses two ranks per GPU)
@@ -1056,6 +1065,7 @@ def main():
                    "parallelism": f"{n_gpus} independent GPU shards, no collective"},
         "roofline": roof,
         "devices": devices,
+        **({"debug_knobs": KNOBS} if KNOBS else {}),
         # every rank's own time (the line's ms_per_step is their max): a
         # straggler GPU shows here on its own
         "ranks_ms_per_step": [round(r["ms_per_step"], 4) for r in ranks],

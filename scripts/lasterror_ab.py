@@ -56,18 +56,20 @@ for path in sys.argv[1:]:
     for kind in ("not_ready", "invalid_device"):
         for call in ("tcsum_batch_peso", "tcsum_host_batch_peso"):
             hip.hipGetLastError()
-            how = dirty(kind)
             out = torch.zeros(b.n, dtype=torch.uint16, device="cuda")
+            ho = np.zeros(b.n, np.uint16)
+            torch.cuda.synchronize()
+            how = dirty(kind)
             if call == "tcsum_batch_peso":
                 rc = L.tcsum_batch_peso(arena.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(), b.total_bytes,
                                         torch.cuda.current_stream().cuda_stream)
-                torch.cuda.synchronize()
-                same = bool((out.cpu().numpy() == want).all())
             else:
-                ho = np.zeros(b.n, np.uint16)
                 rc = L.tcsum_host_batch_peso(0, host.ctypes.data, host.nbytes, b.descs.ctypes.data, b.n,
                                              ho.ctypes.data)
-                same = bool((ho == want).all())
+            left = hip.hipGetLastError()  # what the call left in the slot (then cleared for torch's own checks)
+            torch.cuda.synchronize()
+            same = bool(((out.cpu().numpy() if call == "tcsum_batch_peso" else ho) == want).all())
+            how += f"; slot after the call {left}"
             print(f"{os.path.basename(path):22s} {kind:15s} ({how}) {call:22s} rc {rc:3d} results "
                   f"{'equal' if same else 'NOT equal'}", flush=True)
     hip.hipGetLastError()

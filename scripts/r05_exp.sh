@@ -12,5 +12,4 @@ scripts/gpu_steps.sh \
   "ipv4_db:400:python -u scripts/ipv4_shape_ab.py mixed mixed_rx --db > $out/ipv4_db.txt" \
   "tso_pf:300:python -u scripts/env_ab.py tso pf_dist=512 pf_dist=1024 pf_dist=2048 > $out/tso_pf.txt" \
   "ipv4_r04:300:python -u scripts/ab_lib.py tcp_amd/libtcsum.so abl/libtcsum_r04.so mixed,mixed_rx,mixed_tx > $out/ab_r04_ipv4.txt" \
-  "calib:300:python -u scripts/pmc_calib.py $out/pmc_calib.json > $out/pmc_calib.txt" \
-  "order:900:python -u scripts/bench_order_ab.py 2 > $out/bench_order_ab.txt"
+  "calib:300:python -u scripts/pmc_calib.py $out/pmc_calib.json > $out/pmc_calib.txt"

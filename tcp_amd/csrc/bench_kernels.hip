@@ -833,9 +833,7 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
     const uint32_t per = (uint32_t)wg / G;
     const dim3 grid((n + per - 1u) / per), blk((uint32_t)wg);
     uint8_t *fl = nullptr;
-    // the product's descriptor prefetch distance (debug knob "pf_dist") rides in opts
-    const int64_t pfk = tcsum_debug_get("pf_dist");
-    const uint32_t opts = pfk > 0 ? (uint32_t)pfk << 8 : 0u;
+    const uint32_t opts = 0u;
 #define TCSUM_SH(KERN)                                                                                   \
     note_launch(launch(KERN, grid, blk, 0, stream, arena, pkts, n, out, fl, verdict, opts, xg));          \
     return take_launch_rc();

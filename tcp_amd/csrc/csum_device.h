@@ -229,8 +229,8 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t 
     return b - r + (r & 7u) * xg + (r >> 3);
 }
 
-// Descriptor prefetch (aux >> 8 / opts >> 8: the distance pfd in logical
-// workgroups, 0 = off).  A workgroup's data loads wait on its descriptors,
+// Descriptor prefetch (k_segments_pk's range-by-range path: aux >> 8, the
+// distance pfd in logical workgroups, 0 = off).  A workgroup's data loads wait on its descriptors,
 // and those come from HBM: one memory latency per workgroup with nothing of
 // its own in flight.  Lanes 0-1 of wave 0 touch the descriptor lines of the
 // workgroup pfd logical blocks ahead (a multiple of the XCD run's superblock
@@ -566,9 +566,6 @@ __global__ __launch_bounds__(W * 64) void k_segments_wgx(const uint8_t *__restri
         const uint32_t j = lane_off + u * ustep;
         v[u] = load16<true>(ib + (j < ni ? j : ilast));
     }
-    uint32_t pf = 0;
-    if (const uint32_t pfd = aux >> 8; !PROBE && pfd != 0u && t < 64u) // descriptor prefetch (k_segments_pk)
-        pf = prefetch_descs(descs, (uint64_t)seg + pfd, n, MODE == MODE_PESO ? 24u : 16u, 1u, t);
     if constexpr (PROBE) {
         issue_fence();
         u32x4 x = ev;
@@ -629,8 +626,6 @@ __global__ __launch_bounds__(W * 64) void k_segments_wgx(const uint8_t *__restri
             s += part[w]; // < 16 * 2^23
         out[seg] = finalize<MODE>(s, reinterpret_cast<uintptr_t>(p), d, aux, q16);
     }
-    if (pf == 0x9E3779B9u && n == 0u) // never: keeps the prefetch load alive
-        out[0] = (uint16_t)pf;
 }
 
 // ---------------------------------------------------------------- packed stream
@@ -720,6 +715,67 @@ __device__ __forceinline__ void desc_span(const void *__restrict__ descs, uint32
     len = *reinterpret_cast<const uint32_t *>(x + 8);
 }
 
+// All eight descriptors of a full K = 8 workgroup through the scalar cache
+// (aux bit 0x80, measurement): the vector path re-fetches from HBM the lines
+// the two scalar span loads fetched (scalar-only and vector-only reads of
+// k_segments_pk's descriptors each count 0.667 FETCH_SIZE per byte, both
+// together 1.334: scripts/pmc_calib.hip k_pkdesc, profiles/r05/).  Lane r
+// (r < 8) gets descriptor first + r; the others get a zero-length one.
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+
+template <int MODE>
+__device__ __forceinline__ SegDesc sdesc8(const void *__restrict__ descs, uint32_t first, uint32_t lane)
+{
+    constexpr uint32_t DW = MODE == MODE_PESO ? 6u : 4u; // dwords per descriptor
+    const uint8_t *p = static_cast<const uint8_t *>(descs) + 4ull * DW * first; // workgroup-uniform
+    // the workgroup's 8 x DW dwords in three 64-B scalar loads, all in flight
+    // before one wait (left to the compiler, 48 single-dword loads each
+    // waited for); a reads-only scalar load
+    // (exactly the 8 descriptors: 192 B for checksum_peso's 24-B records,
+    // 128 B for 16-B ones -- never past the workgroup's last descriptor)
+    u32x16 a, b, c = u32x16(0u);
+    if constexpr (DW == 6u)
+        asm volatile("s_load_dwordx16 %0, %3, 0x0\n\t"
+                     "s_load_dwordx16 %1, %3, 0x40\n\t"
+                     "s_load_dwordx16 %2, %3, 0x80\n\t"
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=&s"(a), "=&s"(b), "=&s"(c)
+                     : "s"(p)
+                     : "memory");
+    else
+        asm volatile("s_load_dwordx16 %0, %2, 0x0\n\t"
+                     "s_load_dwordx16 %1, %2, 0x40\n\t"
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=&s"(a), "=&s"(b)
+                     : "s"(p)
+                     : "memory");
+    uint32_t f[DW];
+#pragma unroll
+    for (uint32_t k = 0; k < DW; ++k)
+        f[k] = 0u;
+#pragma unroll
+    for (uint32_t r = 0; r < 8u; ++r)
+#pragma unroll
+        for (uint32_t k = 0; k < DW; ++k) {
+            const uint32_t i = r * DW + k; // a constant once unrolled
+            const uint32_t x = i < 16u ? a[i & 15u] : i < 32u ? b[i & 15u] : c[i & 15u];
+            f[k] = lane == r ? x : f[k];
+        }
+    SegDesc d;
+    d.off = (uint64_t)f[0] | ((uint64_t)f[1] << 32);
+    d.len = lane < 8u ? f[2] : 0u;
+    if constexpr (MODE == MODE_PESO) {
+        d.src = f[3];
+        d.dst = f[4];
+        d.proto = f[5] & 0xFFu;
+        d.pre = 0;
+    } else {
+        d.pre = f[3];
+        d.src = d.dst = d.proto = 0;
+    }
+    return d;
+}
+
 // The per-range path for a workgroup whose ranges are not one region:
 // groups of G lanes, G the widest power of two with one group per range.
 template <int MODE, int G, int UL = 4>
@@ -787,10 +843,7 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     // slower, profiles/r03/packed/ab_vdesc_w8.txt)
     desc_span<MODE>(descs, first, r0, len0);
     desc_span<MODE>(descs, first + kw - 1u, offl, lenl);
-    uint32_t pf = 0;
-    if (const uint32_t pfd = aux >> 8; pfd != 0u && w == 0) // wave-uniform
-        pf = prefetch_descs(descs, (uint64_t)(blk + pfd) * K, n, MODE == MODE_PESO ? 24u : 16u,
-                            (K * (MODE == MODE_PESO ? 24u : 16u) + 127u) / 128u + 1u, lane);
+
     const uint64_t rend = offl + lenl;
     const uint8_t *p = arena + r0;
     const uint32_t s0 = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u);
@@ -803,8 +856,15 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
         // workgroup-uniform, known from the two scalar descriptors: range by
         // range at once (a shuffled batch's usual case), before any stream
         // load or the region check's own descriptor loads -- so its ranges'
-        // descriptors (lines the scalar loads just brought in) and then their
-        // bytes are the only waits
+        // descriptors and then their bytes are the only waits.  The
+        // descriptor lines of the workgroup aux >> 8 logical blocks ahead are
+        // touched on the way (a shuffled batch's workgroups all come here:
+        // 258.0 -> 250.7 us for configs[1]'s ranges shuffled; on the region
+        // path the same prefetch cost 1.6-9 %, profiles/r05/pk_layouts_pf.txt)
+        uint32_t pf = 0;
+        if (const uint32_t pfd = aux >> 8; pfd != 0u && w == 0) // wave-uniform
+            pf = prefetch_descs(descs, (uint64_t)(blk + pfd) * K, n, MODE == MODE_PESO ? 24u : 16u,
+                                (K * (MODE == MODE_PESO ? 24u : 16u) + 127u) / 128u + 1u, lane);
         pk_fallback<MODE>(arena, descs, out, aux, first, kw, T);
         if (pf == 0x9E3779B9u && K == 0u) // never: keeps the prefetch load alive
             out[0] = (uint16_t)pf;
@@ -832,7 +892,10 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     SegDesc d{0, 0, 0, 0, 0, 0};
     uint32_t xs = 0, xe = 0, q16 = 0;
     if (has) {
-        d = load_desc<MODE>(descs, first + rr, mine);
+        if ((aux & 0x80u) && K == 8u && kw == 8u) // workgroup-uniform (wave 0 only: 8 <= 64)
+            d = sdesc8<MODE>(descs, first, lane);
+        else
+            d = load_desc<MODE>(descs, first + rr, mine);
         // P wraps mod 2^32 across passes, so a difference is exact only for a
         // range whose word sum stays below 2^32: < 128 KiB (<= 65536 words)
         const bool inside = !mine || (d.off >= r0 && d.off + d.len <= rend && d.len < (1u << 17));
@@ -928,8 +991,6 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
     if (mine)
         out[first + rr] = finalize<MODE>(pe - ps, reinterpret_cast<uintptr_t>(arena + d.off), d, aux, q16);
-    if (pf == 0x9E3779B9u && K == 0u) // never: keeps the prefetch load alive
-        out[0] = (uint16_t)pf;
 }
 
 // ---------------------------------------------------------------- IPv4
@@ -1377,14 +1438,8 @@ __global__ __launch_bounds__(T) void k_ipv4(uint8_t *__restrict__ arena, const t
                                             uint32_t opts, uint32_t xg)
 {
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
-    uint32_t pf = 0;
-    if (const uint32_t pfd = opts >> 8; pfd != 0u && threadIdx.x < 64u) // wave 0: descriptor prefetch (k_segments_pk)
-        pf = prefetch_descs(pkts, (uint64_t)(blk + pfd) * (T / G), n, 16u, (T / G * 16u + 127u) / 128u + 1u,
-                            threadIdx.x);
     ipv4_packet<G, U, IPM, SKEW>(arena, pkts, blk * (uint32_t)(T / G) + threadIdx.x / G, n, out, flags_out, verdict_out,
                            opts); // no 32-bit wrap for any n
-    if (pf == 0x9E3779B9u && n == 0u) // never: keeps the prefetch load alive
-        out[0] = pf;
 }
 
 // k_ipv4 with two data passes in flight per lane group (measurement)

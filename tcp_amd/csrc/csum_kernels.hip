@@ -338,12 +338,14 @@ Geometry pick_geometry(uint64_t mean_len)
     return g;
 }
 
-// Descriptor prefetch distance in workgroups (debug knob "pf_dist"; 0 = off),
-// passed to the stream / packet kernels in the high bits of aux / opts.
+// Descriptor prefetch distance of k_segments_pk's range-by-range path, in
+// workgroups (in aux >> 8): 2048 -- 1024 / 2048 / 4096 measured alike on a
+// shuffled configs[1] batch (profiles/r05/pk_layouts_pf.txt); debug knob
+// "pf_dist" overrides, 0 = off.
 static uint32_t pf_dist()
 {
     const int64_t v = knob(KNOB_PF_DIST);
-    return v > 0 ? (uint32_t)(v < (1 << 23) ? v : (1 << 23) - 1) : 0u;
+    return v < 0 ? 2048u : (uint32_t)(v < (1 << 23) ? v : (1 << 23) - 1);
 }
 
 // The shapes the router can pick for the per-range kernels (and only those:
@@ -362,8 +364,7 @@ static hipError_t seg_u(int G, int U, uint32_t xg, uint32_t n, const void *arena
     TCSUM_SEG(16, 8) TCSUM_SEG(32, 6)
 #undef TCSUM_SEG
     if (G == 1024 && U == 4) { // one range per 16-wave workgroup, 2 KiB sub-ranges (TSO)
-        return launch(k_segments_wgx<16, 32, 4, MODE>, dim3(n), dim3(1024), 0, s, a, descs, n, out,
-                      aux | (pf_dist() << 8), xg);
+        return launch(k_segments_wgx<16, 32, 4, MODE>, dim3(n), dim3(1024), 0, s, a, descs, n, out, aux, xg);
     }
     if (G == 256 && U == 16) { // one range per workgroup
         return launch(k_segments_wg<16, MODE>, dim3(n), dim3(256), 0, s, a, descs, n, out, aux, xg);
@@ -406,7 +407,7 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
                                                                           : kPkMaxRanges * kPkWaves;
         const uint8_t *a = static_cast<const uint8_t *>(arena);
         const dim3 gr((n + K - 1) / K), bl(kPkWaves * 64);
-        const uint32_t ax = aux | (pf_dist() << 8);
+        const uint32_t ax = aux | (pf_dist() << 8) | (knob(KNOB_PK_SDESC) == 1 ? 0x80u : 0u);
         if (mode == MODE_SEG)
             return launch(k_segments_pk<MODE_SEG>, gr, bl, 0, stream, a, descs, n, out, ax, (uint32_t)g.xcd, K);
         return launch(k_segments_pk<MODE_PESO>, gr, bl, 0, stream, a, descs, n, out, ax, (uint32_t)g.xcd, K);
@@ -429,8 +430,8 @@ static hipError_t ipv4_u(int G, int U, dim3 grid, uint8_t *arena, const tcsum_pk
 {
 #define TCSUM_IP(GG, UU)                                                                             \
     if (G == GG && U == UU) {                                                                      \
-        return launch(k_ipv4<GG, UU, IPM>, grid, dim3(256), 0, s, arena, pkts, n, out, flags, verdict,       \
-                      opts | (pf_dist() << 8), xg);                                                  \
+        return launch(k_ipv4<GG, UU, IPM>, grid, dim3(256), 0, s, arena, pkts, n, out, flags, verdict, opts, \
+                      xg);                                                                           \
     }
     TCSUM_IP(16, 1) TCSUM_IP(16, 2) TCSUM_IP(16, 3) TCSUM_IP(16, 4) TCSUM_IP(16, 6) TCSUM_IP(16, 8)
     TCSUM_IP(32, 6) TCSUM_IP(64, 4) TCSUM_IP(64, 16)

@@ -58,7 +58,8 @@ enum Knob : int {
     KNOB_HOSTQ_DMA_KB, // host-queue batches from this span on go through the copy engine (262144)
     KNOB_HOSTQ_DMA_KEEP_MB, // device arena kept between host-queue calls up to this size (256)
     KNOB_COPY_THREADS, // host threads of a parallel gather / scatter pass (16)
-    KNOB_PF_DIST,      // descriptor prefetch distance of the stream / packet kernels, in workgroups
+    KNOB_PF_DIST,      // descriptor prefetch distance of k_segments_pk's range-by-range path (2048)
+    KNOB_PK_SDESC,     // 1: k_segments_pk loads a full K = 8 workgroup's descriptors through the scalar cache
     KNOB_COUNT
 };
 int64_t knob(Knob k);

@@ -1,10 +1,12 @@
-"""The descriptor prefetch (debug knob "pf_dist", csum_device.h
-prefetch_descs): lanes of wave 0 touch the descriptor lines of the workgroup
-pf_dist logical blocks ahead.  It must never change a result or read past the
-descriptor array: every kernel that takes it (k_segments_pk, its range-by-range
-fallback, k_segments_wgx, k_ipv4 in every mode) against the oracle, with
-distances from 1 to far past the grid, on batches whose descriptor arrays end
-right at an allocation's end."""
+"""k_segments_pk's descriptor variants: the prefetch of its range-by-range
+path (debug knob "pf_dist", csum_device.h prefetch_descs: lanes of wave 0
+touch the descriptor lines of the workgroup pf_dist logical blocks ahead) and
+the all-scalar descriptor reads of a full 8-range workgroup ("pk_sdesc").
+Neither may change a result or read past the descriptor array: both
+descriptor layouts (checksum_peso, pktbuf_checksum16) against the oracle,
+packed, shuffled, TSO-sized and K = 8 batches, distances from 1 to far past
+the grid, descriptor arrays at the end of their allocation; and the IPv4
+kernels, which must be unaffected by the knob."""
 import numpy as np
 import pytest
 
@@ -38,12 +40,15 @@ def _descs_at_end(torch, tc, descs):
     return t
 
 
+@pytest.mark.parametrize("sdesc", [0, 1])
 @pytest.mark.parametrize("pf", DISTANCES)
-@pytest.mark.parametrize("layout", ["packed", "shuffled", "tso"])
-def test_peso_batches_with_prefetch(tc, torch, oracle, pf, layout):
+@pytest.mark.parametrize("layout", ["packed", "shuffled", "tso", "mtu"])
+def test_peso_batches_with_prefetch(tc, torch, oracle, pf, layout, sdesc):
     rng = np.random.default_rng(40 + DISTANCES.index(pf))
     if layout == "tso":
         n, lens = 300, np.full(300, 65536)
+    elif layout == "mtu":  # K = 8 full workgroups, the last one partial: the scalar-descriptor path
+        n, lens = 8 * 1001 + 5, np.full(8 * 1001 + 5, 1500)
     else:
         n = 20011
         lens = rng.integers(0, 3001, n)
@@ -59,9 +64,13 @@ def test_peso_batches_with_prefetch(tc, torch, oracle, pf, layout):
     want = oracle.batch_peso(host, p, nthreads=8)
     arena = torch.from_numpy(host).cuda()
     d = _descs_at_end(torch, tc, p)
-    with tc.debug(pf_dist=pf):
+    with tc.debug(pf_dist=pf, pk_sdesc=sdesc):
         got = tc.batch_peso(arena, d, n, int(lens.sum())).cpu().numpy()
+        segs = np.zeros(n, tc.SEG_DTYPE)  # the same ranges as pktbuf_checksum16 (16-B descriptors)
+        segs["offset"], segs["len"], segs["pre_sum"] = p["offset"], p["len"], rng.integers(0, 1 << 17, n)
+        gs = tc.batch_segments(arena, _descs_at_end(torch, tc, segs), n, 1, int(lens.sum())).cpu().numpy()
     np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(gs, oracle.batch_segments(host, segs, 1, nthreads=8))
 
 
 @pytest.mark.parametrize("pf", DISTANCES)

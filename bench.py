@@ -60,6 +60,11 @@ def parse():
                          "whatever W is; 0 = exactly W launches).  300: with 30 one box read the headline "
                          "at 0.908 against 0.935 with 300 in the same call, and the secondary configs "
                          "1-2.5 %% low (profiles/r04/gap/)")
+    ap.add_argument("--arena-policy", choices=("free", "keep", "prealloc"), default="free",
+                    help="secondary configs' arenas: free each after its config (torch.cuda.empty_cache), keep "
+                         "them all allocated, or allocate them all before the first is timed")
+    ap.add_argument("--gap-ms", type=float, default=0.0,
+                    help="measurement: idle time between the secondary configs")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -169,9 +174,13 @@ SETTLE_MS = 30.0  # set from --settle-ms in main()
 KNOBS: list = []  # --knob KEY=VALUE (measurement), passed on to the profiler children
 
 
-def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None, probes=True):
-    batch = workload.make_batch(config, rank=rank)
-    arena, descs = workload.materialize(batch)
+def time_config(torch, tc, workload, config, rank, steps, warmup, dist=None, probes=True, pre=None):
+    """pre: (batch, arena, descs) materialized beforehand (--arena-policy prealloc)."""
+    if pre is not None:
+        batch, arena, descs = pre
+    else:
+        batch = workload.make_batch(config, rank=rank)
+        arena, descs = workload.materialize(batch)
     dt = torch.uint16 if batch.kind == "peso" else torch.int8 if batch.op == "rx" else torch.uint32
     out = torch.empty(batch.n, dtype=dt, device=arena.device)
     flags = torch.empty(batch.n, dtype=torch.uint8, device=arena.device) if batch.op == "txo" else None
@@ -1092,8 +1101,17 @@ def main():
         # than on its own (0.925 against 0.958 of spec, the same kernel's probe
         # rounds unaffected; profiles/r03/bench_tso_secondary_{plain,full}.json)
         extra = {}
-        for cfg in [c for c in args.secondary.split(",") if c and c != args.config]:
-            r = time_config(torch, tc, workload, cfg, 0, max(5, args.steps // 2), args.warmup)
+        cfgs = [c for c in args.secondary.split(",") if c and c != args.config]
+        pre, kept = {}, []
+        if args.arena_policy == "prealloc":
+            for cfg in cfgs:
+                b2 = workload.make_batch(cfg)
+                pre[cfg] = (b2,) + tuple(workload.materialize(b2))
+            torch.cuda.synchronize()
+        for i, cfg in enumerate(cfgs):
+            if i and args.gap_ms > 0:
+                time.sleep(args.gap_ms / 1e3)
+            r = time_config(torch, tc, workload, cfg, 0, max(5, args.steps // 2), args.warmup, pre=pre.pop(cfg, None))
             extra[cfg] = result_entry(r, max(5, args.steps // 2))
             if cfg in ("tso", "mixed") and not args.no_cpu:  # CPU numbers for configs 2-4
                 try:
@@ -1101,9 +1119,16 @@ def main():
                                                               cache_sample=False)
                 except Exception as e:
                     extra[cfg]["cpu_baseline"] = {"value": None, "error": repr(e)}
+            if args.arena_policy == "keep":
+                kept.append((r["arena"], r["descs"]))
             del r
-            torch.cuda.empty_cache()
+            if args.arena_policy == "free":
+                torch.cuda.empty_cache()
+        del kept
+        torch.cuda.empty_cache()
         line["configs"] = extra
+        if args.arena_policy != "free" or args.gap_ms:
+            line["secondary_arenas"] = {"policy": args.arena_policy, "gap_ms": args.gap_ms}
         if not args.no_cpu:
             try:
                 line["cpu_baseline"] = cpu_baseline(torch, head, args.cpu_seconds, args.cpu_kind)

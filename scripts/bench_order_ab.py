@@ -9,6 +9,9 @@ rounds, and prints every secondary config's roofline frac per variant:
   no_cpu      the same without the CPU-baseline legs
   mixed_first the secondaries with mixed before tso (no CPU legs)
   alone       `--config mixed` alone (its own line)
+With --arenas instead: free (the default's arena handling), keep (no
+secondary arena freed), prealloc (all allocated before the first is timed),
+gap2s (2 s idle between the secondary configs).
 
   python scripts/bench_order_ab.py [ROUNDS] > out.txt
 The host-memory legs (e2e, PMC and trace children) are off in every variant.
@@ -27,6 +30,13 @@ VARIANTS = {
     "mixed_first": ["--secondary", "mixed,tso,mixed_aligned,mixed_rx", "--no-cpu"],
     "alone": ["--config", "mixed", "--secondary", "", "--no-cpu"],
 }
+if "--arenas" in sys.argv:  # round 5's second pass: what about running after TSO slows the next config
+    VARIANTS = {
+        "free": ["--secondary", SEC, "--no-cpu"],
+        "keep": ["--secondary", SEC, "--no-cpu", "--arena-policy", "keep"],
+        "prealloc": ["--secondary", SEC, "--no-cpu", "--arena-policy", "prealloc"],
+        "gap2s": ["--secondary", SEC, "--no-cpu", "--gap-ms", "2000"],
+    }
 
 
 def run(args):
@@ -43,7 +53,7 @@ def run(args):
 
 
 def main():
-    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 2
     names = list(VARIANTS)
     res = {k: [] for k in names}
     for r in range(rounds):

@@ -715,67 +715,6 @@ __device__ __forceinline__ void desc_span(const void *__restrict__ descs, uint32
     len = *reinterpret_cast<const uint32_t *>(x + 8);
 }
 
-// All eight descriptors of a full K = 8 workgroup through the scalar cache
-// (aux bit 0x80, measurement): the vector path re-fetches from HBM the lines
-// the two scalar span loads fetched (scalar-only and vector-only reads of
-// k_segments_pk's descriptors each count 0.667 FETCH_SIZE per byte, both
-// together 1.334: scripts/pmc_calib.hip k_pkdesc, profiles/r05/).  Lane r
-// (r < 8) gets descriptor first + r; the others get a zero-length one.
-typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
-
-template <int MODE>
-__device__ __forceinline__ SegDesc sdesc8(const void *__restrict__ descs, uint32_t first, uint32_t lane)
-{
-    constexpr uint32_t DW = MODE == MODE_PESO ? 6u : 4u; // dwords per descriptor
-    const uint8_t *p = static_cast<const uint8_t *>(descs) + 4ull * DW * first; // workgroup-uniform
-    // the workgroup's 8 x DW dwords in three 64-B scalar loads, all in flight
-    // before one wait (left to the compiler, 48 single-dword loads each
-    // waited for); a reads-only scalar load
-    // (exactly the 8 descriptors: 192 B for checksum_peso's 24-B records,
-    // 128 B for 16-B ones -- never past the workgroup's last descriptor)
-    u32x16 a, b, c = u32x16(0u);
-    if constexpr (DW == 6u)
-        asm volatile("s_load_dwordx16 %0, %3, 0x0\n\t"
-                     "s_load_dwordx16 %1, %3, 0x40\n\t"
-                     "s_load_dwordx16 %2, %3, 0x80\n\t"
-                     "s_waitcnt lgkmcnt(0)"
-                     : "=&s"(a), "=&s"(b), "=&s"(c)
-                     : "s"(p)
-                     : "memory");
-    else
-        asm volatile("s_load_dwordx16 %0, %2, 0x0\n\t"
-                     "s_load_dwordx16 %1, %2, 0x40\n\t"
-                     "s_waitcnt lgkmcnt(0)"
-                     : "=&s"(a), "=&s"(b)
-                     : "s"(p)
-                     : "memory");
-    uint32_t f[DW];
-#pragma unroll
-    for (uint32_t k = 0; k < DW; ++k)
-        f[k] = 0u;
-#pragma unroll
-    for (uint32_t r = 0; r < 8u; ++r)
-#pragma unroll
-        for (uint32_t k = 0; k < DW; ++k) {
-            const uint32_t i = r * DW + k; // a constant once unrolled
-            const uint32_t x = i < 16u ? a[i & 15u] : i < 32u ? b[i & 15u] : c[i & 15u];
-            f[k] = lane == r ? x : f[k];
-        }
-    SegDesc d;
-    d.off = (uint64_t)f[0] | ((uint64_t)f[1] << 32);
-    d.len = lane < 8u ? f[2] : 0u;
-    if constexpr (MODE == MODE_PESO) {
-        d.src = f[3];
-        d.dst = f[4];
-        d.proto = f[5] & 0xFFu;
-        d.pre = 0;
-    } else {
-        d.pre = f[3];
-        d.src = d.dst = d.proto = 0;
-    }
-    return d;
-}
-
 // The per-range path for a workgroup whose ranges are not one region:
 // groups of G lanes, G the widest power of two with one group per range.
 template <int MODE, int G, int UL = 4>
@@ -892,10 +831,7 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     SegDesc d{0, 0, 0, 0, 0, 0};
     uint32_t xs = 0, xe = 0, q16 = 0;
     if (has) {
-        if ((aux & 0x80u) && K == 8u && kw == 8u) // workgroup-uniform (wave 0 only: 8 <= 64)
-            d = sdesc8<MODE>(descs, first, lane);
-        else
-            d = load_desc<MODE>(descs, first + rr, mine);
+        d = load_desc<MODE>(descs, first + rr, mine);
         // P wraps mod 2^32 across passes, so a difference is exact only for a
         // range whose word sum stays below 2^32: < 128 KiB (<= 65536 words)
         const bool inside = !mine || (d.off >= r0 && d.off + d.len <= rend && d.len < (1u << 17));

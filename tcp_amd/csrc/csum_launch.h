@@ -45,7 +45,6 @@ enum Knob : int {
     KNOB_LOADS,      // per-range loads per lane (U)
     KNOB_XCD,        // XCD run length
     KNOB_PACKED,     // 0 / 1: k_segments_pk off / on
-    KNOB_RESERVED_4, // round 4's "flat" (the byte-window stream, now libtcsum_bench.so's tcsum_flat_ipv4)
     KNOB_TX_SPLIT,   // 0 / 1: tx fill stores in the kernel / deferred to k_tx_scatter
     KNOB_ARGS_LAUNCH, // 0: drop-in launch path with its descriptor in pinned memory
     KNOB_SYNC_BLOCK, // 1: drop-in calls block in hipStreamSynchronize instead of spinning
@@ -59,7 +58,6 @@ enum Knob : int {
     KNOB_HOSTQ_DMA_KEEP_MB, // device arena kept between host-queue calls up to this size (256)
     KNOB_COPY_THREADS, // host threads of a parallel gather / scatter pass (16)
     KNOB_PF_DIST,      // descriptor prefetch distance of k_segments_pk's range-by-range path (2048)
-    KNOB_PK_SDESC,     // 1: k_segments_pk loads a full K = 8 workgroup's descriptors through the scalar cache
     KNOB_COUNT
 };
 int64_t knob(Knob k);

@@ -1,8 +1,7 @@
-"""k_segments_pk's descriptor variants: the prefetch of its range-by-range
-path (debug knob "pf_dist", csum_device.h prefetch_descs: lanes of wave 0
-touch the descriptor lines of the workgroup pf_dist logical blocks ahead) and
-the all-scalar descriptor reads of a full 8-range workgroup ("pk_sdesc").
-Neither may change a result or read past the descriptor array: both
+"""k_segments_pk's descriptor prefetch on its range-by-range path (debug
+knob "pf_dist", csum_device.h prefetch_descs: lanes of wave 0 touch the
+descriptor lines of the workgroup pf_dist logical blocks ahead).  It may not
+change a result or read past the descriptor array: both
 descriptor layouts (checksum_peso, pktbuf_checksum16) against the oracle,
 packed, shuffled, TSO-sized and K = 8 batches, distances from 1 to far past
 the grid, descriptor arrays at the end of their allocation; and the IPv4
@@ -40,14 +39,13 @@ def _descs_at_end(torch, tc, descs):
     return t
 
 
-@pytest.mark.parametrize("sdesc", [0, 1])
 @pytest.mark.parametrize("pf", DISTANCES)
 @pytest.mark.parametrize("layout", ["packed", "shuffled", "tso", "mtu"])
-def test_peso_batches_with_prefetch(tc, torch, oracle, pf, layout, sdesc):
+def test_peso_batches_with_prefetch(tc, torch, oracle, pf, layout):
     rng = np.random.default_rng(40 + DISTANCES.index(pf))
     if layout == "tso":
         n, lens = 300, np.full(300, 65536)
-    elif layout == "mtu":  # K = 8 full workgroups, the last one partial: the scalar-descriptor path
+    elif layout == "mtu":  # K = 8 full workgroups, the last one partial
         n, lens = 8 * 1001 + 5, np.full(8 * 1001 + 5, 1500)
     else:
         n = 20011
@@ -64,7 +62,7 @@ def test_peso_batches_with_prefetch(tc, torch, oracle, pf, layout, sdesc):
     want = oracle.batch_peso(host, p, nthreads=8)
     arena = torch.from_numpy(host).cuda()
     d = _descs_at_end(torch, tc, p)
-    with tc.debug(pf_dist=pf, pk_sdesc=sdesc):
+    with tc.debug(pf_dist=pf):
         got = tc.batch_peso(arena, d, n, int(lens.sum())).cpu().numpy()
         segs = np.zeros(n, tc.SEG_DTYPE)  # the same ranges as pktbuf_checksum16 (16-B descriptors)
         segs["offset"], segs["len"], segs["pre_sum"] = p["offset"], p["len"], rng.integers(0, 1 << 17, n)

@@ -60,9 +60,11 @@ def parse():
                          "whatever W is; 0 = exactly W launches).  300: with 30 one box read the headline "
                          "at 0.908 against 0.935 with 300 in the same call, and the secondary configs "
                          "1-2.5 %% low (profiles/r04/gap/)")
-    ap.add_argument("--arena-policy", choices=("free", "keep", "prealloc"), default="free",
-                    help="secondary configs' arenas: free each after its config (torch.cuda.empty_cache), keep "
-                         "them all allocated, or allocate them all before the first is timed")
+    ap.add_argument("--arena-policy", choices=("free", "keep", "prealloc"), default="prealloc",
+                    help="secondary configs' arenas: allocated and filled all before the first is timed (default), "
+                         "kept, or freed after each config (round 4's: the config timed right after the 16-GiB "
+                         "TSO arena was freed read 1.4-3.3 %% slow while the driver released it, "
+                         "profiles/r05/order/)")
     ap.add_argument("--gap-ms", type=float, default=0.0,
                     help="measurement: idle time between the secondary configs")
     ap.add_argument("--no-pmc", action="store_true")
@@ -1127,8 +1129,7 @@ def main():
         del kept
         torch.cuda.empty_cache()
         line["configs"] = extra
-        if args.arena_policy != "free" or args.gap_ms:
-            line["secondary_arenas"] = {"policy": args.arena_policy, "gap_ms": args.gap_ms}
+        line["secondary_arenas"] = {"policy": args.arena_policy, "gap_ms": args.gap_ms}
         if not args.no_cpu:
             try:
                 line["cpu_baseline"] = cpu_baseline(torch, head, args.cpu_seconds, args.cpu_kind)

@@ -65,6 +65,10 @@ def parse():
                          "kept, or freed after each config (round 4's: the config timed right after the 16-GiB "
                          "TSO arena was freed read 1.4-3.3 %% slow while the driver released it, "
                          "profiles/r05/order/)")
+    ap.add_argument("--child-gap-ms", type=float, default=2000.0,
+                    help="idle time after the PMC / trace children exit, before this process allocates: the "
+                         "driver releases a freed multi-GiB allocation in the background for ~1-2 s, and a "
+                         "config timed meanwhile reads slow (profiles/r05/order/)")
     ap.add_argument("--gap-ms", type=float, default=0.0,
                     help="measurement: idle time between the secondary configs")
     ap.add_argument("--no-pmc", action="store_true")
@@ -971,6 +975,8 @@ def main():
         traffic, pmc_note, pmc_detail = pmc_traffic(args.config)  # before this process touches the GPU
     if not args.pmc_child and world == 1 and not args.no_trace:
         trace, trace_note = rocprof_trace(args.config, args.steps, args.warmup, args.settle_ms)
+    if not args.pmc_child and world == 1 and not (args.no_pmc and args.no_trace) and args.child_gap_ms > 0:
+        time.sleep(args.child_gap_ms / 1e3)
 
     import torch
     from tcp_amd import build

@@ -11,7 +11,9 @@ rounds, and prints every secondary config's roofline frac per variant:
   alone       `--config mixed` alone (its own line)
 With --arenas instead: free (the default's arena handling), keep (no
 secondary arena freed), prealloc (all allocated before the first is timed),
-gap2s (2 s idle between the secondary configs).
+gap2s (2 s idle between the secondary configs).  With --children: the
+headline after its PMC / trace children with and without bench.py's pause
+after them, and with no children at all.
 
   python scripts/bench_order_ab.py [ROUNDS] > out.txt
 The host-memory legs (e2e, PMC and trace children) are off in every variant.
@@ -30,7 +32,14 @@ VARIANTS = {
     "mixed_first": ["--secondary", "mixed,tso,mixed_aligned,mixed_rx", "--no-cpu"],
     "alone": ["--config", "mixed", "--secondary", "", "--no-cpu"],
 }
-if "--arenas" in sys.argv:  # round 5's second pass: what about running after TSO slows the next config
+if "--children" in sys.argv:  # the headline after the PMC / trace children, with and without the pause
+    BASE = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--no-e2e", "--no-cpu", "--secondary", ""]
+    VARIANTS = {
+        "children_gap2s": [],
+        "children_nogap": ["--child-gap-ms", "0"],
+        "no_children": ["--no-pmc", "--no-trace"],
+    }
+elif "--arenas" in sys.argv:  # round 5's second pass: what about running after TSO slows the next config
     VARIANTS = {
         "free": ["--secondary", SEC, "--no-cpu"],
         "keep": ["--secondary", SEC, "--no-cpu", "--arena-policy", "keep"],

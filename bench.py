@@ -65,10 +65,10 @@ def parse():
                          "kept, or freed after each config (round 4's: the config timed right after the 16-GiB "
                          "TSO arena was freed read 1.4-3.3 %% slow while the driver released it, "
                          "profiles/r05/order/)")
-    ap.add_argument("--child-gap-ms", type=float, default=2000.0,
-                    help="idle time after the PMC / trace children exit, before this process allocates: the "
-                         "driver releases a freed multi-GiB allocation in the background for ~1-2 s, and a "
-                         "config timed meanwhile reads slow (profiles/r05/order/)")
+    ap.add_argument("--child-gap-ms", type=float, default=0.0,
+                    help="measurement: idle time after the PMC / trace children exit, before this process "
+                         "allocates (a 2-s pause changed nothing for the headline: 0.9400-0.9409 with it, "
+                         "0.9386-0.9407 without, 0.9399-0.9402 with no children; profiles/r05/order/)")
     ap.add_argument("--gap-ms", type=float, default=0.0,
                     help="measurement: idle time between the secondary configs")
     ap.add_argument("--no-pmc", action="store_true")

@@ -21,6 +21,7 @@ extern "C" {
 /* Set a knob; value -1 gives the choice back to the router.  Keys:
  *   "pf_dist"         descriptor prefetch distance, in workgroups, of the
  *                     packed kernel's range-by-range path (2048; 0 = off)
+ *   "pf_range"        the same for the per-range kernels (0 = off)
  *   "lanes", "loads"  per-range kernel shape (lanes per range x 16-B loads per
  *                     lane): one of the shapes the router picks -- 4x1, 4x2,
  *                     8x4, 16x3, 16x4, 16x6, 16x8, 32x6, 256x16, 1024x4 (IPv4

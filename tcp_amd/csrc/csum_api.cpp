@@ -471,7 +471,7 @@ static const struct {
     {"server_max", tcsum::KNOB_SERVER_MAX}, {"server_trace", tcsum::KNOB_SERVER_TRACE},
     {"server_idle_ms", tcsum::KNOB_SERVER_IDLE_MS}, {"server_wgs", tcsum::KNOB_SERVER_WGS},
     {"hostq_dma_kb", tcsum::KNOB_HOSTQ_DMA_KB}, {"hostq_dma_keep_mb", tcsum::KNOB_HOSTQ_DMA_KEEP_MB},
-    {"copy_threads", tcsum::KNOB_COPY_THREADS}, {"pf_dist", tcsum::KNOB_PF_DIST},
+    {"copy_threads", tcsum::KNOB_COPY_THREADS}, {"pf_dist", tcsum::KNOB_PF_DIST}, {"pf_range", tcsum::KNOB_PF_RANGE},
 };
 
 static int knob_of(const char *key)

@@ -348,6 +348,14 @@ static uint32_t pf_dist()
     return v < 0 ? 2048u : (uint32_t)(v < (1 << 23) ? v : (1 << 23) - 1);
 }
 
+// The per-range kernel's descriptor prefetch distance (debug knob
+// "pf_range"; 0 = off, the default while unmeasured)
+static uint32_t pf_range()
+{
+    const int64_t v = knob(KNOB_PF_RANGE);
+    return v <= 0 ? 0u : (uint32_t)(v < (1 << 23) ? v : (1 << 23) - 1);
+}
+
 // The shapes the router can pick for the per-range kernels (and only those:
 // a debug override naming another shape is refused).
 template <int MODE>
@@ -358,7 +366,7 @@ static hipError_t seg_u(int G, int U, uint32_t xg, uint32_t n, const void *arena
 #define TCSUM_SEG(GG, UU)                                                                                     \
     if (G == GG && U == UU) {                                                                               \
         return launch(k_segments<GG, UU, MODE>, dim3((n + 256u / GG - 1) / (256u / GG)), dim3(256), 0, s, a,     \
-                      descs, n, out, aux, xg);                                                               \
+                      descs, n, out, aux | (pf_range() << 8), xg);                                            \
     }
     TCSUM_SEG(4, 1) TCSUM_SEG(4, 2) TCSUM_SEG(8, 4) TCSUM_SEG(16, 3) TCSUM_SEG(16, 4) TCSUM_SEG(16, 6)
     TCSUM_SEG(16, 8) TCSUM_SEG(32, 6)

@@ -58,6 +58,7 @@ enum Knob : int {
     KNOB_HOSTQ_DMA_KEEP_MB, // device arena kept between host-queue calls up to this size (256)
     KNOB_COPY_THREADS, // host threads of a parallel gather / scatter pass (16)
     KNOB_PF_DIST,      // descriptor prefetch distance of k_segments_pk's range-by-range path (2048)
+    KNOB_PF_RANGE,     // descriptor prefetch distance of the per-range kernels k_segments (0)
     KNOB_COUNT
 };
 int64_t knob(Knob k);

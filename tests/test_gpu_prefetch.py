@@ -69,6 +69,10 @@ def test_peso_batches_with_prefetch(tc, torch, oracle, pf, layout):
         gs = tc.batch_segments(arena, _descs_at_end(torch, tc, segs), n, 1, int(lens.sum())).cpu().numpy()
     np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(gs, oracle.batch_segments(host, segs, 1, nthreads=8))
+    # the per-range kernels (the SHUFFLED route) with their own prefetch knob
+    with tc.debug(pf_range=pf):
+        gr, _, _ = tc.batch(tc.OP_PESO, arena, d, n, total_bytes=int(lens.sum()), layout=tc.LAYOUT_SHUFFLED)
+    np.testing.assert_array_equal(gr.cpu().numpy(), want)
 
 
 @pytest.mark.parametrize("pf", DISTANCES)

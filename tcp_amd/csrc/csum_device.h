@@ -753,13 +753,19 @@ __device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, c
                                             uint16_t *__restrict__ out, uint32_t aux, uint32_t first, uint32_t kw,
                                             uint32_t T)
 {
+    // K was chosen so that K mean-length ranges fill a 12-KiB pass: a range is
+    // about 12 KiB / K, and each group's pass is sized to hold one (32 x 3 =
+    // 1.5 KiB at K = 8; 16 x 6 for K = 9..16; 8 x 6 = 768 B for the 21
+    // ranges of 576 B)
     const uint32_t lanes_per = T / kw;
     if (lanes_per >= 64)
         pk_ranges<MODE, 64>(arena, descs, out, aux, first, kw, T);
     else if (lanes_per >= 32)
         pk_ranges<MODE, 32, 3>(arena, descs, out, aux, first, kw, T);
     else if (lanes_per >= 16)
-        pk_ranges<MODE, 16>(arena, descs, out, aux, first, kw, T);
+        pk_ranges<MODE, 16, 6>(arena, descs, out, aux, first, kw, T);
+    else if (kw <= 32u)
+        pk_ranges<MODE, 8, 6>(arena, descs, out, aux, first, kw, T);
     else
         pk_ranges<MODE, 8>(arena, descs, out, aux, first, kw, T);
 }

@@ -25,6 +25,7 @@ import tcp_amd as tc  # noqa: E402
 from tcp_amd.csum import PESO_DTYPE  # noqa: E402
 
 variants = [{}] + [dict(kv.split("=", 1) for kv in a.split(",")) for a in sys.argv[1:] if "=" in a]
+ROUNDS = int(os.environ.get("AB_ROUNDS", "8"))
 TOTAL = 1500 << 20
 rng = np.random.default_rng(7)
 
@@ -110,8 +111,9 @@ for name in NAMES:
             run(i)
     torch.cuda.synchronize()
     ts = [[] for _ in variants]
-    for _ in range(7):
-        for i in range(len(variants)):
+    for r in range(ROUNDS):
+        for k in range(len(variants)):  # the variant timed first rotates (the first of a round can run ~1 % slow)
+            i = (r + k) % len(variants)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(10):

@@ -29,7 +29,8 @@ extern "C" {
  *                     batch call return TCSUM_ERR_PARAM
  *   "xcd"             workgroups per XCD run (1 = dispatch order)
  *   "packed"          0 / 1: checksum_peso / pktbuf_checksum16 batches on the
- *                     packed-stream kernel (k_segments_pk) off / on
+ *                     packed-stream kernel (k_segments_pk) off / on; K > 1: on,
+ *                     with K ranges per workgroup (measurement)
  *   "tx_split"        0 / 1: the tx fill's stores in the kernel / deferred
  *   "args_launch"     0: drop-in calls pass their descriptor in pinned memory
  *   "sync_block"      1: drop-in calls block in hipStreamSynchronize

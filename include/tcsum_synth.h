@@ -115,7 +115,10 @@ int tcsum_flat_ipv4(int mode, void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[
  * thread workgroups (rx: 256 / 1024), or with wg = 256 held to occ waves per
  * SIMD (sums: 8; rx: 7 or 8; 0 = as built), or (occ = 100 + s, wg = 256)
  * with its data pass starting s bytes past a 128-B line instead of on one
- * (sums: s = 16, 64; rx: 16).  Others: TCSUM_ERR_PARAM. */
+ * (sums: s = 16, 64; rx: 16), or (occ = 200) two data passes in flight, or
+ * (occ = 300 + M, wg = 256; sums M = 2, 4, 8, 16, rx 2, 4, 8) M packets per
+ * lane group handed out inside the workgroup (k_ipv4_dyn).  Others:
+ * TCSUM_ERR_PARAM. */
 int tcsum_probe_ipv4_shape(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n, int mode, int wg,
                            int occ, uint32_t *out /*[dev]*/, int8_t *verdict /*[dev] or NULL*/, void *stream);
 

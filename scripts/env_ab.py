@@ -70,7 +70,9 @@ for v in variants[1:]:
         assert torch.equal(arena, arena_ref), f"{v} changed the filled packets"
 times = [[] for _ in variants]
 for r in range(7):
-    for i, v in enumerate(variants):
+    for j in range(len(variants)):  # the variant timed first rotates (it reads ~1 % slow)
+        i = (r + j) % len(variants)
+        v = variants[i]
         def timed():
             run()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -82,7 +84,7 @@ for r in range(7):
             return e0.elapsed_time(e1) / 10
         times[i].append(with_env(v, timed))
 base = np.median(times[0])
-print(f"# {cfg}: {n} packets, {b.total_bytes} B; median of 7 rounds x 10 launches, interleaved")
+print(f"# {cfg}: {n} packets, {b.total_bytes} B; median of 7 rounds x 10 launches, interleaved, first-timed rotated")
 for v, t in zip(variants, times):
     m = np.median(t)
     print(f"{(','.join(f'{k}={x}' for k, x in v.items()) or 'default'):40s} {m*1e3:9.1f} us  {m/base:6.3f}x")

@@ -20,6 +20,7 @@ from tcp_amd import _lib, workload  # noqa: E402
 B = _lib.bench_lib()
 SKEW_ONLY = "--skew" in sys.argv
 DB_ONLY = "--db" in sys.argv  # two data passes in flight, with and without the descriptor prefetch
+DYN_ONLY = "--dyn" in sys.argv  # packets handed out inside the workgroup (k_ipv4_dyn), M per lane group
 for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mixed_aligned", "mixed_rx"]):
     b = workload.make_batch(cfg)
     arena, descs = workload.materialize(b)
@@ -55,7 +56,11 @@ for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mi
                 f(o, v)
         return g
 
-    if DB_ONLY:
+    if DYN_ONLY:
+        kinds.update({f"dyn M={m}": shape(256, 300 + m) for m in ((2, 4, 8) if rx else (2, 4, 8, 16))})
+        for w in ((6, 7) if rx else (7, 8)):  # M = 4 held to w waves per SIMD
+            kinds[f"dyn M=4, {w} waves/SIMD"] = shape(256, 300 + 16 * w + 4)
+    elif DB_ONLY:
         kinds.update({"two passes in flight": shape(256, 200),
                       "product, pf_dist 2048": with_pf(product, 2048),
                       "two passes in flight, pf_dist 2048": with_pf(shape(256, 200), 2048)})
@@ -79,8 +84,11 @@ for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mi
         if rx:
             assert torch.equal(bufs[k][1], v0), k
     times = {k: [] for k in kinds}
+    names = list(kinds)
     for r in range(7):
-        for k, fn in kinds.items():
+        for i in range(len(names)):  # the variant timed first rotates
+            k = names[(r + i) % len(names)]
+            fn = kinds[k]
             fn(*bufs[k])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -91,7 +99,7 @@ for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mi
             times[k].append(e0.elapsed_time(e1) / 10)
     alg = b.total_bytes + (17 if rx else 20) * n
     base = np.median(times["product (256 threads)"])
-    print(f"# {cfg}: {n} packets, {b.total_bytes} B; median of 7 rounds x 10 launches, interleaved; results equal")
+    print(f"# {cfg}: {n} packets, {b.total_bytes} B; median of 7 rounds x 10 launches, interleaved, first-timed rotated; results equal")
     for k, t in times.items():
         m = np.median(t)
         print(f"{k:42s} {m*1e3:9.1f} us  {m/base:6.3f}x  {alg / (m*1e-3) / 8e12:6.4f} of 8 TB/s", flush=True)

@@ -830,7 +830,8 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
     const uint32_t G = mode == IP_RX ? 16u : 32u;
     if (wg != 256 && wg != 512 && wg != 1024)
         return hipErrorInvalidValue;
-    const uint32_t per = (uint32_t)wg / G;
+    const uint32_t dyn_m = occ > 300 && occ < 500 ? (uint32_t)((occ - 300) & 15 ? (occ - 300) & 15 : 16) : 1u; // k_ipv4_dyn's M
+    const uint32_t per = (uint32_t)wg / G * dyn_m;
     const dim3 grid((n + per - 1u) / per), blk((uint32_t)wg);
     uint8_t *fl = nullptr;
     const uint32_t opts = 0u;
@@ -845,7 +846,20 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 100 + 16 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 16>)) } // data pass skewed 16 B
         if (occ == 200 && wg == 256) { TCSUM_SH((k_ipv4_db<32, 6, IP_SUMS>)) } // two passes in flight
         if (occ == 100 + 64 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 64>)) }
+        // packets handed out inside the workgroup, M = occ - 300 per lane group
+        if (occ == 302 && wg == 256) { TCSUM_SH((k_ipv4_dyn<32, 6, IP_SUMS, 2>)) }
+        if (occ == 304 && wg == 256) { TCSUM_SH((k_ipv4_dyn<32, 6, IP_SUMS, 4>)) }
+        if (occ == 308 && wg == 256) { TCSUM_SH((k_ipv4_dyn<32, 6, IP_SUMS, 8>)) }
+        if (occ == 316 && wg == 256) { TCSUM_SH((k_ipv4_dyn<32, 6, IP_SUMS, 16>)) }
+        // the same held to 7 / 8 waves per SIMD (occ = 300 + 16 * waves + M)
+        if (occ == 300 + 16 * 7 + 4 && wg == 256) { TCSUM_SH((k_ipv4_dyn<32, 6, IP_SUMS, 4, 7>)) }
+        if (occ == 300 + 16 * 8 + 4 && wg == 256) { TCSUM_SH((k_ipv4_dyn<32, 6, IP_SUMS, 4, 8>)) }
     } else if (mode == IP_RX && verdict) {
+        if (occ == 302 && wg == 256) { TCSUM_SH((k_ipv4_dyn<16, 6, IP_RX, 2>)) }
+        if (occ == 304 && wg == 256) { TCSUM_SH((k_ipv4_dyn<16, 6, IP_RX, 4>)) }
+        if (occ == 308 && wg == 256) { TCSUM_SH((k_ipv4_dyn<16, 6, IP_RX, 8>)) }
+        if (occ == 300 + 16 * 6 + 4 && wg == 256) { TCSUM_SH((k_ipv4_dyn<16, 6, IP_RX, 4, 6>)) }
+        if (occ == 300 + 16 * 7 + 4 && wg == 256) { TCSUM_SH((k_ipv4_dyn<16, 6, IP_RX, 4, 7>)) }
         if (occ == 0 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256>)) }
         if (occ == 0 && wg == 1024) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 1024>)) }
         if (occ == 7 && wg == 256) { TCSUM_SH((k_ipv4_occ<16, 6, IP_RX, 7>)) }

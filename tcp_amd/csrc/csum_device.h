@@ -1404,6 +1404,35 @@ __global__ __launch_bounds__(256) void k_ipv4_db(uint8_t *__restrict__ arena, co
                                     opts);
 }
 
+// k_ipv4 with the packets handed out inside the workgroup: M * (256 / G)
+// consecutive packets per workgroup, each lane group taking the next one
+// (an LDS counter) as soon as its own is summed, so a group whose packet was
+// short does not idle until the workgroup's longest packet is done.
+template <int G, int U, int IPM, int M, int OCC = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1))) void k_ipv4_dyn(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
+                                                  uint32_t n, uint32_t *__restrict__ out,
+                                                  uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
+                                                  uint32_t opts, uint32_t xg)
+{
+    constexpr uint32_t NG = 256u / G, PER = NG * (uint32_t)M;
+    __shared__ uint32_t next;
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    const uint64_t first = (uint64_t)blk * PER;
+    const uint32_t lim = n - first < PER ? (uint32_t)(n - first) : PER; // >= 1: grid = ceil(n / PER)
+    if (threadIdx.x == 0)
+        next = NG;
+    __syncthreads();
+    const uint32_t gl = threadIdx.x & (G - 1u), lead = threadIdx.x & 63u & ~(G - 1u);
+    uint32_t k = threadIdx.x / G;
+    while (k < lim) { // group-uniform; the group reductions stay inside the group
+        ipv4_packet<G, U, IPM>(arena, pkts, (uint32_t)(first + k), n, out, flags_out, verdict_out, opts);
+        uint32_t c = 0;
+        if (gl == 0)
+            c = atomicAdd(&next, 1u);
+        k = (uint32_t)__shfl((int)c, (int)lead, 64);
+    }
+}
+
 // k_ipv4 held to OCC waves per SIMD (the sums form takes 66 VGPRs, i.e. 7
 // waves; rx 74, 6): measurement (libtcsum_bench.so, tcsum_probe_ipv4_shape)
 template <int G, int U, int IPM, int OCC>

@@ -334,6 +334,8 @@ Geometry pick_geometry(uint64_t mean_len)
         const uint64_t kmax = (uint64_t)kPkMaxRanges * kPkWaves;
         if (k >= 3)
             g.packed = (int)(k > kmax ? kmax : k);
+        if (kp > 1) // measurement: K itself
+            g.packed = (int)((uint64_t)kp > kmax ? kmax : (uint64_t)kp);
     }
     return g;
 }

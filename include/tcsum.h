@@ -94,7 +94,8 @@ typedef struct tcsum_pkt {
 /* What a caller knows of where its ranges lie (tcsum_batch's hint). */
 #define TCSUM_LAYOUT_UNKNOWN 0  /* the calls below: the stream kernels check per workgroup */
 #define TCSUM_LAYOUT_ORDERED 1  /* descriptors in arena order, ranges disjoint (gaps allowed) */
-#define TCSUM_LAYOUT_SHUFFLED 2 /* no order to exploit: per-range / per-packet kernels only */
+#define TCSUM_LAYOUT_SHUFFLED 2 /* no order to exploit: the per-range / per-packet kernels (ranges of
+                                 * ~1.5 KiB and up: the packed kernel's range-by-range path, faster) */
 
 typedef struct tcsum_hint {
     uint64_t total_bytes; /* sum of the lengths; 0 = unknown (read as 1500-B ranges) */

@@ -22,6 +22,15 @@ extern "C" {
  *   "pf_dist"         descriptor prefetch distance, in workgroups, of the
  *                     packed kernel's range-by-range path (2048; 0 = off)
  *   "pf_range"        the same for the per-range kernels (0 = off)
+ *   "page_stage"      0 / 1 (default 1): tcsum_host_batch_peso copies a
+ *                     pageable arena through the context's pinned slots (0:
+ *                     the runtime's own pageable copy, measurement only)
+ *   "pk_early"        0 / 1 (default 1): the packed kernel's range-by-range
+ *                     path (a workgroup whose ranges are not one region, up
+ *                     to 32 of them) reads its descriptors with scalar loads
+ *                     -- lines its span check just cached -- instead of
+ *                     vector loads through the L2; with 0, SHUFFLED batches
+ *                     always take the per-range kernel
  *   "lanes", "loads"  per-range kernel shape (lanes per range x 16-B loads per
  *                     lane): one of the shapes the router picks -- 4x1, 4x2,
  *                     8x4, 16x3, 16x4, 16x6, 16x8, 32x6, 256x16, 1024x4 (IPv4
@@ -56,8 +65,9 @@ int tcsum_debug_set(const char *key, int64_t value);
  * the calling thread's device) and "last_sys_error": the last HIP call that
  * failed under any TCSUM_ERR_SYS / TCSUM_ERR_MEM return of the library, as
  * step * 1000 + its hipError_t (0 = none yet).  Steps:
- *    1-16  tcsum_host_batch_peso (1 set device, 2-5 copies, 6-7 events,
- *          8 launch, 9 results copy, 10-11 stream syncs, 13-16 allocations)
+ *    1-17  tcsum_host_batch_peso (1 set device, 2-5 copies, 6-7 events,
+ *          8 launch, 9 results copy, 10-11 stream syncs, 13-16 allocations,
+ *          17 the pageable staging slots' events)
  *   20-25  device context init (any entry point that creates it)
  *   31-37  host-queue IPv4 batches (31 set device, 32-33 pinned staging,
  *          34-35 copy-engine pieces, 36 launch, 37 wait)
@@ -73,7 +83,7 @@ int64_t tcsum_debug_get(const char *key);
  * of host bytes [lo, hi) into device buffer 0 (the lead's) or 1 (the
  * arena's), {1, buffer, i0, i1, arena offset of the buffer's byte 0} for a
  * kernel over segments [i0, i1) reading that buffer ({2, ...}: the same, the
- * segments out of offset order, so the per-range kernel) -- at most max_rows of
+ * segments out of offset order, so tcsum_batch's SHUFFLED route) -- at most max_rows of
  * them written; buf_bytes[0..1]: the two buffers' sizes (0: unused).  Uses
  * the "e2e_chunk_mb" knob like the call.  Returns the row count, or
  * TCSUM_ERR_PARAM (a segment outside the arena, as the call would). */

@@ -117,7 +117,11 @@ int tcsum_flat_ipv4(int mode, void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[
  * with its data pass starting s bytes past a 128-B line instead of on one
  * (sums: s = 16, 64; rx: 16), or (occ = 200) two data passes in flight, or
  * (occ = 300 + M, wg = 256; sums M = 2, 4, 8, 16, rx 2, 4, 8) M packets per
- * lane group handed out inside the workgroup (k_ipv4_dyn).  Others:
+ * lane group handed out inside the workgroup (k_ipv4_dyn), or (occ = 500 +
+ * v) the rolling load slots (each slot reissued for the next pass as soon as
+ * its chunk is taken): v = 0 the mode's shape, 4 = 4 loads, sums 8 = 8 loads,
+ * 16 = 16 lanes x 6, rx 32 = 32 lanes x 6, sums 7 / rx 6 = the mode's shape
+ * held to that many waves per SIMD.  Others:
  * TCSUM_ERR_PARAM. */
 int tcsum_probe_ipv4_shape(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n, int mode, int wg,
                            int occ, uint32_t *out /*[dev]*/, int8_t *verdict /*[dev] or NULL*/, void *stream);

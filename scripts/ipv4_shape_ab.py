@@ -21,6 +21,7 @@ B = _lib.bench_lib()
 SKEW_ONLY = "--skew" in sys.argv
 DB_ONLY = "--db" in sys.argv  # two data passes in flight, with and without the descriptor prefetch
 DYN_ONLY = "--dyn" in sys.argv  # packets handed out inside the workgroup (k_ipv4_dyn), M per lane group
+ROLL_ONLY = "--roll" in sys.argv  # rolling load slots: a multi-pass packet keeps its loads in flight
 for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mixed_aligned", "mixed_rx"]):
     b = workload.make_batch(cfg)
     arena, descs = workload.materialize(b)
@@ -56,7 +57,14 @@ for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mi
                 f(o, v)
         return g
 
-    if DYN_ONLY:
+    if ROLL_ONLY:
+        kinds.update({"rolling slots": shape(256, 500), "rolling, 4 loads": shape(256, 504),
+                      "rolling, held to the route's waves/SIMD": shape(256, 506 if rx else 507)})
+        if rx:
+            kinds["rolling, 32 lanes x 6"] = shape(256, 532)
+        else:
+            kinds.update({"rolling, 8 loads": shape(256, 508), "rolling, 16 lanes x 6": shape(256, 516)})
+    elif DYN_ONLY:
         kinds.update({f"dyn M={m}": shape(256, 300 + m) for m in ((2, 4, 8) if rx else (2, 4, 8, 16))})
         for w in ((6, 7) if rx else (7, 8)):  # M = 4 held to w waves per SIMD
             kinds[f"dyn M=4, {w} waves/SIMD"] = shape(256, 300 + 16 * w + 4)

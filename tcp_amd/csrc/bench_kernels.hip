@@ -827,7 +827,7 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
     if (n == 0)
         return hipSuccess;
     const uint32_t xg = (uint32_t)route(1500).xcd;
-    const uint32_t G = mode == IP_RX ? 16u : 32u;
+    const uint32_t G = occ == 516 ? 16u : occ == 532 ? 32u : mode == IP_RX ? 16u : 32u;
     if (wg != 256 && wg != 512 && wg != 1024)
         return hipErrorInvalidValue;
     const uint32_t dyn_m = occ > 300 && occ < 500 ? (uint32_t)((occ - 300) & 15 ? (occ - 300) & 15 : 16) : 1u; // k_ipv4_dyn's M
@@ -845,6 +845,11 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 8 && wg == 256) { TCSUM_SH((k_ipv4_occ<32, 6, IP_SUMS, 8>)) }
         if (occ == 100 + 16 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 16>)) } // data pass skewed 16 B
         if (occ == 200 && wg == 256) { TCSUM_SH((k_ipv4_db<32, 6, IP_SUMS>)) } // two passes in flight
+        if (occ == 500 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 0, 2>)) } // rolling load slots
+        if (occ == 504 && wg == 256) { TCSUM_SH((k_ipv4<32, 4, IP_SUMS, 256, 0, 2>)) }
+        if (occ == 508 && wg == 256) { TCSUM_SH((k_ipv4<32, 8, IP_SUMS, 256, 0, 2>)) }
+        if (occ == 516 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_SUMS, 256, 0, 2>)) }
+        if (occ == 507 && wg == 256) { TCSUM_SH((k_ipv4_occ<32, 6, IP_SUMS, 7, 2>)) } // rolling, <= 72 VGPRs
         if (occ == 100 + 64 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 64>)) }
         // packets handed out inside the workgroup, M = occ - 300 per lane group
         if (occ == 302 && wg == 256) { TCSUM_SH((k_ipv4_dyn<32, 6, IP_SUMS, 2>)) }
@@ -866,6 +871,10 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 8 && wg == 256) { TCSUM_SH((k_ipv4_occ<16, 6, IP_RX, 8>)) }
         if (occ == 100 + 16 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256, 16>)) }
         if (occ == 200 && wg == 256) { TCSUM_SH((k_ipv4_db<16, 6, IP_RX>)) } // two passes in flight
+        if (occ == 500 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256, 0, 2>)) } // rolling load slots
+        if (occ == 504 && wg == 256) { TCSUM_SH((k_ipv4<16, 4, IP_RX, 256, 0, 2>)) }
+        if (occ == 532 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_RX, 256, 0, 2>)) }
+        if (occ == 506 && wg == 256) { TCSUM_SH((k_ipv4_occ<16, 6, IP_RX, 6, 2>)) } // rolling, <= 80 VGPRs
     }
 #undef TCSUM_SH
     return hipErrorInvalidValue;

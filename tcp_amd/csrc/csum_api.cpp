@@ -45,6 +45,8 @@ using tcsum::Geometry;
 constexpr int kMaxDev = 16;
 constexpr int kHostStreams = 2; // host batches: one copy stream, one kernel stream
 constexpr int kHostEvents = 8; // ring of copy-done events (host batches)
+constexpr int kPageSlots = 3;  // pinned staging slots of a pageable tcsum_host_batch_peso arena
+constexpr uint64_t kPageSlot = 32ull << 20;
 
 // Grow-only pinned, coherent host buffer with its device-side address.
 struct Pinned {
@@ -106,6 +108,11 @@ struct Ctx {
     // host-queue batches: pinned, fine-grained descriptors / results / a copy
     // of a pageable arena, all read and written by the kernel over PCIe
     Pinned q_desc, q_res, q_arena;
+    // tcsum_host_batch_peso from pageable memory: pinned slots the bytes pass
+    // through on their way to the copy engine, each with its copy-done event
+    Pinned q_page[kPageSlots];
+    hipEvent_t pev[kPageSlots] = {};
+    bool pev_ok = false;
     // queue server (tcsum_queue_server): a resident grid serving host-queue
     // jobs posted through pinned memory, instead of a launch + wait per job
     bool srv_on = false;      // enabled for this device
@@ -472,6 +479,7 @@ static const struct {
     {"server_idle_ms", tcsum::KNOB_SERVER_IDLE_MS}, {"server_wgs", tcsum::KNOB_SERVER_WGS},
     {"hostq_dma_kb", tcsum::KNOB_HOSTQ_DMA_KB}, {"hostq_dma_keep_mb", tcsum::KNOB_HOSTQ_DMA_KEEP_MB},
     {"copy_threads", tcsum::KNOB_COPY_THREADS}, {"pf_dist", tcsum::KNOB_PF_DIST}, {"pf_range", tcsum::KNOB_PF_RANGE},
+    {"pk_early", tcsum::KNOB_PK_EARLY}, {"page_stage", tcsum::KNOB_PAGE_STAGE},
 };
 
 static int knob_of(const char *key)
@@ -528,13 +536,15 @@ static uint64_t mean_of(uint64_t total, uint32_t n) { return total && n ? total 
 static constexpr uint32_t kTxSplitMin = 131072;
 
 // The route for a batch and what its caller knows of the layout
-// (tcsum_hint_t): SHUFFLED skips the stream kernel, which would find out
-// per workgroup; the debug knob "packed" set to 1 keeps it on regardless.
+// (tcsum_hint_t): SHUFFLED skips the stream kernel where its workgroups,
+// finding out one by one, would be slower than the per-range kernel
+// (tcsum::shuffled_route: ranges under ~1.5 KiB); the debug knob "packed" set
+// to 1 keeps it on regardless.
 static Geometry route_for(uint64_t total, uint32_t n, uint32_t layout)
 {
     Geometry g = tcsum::pick_geometry(mean_of(total, n));
-    if (layout == TCSUM_LAYOUT_SHUFFLED && tcsum::knob(tcsum::KNOB_PACKED) != 1)
-        g.packed = 0;
+    if (layout == TCSUM_LAYOUT_SHUFFLED)
+        tcsum::shuffled_route(g, tcsum::knob(tcsum::KNOB_PACKED));
     return g;
 }
 
@@ -917,12 +927,53 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         cap = need;
         return hipSuccess;
     };
+    // Pageable caller memory passes through the context's pinned slots (host
+    // threads fill one while the copy engine drains the others), so no copy
+    // ever reads the caller's pages through the runtime's own pageable path.
+    // Two suites stopped on that path: round 4 (TCSUM_ERR_SYS, fuzz seed 26)
+    // and round 5 (hipErrorIllegalAddress from this call's first copy, fuzz
+    // seed 27), each in the batch right after a hipHostRegister'ed arena was
+    // unregistered and freed.  Debug knob "page_stage" = 0: the
+    // runtime's path (measurement).
+    const bool pageable = tcsum::knob(tcsum::KNOB_PAGE_STAGE) != 0 && mapped_host(host_arena) == nullptr;
+    if (pageable && !c.pev_ok) {
+        for (auto &e : c.pev)
+            if (const hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming); r != hipSuccess)
+                return note_sys(17, r);
+        c.pev_ok = true;
+    }
+    bool slot_busy[kPageSlots] = {};
+    int slot_turn = 0;
+    auto copy_staged = [&](uint8_t *dst, const uint8_t *src, uint64_t bytes) -> hipError_t {
+        for (uint64_t o = 0; o < bytes; o += kPageSlot) {
+            const int s = slot_turn;
+            slot_turn = (slot_turn + 1) % kPageSlots;
+            if (slot_busy[s])
+                if (const hipError_t e = hipEventSynchronize(c.pev[s]); e != hipSuccess)
+                    return e;
+            const uint64_t len = std::min(kPageSlot, bytes - o);
+            if (const hipError_t e = c.q_page[s].reserve(kPageSlot); e != hipSuccess)
+                return e;
+            par_memcpy(c.q_page[s].h, src + o, len);
+            if (const hipError_t e = hipMemcpyAsync(dst + o, c.q_page[s].h, len, hipMemcpyHostToDevice, cs);
+                e != hipSuccess)
+                return e;
+            if (const hipError_t e = hipEventRecord(c.pev[s], cs); e != hipSuccess)
+                return e;
+            slot_busy[s] = true;
+        }
+        return hipSuccess;
+    };
     // copy a span into buffer `buf` of the plan
     uint8_t *base[2] = {nullptr, nullptr}; // device address arena offset 0 has in each buffer
     auto copy_span = [&](int buf, const HostSpan &sp) {
         uint64_t lo, hi;
         span_copy(sp, arena_bytes, lo, hi);
-        return hi > lo ? hipMemcpyAsync(base[buf] + lo, h + lo, hi - lo, hipMemcpyHostToDevice, cs) : hipSuccess;
+        if (hi <= lo)
+            return hipSuccess;
+        if (pageable)
+            return copy_staged(base[buf] + lo, h + lo, hi - lo);
+        return hipMemcpyAsync(base[buf] + lo, h + lo, hi - lo, hipMemcpyHostToDevice, cs);
     };
     // once a copy is queued, an error return first drains both streams: no
     // copy may still read the caller's memory after the call returns
@@ -1014,12 +1065,12 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         const uint32_t i1 = (uint32_t)std::min<uint64_t>(n, (uint64_t)ch[k].b1 * kSpanBlock);
         if (i1 <= i0)
             continue;
-        // the host saw the order: segments out of offset order go straight to
-        // the per-range kernel (tcsum_batch's SHUFFLED), not the packed stream,
-        // whose workgroups would each find out and sum range by range
+        // the host saw the order: segments out of offset order take
+        // tcsum_batch's SHUFFLED route (the per-range kernel unless the
+        // packed kernel's range-by-range path is the faster)
         tcsum::Geometry g = tcsum::pick_geometry(mean_of(ch[k].sp.bytes, i1 - i0));
-        if (!ch[k].sp.ordered && tcsum::knob(tcsum::KNOB_PACKED) != 1)
-            g.packed = 0;
+        if (!ch[k].sp.ordered)
+            tcsum::shuffled_route(g, tcsum::knob(tcsum::KNOB_PACKED));
         const hipError_t e = tcsum::launch_segments(tcsum::MODE_SEG, g, base[ch[k].buf], c.d_descs + i0, i1 - i0,
                                                     c.d_out + i0, 1u, ks);
         if (e != hipSuccess)
@@ -1724,7 +1775,7 @@ int release_ctx(Ctx &c, int dev)
     c.d_descs = nullptr;
     c.d_out = nullptr;
     c.d_arena_cap = c.d_descs_cap = c.d_out_cap = 0;
-    for (Pinned *q : {&c.q_desc, &c.q_res, &c.q_arena}) {
+    for (Pinned *q : {&c.q_desc, &c.q_res, &c.q_arena, &c.q_page[0], &c.q_page[1], &c.q_page[2]}) {
         if (q->h)
             (void)tcsum::quiet(hipHostFree(q->h));
         q->h = q->d = nullptr;

@@ -725,14 +725,16 @@ __device__ __forceinline__ void desc_span(const void *__restrict__ descs, uint32
 
 // The per-range path for a workgroup whose ranges are not one region:
 // groups of G lanes, G the widest power of two with one group per range.
-template <int MODE, int G, int UL = 4>
+// HAVE0: the lane's first range's descriptor may have been read already
+// (e0, when have0: k_segments_pk's scalar reads, K <= 32)
+template <int MODE, int G, int UL = 4, bool HAVE0 = false>
 __device__ __forceinline__ void pk_ranges(const uint8_t *__restrict__ arena, const void *__restrict__ descs,
                                           uint16_t *__restrict__ out, uint32_t aux, uint32_t first, uint32_t kw,
-                                          uint32_t T)
+                                          uint32_t T, const SegDesc &e0, bool have0)
 {
     const uint32_t t = threadIdx.x, gl = t & (G - 1u);
     for (uint32_t r = t / G; r < kw; r += T / G) {
-        const SegDesc e = load_desc<MODE>(descs, first + r, true);
+        const SegDesc e = HAVE0 && have0 && r == t / G ? e0 : load_desc<MODE>(descs, first + r, true);
         uint32_t q = 0;
         uint32_t acc = sum_range<G, UL, false>(arena, e.off, e.len, gl, [&] {
             if constexpr (MODE == MODE_PESO)
@@ -745,13 +747,61 @@ __device__ __forceinline__ void pk_ranges(const uint8_t *__restrict__ arena, con
 }
 
 constexpr uint32_t kPkMaxPasses = 64; // longer regions go range by range
+constexpr uint32_t kPkEarly = 1u << 7; // aux: the range-by-range path's descriptors by scalar loads (pk_wave_descs)
+
+// Lanes per range on k_segments_pk's range-by-range path for kw ranges.
+__device__ __forceinline__ uint32_t pk_group(uint32_t T, uint32_t kw)
+{
+    const uint32_t lanes_per = T / kw;
+    return lanes_per >= 64 ? 64u : lanes_per >= 32 ? 32u : lanes_per >= 16 ? 16u : 8u;
+}
+
+// The descriptors of this wave's PER lane groups' ranges (k_segments_pk's
+// range-by-range path, 64 / PER lanes per group), read with scalar loads --
+// all issued before any is used -- and each group's own picked into x.
+// Ranges past kw read the workgroup's last descriptor (a group past kw takes
+// no range).
+template <int MODE, uint32_t PER>
+__device__ __forceinline__ void pk_wave_descs(const void *__restrict__ descs, uint32_t first, uint32_t kw,
+                                              uint32_t (&x)[6])
+{
+    constexpr uint32_t DW = MODE == MODE_PESO ? 6u : 4u; // dwords per descriptor
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t gi = (threadIdx.x & 63u) / (64u / PER);
+    uint32_t sd[PER][DW];
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        const uint32_t r = wv * PER + j < kw ? wv * PER + j : kw - 1u;
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(descs) + (uint64_t)DW * (first + r);
+#pragma unroll
+        for (uint32_t i = 0; i < DW; ++i)
+            sd[j][i] = q[i];
+    }
+    // pinned in scalar registers: otherwise the compiler folds the per-group
+    // choice into one vector load from a chosen address -- the L2 round trip
+    // this is here to avoid
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j)
+#pragma unroll
+        for (uint32_t i = 0; i < DW; ++i)
+            asm volatile("" : "+s"(sd[j][i]));
+#pragma unroll
+    for (uint32_t i = 0; i < DW; ++i) {
+        uint32_t v = sd[0][i];
+#pragma unroll
+        for (uint32_t j = 1; j < PER; ++j)
+            v = gi == j ? sd[j][i] : v;
+        x[i] = v;
+    }
+}
 
 // A workgroup of k_segments_pk whose kw ranges are not one region: G lanes
-// per range, G the widest power of two that gives every range a group.
+// per range, G the widest power of two that gives every range a group
+// (pk_group).  e0: this lane's first range's descriptor when have0.
 template <int MODE>
 __device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, const void *__restrict__ descs,
                                             uint16_t *__restrict__ out, uint32_t aux, uint32_t first, uint32_t kw,
-                                            uint32_t T)
+                                            uint32_t T, const SegDesc &e0, bool have0)
 {
     // K was chosen so that K mean-length ranges fill a 12-KiB pass: a range is
     // about 12 KiB / K, and each group's pass is sized to hold one (32 x 3 =
@@ -759,15 +809,15 @@ __device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, c
     // ranges of 576 B)
     const uint32_t lanes_per = T / kw;
     if (lanes_per >= 64)
-        pk_ranges<MODE, 64>(arena, descs, out, aux, first, kw, T);
+        pk_ranges<MODE, 64, 4, true>(arena, descs, out, aux, first, kw, T, e0, have0);
     else if (lanes_per >= 32)
-        pk_ranges<MODE, 32, 3>(arena, descs, out, aux, first, kw, T);
+        pk_ranges<MODE, 32, 3, true>(arena, descs, out, aux, first, kw, T, e0, have0);
     else if (lanes_per >= 16)
-        pk_ranges<MODE, 16, 6>(arena, descs, out, aux, first, kw, T);
+        pk_ranges<MODE, 16, 6, true>(arena, descs, out, aux, first, kw, T, e0, have0);
     else if (kw <= 32u)
-        pk_ranges<MODE, 8, 6>(arena, descs, out, aux, first, kw, T);
+        pk_ranges<MODE, 8, 6, true>(arena, descs, out, aux, first, kw, T, e0, have0);
     else
-        pk_ranges<MODE, 8>(arena, descs, out, aux, first, kw, T);
+        pk_ranges<MODE, 8>(arena, descs, out, aux, first, kw, T, e0, have0);
 }
 
 
@@ -818,7 +868,36 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
         if (const uint32_t pfd = aux >> 8; pfd != 0u && w == 0) // wave-uniform
             pf = prefetch_descs(descs, (uint64_t)(blk + pfd) * K, n, MODE == MODE_PESO ? 24u : 16u,
                                 (K * (MODE == MODE_PESO ? 24u : 16u) + 127u) / 128u + 1u, lane);
-        pk_fallback<MODE>(arena, descs, out, aux, first, kw, T);
+        // aux bit 7 (debug knob "pk_early"), K <= 32 (one range per lane
+        // group): each wave reads the descriptors of its lane groups' ranges
+        // with scalar loads -- lines the span's loads just brought into the
+        // scalar cache -- instead of every lane's vector load going to the L2
+        // for them, and each group picks its own
+        const uint32_t G = pk_group(T, kw);
+        const bool early = (aux & kPkEarly) != 0u && kw <= 32u; // workgroup-uniform
+        SegDesc e0{0, 0, 0, 0, 0, 0};
+        if (early) {
+            uint32_t x[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+            // per = 64 / G ranges per wave, every load issued before any is used
+            if (G == 64u)
+                pk_wave_descs<MODE, 1>(descs, first, kw, x);
+            else if (G == 32u)
+                pk_wave_descs<MODE, 2>(descs, first, kw, x);
+            else if (G == 16u)
+                pk_wave_descs<MODE, 4>(descs, first, kw, x);
+            else
+                pk_wave_descs<MODE, 8>(descs, first, kw, x);
+            e0.off = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
+            e0.len = x[2];
+            if constexpr (MODE == MODE_PESO) {
+                e0.src = x[3];
+                e0.dst = x[4];
+                e0.proto = x[5] & 0xFFu;
+            } else {
+                e0.pre = x[3];
+            }
+        }
+        pk_fallback<MODE>(arena, descs, out, aux, first, kw, T, e0, early);
         if (pf == 0x9E3779B9u && K == 0u) // never: keeps the prefetch load alive
             out[0] = (uint16_t)pf;
         return;
@@ -936,7 +1015,8 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
             __syncthreads(); // the next pass overwrites dat / ex / subtot
     }
     if (ranges) { // a range outside the region, found by the descriptor check
-        pk_fallback<MODE>(arena, descs, out, aux, first, kw, T);
+        // (e0 is not carried here: it would stay live through the region path)
+        pk_fallback<MODE>(arena, descs, out, aux, first, kw, T, SegDesc{0, 0, 0, 0, 0, 0}, false);
         return;
     }
     if (mine)
@@ -1207,9 +1287,12 @@ __device__ __forceinline__ void ip_finish(const IpHdr &ih, uint32_t fl, bool big
 // SKEW (measurement): the data pass starts SKEW bytes past the packet's
 // 128-B line instead of on it, for packets that start that far in (0: the
 // route)
-// DB (measurement): each later pass's loads are issued before the previous
-// pass is summed (two passes in flight per lane group, more registers).
-template <int G, int U, int IPM, int SKEW = 0, bool DB = false>
+// PIPE (measurement): 1 = each later pass's loads are issued before the
+// previous pass is summed (two passes in flight per lane group, more
+// registers); 2 = rolling -- each load slot is reissued for the next pass as
+// soon as its chunk is taken, so a multi-pass packet keeps U loads in flight
+// per lane with no more registers than one pass.
+template <int G, int U, int IPM, int SKEW = 0, int PIPE = 0>
 __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                             uint32_t pk, uint32_t n, uint32_t *__restrict__ out,
                                             uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
@@ -1339,7 +1422,43 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
         acc_h += ph; // header <= 60 bytes: no overflow
         acc_l = fold_step(acc_l + pl);
     };
-    if constexpr (DB) {
+    if constexpr (PIPE == 2) {
+        for (uint32_t b0 = 0; b0 < dch; b0 += G * U) {
+            const bool more = b0 + G * U < dch; // group-uniform
+            uint32_t ph = 0, pl = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const u32x4 x = v[u];
+                { // unconditional (the last pass reloads its last chunk): a branch here
+                  // makes the compiler wait for every load in flight at the join
+                    const uint32_t nidx = more ? b0 + G * U + u * G + gl : dlast;
+                    v[u] = load16<true>(dbase + (nidx < dch ? nidx : dlast));
+                }
+                const uint32_t idx = b0 + u * G + gl;
+                const bool valid = idx < dch;
+                const int c = (int)(16u * idx);
+                const bool inner = valid && c >= h_end && c + 16 <= l_end && (f0 + 2 <= c || f0 >= c + 16);
+                if (valid && !inner) {
+                    uint32_t th = region_sum(x, c, (int)sl, h_end);
+                    uint32_t tl4 = region_sum(x, c, h_end, l_end);
+                    if (field_on) {
+                        const uint32_t tf = region_sum(x, c, f0, f0 + 2);
+                        if (IPM == IP_TX)
+                            tl4 -= tf;
+                        else
+                            acc_f += tf;
+                    }
+                    if (IPM == IP_TX)
+                        th -= region_sum(x, c, i0, i0 + 2);
+                    ph += th;
+                    pl += tl4;
+                }
+                pl = chunk_sum_w(pl, x, inner ? 0x00010001u : 0u);
+            }
+            acc_h += ph;
+            acc_l = fold_step(acc_l + pl);
+        }
+    } else if constexpr (PIPE == 1) {
         u32x4 nx[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1381,15 +1500,15 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
                        verdict_out, opts);
 }
 
-template <int G, int U, int IPM, int T = 256, int SKEW = 0>
+template <int G, int U, int IPM, int T = 256, int SKEW = 0, int PIPE = 0>
 __global__ __launch_bounds__(T) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                             uint32_t n, uint32_t *__restrict__ out,
                                             uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
                                             uint32_t opts, uint32_t xg)
 {
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
-    ipv4_packet<G, U, IPM, SKEW>(arena, pkts, blk * (uint32_t)(T / G) + threadIdx.x / G, n, out, flags_out, verdict_out,
-                           opts); // no 32-bit wrap for any n
+    ipv4_packet<G, U, IPM, SKEW, PIPE>(arena, pkts, blk * (uint32_t)(T / G) + threadIdx.x / G, n, out, flags_out,
+                                       verdict_out, opts); // no 32-bit wrap for any n
 }
 
 // k_ipv4 with two data passes in flight per lane group (measurement)
@@ -1400,7 +1519,7 @@ __global__ __launch_bounds__(256) void k_ipv4_db(uint8_t *__restrict__ arena, co
                                                  uint32_t opts, uint32_t xg)
 {
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
-    ipv4_packet<G, U, IPM, 0, true>(arena, pkts, blk * (256u / G) + threadIdx.x / G, n, out, flags_out, verdict_out,
+    ipv4_packet<G, U, IPM, 0, 1>(arena, pkts, blk * (256u / G) + threadIdx.x / G, n, out, flags_out, verdict_out,
                                     opts);
 }
 
@@ -1435,13 +1554,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC ? OCC :
 
 // k_ipv4 held to OCC waves per SIMD (the sums form takes 66 VGPRs, i.e. 7
 // waves; rx 74, 6): measurement (libtcsum_bench.so, tcsum_probe_ipv4_shape)
-template <int G, int U, int IPM, int OCC>
+template <int G, int U, int IPM, int OCC, int PIPE = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void k_ipv4_occ(
     uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts, uint32_t n, uint32_t *__restrict__ out,
     uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out, uint32_t opts, uint32_t xg)
 {
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
-    ipv4_packet<G, U, IPM>(arena, pkts, blk * (256u / G) + threadIdx.x / G, n, out, flags_out, verdict_out, opts);
+    ipv4_packet<G, U, IPM, 0, PIPE>(arena, pkts, blk * (256u / G) + threadIdx.x / G, n, out, flags_out, verdict_out,
+                                    opts);
 }
 
 // The deferred tx stores (IP_OPT_DEFER): one lane per packet writes the values

@@ -350,6 +350,16 @@ static uint32_t pf_dist()
     return v < 0 ? 2048u : (uint32_t)(v < (1 << 23) ? v : (1 << 23) - 1);
 }
 
+// k_segments_pk's range-by-range path reads its descriptors with scalar
+// loads (debug knob "pk_early", on unless 0): one-box A/B, descriptors
+// shuffled, against the vector loads: 1500-B ranges 0.940x, ragged
+// 64..2936 B 0.939x, 4000 B 0.960x, 576 B 0.977x; packed layouts 1.000-1.004x
+// (profiles/r05/pk_early/pk_early6.txt)
+bool pk_early()
+{
+    return knob(KNOB_PK_EARLY) != 0;
+}
+
 // The per-range kernel's descriptor prefetch distance (debug knob
 // "pf_range"; 0 = off, the default while unmeasured)
 static uint32_t pf_range()
@@ -417,7 +427,7 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
                                                                           : kPkMaxRanges * kPkWaves;
         const uint8_t *a = static_cast<const uint8_t *>(arena);
         const dim3 gr((n + K - 1) / K), bl(kPkWaves * 64);
-        const uint32_t ax = aux | (pf_dist() << 8);
+        const uint32_t ax = aux | (pf_dist() << 8) | (pk_early() ? kPkEarly : 0u);
         if (mode == MODE_SEG)
             return launch(k_segments_pk<MODE_SEG>, gr, bl, 0, stream, a, descs, n, out, ax, (uint32_t)g.xcd, K);
         return launch(k_segments_pk<MODE_PESO>, gr, bl, 0, stream, a, descs, n, out, ax, (uint32_t)g.xcd, K);

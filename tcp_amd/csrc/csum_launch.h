@@ -59,12 +59,27 @@ enum Knob : int {
     KNOB_COPY_THREADS, // host threads of a parallel gather / scatter pass (16)
     KNOB_PF_DIST,      // descriptor prefetch distance of k_segments_pk's range-by-range path (2048)
     KNOB_PF_RANGE,     // descriptor prefetch distance of the per-range kernels k_segments (0)
+    KNOB_PK_EARLY,     // 0 / 1: k_segments_pk's range-by-range path reads its descriptors with scalar loads (1)
+    KNOB_PAGE_STAGE,   // 0 / 1: tcsum_host_batch_peso copies a pageable arena through its own pinned slots (1)
     KNOB_COUNT
 };
 int64_t knob(Knob k);
 void set_knob(Knob k, int64_t v);
 
 Geometry pick_geometry(uint64_t mean_len);
+
+// Whether k_segments_pk's range-by-range path reads its descriptors with
+// scalar loads (debug knob "pk_early"; on by default).
+bool pk_early();
+
+// The route for ranges known to be out of offset order: the packed kernel
+// only where its range-by-range path beats the per-range kernels (K <= 8,
+// i.e. ranges of ~1.5 KiB and up, with pk_early), else the per-range kernel.
+inline void shuffled_route(Geometry &g, int64_t packed_knob)
+{
+    if (packed_knob != 1 && !(g.packed > 0 && g.packed <= 8 && pk_early()))
+        g.packed = 0;
+}
 
 // aux: MODE_SEG -> complement; MODE_EXACT -> complement | (offset parity << 1).
 hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void *descs,

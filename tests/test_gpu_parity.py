@@ -789,6 +789,20 @@ def test_host_batch_end_to_end(tc, oracle, knobs, order, chunk_mb):
     np.testing.assert_array_equal(out, oracle.batch_peso(host, d, nthreads=8))
 
 
+@pytest.mark.parametrize("order", ["offset", "permuted"])
+def test_host_batch_pageable_staging(tc, oracle, order):
+    """A pageable arena crosses through the context's three 32-MiB pinned
+    slots -- 150 MB, so every slot is refilled after its copy-done event.
+    (The runtime's own pageable copy, debug knob page_stage = 0, is not run
+    here: DESIGN.md §5.)"""
+    from tcp_amd import workload
+    b = workload.make_batch("mtu", n=100000)
+    host = oracle.synth_fill(b.byte_base, b.alloc_bytes, b.seed)
+    d = b.descs[np.random.default_rng(8).permutation(b.n)] if order == "permuted" else b.descs
+    out = tc.host_batch_peso(host, d)
+    np.testing.assert_array_equal(out, oracle.batch_peso(host, d, nthreads=8))
+
+
 @pytest.mark.parametrize("case", ["late_low", "rest_empty", "lead_sparse", "chunks"])
 def test_host_batch_lead_and_rest(tc, oracle, knobs, case):
     """The host batch's lead (its first 64 MiB of segments, copied before the

@@ -5,7 +5,8 @@ change a result or read past the descriptor array: both
 descriptor layouts (checksum_peso, pktbuf_checksum16) against the oracle,
 packed, shuffled, TSO-sized and K = 8 batches, distances from 1 to far past
 the grid, descriptor arrays at the end of their allocation; and the IPv4
-kernels, which must be unaffected by the knob."""
+kernels, which must be unaffected by the knob.  Also the same path's scalar
+descriptor reads (debug knob "pk_early") for every group width."""
 import numpy as np
 import pytest
 
@@ -69,8 +70,8 @@ def test_peso_batches_with_prefetch(tc, torch, oracle, pf, layout):
         gs = tc.batch_segments(arena, _descs_at_end(torch, tc, segs), n, 1, int(lens.sum())).cpu().numpy()
     np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(gs, oracle.batch_segments(host, segs, 1, nthreads=8))
-    # the per-range kernels (the SHUFFLED route) with their own prefetch knob
-    with tc.debug(pf_range=pf):
+    # the per-range kernels (the SHUFFLED route for short ranges) with their own prefetch knob
+    with tc.debug(pf_range=pf, packed=0):
         gr, _, _ = tc.batch(tc.OP_PESO, arena, d, n, total_bytes=int(lens.sum()), layout=tc.LAYOUT_SHUFFLED)
     np.testing.assert_array_equal(gr.cpu().numpy(), want)
 
@@ -97,3 +98,51 @@ def test_ipv4_batches_with_prefetch(tc, torch, oracle, pf):
     np.testing.assert_array_equal(out.cpu().numpy(), eo)
     np.testing.assert_array_equal(fl.cpu().numpy(), ef)
     np.testing.assert_array_equal(v.cpu().numpy(), ev)
+
+
+EARLY_LAYOUTS = ["packed", "shuffled", "mtu", "wide", "tail", "mid", "small", "tiny"]
+
+
+@pytest.mark.parametrize("early", [1, 0])
+@pytest.mark.parametrize("layout", EARLY_LAYOUTS)
+def test_pk_early_descriptors(tc, torch, oracle, layout, early):
+    """debug "pk_early" (default 1): a packed-kernel workgroup on its
+    range-by-range path (K <= 32) reads its ranges' descriptors with scalar
+    loads, each lane group picking its own (0: vector loads); both descriptor layouts, a last workgroup with fewer
+    ranges (tail), K = 3 (wide: 64-lane groups), 8 (32), ~12 (mid: 16),
+    ~21 (small: 8), ~190 (tiny: K > 32, not covered: vector loads), shuffled
+    and packed, against the oracle."""
+    rng = np.random.default_rng(77 + EARLY_LAYOUTS.index(layout))
+    if layout == "mid":
+        n, lens = 15013, rng.integers(800, 1200, 15013)
+    elif layout == "small":
+        n, lens = 30011, np.full(30011, 576)
+    elif layout == "tiny":
+        n, lens = 60013, rng.integers(1, 128, 60013)
+    elif layout == "mtu":
+        n, lens = 8 * 1001, np.full(8 * 1001, 1500)
+    elif layout == "wide":  # ~4 KiB ranges: K = 3, one 64-lane group per range
+        n, lens = 3001, rng.integers(3500, 4500, 3001)
+    elif layout == "tail":
+        n, lens = 8 * 997 + 3, np.full(8 * 997 + 3, 1500)
+    else:
+        n = 20011
+        lens = rng.integers(1000, 2000, n)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64) + 5
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    p = np.zeros(n, tc.PESO_DTYPE)
+    p["offset"], p["len"] = offs, lens
+    p["src"] = rng.integers(0, 256, (n, 4))
+    p["dst"] = rng.integers(0, 256, (n, 4))
+    p["protocol"] = rng.choice([6, 17], n)
+    if layout in ("shuffled", "wide", "tail", "mid", "small", "tiny"):
+        p = p[rng.permutation(n)]
+    want = oracle.batch_peso(host, p, nthreads=8)
+    arena = torch.from_numpy(host).cuda()
+    segs = np.zeros(n, tc.SEG_DTYPE)
+    segs["offset"], segs["len"], segs["pre_sum"] = p["offset"], p["len"], rng.integers(0, 1 << 17, n)
+    with tc.debug(pk_early=early, packed=1):
+        got = tc.batch_peso(arena, _descs_at_end(torch, tc, p), n, int(lens.sum())).cpu().numpy()
+        gs = tc.batch_segments(arena, _descs_at_end(torch, tc, segs), n, 1, int(lens.sum())).cpu().numpy()
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(gs, oracle.batch_segments(host, segs, 1, nthreads=8))

@@ -22,6 +22,7 @@ SKEW_ONLY = "--skew" in sys.argv
 DB_ONLY = "--db" in sys.argv  # two data passes in flight, with and without the descriptor prefetch
 DYN_ONLY = "--dyn" in sys.argv  # packets handed out inside the workgroup (k_ipv4_dyn), M per lane group
 ROLL_ONLY = "--roll" in sys.argv  # rolling load slots: a multi-pass packet keeps its loads in flight
+HDRX_ONLY = "--hdrx" in sys.argv  # header chunks shuffled from the first data pass instead of loaded
 for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mixed_aligned", "mixed_rx"]):
     b = workload.make_batch(cfg)
     arena, descs = workload.materialize(b)
@@ -57,7 +58,9 @@ for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mi
                 f(o, v)
         return g
 
-    if ROLL_ONLY:
+    if HDRX_ONLY:
+        kinds.update({"header from the data pass": shape(256, 600)})
+    elif ROLL_ONLY:
         kinds.update({"rolling slots": shape(256, 500), "rolling, 4 loads": shape(256, 504),
                       "rolling, held to the route's waves/SIMD": shape(256, 506 if rx else 507)})
         if rx:

@@ -1291,7 +1291,8 @@ __device__ __forceinline__ void ip_finish(const IpHdr &ih, uint32_t fl, bool big
 // previous pass is summed (two passes in flight per lane group, more
 // registers); 2 = rolling -- each load slot is reissued for the next pass as
 // soon as its chunk is taken, so a multi-pass packet keeps U loads in flight
-// per lane with no more registers than one pass.
+// per lane with no more registers than one pass; 3 = no header loads, the
+// header chunks taken from the lanes whose first data-pass load holds them.
 template <int G, int U, int IPM, int SKEW = 0, int PIPE = 0>
 __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                             uint32_t pk, uint32_t n, uint32_t *__restrict__ out,
@@ -1323,16 +1324,20 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     // loads the same chunks: no different in time or traffic,
     // profiles/r02/ab_hdr_nt_*.txt)
     auto hload = [](const u32x4 *q) { return load16<false>(q); };
-    const u32x4 h0 = hload(hb);
-    const u32x4 h1 = hload(hb + h1i);
-    u32x4 h2, c2 = u32x4(0u), c3 = u32x4(0u);
-    if constexpr (IPM == IP_RX) {
+    u32x4 h0 = u32x4(0u), h1 = u32x4(0u), h2 = u32x4(0u), c2 = u32x4(0u), c3 = u32x4(0u);
+    if constexpr (PIPE == 3) {
+        // (PIPE 3: no header loads -- the chunks come from the data pass below)
+    } else if constexpr (IPM == IP_RX) {
+        h0 = hload(hb);
+        h1 = hload(hb + h1i);
         // chunks 2 and 3 as well: an IHL-5 packet's TCP/UDP ports, data offset
         // and flags (L4 bytes 0-3, 12-13) lie in chunks 1..3
         c2 = hload(nch > 2 ? base + 2 : &g_zero_chunk);
         c3 = hload(nch > 3 && s0 >= 12 ? base + 3 : &g_zero_chunk);
         h2 = s0 > 12 ? c2 : u32x4(0u);
     } else {
+        h0 = hload(hb);
+        h1 = hload(hb + h1i);
         const u32x4 h2v = hload(hb + (big_enough ? (s0 > 12 ? 2u : 1u) : 0u));
         h2 = s0 > 12 ? h2v : u32x4(0u);
     }
@@ -1360,6 +1365,31 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
         v[u] = load16<true>(dbase + (idx < dch ? idx : dlast));
     }
     issue_fence();
+    if constexpr (PIPE == 3) {
+        // the header chunks from the lanes of the group whose first-pass load
+        // holds them: packet chunk j is pass chunk (sl >> 4) + j <= 10 < G,
+        // i.e. load 0 of lane (sl >> 4) + j; zero past the packet
+        static_assert(G >= 16 && SKEW == 0, "the header chunks lie in the first 11 lanes of the group");
+        const int gb = (int)((threadIdx.x & 63u) & ~(uint32_t)(G - 1));
+        auto hc = [&](uint32_t j) {
+            const int src = gb + (int)((sl >> 4) + j);
+            u32x4 r;
+            r.x = (uint32_t)__shfl((int)v[0].x, src, 64);
+            r.y = (uint32_t)__shfl((int)v[0].y, src, 64);
+            r.z = (uint32_t)__shfl((int)v[0].z, src, 64);
+            r.w = (uint32_t)__shfl((int)v[0].w, src, 64);
+            return j < nch ? r : u32x4(0u);
+        };
+        h0 = hc(0);
+        h1 = hc(1);
+        if constexpr (IPM == IP_RX) {
+            c2 = hc(2);
+            c3 = s0 >= 12 ? hc(3) : u32x4(0u);
+            h2 = s0 > 12 ? c2 : u32x4(0u);
+        } else {
+            h2 = s0 > 12 ? hc(2) : u32x4(0u);
+        }
+    }
 
     const Hdr5 hd = header_dwords(h0, h1, h2, s0);
     // rx: the TCP/UDP header words (L4 bytes 0-3: ports; 12-15: data offset,

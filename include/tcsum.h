@@ -242,7 +242,9 @@ int tcsum_batch_ipv4_rx_verify(const void *arena /*[dev]*/, const tcsum_pkt_t *p
  * stream; each chunk's kernel on a second stream behind that chunk's copy) ->
  * tcsum_batch_peso -> D2H of the results; returns after the results are in
  * host_out.  host_arena should come from tcsum_host_alloc (pinned) for full
- * PCIe rate.  Segments may be in any order (in offset order the copies and
+ * PCIe rate; a pageable host_arena crosses through the library's own pinned
+ * slots (the host threads copy, the copy engine reads only memory the
+ * library owns: ~0.96 of the pinned rate).  Segments may be in any order (in offset order the copies and
  * kernels pipeline; otherwise the batch's byte span is copied once).  The
  * first ~64 MiB of segments are checked before anything else; a bad segment
  * after them is found while their copy runs (the call drains it and returns

@@ -24,9 +24,21 @@ def tc():
     return tcp_amd
 
 
+# Every buffer a test has registered stays allocated for the rest of the
+# process after it is unregistered, so its pages are never handed to a later
+# array.  Three suites (rounds 4 and 5) stopped on hipErrorIllegalAddress from
+# the runtime's own pageable host-to-device copy -- twice in
+# tcsum_host_batch_peso's first copy right after a registered fuzz case, once
+# in a torch .cuda() of a fresh 2-MB array some tests after this file's
+# registered cases -- with no kernel in flight; a freed, once-registered range
+# handed to a new array is the one thing they share.
+_RETIRED = []
+
+
 class _Registered:
     """Pageable memory pinned in place with tcsum_host_register (the way the
-    stack would pin its static block pool, pktbuf.c:13); unpinned on release."""
+    stack would pin its static block pool, pktbuf.c:13); unpinned on release,
+    its pages then kept (_RETIRED)."""
 
     def __init__(self, tc, n):
         self.tc = tc
@@ -40,6 +52,7 @@ class _Registered:
             self.tc.host_unregister(self.region)
         except Exception:
             pass
+        _RETIRED.append(self.raw)
 
 
 def host_copy(tc, data: np.ndarray, where: str, shift: int = 0):

@@ -982,7 +982,10 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         (void)tcsum::quiet(hipStreamSynchronize(cs));
         return code;
     };
-    auto fail_sys = [&](int step, hipError_t e) { return fail(note_sys(step, e)); };
+    // (a pinned staging slot that cannot be allocated is TCSUM_ERR_MEM)
+    auto fail_sys = [&](int step, hipError_t e) {
+        return fail(e == hipErrorOutOfMemory ? note_mem(step, e) : note_sys(step, e));
+    };
     if (pl.early) {
         if (const hipError_t e = grow(c.d_lead, c.d_lead_cap, span_bytes(pl.lead)); e != hipSuccess)
             return note_mem(13, e);

@@ -108,8 +108,8 @@ int tcsum_debug_shards(tcsum_shard_stat_t *out, int max);
 
 /* The route a batch call would take for a mean range length, with the knobs
  * applied: out[0] lanes, out[1] loads, out[2] xcd, out[3] packed K (0 = off),
- * out[4] reserved (0; round 4's byte-window stream is libtcsum_bench.so's
- * tcsum_flat_ipv4 since round 5).  libtcsum_bench.so's probes follow it. */
+ * out[4] the packed K a TCSUM_LAYOUT_SHUFFLED batch of that mean takes (0:
+ * the per-range kernel).  libtcsum_bench.so's probes follow it. */
 void tcsum_debug_route(uint64_t mean_len, int32_t out[5]);
 
 #ifdef __cplusplus

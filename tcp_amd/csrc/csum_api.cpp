@@ -520,7 +520,9 @@ void tcsum_debug_route(uint64_t mean_len, int32_t out[5])
         out[1] = g.loads;
         out[2] = g.xcd;
         out[3] = g.packed;
-        out[4] = 0; // reserved (round 4's byte-window stream: libtcsum_bench.so)
+        Geometry s = g; // what a SHUFFLED batch (or a host chunk out of offset order) takes
+        tcsum::shuffled_route(s, tcsum::knob(tcsum::KNOB_PACKED));
+        out[4] = s.packed;
     }
 }
 

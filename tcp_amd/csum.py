@@ -423,10 +423,11 @@ def pick_geometry(mean_len: int):
 
 def route(mean_len: int) -> dict:
     """The route the batch calls take for a mean range length (debug knobs
-    applied): lanes, loads, xcd, packed K (0 = off) (tcsum_debug_route)."""
+    applied): lanes, loads, xcd, packed K (0 = off), and the packed K of a
+    SHUFFLED batch (0 = the per-range kernel) (tcsum_debug_route)."""
     r = (ctypes.c_int32 * 5)()
     _lib.lib().tcsum_debug_route(mean_len, r)
-    return dict(zip(("lanes", "loads", "xcd", "packed"), list(r)[:4]))
+    return dict(zip(("lanes", "loads", "xcd", "packed", "shuffled_packed"), list(r)))
 
 
 def flat_ipv4(mode: int, arena, pkts, n: int, total_bytes: int, out=None, flags=None, verdict=None, stream=None):

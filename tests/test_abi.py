@@ -121,6 +121,21 @@ def test_product_reads_only_deployment_variables(libpath):
     assert names <= {b"TCSUM_DEVICE", b"TCSUM_CALL_SERVER"}, names
 
 
+def test_shuffled_route(libpath):
+    """What a SHUFFLED batch (or a host chunk out of offset order) takes: the
+    packed kernel, whose range-by-range path reads its descriptors with
+    scalar loads, for K <= 8 ranges per workgroup (means from ~1.5 KiB), the
+    per-range kernel for shorter ranges and whenever that path is off."""
+    import tcp_amd as tc
+    assert tc.route(1500)["shuffled_packed"] == 8 and tc.route(4000)["shuffled_packed"] == 3
+    assert tc.route(576)["packed"] == 21 and tc.route(576)["shuffled_packed"] == 0
+    assert tc.route(65536)["shuffled_packed"] == 0  # no packed kernel at all (TSO shape)
+    with tc.debug(pk_early=0):
+        assert tc.route(1500)["packed"] == 8 and tc.route(1500)["shuffled_packed"] == 0
+    with tc.debug(packed=1):  # "packed" = 1 keeps the stream kernel for every SHUFFLED batch
+        assert tc.route(576)["shuffled_packed"] == 21
+
+
 def test_debug_knobs(libpath):
     import tcp_amd as tc
     assert tc.debug_get("lanes") == -1 and tc.debug_get("no_such_knob") == -2

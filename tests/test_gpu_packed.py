@@ -241,19 +241,27 @@ def test_packed_fuzz(tc, torch, oracle, seed):
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_segments(host, s, comp, nthreads=8))
 
 
-@pytest.mark.parametrize("layout", ["mtu", "shuffled", "ragged_gaps"])
+HINT_LAYOUTS = ["mtu", "shuffled", "ragged_gaps", "shuffled576", "shuffled4000"]
+
+
+@pytest.mark.parametrize("layout", HINT_LAYOUTS)
 def test_layout_hints_give_the_same_results(tc, torch, oracle, layout):
     """tcsum_batch's layout hint changes only the kernel, never a result --
-    also when the caller's ORDERED promise is false (a shuffled batch)."""
-    rng = np.random.default_rng(["mtu", "shuffled", "ragged_gaps"].index(layout) + 100)
+    also when the caller's ORDERED promise is false (a shuffled batch).
+    SHUFFLED takes the packed kernel for ~1.5-KiB-and-up ranges (K <= 8) and
+    the per-range kernel below (shuffled576)."""
+    rng = np.random.default_rng(HINT_LAYOUTS.index(layout) + 100)
     n = 20000
-    lens = np.full(n, 1500, np.int64) if layout != "ragged_gaps" else rng.integers(1, 3000, n)
+    if layout.startswith("shuffled") and layout != "shuffled":
+        lens = np.full(n, int(layout[len("shuffled"):]), np.int64)
+    else:
+        lens = np.full(n, 1500, np.int64) if layout != "ragged_gaps" else rng.integers(1, 3000, n)
     offs = _packed_offs(lens, 5).astype(np.int64)
     if layout == "ragged_gaps":
         offs += np.cumsum(rng.integers(0, 40, n))
     host = _arena(rng, int(offs.max() + lens.max()) + 4096)
     p = _peso(tc, offs.astype(np.uint64), lens.astype(np.uint32), rng)
-    if layout == "shuffled":
+    if layout.startswith("shuffled"):
         p = p[rng.permutation(n)]
     want = oracle.batch_peso(host, p, nthreads=8)
     arena = torch.from_numpy(host).cuda()

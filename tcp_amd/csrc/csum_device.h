@@ -753,7 +753,7 @@ constexpr uint32_t kPkEarly = 1u << 7; // aux: the range-by-range path's descrip
 __device__ __forceinline__ uint32_t pk_group(uint32_t T, uint32_t kw)
 {
     const uint32_t lanes_per = T / kw;
-    return lanes_per >= 64 ? 64u : lanes_per >= 32 ? 32u : lanes_per >= 16 ? 16u : 8u;
+    return lanes_per >= 64 ? 64u : lanes_per >= 32 ? 32u : lanes_per >= 16 || kw <= 22u ? 16u : 8u;
 }
 
 // The descriptors of this wave's PER lane groups' ranges (k_segments_pk's
@@ -812,8 +812,14 @@ __device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, c
         pk_ranges<MODE, 64, 4, true>(arena, descs, out, aux, first, kw, T, e0, have0);
     else if (lanes_per >= 32)
         pk_ranges<MODE, 32, 3, true>(arena, descs, out, aux, first, kw, T, e0, have0);
+    else if (lanes_per >= 16 && kw >= 12u) // ranges of ~1 KiB and less: 1-KiB passes
+        pk_ranges<MODE, 16, 4, true>(arena, descs, out, aux, first, kw, T, e0, have0);
     else if (lanes_per >= 16)
         pk_ranges<MODE, 16, 6, true>(arena, descs, out, aux, first, kw, T, e0, have0);
+    else if (kw <= 22u) // 17..22 ranges of ~560..720 B: 16 lanes x 3 loads, a second round for the last few
+        pk_ranges<MODE, 16, 3, true>(arena, descs, out, aux, first, kw, T, e0, have0);
+    else if (kw >= 23u && kw <= 32u) // ~530 B and less: 512-B passes
+        pk_ranges<MODE, 8, 4, true>(arena, descs, out, aux, first, kw, T, e0, have0);
     else if (kw <= 32u)
         pk_ranges<MODE, 8, 6, true>(arena, descs, out, aux, first, kw, T, e0, have0);
     else

@@ -804,9 +804,11 @@ __device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, c
                                             uint32_t T, const SegDesc &e0, bool have0)
 {
     // K was chosen so that K mean-length ranges fill a 12-KiB pass: a range is
-    // about 12 KiB / K, and each group's pass is sized to hold one (32 x 3 =
-    // 1.5 KiB at K = 8; 16 x 6 for K = 9..16; 8 x 6 = 768 B for the 21
-    // ranges of 576 B)
+    // about 12 KiB / K, and each group's pass is sized to hold one, as the
+    // per-range kernel would size it (32 x 3 = 1.5 KiB at K = 8; 16 x 6 for
+    // K = 9..11, 16 x 4 = 1 KiB for 12..16, 16 x 3 = 768 B for 17..22 -- a
+    // second round for the ranges past 16 -- and 8 x 4 = 512 B for 23..32;
+    // profiles/r05/pk_early/pk_mid*.txt)
     const uint32_t lanes_per = T / kw;
     if (lanes_per >= 64)
         pk_ranges<MODE, 64, 4, true>(arena, descs, out, aux, first, kw, T, e0, have0);

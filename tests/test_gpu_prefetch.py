@@ -100,7 +100,7 @@ def test_ipv4_batches_with_prefetch(tc, torch, oracle, pf):
     np.testing.assert_array_equal(v.cpu().numpy(), ev)
 
 
-EARLY_LAYOUTS = ["packed", "shuffled", "mtu", "wide", "tail", "mid", "small", "tiny"]
+EARLY_LAYOUTS = ["packed", "shuffled", "mtu", "wide", "tail", "mid", "small", "tiny", "k17", "s400"]
 
 
 @pytest.mark.parametrize("early", [1, 0])
@@ -110,8 +110,9 @@ def test_pk_early_descriptors(tc, torch, oracle, layout, early):
     range-by-range path (K <= 32) reads its ranges' descriptors with scalar
     loads, each lane group picking its own (0: vector loads); both descriptor layouts, a last workgroup with fewer
     ranges (tail), K = 3 (wide: 64-lane groups), 8 (32), ~12 (mid: 16),
-    ~21 (small: 8), ~190 (tiny: K > 32, not covered: vector loads), shuffled
-    and packed, against the oracle."""
+    ~21 (small) and 17 (k17: 16 lanes, a second round for the last ranges),
+    ~30 (s400: 8 lanes x 4 loads), ~190 (tiny: K > 32, not covered: vector
+    loads), shuffled and packed, against the oracle."""
     rng = np.random.default_rng(77 + EARLY_LAYOUTS.index(layout))
     if layout == "mid":
         n, lens = 15013, rng.integers(800, 1200, 15013)
@@ -119,6 +120,10 @@ def test_pk_early_descriptors(tc, torch, oracle, layout, early):
         n, lens = 30011, np.full(30011, 576)
     elif layout == "tiny":
         n, lens = 60013, rng.integers(1, 128, 60013)
+    elif layout == "k17":
+        n, lens = 17 * 1003 + 9, rng.integers(650, 790, 17 * 1003 + 9)
+    elif layout == "s400":
+        n, lens = 40009, rng.integers(300, 500, 40009)
     elif layout == "mtu":
         n, lens = 8 * 1001, np.full(8 * 1001, 1500)
     elif layout == "wide":  # ~4 KiB ranges: K = 3, one 64-lane group per range
@@ -135,7 +140,7 @@ def test_pk_early_descriptors(tc, torch, oracle, layout, early):
     p["src"] = rng.integers(0, 256, (n, 4))
     p["dst"] = rng.integers(0, 256, (n, 4))
     p["protocol"] = rng.choice([6, 17], n)
-    if layout in ("shuffled", "wide", "tail", "mid", "small", "tiny"):
+    if layout in ("shuffled", "wide", "tail", "mid", "small", "tiny", "k17", "s400"):
         p = p[rng.permutation(n)]
     want = oracle.batch_peso(host, p, nthreads=8)
     arena = torch.from_numpy(host).cuda()

@@ -726,7 +726,9 @@ __device__ __forceinline__ void desc_span(const void *__restrict__ descs, uint32
 // The per-range path for a workgroup whose ranges are not one region:
 // groups of G lanes, G the widest power of two with one group per range.
 // HAVE0: the lane's first range's descriptor may have been read already
-// (e0, when have0: k_segments_pk's scalar reads, K <= 32)
+// (e0, when have0: k_segments_pk's scalar reads, K <= 32).  (Loading each
+// round's successor descriptor ahead, for K > 32, measured no gain:
+// profiles/r05/pk_early/pk_tiny3.txt.)
 template <int MODE, int G, int UL = 4, bool HAVE0 = false>
 __device__ __forceinline__ void pk_ranges(const uint8_t *__restrict__ arena, const void *__restrict__ descs,
                                           uint16_t *__restrict__ out, uint32_t aux, uint32_t first, uint32_t kw,
@@ -807,8 +809,8 @@ __device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, c
     // about 12 KiB / K, and each group's pass is sized to hold one, as the
     // per-range kernel would size it (32 x 3 = 1.5 KiB at K = 8; 16 x 6 for
     // K = 9..11, 16 x 4 = 1 KiB for 12..16, 16 x 3 = 768 B for 17..22 -- a
-    // second round for the ranges past 16 -- and 8 x 4 = 512 B for 23..32;
-    // profiles/r05/pk_early/pk_mid*.txt)
+    // second round for the ranges past 16 -- and 8 x 4 = 512 B for 23..64,
+    // 4 x 2 = 128 B for more; profiles/r05/pk_early/pk_mid*.txt, pk_tiny*.txt)
     const uint32_t lanes_per = T / kw;
     if (lanes_per >= 64)
         pk_ranges<MODE, 64, 4, true>(arena, descs, out, aux, first, kw, T, e0, have0);
@@ -824,8 +826,10 @@ __device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, c
         pk_ranges<MODE, 8, 4, true>(arena, descs, out, aux, first, kw, T, e0, have0);
     else if (kw <= 32u)
         pk_ranges<MODE, 8, 6, true>(arena, descs, out, aux, first, kw, T, e0, have0);
-    else
+    else if (kw <= 64u) // ~190..370 B: 8 lanes x 4 loads, two rounds
         pk_ranges<MODE, 8>(arena, descs, out, aux, first, kw, T, e0, have0);
+    else // shorter: 4 lanes x 2 loads (128 B), 64 ranges a round
+        pk_ranges<MODE, 4, 2>(arena, descs, out, aux, first, kw, T, e0, have0);
 }
 
 

@@ -837,7 +837,7 @@ def self_check(torch, tc, workload, head, seed: int) -> dict:
     if b.op == "tx":
         lens = np.minimum(b.descs["len"][idx].astype(np.int64), 78)  # the fill writes only there
         offs = b.descs["offset"][idx].astype(np.int64)
-        pos = torch.from_numpy(np.concatenate([o + np.arange(k) for o, k in zip(offs, lens)])).to(arena.device)
+        pos = torch.from_numpy(np.concatenate([o + np.arange(k) for o, k in zip(offs, lens)])).pin_memory().to(arena.device)
         before = arena[pos].cpu().numpy()
         tc.batch_ipv4_tx_fill(arena, sub, n, 0, want_flags=False)
         bad = int((arena[pos].cpu().numpy() != before).sum())

@@ -25,6 +25,9 @@ extern "C" {
  *   "page_stage"      0 / 1 (default 1): tcsum_host_batch_peso copies a
  *                     pageable arena through the context's pinned slots (0:
  *                     the runtime's own pageable copy, measurement only)
+ *   "seg_sdesc"       0 / 1 (default 1): the per-range kernel with 8 or 16
+ *                     lanes per range reads its wave's descriptors with
+ *                     scalar loads, each lane group picking its own
  *   "pk_early"        0 / 1 (default 1): the packed kernel's range-by-range
  *                     path (a workgroup whose ranges are not one region, up
  *                     to 32 of them) reads its descriptors with scalar loads

@@ -446,6 +446,62 @@ __device__ __forceinline__ uint16_t finalize(uint32_t acc, uintptr_t start, cons
     return (uint16_t)r;
 }
 
+// The descriptors of this wave's PER lane groups' ranges (k_segments_pk's
+// range-by-range path, and the per-range kernel with aux bit 7; 64 / PER
+// lanes per group), read with scalar loads -- all issued before any is used --
+// and each group's own picked into x.  Ranges past kw read the workgroup's
+// last descriptor (a group past kw takes no range).
+template <int MODE, uint32_t PER>
+__device__ __forceinline__ void pk_wave_descs(const void *__restrict__ descs, uint32_t first, uint32_t kw,
+                                              uint32_t (&x)[6])
+{
+    constexpr uint32_t DW = MODE == MODE_PESO ? 6u : 4u; // dwords per descriptor
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t gi = (threadIdx.x & 63u) / (64u / PER);
+    uint32_t sd[PER][DW];
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        const uint32_t r = wv * PER + j < kw ? wv * PER + j : kw - 1u;
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(descs) + (uint64_t)DW * (first + r);
+#pragma unroll
+        for (uint32_t i = 0; i < DW; ++i)
+            sd[j][i] = q[i];
+    }
+    // pinned in scalar registers: otherwise the compiler folds the per-group
+    // choice into one vector load from a chosen address -- the L2 round trip
+    // this is here to avoid
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j)
+#pragma unroll
+        for (uint32_t i = 0; i < DW; ++i)
+            asm volatile("" : "+s"(sd[j][i]));
+#pragma unroll
+    for (uint32_t i = 0; i < DW; ++i) {
+        uint32_t v = sd[0][i];
+#pragma unroll
+        for (uint32_t j = 1; j < PER; ++j)
+            v = gi == j ? sd[j][i] : v;
+        x[i] = v;
+    }
+}
+
+// A descriptor from the dwords pk_wave_descs picked (len 0 unless live).
+template <int MODE>
+__device__ __forceinline__ SegDesc desc_of(const uint32_t (&x)[6], bool live)
+{
+    SegDesc d{0, 0, 0, 0, 0, 0};
+    d.off = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
+    d.len = live ? x[2] : 0u;
+    if constexpr (MODE == MODE_PESO) {
+        d.src = x[3];
+        d.dst = x[4];
+        d.proto = x[5] & 0xFFu;
+    } else {
+        d.pre = x[3];
+    }
+    return d;
+}
+
 // One wave-slice of packets per wave, one launch-wide pass.
 //
 // Results leave through the workgroup's LAST wave: each wave puts its packets'
@@ -455,6 +511,8 @@ __device__ __forceinline__ uint16_t finalize(uint32_t acc, uintptr_t start, cons
 // headline ran 1.1 % slower -- as slow as its loads plus the stores' tail in
 // every wave; with the gathered store it matches the same kernel with no
 // store at all (profiles/r02/ab_store.txt).  A nontemporal store cost 4 %.
+constexpr uint32_t kSegScalarDesc = 1u << 7; // aux of k_segments: descriptors by scalar loads
+
 template <int G, int U, int MODE, int T = 256>
 __global__ __launch_bounds__(T) void k_segments(const uint8_t *__restrict__ arena,
                                                 const void *__restrict__ descs, uint32_t n,
@@ -472,7 +530,25 @@ __global__ __launch_bounds__(T) void k_segments(const uint8_t *__restrict__ aren
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
     const uint32_t seg = blk * PER + threadIdx.x / G; // no 32-bit wrap for any n
     const bool live = seg < n;
-    const SegDesc d = load_desc<MODE>(descs, seg, live);
+    SegDesc d;
+    if constexpr (G >= 8 && G <= 16) {
+        // aux bit 7 (debug knob "seg_sdesc", on unless 0): each wave reads its
+        // 4 or 8 groups' descriptors with scalar loads instead of every lane
+        // loading its own: shuffled 576-B ranges 329 -> 304 us, 1,000 B 256
+        // -> 249, 200 B 625 -> 606, packed 576 B 293 -> 272 (with 32 or 64
+        // lanes per range, 1-2 ranges a wave: +0.5 %, not taken;
+        // profiles/r05/seg_sdesc/)
+        if ((aux & kSegScalarDesc) != 0u) {
+            const uint32_t first = blk * PER, kw = n - first < PER ? n - first : PER;
+            uint32_t x[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+            pk_wave_descs<MODE, 64u / G>(descs, first, kw, x);
+            d = desc_of<MODE>(x, live);
+        } else {
+            d = load_desc<MODE>(descs, seg, live);
+        }
+    } else {
+        d = load_desc<MODE>(descs, seg, live);
+    }
     // descriptor prefetch (aux >> 8, k_segments_pk's fallback's): issued after
     // this workgroup's own descriptor load, so that load's wait is not its
     uint32_t pf = 0;
@@ -758,45 +834,6 @@ __device__ __forceinline__ uint32_t pk_group(uint32_t T, uint32_t kw)
     return lanes_per >= 64 ? 64u : lanes_per >= 32 ? 32u : lanes_per >= 16 || kw <= 22u ? 16u : 8u;
 }
 
-// The descriptors of this wave's PER lane groups' ranges (k_segments_pk's
-// range-by-range path, 64 / PER lanes per group), read with scalar loads --
-// all issued before any is used -- and each group's own picked into x.
-// Ranges past kw read the workgroup's last descriptor (a group past kw takes
-// no range).
-template <int MODE, uint32_t PER>
-__device__ __forceinline__ void pk_wave_descs(const void *__restrict__ descs, uint32_t first, uint32_t kw,
-                                              uint32_t (&x)[6])
-{
-    constexpr uint32_t DW = MODE == MODE_PESO ? 6u : 4u; // dwords per descriptor
-    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint32_t gi = (threadIdx.x & 63u) / (64u / PER);
-    uint32_t sd[PER][DW];
-#pragma unroll
-    for (uint32_t j = 0; j < PER; ++j) {
-        const uint32_t r = wv * PER + j < kw ? wv * PER + j : kw - 1u;
-        const uint32_t *q = reinterpret_cast<const uint32_t *>(descs) + (uint64_t)DW * (first + r);
-#pragma unroll
-        for (uint32_t i = 0; i < DW; ++i)
-            sd[j][i] = q[i];
-    }
-    // pinned in scalar registers: otherwise the compiler folds the per-group
-    // choice into one vector load from a chosen address -- the L2 round trip
-    // this is here to avoid
-#pragma unroll
-    for (uint32_t j = 0; j < PER; ++j)
-#pragma unroll
-        for (uint32_t i = 0; i < DW; ++i)
-            asm volatile("" : "+s"(sd[j][i]));
-#pragma unroll
-    for (uint32_t i = 0; i < DW; ++i) {
-        uint32_t v = sd[0][i];
-#pragma unroll
-        for (uint32_t j = 1; j < PER; ++j)
-            v = gi == j ? sd[j][i] : v;
-        x[i] = v;
-    }
-}
-
 // A workgroup of k_segments_pk whose kw ranges are not one region: G lanes
 // per range, G the widest power of two that gives every range a group
 // (pk_group).  e0: this lane's first range's descriptor when have0.
@@ -899,15 +936,7 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
                 pk_wave_descs<MODE, 4>(descs, first, kw, x);
             else
                 pk_wave_descs<MODE, 8>(descs, first, kw, x);
-            e0.off = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
-            e0.len = x[2];
-            if constexpr (MODE == MODE_PESO) {
-                e0.src = x[3];
-                e0.dst = x[4];
-                e0.proto = x[5] & 0xFFu;
-            } else {
-                e0.pre = x[3];
-            }
+            e0 = desc_of<MODE>(x, true);
         }
         pk_fallback<MODE>(arena, descs, out, aux, first, kw, T, e0, early);
         if (pf == 0x9E3779B9u && K == 0u) // never: keeps the prefetch load alive

@@ -378,7 +378,8 @@ static hipError_t seg_u(int G, int U, uint32_t xg, uint32_t n, const void *arena
 #define TCSUM_SEG(GG, UU)                                                                                     \
     if (G == GG && U == UU) {                                                                               \
         return launch(k_segments<GG, UU, MODE>, dim3((n + 256u / GG - 1) / (256u / GG)), dim3(256), 0, s, a,     \
-                      descs, n, out, aux | (pf_range() << 8), xg);                                            \
+                      descs, n, out, aux | (pf_range() << 8) | (knob(KNOB_SEG_SDESC) != 0 ? kSegScalarDesc : 0u), \
+                      xg);                                                                                    \
     }
     TCSUM_SEG(4, 1) TCSUM_SEG(4, 2) TCSUM_SEG(8, 4) TCSUM_SEG(16, 3) TCSUM_SEG(16, 4) TCSUM_SEG(16, 6)
     TCSUM_SEG(16, 8) TCSUM_SEG(32, 6)

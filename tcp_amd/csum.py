@@ -61,10 +61,12 @@ def _torch():
 
 
 def descs_to_device(descs: np.ndarray, device="cuda"):
-    """Copy a structured descriptor array to the device as raw bytes."""
+    """Copy a structured descriptor array to the device as raw bytes, through
+    pinned host memory: the runtime's own pageable host-to-device path is the
+    one three GPU suites stopped on."""
     torch = _torch()
     raw = np.ascontiguousarray(descs).view(np.uint8)
-    return torch.from_numpy(raw.copy()).to(device)
+    return torch.from_numpy(raw.copy()).pin_memory().to(device)
 
 
 def _stream_ptr(stream) -> int | None:

@@ -92,7 +92,7 @@ def tc(prod, torch):
 def to_dev(torch, a: np.ndarray, pad: int = 256):
     t = torch.zeros(a.nbytes + pad, dtype=torch.uint8)
     t[: a.nbytes] = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1))
-    return t.cuda()
+    return t.pin_memory().cuda()
 
 
 def _all_modes(tc, torch, oracle, host, pk, hint=None, tx=True):
@@ -317,7 +317,7 @@ def test_flat_full_mixed_config(tc, torch, oracle, config):
     rng = np.random.default_rng(55)
     bad = rng.choice(b.n, 2000, replace=False)
     pos = (b.descs["offset"][bad] + 20 + (rng.integers(0, 1 << 30, bad.size) % (b.descs["len"][bad] - 20)))
-    arena[torch.from_numpy(pos.astype(np.int64)).cuda()] ^= 0x04
+    arena[torch.from_numpy(pos.astype(np.int64)).pin_memory().cuda()] ^= 0x04
     verdict, flags = tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes)
     v = verdict.cpu().numpy()
     ev, ef = oracle.batch_ipv4_rx_verify(arena.cpu().numpy(), b.descs, nthreads=16)

@@ -68,7 +68,7 @@ def test_packed_mtu_vs_oracle(tc, torch, oracle, packed, n, start):
     lens = np.full(n, 1500, np.uint32)
     host = _arena(rng, start + 1500 * n + 4096)
     p = _peso(tc, _packed_offs(lens, start), lens, rng)
-    out = tc.batch_peso(torch.from_numpy(host).cuda(), tc.descs_to_device(p), n, int(lens.sum()))
+    out = tc.batch_peso(torch.from_numpy(host).pin_memory().cuda(), tc.descs_to_device(p), n, int(lens.sum()))
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
 
 
@@ -84,7 +84,7 @@ def test_packed_ragged_lengths(tc, torch, oracle, packed, seed):
     host = _arena(rng, start + int(lens.sum()) + 4096)
     p = _peso(tc, _packed_offs(lens, start), lens, rng)
     hint = int(rng.choice([int(lens.sum()), 1500 * n, 700 * n]))  # K from the hint only
-    out = tc.batch_peso(torch.from_numpy(host).cuda(), tc.descs_to_device(p), n, hint)
+    out = tc.batch_peso(torch.from_numpy(host).pin_memory().cuda(), tc.descs_to_device(p), n, hint)
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
 
 
@@ -129,7 +129,7 @@ def test_packed_irregular_layouts(tc, torch, oracle, packed, layout):
         offs, lens = offs[perm], lens[perm]
     host = _arena(rng, int((offs + lens).max()) + 4096)
     p = _peso(tc, offs.astype(np.uint64), lens.astype(np.uint32), rng)
-    out = tc.batch_peso(torch.from_numpy(host).cuda(), tc.descs_to_device(p), n, int(lens.sum()))
+    out = tc.batch_peso(torch.from_numpy(host).pin_memory().cuda(), tc.descs_to_device(p), n, int(lens.sum()))
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
 
 
@@ -144,7 +144,7 @@ def test_packed_multi_pass_regions(tc, torch, oracle, packed, hint_mean):
     start = int(rng.integers(0, 16))
     host = _arena(rng, start + int(lens.sum()) + 4096)
     p = _peso(tc, _packed_offs(lens, start), lens, rng)
-    out = tc.batch_peso(torch.from_numpy(host).cuda(), tc.descs_to_device(p), n, hint_mean * n)
+    out = tc.batch_peso(torch.from_numpy(host).pin_memory().cuda(), tc.descs_to_device(p), n, hint_mean * n)
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
 
 
@@ -161,7 +161,7 @@ def test_packed_long_range_word_sum_past_2_32(tc, torch, oracle, packed):
     for i in (37, 150):
         host[int(offs[i]): int(offs[i]) + int(lens[i])] = 0xFF
     p = _peso(tc, offs, lens, rng)
-    out = tc.batch_peso(torch.from_numpy(host).cuda(), tc.descs_to_device(p), n, 1500 * n)
+    out = tc.batch_peso(torch.from_numpy(host).pin_memory().cuda(), tc.descs_to_device(p), n, 1500 * n)
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
 
 
@@ -176,7 +176,7 @@ def test_packed_segments_mode(tc, torch, oracle, packed, comp):
     s = np.zeros(n, tc.SEG_DTYPE)
     s["offset"], s["len"] = _packed_offs(lens, 3), lens
     s["pre_sum"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
-    out = tc.batch_segments(torch.from_numpy(host).cuda(), tc.descs_to_device(s), n, comp, int(lens.sum()))
+    out = tc.batch_segments(torch.from_numpy(host).pin_memory().cuda(), tc.descs_to_device(s), n, comp, int(lens.sum()))
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_segments(host, s, comp, nthreads=8))
 
 
@@ -191,7 +191,7 @@ def test_packed_exact_region_edges(tc, torch, oracle, packed):
         lens = np.full(n, L, np.uint32)
         host = _arena(rng, start + L * n + 4096)
         p = _peso(tc, _packed_offs(lens, start), lens, rng)
-        out = tc.batch_peso(torch.from_numpy(host).cuda(), tc.descs_to_device(p), n, L * n)
+        out = tc.batch_peso(torch.from_numpy(host).pin_memory().cuda(), tc.descs_to_device(p), n, L * n)
         np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
 
 
@@ -228,7 +228,7 @@ def test_packed_fuzz(tc, torch, oracle, seed):
         offs[a:b], lens[a:b] = offs[perm], lens[perm]
     size = int((offs + lens).max()) + 4096
     host = _arena(rng, size)
-    arena = torch.from_numpy(host).cuda()
+    arena = torch.from_numpy(host).pin_memory().cuda()
     hint = int(rng.choice([int(lens.sum()), 300 * n, 1500 * n, 4000 * n]))
     p = _peso(tc, offs.astype(np.uint64), lens.astype(np.uint32), rng)
     out = tc.batch_peso(arena, tc.descs_to_device(p), n, hint)
@@ -264,7 +264,7 @@ def test_layout_hints_give_the_same_results(tc, torch, oracle, layout):
     if layout.startswith("shuffled"):
         p = p[rng.permutation(n)]
     want = oracle.batch_peso(host, p, nthreads=8)
-    arena = torch.from_numpy(host).cuda()
+    arena = torch.from_numpy(host).pin_memory().cuda()
     d = tc.descs_to_device(p)
     s = np.zeros(n, tc.SEG_DTYPE)
     s["offset"], s["len"] = p["offset"], p["len"]

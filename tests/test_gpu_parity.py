@@ -65,7 +65,7 @@ def geometry(knobs):
 def to_dev(torch, a: np.ndarray, pad: int = 64):
     t = torch.zeros(a.nbytes + pad, dtype=torch.uint8)
     t[: a.nbytes] = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1))
-    return t.cuda()
+    return t.pin_memory().cuda()
 
 
 def test_native_library_is_loaded(tc):
@@ -503,7 +503,7 @@ def test_tx_then_rx_full_mixed(tc, torch, oracle):
     rng = np.random.default_rng(5)
     bad = rng.choice(b.n, 2000, replace=False)
     pos = (b.descs["offset"][bad] + 20 + (rng.integers(0, 1 << 30, bad.size) % (b.descs["len"][bad] - 20))).astype(np.int64)
-    idx = torch.from_numpy(pos).cuda()
+    idx = torch.from_numpy(pos).pin_memory().cuda()
     arena[idx] ^= 0x04
     verdict, flags = tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes)
     v = verdict.cpu().numpy()
@@ -571,7 +571,7 @@ def test_edge_segments(tc, torch, oracle):
     s["len"] = [n for _, n in segs]
     s["pre_sum"] = rng.integers(0, 1 << 32, len(segs), dtype=np.uint64).astype(np.uint32)
     s["pre_sum"][:12] = 0
-    arena = torch.from_numpy(host).cuda()  # no padding: the last chunk ends the allocation
+    arena = torch.from_numpy(host).pin_memory().cuda()  # no padding: the last chunk ends the allocation
     for comp in (0, 1):
         out = tc.batch_segments(arena, tc.descs_to_device(s), s.size, comp).cpu().numpy()
         exp = oracle.batch_segments(host, s, comp, nthreads=8)
@@ -599,7 +599,7 @@ def test_unsorted_overlapping_duplicate_descriptors(tc, torch, oracle):
     p["src"] = rng.integers(0, 256, (n, 4))
     p["dst"] = rng.integers(0, 256, (n, 4))
     p["protocol"] = rng.choice([6, 17, 1, 99], n)
-    arena = torch.from_numpy(host).cuda()
+    arena = torch.from_numpy(host).pin_memory().cuda()
     for mean in (0, 64, 1500, 70000):
         out = tc.batch_peso(arena, tc.descs_to_device(p), n, mean * n).cpu().numpy()
         np.testing.assert_array_equal(out, oracle.batch_peso(host, p, nthreads=8))
@@ -721,7 +721,7 @@ def test_huge_batch_index_math(tc, torch, oracle, geometry):
     s["offset"] = rng.integers(0, (1 << 16) - 40, n)
     s["len"] = rng.integers(0, 33, n)
     s["pre_sum"] = rng.integers(0, 1 << 16, n)
-    arena = torch.from_numpy(host).cuda()
+    arena = torch.from_numpy(host).pin_memory().cuda()
     d = tc.descs_to_device(s)
     out = tc.batch_segments(arena, d, n, 1)
     exp = oracle.batch_segments(host, s, 1, nthreads=16)
@@ -750,10 +750,10 @@ def test_huge_ipv4_batch_index_math(tc, torch, oracle, geometry):
     spk = np.zeros(idx.size, tc.PKT_DTYPE)
     spk["offset"] = np.arange(idx.size, dtype=np.uint64) * np.uint64(L)
     spk["len"] = L
-    arena = torch.from_numpy(host.reshape(-1)).cuda()
+    arena = torch.from_numpy(host.reshape(-1)).pin_memory().cuda()
     del host
     d = tc.descs_to_device(pk)
-    tidx = torch.from_numpy(idx).cuda()
+    tidx = torch.from_numpy(idx).pin_memory().cuda()
 
     out, flags = tc.batch_ipv4(arena, d, n, n * L)
     eo, ef = oracle.batch_ipv4(sample, spk)
@@ -969,7 +969,7 @@ def test_full_tso_batch_properties(tc, torch, oracle):
     # incremental update: rewrite the word at offset 100 of every segment
     words = arena[: b.n * 65536].view(b.n, 65536)
     old = words[:, 100:102].cpu().numpy().copy().view("<u2").reshape(-1).astype(np.uint32)
-    new_bytes = torch.from_numpy(rng.integers(0, 256, (b.n, 2), dtype=np.uint8)).cuda()
+    new_bytes = torch.from_numpy(rng.integers(0, 256, (b.n, 2), dtype=np.uint8)).pin_memory().cuda()
     words[:, 100:102] = new_bytes
     new = new_bytes.cpu().numpy().copy().view("<u2").reshape(-1).astype(np.uint32)
     out4 = tc.batch_peso(arena, descs, b.n, b.total_bytes).cpu().numpy().astype(np.uint32)
@@ -1004,7 +1004,7 @@ def test_fuzz_vs_oracle(tc, torch, oracle, geometry, seed):
     rng = np.random.default_rng(9000 + seed)
     size = 8 << 20
     host = _fuzz_arena(rng, size)
-    arena = torch.from_numpy(host).cuda()
+    arena = torch.from_numpy(host).pin_memory().cuda()
     geometry(*GEOMS_SEG[int(rng.integers(0, len(GEOMS_SEG)))])
     n = 4000
     lens = _fuzz_lens(rng, n, 70000)
@@ -1048,7 +1048,7 @@ def test_fuzz_vs_oracle(tc, torch, oracle, geometry, seed):
         if ln >= 40 and rng.random() < 0.2:
             ip[o + 20 + 16: o + 20 + 18] = 0  # TCP checksum field zero (rx skip rule)
             ip[o + 20 + 6: o + 20 + 8] = 0    # UDP checksum field zero
-    d_ip = torch.from_numpy(ip).cuda()
+    d_ip = torch.from_numpy(ip).pin_memory().cuda()
     d_pk = tc.descs_to_device(pk)
     out, fl = tc.batch_ipv4(d_ip, d_pk, m)
     exp, efl = oracle.batch_ipv4(ip, pk, nthreads=8)
@@ -1100,7 +1100,7 @@ def test_ragged_batch_sizes_write_only_their_results(tc, torch, oracle, geometry
     result equals the oracle's and nothing past out[n) is written."""
     rng = np.random.default_rng(77)
     host = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
-    arena = torch.from_numpy(host).cuda()
+    arena = torch.from_numpy(host).pin_memory().cuda()
     geometry(g, u)
     for n in (1, 2, 3, 15, 17, 63, 65, 1001):
         p = np.zeros(n, tc.PESO_DTYPE)

@@ -36,7 +36,7 @@ def _descs_at_end(torch, tc, descs):
     past the array would leave it (and the allocator's page)."""
     raw = np.ascontiguousarray(descs).view(np.uint8)
     t = torch.empty(raw.size, dtype=torch.uint8, device="cuda")
-    t.copy_(torch.from_numpy(raw.copy()))
+    t.copy_(torch.from_numpy(raw.copy()).pin_memory())
     return t
 
 
@@ -61,7 +61,7 @@ def test_peso_batches_with_prefetch(tc, torch, oracle, pf, layout):
     if layout == "shuffled":
         p = p[rng.permutation(n)]
     want = oracle.batch_peso(host, p, nthreads=8)
-    arena = torch.from_numpy(host).cuda()
+    arena = torch.from_numpy(host).pin_memory().cuda()
     d = _descs_at_end(torch, tc, p)
     with tc.debug(pf_dist=pf):
         got = tc.batch_peso(arena, d, n, int(lens.sum())).cpu().numpy()
@@ -143,11 +143,42 @@ def test_pk_early_descriptors(tc, torch, oracle, layout, early):
     if layout in ("shuffled", "wide", "tail", "mid", "small", "tiny", "k17", "s400"):
         p = p[rng.permutation(n)]
     want = oracle.batch_peso(host, p, nthreads=8)
-    arena = torch.from_numpy(host).cuda()
+    arena = torch.from_numpy(host).pin_memory().cuda()
     segs = np.zeros(n, tc.SEG_DTYPE)
     segs["offset"], segs["len"], segs["pre_sum"] = p["offset"], p["len"], rng.integers(0, 1 << 17, n)
     with tc.debug(pk_early=early, packed=1):
         got = tc.batch_peso(arena, _descs_at_end(torch, tc, p), n, int(lens.sum())).cpu().numpy()
         gs = tc.batch_segments(arena, _descs_at_end(torch, tc, segs), n, 1, int(lens.sum())).cpu().numpy()
     np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(gs, oracle.batch_segments(host, segs, 1, nthreads=8))
+
+
+@pytest.mark.parametrize("sdesc", [1, 0])
+@pytest.mark.parametrize("shape", [(8, 4), (16, 3), (16, 4), (16, 6), (16, 8), (32, 6), (4, 2)])
+def test_per_range_scalar_descriptors(tc, torch, oracle, shape, sdesc):
+    """debug "seg_sdesc" (default 1): the per-range kernel with 8 or 16 lanes
+    per range reads its wave's descriptors with scalar loads, each lane group
+    picking its own; other widths keep their vector loads.  Every forced
+    shape, both descriptor layouts, a last workgroup with fewer ranges and the
+    descriptor array at the end of its allocation, shuffled, against the
+    oracle."""
+    g, u = shape
+    rng = np.random.default_rng(500 + 10 * g + u + sdesc)
+    n = 7 * (256 // g) + 3  # a short last workgroup
+    lens = rng.integers(0, 1200, n)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64) + 1
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    p = np.zeros(n, tc.PESO_DTYPE)
+    p["offset"], p["len"] = offs, lens
+    p["src"] = rng.integers(0, 256, (n, 4))
+    p["dst"] = rng.integers(0, 256, (n, 4))
+    p["protocol"] = rng.choice([6, 17], n)
+    p = p[rng.permutation(n)]
+    segs = np.zeros(n, tc.SEG_DTYPE)
+    segs["offset"], segs["len"], segs["pre_sum"] = p["offset"], p["len"], rng.integers(0, 1 << 17, n)
+    arena = torch.from_numpy(host).pin_memory().cuda()
+    with tc.debug(seg_sdesc=sdesc, packed=0, lanes=g, loads=u):
+        got = tc.batch_peso(arena, _descs_at_end(torch, tc, p), n, int(lens.sum())).cpu().numpy()
+        gs = tc.batch_segments(arena, _descs_at_end(torch, tc, segs), n, 1, int(lens.sum())).cpu().numpy()
+    np.testing.assert_array_equal(got, oracle.batch_peso(host, p, nthreads=8))
     np.testing.assert_array_equal(gs, oracle.batch_segments(host, segs, 1, nthreads=8))

@@ -43,7 +43,7 @@ def _batch(tc, seed):
 def _written(tc, torch, host, pk):
     """Byte positions the fill writes: apply all-zero and all-one values
     through the product's offload flags and see which bytes differ."""
-    arena = torch.from_numpy(host.copy()).cuda()
+    arena = torch.from_numpy(host.copy()).pin_memory().cuda()
     d = tc.descs_to_device(pk)
     _, fl = tc.batch_ipv4_tx_offload(arena, d, pk.size, int(pk["len"].sum()))
     fl = fl.cpu().numpy()
@@ -60,7 +60,7 @@ def test_txfloor_writes_the_fills_fields(tc, torch, seed):
     assert expect, "the batch has fields to fill"
     for deferred in (False, True):
         arena = torch.zeros(host.size + 256, dtype=torch.uint8, device="cuda")
-        arena[: host.size] = torch.from_numpy(host).cuda()
+        arena[: host.size] = torch.from_numpy(host).pin_memory().cuda()
         d = tc.descs_to_device(pk)
         h = tc.txfloor_prepare(arena, host.size, d, pk.size, int(pk["len"].sum()))
         fpos = h["fpos"].cpu().numpy()

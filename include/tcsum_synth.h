@@ -122,7 +122,8 @@ int tcsum_flat_ipv4(int mode, void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[
  * its chunk is taken): v = 0 the mode's shape, 4 = 4 loads, sums 8 = 8 loads,
  * 16 = 16 lanes x 6, rx 32 = 32 lanes x 6, sums 7 / rx 6 = the mode's shape
  * held to that many waves per SIMD; or (occ = 600) no header loads, the
- * header chunks shuffled from the first data pass.  Others:
+ * header chunks shuffled from the first data pass, or (occ = 700) the
+ * descriptors by scalar loads.  Others:
  * TCSUM_ERR_PARAM. */
 int tcsum_probe_ipv4_shape(void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev]*/, uint32_t n, int mode, int wg,
                            int occ, uint32_t *out /*[dev]*/, int8_t *verdict /*[dev] or NULL*/, void *stream);

@@ -23,6 +23,7 @@ DB_ONLY = "--db" in sys.argv  # two data passes in flight, with and without the 
 DYN_ONLY = "--dyn" in sys.argv  # packets handed out inside the workgroup (k_ipv4_dyn), M per lane group
 ROLL_ONLY = "--roll" in sys.argv  # rolling load slots: a multi-pass packet keeps its loads in flight
 HDRX_ONLY = "--hdrx" in sys.argv  # header chunks shuffled from the first data pass instead of loaded
+SDESC_ONLY = "--sdesc" in sys.argv  # the descriptors by scalar loads
 for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mixed_aligned", "mixed_rx"]):
     b = workload.make_batch(cfg)
     arena, descs = workload.materialize(b)
@@ -58,7 +59,9 @@ for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mi
                 f(o, v)
         return g
 
-    if HDRX_ONLY:
+    if SDESC_ONLY:
+        kinds.update({"descriptors by scalar loads": shape(256, 700)})
+    elif HDRX_ONLY:
         kinds.update({"header from the data pass": shape(256, 600)})
     elif ROLL_ONLY:
         kinds.update({"rolling slots": shape(256, 500), "rolling, 4 loads": shape(256, 504),

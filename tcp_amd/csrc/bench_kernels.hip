@@ -851,6 +851,7 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 516 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_SUMS, 256, 0, 2>)) }
         if (occ == 507 && wg == 256) { TCSUM_SH((k_ipv4_occ<32, 6, IP_SUMS, 7, 2>)) } // rolling, <= 72 VGPRs
         if (occ == 600 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 0, 3>)) } // header from the data pass
+        if (occ == 700 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 0, 4>)) } // scalar descriptors
         if (occ == 100 + 64 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 64>)) }
         // packets handed out inside the workgroup, M = occ - 300 per lane group
         if (occ == 302 && wg == 256) { TCSUM_SH((k_ipv4_dyn<32, 6, IP_SUMS, 2>)) }
@@ -877,6 +878,7 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 532 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_RX, 256, 0, 2>)) }
         if (occ == 506 && wg == 256) { TCSUM_SH((k_ipv4_occ<16, 6, IP_RX, 6, 2>)) } // rolling, <= 80 VGPRs
         if (occ == 600 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256, 0, 3>)) } // header from the data pass
+        if (occ == 700 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256, 0, 4>)) } // scalar descriptors
     }
 #undef TCSUM_SH
     return hipErrorInvalidValue;

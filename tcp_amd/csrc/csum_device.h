@@ -1333,7 +1333,8 @@ __device__ __forceinline__ void ip_finish(const IpHdr &ih, uint32_t fl, bool big
 // registers); 2 = rolling -- each load slot is reissued for the next pass as
 // soon as its chunk is taken, so a multi-pass packet keeps U loads in flight
 // per lane with no more registers than one pass; 3 = no header loads, the
-// header chunks taken from the lanes whose first data-pass load holds them.
+// header chunks taken from the lanes whose first data-pass load holds them;
+// 4 = the descriptors by scalar loads, a wave's 2 or 4 at once.
 template <int G, int U, int IPM, int SKEW = 0, int PIPE = 0>
 __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                             uint32_t pk, uint32_t n, uint32_t *__restrict__ out,
@@ -1344,7 +1345,22 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     const bool live = pk < n;
 
     // unconditional loads throughout (dead lanes read descriptor 0 / the zero chunk)
-    const u32x4 dv = *reinterpret_cast<const u32x4 *>(pkts + (live ? pk : 0u));
+    u32x4 dv;
+    if constexpr (PIPE == 4) {
+        // the wave's packets' descriptors by scalar loads (16 B each, the
+        // pktbuf_checksum16 layout), each lane group picking its own
+        static_assert(G >= 16, "at most 4 descriptors a wave");
+        const uint32_t firstp = pk - threadIdx.x / G; // the workgroup's first packet
+        const uint32_t kwp = n > firstp ? (n - firstp < 256u / G ? n - firstp : 256u / G) : 1u;
+        uint32_t x[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+        pk_wave_descs<MODE_SEG, 64u / G>(pkts, n > firstp ? firstp : 0u, kwp, x);
+        dv.x = x[0];
+        dv.y = x[1];
+        dv.z = x[2];
+        dv.w = x[3];
+    } else {
+        dv = *reinterpret_cast<const u32x4 *>(pkts + (live ? pk : 0u));
+    }
     const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
     const uint32_t frame = live ? dv.z : 0u;
     const bool big_enough = frame >= 20;

@@ -5,7 +5,11 @@ first-timed leg rotated: t(n) = a + b * bytes, fitted per shape.  a is what
 every launch pays whatever its size (the grid filling and draining the
 machine); 1 / b is the rate a launch approaches as it grows.
 
-  python scripts/launch_overhead.py [ROUNDS]
+  python scripts/launch_overhead.py [ROUNDS] [K,K,...]
+
+With a K list, configs[1]'s shape is also timed with the packed kernel's
+ranges per workgroup forced to each K (debug knob "packed"): how the fixed
+cost and the rate move with the workgroup's size.
 """
 import os
 import sys
@@ -35,12 +39,24 @@ def per_launch(fn, reps=20):
     return e0.elapsed_time(e1) / reps * 1e3
 
 
+KS = [int(k) for k in sys.argv[2].split(",")] if len(sys.argv) > 2 else []
+
+
+def knobbed(fn, **kn):
+    def g():
+        with tc.debug(**kn):
+            fn()
+    return g
+
+
 legs = {}
 for s in SCALES:
     n = int(N1 * s)
     out = torch.empty(n, dtype=torch.uint16, device="cuda")
     nbytes = n * 1500 + 26 * n
     legs[f"mtu x{s}"] = ((lambda n=n, o=out: tc.batch_peso(arena, descs_all, n, n * 1500, out=o)), nbytes)
+    for K in KS:
+        legs[f"mtuK{K} x{s}"] = (knobbed(legs[f"mtu x{s}"][0], packed=K), nbytes)
     L = 65536
     n64 = -(-nbytes // (L + 26))
     d = np.zeros(n64, PESO_DTYPE)
@@ -61,7 +77,7 @@ for r in range(rounds):
         k = names[(r + i) % len(names)]
         ts[k].append(per_launch(legs[k][0]))
 print(f"# {rounds} rounds x 20 launches, first-timed leg rotated", flush=True)
-for shape in ("mtu", "tso"):
+for shape in ["mtu", "tso"] + [f"mtuK{K}" for K in KS]:
     xs, ys = [], []
     for s in SCALES:
         k = f"{shape} x{s}"
@@ -69,7 +85,7 @@ for shape in ("mtu", "tso"):
         nb = legs[k][1]
         xs.append(nb)
         ys.append(us)
-        print(f"{k:9s} {nb / 1e9:7.4f} GB  {us:8.1f} us  {nb / us / 1e3:8.1f} GB/s  frac {nb / us / 1e3 / 8000:.4f}",
+        print(f"{k:11s} {nb / 1e9:7.4f} GB  {us:8.1f} us  {nb / us / 1e3:8.1f} GB/s  frac {nb / us / 1e3 / 8000:.4f}",
               flush=True)
     b, a = np.polyfit(np.array(xs), np.array(ys), 1)
     print(f"{shape}: t = {a:.2f} us + bytes / {1 / b / 1e3:.1f} GB/s  (asymptotic frac {1 / b / 1e3 / 8000:.4f}; "

@@ -45,6 +45,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table
 METRIC = "Internet-checksum GiB/s (device-resident), 1500B & 64KB packet batches"
 
 
+def _host(t):
+    """A device tensor's values as numpy, copied through pinned memory only
+    (tcp_amd.to_host)."""
+    from tcp_amd import to_host
+    return to_host(t)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -554,7 +561,7 @@ def cpu_baseline(torch, r, seconds, kind="reference", cache_sample=True):
         n = int(np.searchsorted(np.cumsum(lens), max_bytes)) + 1
         n = max(1, min(b.n, n))
         end = int(b.descs["offset"][n - 1] + b.descs["len"][n - 1])
-        host = r["arena"][: end + 16].cpu().numpy()
+        host = _host(r["arena"][: end + 16])
         if b.kind == "peso":
             segs = b.descs[:n].copy()
             want = int(r["out"][:n].to(torch.int64).sum().item())
@@ -622,7 +629,7 @@ def e2e(torch, tc, r):
         return None
     try:
         host = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p))
-        host[:] = r["arena"][:nbytes].cpu().numpy()
+        host[:] = _host(r["arena"][:nbytes])
         out = np.zeros(b.n, np.uint16)
         tc.host_batch_peso(host, b.descs)  # warm (allocates device buffers)
         t0 = time.perf_counter()
@@ -630,7 +637,7 @@ def e2e(torch, tc, r):
         for _ in range(reps):
             out = tc.host_batch_peso(host, b.descs)
         dt = (time.perf_counter() - t0) / reps
-        same = bool((out == r["out"].cpu().numpy()).all())
+        same = bool((out == _host(r["out"])).all())
         # the host link itself: one plain pinned -> device copy of the same bytes
         src = torch.from_numpy(host)
         dst = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
@@ -667,10 +674,10 @@ def e2e_host_queue_rx(torch, tc):
     b = workload.make_batch("mixed_rx")
     arena, descs = workload.materialize(b)
     want, _ = tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes, want_flags=False)
-    want = want.cpu().numpy()
+    want = _host(want)
     ha = tc.HostArena(arena.numel())
     try:
-        ha.array[:] = arena.cpu().numpy()
+        ha.array[:] = _host(arena)
         del arena, descs
         torch.cuda.empty_cache()
         v, _, _ = tc.host_batch_ipv4_rx_verify(ha, b.descs)  # warm (device buffers)
@@ -731,7 +738,7 @@ def e2e_multi_main(config: str) -> None:
     ident = lambda d: device_identity(torch, d)  # noqa: E731
     b = workload.make_batch(config)
     arena, descs = workload.materialize(b)
-    want = tc.batch_peso(arena, descs, b.n, b.total_bytes).cpu().numpy()
+    want = _host(tc.batch_peso(arena, descs, b.n, b.total_bytes))
     L = _lib.lib()
     p = L.tcsum_host_alloc(b.alloc_bytes)
     if not p:
@@ -739,7 +746,7 @@ def e2e_multi_main(config: str) -> None:
     res = {"gpus": len(devs)}
     try:
         host = np.ctypeslib.as_array((ctypes.c_uint8 * b.alloc_bytes).from_address(p))
-        host[:] = arena[: b.alloc_bytes].cpu().numpy()
+        host[:] = _host(arena[: b.alloc_bytes])
         del arena, descs
         torch.cuda.empty_cache()
         out = tc.host_batch_peso_multi(host, b.descs, devs)
@@ -756,10 +763,10 @@ def e2e_multi_main(config: str) -> None:
         rb = workload.make_batch("mixed_rx")
         arena, descs = workload.materialize(rb)
         wv, _ = tc.batch_ipv4_rx_verify(arena, descs, rb.n, rb.total_bytes, want_flags=False)
-        wv = wv.cpu().numpy()
+        wv = _host(wv)
         ha = tc.HostArena(arena.numel())
         try:
-            ha.array[:] = arena.cpu().numpy()
+            ha.array[:] = _host(arena)
             del arena, descs
             torch.cuda.empty_cache()
             v, _, _ = tc.host_batch_ipv4_rx_verify(ha, rb.descs, devices=devs)
@@ -838,9 +845,9 @@ def self_check(torch, tc, workload, head, seed: int) -> dict:
         lens = np.minimum(b.descs["len"][idx].astype(np.int64), 78)  # the fill writes only there
         offs = b.descs["offset"][idx].astype(np.int64)
         pos = torch.from_numpy(np.concatenate([o + np.arange(k) for o, k in zip(offs, lens)])).pin_memory().to(arena.device)
-        before = arena[pos].cpu().numpy()
+        before = _host(arena[pos])
         tc.batch_ipv4_tx_fill(arena, sub, n, 0, want_flags=False)
-        bad = int((arena[pos].cpu().numpy() != before).sum())
+        bad = int((_host(arena[pos]) != before).sum())
         return {"segments": n, "mismatches": bad}
     if b.kind == "peso":
         got = tc.batch_peso(arena, sub, n, 0)
@@ -851,7 +858,7 @@ def self_check(torch, tc, workload, head, seed: int) -> dict:
     else:
         got, _ = tc.batch_ipv4(arena, sub, n, 0, want_flags=False)
     torch.cuda.synchronize()
-    bad = int((got.cpu().numpy() != out.cpu().numpy()[idx]).sum())  # uint16 / uint32: no CUDA gather for them
+    bad = int((_host(got) != _host(out)[idx]).sum())  # uint16 / uint32: no CUDA gather for them
     return {"segments": n, "mismatches": bad}
 
 

@@ -69,6 +69,40 @@ def descs_to_device(descs: np.ndarray, device="cuda"):
     return torch.from_numpy(raw.copy()).pin_memory().to(device)
 
 
+_HOST_CHUNK = 64 << 20
+
+
+def to_host_tensor(t):
+    """A device tensor's values in host memory, copied by the GPU only into
+    pinned memory: the runtime's pageable device-to-host path is, with the
+    host-to-device one, where the round-5 GPU suites stopped.
+    Up to 64 MiB: one pinned tensor; larger: chunk by chunk through a 64-MiB
+    pinned bounce buffer into a pageable tensor (a power-of-two pinned block
+    per multi-GB result would pin twice its size).  Synchronous, like
+    `.cpu()`; a host tensor is returned as it is."""
+    torch = _torch()
+    if t.device.type != "cuda":
+        return t
+    src = t.contiguous().reshape(-1)
+    per = max(1, _HOST_CHUNK // src.element_size())
+    if src.numel() <= per:
+        h = torch.empty(src.numel(), dtype=src.dtype, pin_memory=True)
+        h.copy_(src)
+        return h.reshape(t.shape)
+    out = torch.empty(src.numel(), dtype=src.dtype)
+    bounce = torch.empty(per, dtype=src.dtype, pin_memory=True)
+    for o in range(0, src.numel(), per):
+        k = min(per, src.numel() - o)
+        bounce[:k].copy_(src[o:o + k])
+        out[o:o + k].copy_(bounce[:k])
+    return out.reshape(t.shape)
+
+
+def to_host(t) -> np.ndarray:
+    """to_host_tensor(t) as a numpy array."""
+    return to_host_tensor(t).numpy()
+
+
 def _stream_ptr(stream) -> int | None:
     torch = _torch()
     s = stream if stream is not None else torch.cuda.current_stream()

@@ -100,7 +100,8 @@ def test_ipv4_batches_with_prefetch(tc, torch, oracle, pf):
     np.testing.assert_array_equal(v.cpu().numpy(), ev)
 
 
-EARLY_LAYOUTS = ["packed", "shuffled", "mtu", "wide", "tail", "mid", "small", "tiny", "k17", "s400"]
+EARLY_LAYOUTS = ["packed", "shuffled", "mtu", "wide", "tail", "mid", "small", "tiny", "k17", "s400",
+                 "s200", "tinyp", "tinyswap"]
 
 
 @pytest.mark.parametrize("early", [1, 0])
@@ -108,18 +109,24 @@ EARLY_LAYOUTS = ["packed", "shuffled", "mtu", "wide", "tail", "mid", "small", "t
 def test_pk_early_descriptors(tc, torch, oracle, layout, early):
     """debug "pk_early" (default 1): a packed-kernel workgroup on its
     range-by-range path (K <= 32) reads its ranges' descriptors with scalar
-    loads, each lane group picking its own (0: vector loads); both descriptor layouts, a last workgroup with fewer
-    ranges (tail), K = 3 (wide: 64-lane groups), 8 (32), ~12 (mid: 16),
-    ~21 (small) and 17 (k17: 16 lanes, a second round for the last ranges),
-    ~30 (s400: 8 lanes x 4 loads), ~190 (tiny: K > 32, not covered: vector
-    loads), shuffled and packed, against the oracle."""
+    loads, each lane group picking its own (0: vector loads; K > 32 always
+    vector loads, one per round of ranges).  Both descriptor layouts, a last
+    workgroup with fewer ranges (tail), K = 3 (wide: 64-lane groups), 8 (32),
+    ~12 (mid: 16), ~21 (small) and 17 (k17: 16 lanes, a second round for the
+    last ranges), ~30 (s400: 8 lanes x 4 loads), ~61 (s200: 8 lanes, two
+    rounds), ~190 (tiny: 4 lanes, three rounds; tinyp: packed, the region
+    path; tinyswap: packed with middle ranges swapped between workgroups 100
+    apart, so the span holds and the region check fails), shuffled and
+    packed, against the oracle; the descriptors end their allocation."""
     rng = np.random.default_rng(77 + EARLY_LAYOUTS.index(layout))
     if layout == "mid":
         n, lens = 15013, rng.integers(800, 1200, 15013)
     elif layout == "small":
         n, lens = 30011, np.full(30011, 576)
-    elif layout == "tiny":
+    elif layout in ("tiny", "tinyp", "tinyswap"):
         n, lens = 60013, rng.integers(1, 128, 60013)
+    elif layout == "s200":
+        n, lens = 40009, rng.integers(150, 250, 40009)
     elif layout == "k17":
         n, lens = 17 * 1003 + 9, rng.integers(650, 790, 17 * 1003 + 9)
     elif layout == "s400":
@@ -140,8 +147,14 @@ def test_pk_early_descriptors(tc, torch, oracle, layout, early):
     p["src"] = rng.integers(0, 256, (n, 4))
     p["dst"] = rng.integers(0, 256, (n, 4))
     p["protocol"] = rng.choice([6, 17], n)
-    if layout in ("shuffled", "wide", "tail", "mid", "small", "tiny", "k17", "s400"):
+    if layout in ("shuffled", "wide", "tail", "mid", "small", "tiny", "k17", "s400", "s200"):
         p = p[rng.permutation(n)]
+    elif layout == "tinyswap":
+        K = tc.route(int(lens.mean()))["packed"]
+        assert K > 32
+        for k in range(0, n // K - 100, 7):
+            i, j = K * k + K // 2, K * (k + 100) + K // 3
+            p[[i, j]] = p[[j, i]]
     want = oracle.batch_peso(host, p, nthreads=8)
     arena = torch.from_numpy(host).pin_memory().cuda()
     segs = np.zeros(n, tc.SEG_DTYPE)

@@ -75,7 +75,8 @@ int tcsum_debug_set(const char *key, int64_t value);
  *   31-37  host-queue IPv4 batches (31 set device, 32-33 pinned staging,
  *          34-35 copy-engine pieces, 36 launch, 37 wait)
  *   40-49  queue / call server set-up, launch, stop
- *   50-52  tcsum_release;  60-61 tcsum_host_register / unregister
+ *   50-54  tcsum_release (53: a stream did not drain, 54: the device sync);
+ *          60-61 tcsum_host_register / unregister
  *   70     a device-resident batch call's launch */
 int64_t tcsum_debug_get(const char *key);
 

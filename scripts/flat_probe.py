@@ -77,7 +77,7 @@ if extra:
                 tc.batch_ipv4(arena, descs, n, b.total_bytes, out=out, want_flags=False)
         kinds[f"k_ipv4 {g}x{u} (knob)"] = shaped
 # the variants that compute real sums must equal the product's
-for name in ["flat 4x3 (product, knob)"] + [f"flat {w}x{u} v0" for w, u in shapes if 0 in variants] + \
+for name in ["flat 4x3 (tcsum_flat_ipv4)"] + [f"flat {w}x{u} v0" for w, u in shapes if 0 in variants] + \
         [k for k in kinds if k.startswith("k_ipv4 ") and "knob" in k]:
     out.zero_()
     kinds[name]()

@@ -162,12 +162,17 @@ int g_default_dev = -1;
 // step * 1000 + the hipError_t (tcsum_debug_get "last_sys_error"; 0 = none
 // yet).  Steps: include/tcsum_debug.h.  Returns `rc`.
 std::atomic<int64_t> g_last_sys{0};
-int note_err(int step, hipError_t e, int rc)
+// `from_runtime`: e is what a runtime call just returned.  A code the
+// library makes up itself (a refused shape, its own time-out) is recorded
+// only: the caller's last-error slot may hold the same code as the caller's
+// own error, and that stays.
+int note_err(int step, hipError_t e, int rc, bool from_runtime = true)
 {
     g_last_sys.store((int64_t)step * 1000 + (int64_t)e, std::memory_order_relaxed);
     // the failed call's error is returned as rc: it must not also reach the
     // caller's next hipGetLastError() as an error of the caller's own
-    (void)tcsum::quiet(e);
+    if (from_runtime)
+        (void)tcsum::quiet(e);
     return rc;
 }
 int note_sys(int step, hipError_t e) { return note_err(step, e, TCSUM_ERR_SYS); }
@@ -530,7 +535,10 @@ void tcsum_debug_route(uint64_t mean_len, int32_t out[5])
 // hipErrorInvalidValue from a launcher: a shape or size it refuses
 static int rc_of(hipError_t e)
 {
-    return e == hipSuccess ? TCSUM_OK : e == hipErrorInvalidValue ? note_err(70, e, TCSUM_ERR_PARAM) : note_sys(70, e);
+    if (e == hipSuccess)
+        return TCSUM_OK;
+    const bool mine = tcsum::take_refused() && e == hipErrorInvalidValue;
+    return e == hipErrorInvalidValue ? note_err(70, e, TCSUM_ERR_PARAM, !mine) : note_sys(70, e);
 }
 
 static uint64_t mean_of(uint64_t total, uint32_t n) { return total && n ? total / n : 1500; }
@@ -940,9 +948,12 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     // runtime's path (measurement).
     const bool pageable = tcsum::knob(tcsum::KNOB_PAGE_STAGE) != 0 && mapped_host(host_arena) == nullptr;
     if (pageable && !c.pev_ok) {
-        for (auto &e : c.pev)
-            if (const hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming); r != hipSuccess)
-                return note_sys(17, r);
+        for (auto &e : c.pev) // a failure part-way keeps those made: the next call makes only the rest
+            if (!e)
+                if (const hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming); r != hipSuccess) {
+                    e = nullptr;
+                    return note_sys(17, r);
+                }
         c.pev_ok = true;
     }
     bool slot_busy[kPageSlots] = {};
@@ -1574,7 +1585,7 @@ int srv_submit(Ctx &c, int op, uint8_t *d_arena, const tcsum_pkt_t *d_pkts, uint
                         return rc;
                 }
                 if (now - t0 > std::chrono::seconds(10))
-                    return note_sys(45, hipErrorLaunchTimeOut);
+                    return note_err(45, hipErrorLaunchTimeOut, TCSUM_ERR_SYS, false); // the library's own time-out
                 check = now + std::chrono::microseconds(100);
             }
         }
@@ -1769,9 +1780,14 @@ int release_ctx(Ctx &c, int dev)
         return note_sys(51, e);
     if ((c.srv_running && srv_stop(c) != TCSUM_OK) || (c.cs_running && cs_stop(c) != TCSUM_OK))
         return TCSUM_ERR_SYS;
+    // a stream that does not drain (a faulted device) is the caller's to
+    // know: nothing is freed under work that may still be reading it
     for (hipStream_t st : c.hs)
-        (void)tcsum::quiet(hipStreamSynchronize(st));
-    (void)tcsum::quiet(hipStreamSynchronize(c.stream));
+        if (st)
+            if (const hipError_t e = hipStreamSynchronize(st); e != hipSuccess)
+                return note_sys(53, e);
+    if (const hipError_t e = hipStreamSynchronize(c.stream); e != hipSuccess)
+        return note_sys(53, e);
     for (void *p : {(void *)c.d_arena, (void *)c.d_lead, (void *)c.d_descs, (void *)c.d_out})
         if (p)
             (void)tcsum::quiet(hipFree(p));
@@ -1789,7 +1805,8 @@ int release_ctx(Ctx &c, int dev)
     }
     // the tx fill's pooled scratch (every stream of this context is idle;
     // a caller's own stream on this device must be too, tcsum.h)
-    (void)tcsum::quiet(hipDeviceSynchronize());
+    if (const hipError_t e = hipDeviceSynchronize(); e != hipSuccess)
+        return note_sys(54, e);
     if (const hipError_t e = tcsum::scratch_trim(c.device); e != hipSuccess)
         return note_sys(52, e);
     return TCSUM_OK;

@@ -245,6 +245,24 @@ __global__ __launch_bounds__(64) void k_call(CallBox *__restrict__ box, const ui
 
 // ---------------------------------------------------------------- dispatch
 
+// A shape or size a launcher refuses without calling the runtime: the
+// status is the library's own, so it never touches the caller's last-error
+// slot (rc_of, csum_api.cpp, asks which it was).
+static thread_local bool t_refused = false;
+
+hipError_t refused()
+{
+    t_refused = true;
+    return hipErrorInvalidValue;
+}
+
+bool take_refused()
+{
+    const bool r = t_refused;
+    t_refused = false;
+    return r;
+}
+
 // Test and measurement overrides (include/tcsum_debug.h): set only by an
 // explicit tcsum_debug_set call -- nothing in the environment changes a route.
 static std::atomic<int64_t> g_knobs[KNOB_COUNT] = {};
@@ -390,7 +408,7 @@ static hipError_t seg_u(int G, int U, uint32_t xg, uint32_t n, const void *arena
     if (G == 256 && U == 16) { // one range per workgroup
         return launch(k_segments_wg<16, MODE>, dim3(n), dim3(256), 0, s, a, descs, n, out, aux, xg);
     }
-    return hipErrorInvalidValue;
+    return refused();
 }
 
 // The AQL dispatch packet counts work-items in 32 bits: one launch may carry
@@ -457,7 +475,7 @@ static hipError_t ipv4_u(int G, int U, dim3 grid, uint8_t *arena, const tcsum_pk
     TCSUM_IP(16, 1) TCSUM_IP(16, 2) TCSUM_IP(16, 3) TCSUM_IP(16, 4) TCSUM_IP(16, 6) TCSUM_IP(16, 8)
     TCSUM_IP(32, 6) TCSUM_IP(64, 4) TCSUM_IP(64, 16)
 #undef TCSUM_IP
-    return hipErrorInvalidValue;
+    return refused();
 }
 
 
@@ -721,7 +739,7 @@ hipError_t launch_inline16(Mode mode, const void *bytes, uint32_t len, uint32_t 
                            uint16_t *out, hipStream_t stream)
 {
     if (len + odd > kCallInline || (mode != MODE_EXACT && mode != MODE_SEG))
-        return hipErrorInvalidValue;
+        return refused();
     uint32_t w[6] = {0u, 0u, 0u, 0u, 0u, 0u};
     if (len)
         memcpy(reinterpret_cast<uint8_t *>(w) + odd, bytes, len);

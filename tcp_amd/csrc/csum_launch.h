@@ -23,6 +23,12 @@ inline hipError_t quiet(hipError_t e)
     return e;
 }
 
+// hipErrorInvalidValue for a shape or size a launcher refuses itself (no
+// runtime call made); take_refused(): whether the last such status of this
+// thread was one, clearing the mark.
+hipError_t refused();
+bool take_refused();
+
 // What a segment kernel computes per range (see csum_kernels.hip).
 enum Mode : int {
     MODE_SEG = 0,   // pktbuf_checksum16: u16 pre_sum, optional complement

@@ -11,28 +11,6 @@ for p in (ROOT, os.path.join(ROOT, "tests")):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
-    _pinned_cpu_copies()
-
-
-def _pinned_cpu_copies():
-    """Every CUDA tensor's `.cpu()` in these tests copies through pinned
-    memory (tcp_amd.to_host_tensor), as every upload already goes through
-    pin_memory(): the runtime's pageable copies, in both directions, are
-    where the round-5 GPU suites stopped.  Same values, same
-    shape and dtype, synchronous like `.cpu()`."""
-    import torch
-
-    from tcp_amd.csum import to_host_tensor
-    plain = torch.Tensor.cpu
-    if getattr(plain, "_pinned", False):
-        return
-
-    def cpu(self, *args, **kwargs):
-        if self.device.type == "cuda" and not args and not kwargs:
-            return to_host_tensor(self)
-        return plain(self, *args, **kwargs)
-    cpu._pinned = True
-    torch.Tensor.cpu = cpu
 
 
 @pytest.fixture(scope="session")
@@ -57,3 +35,32 @@ def dbg():
     yield set_
     for k in touched:
         tcp_amd.debug_set(k, -1)
+
+
+@pytest.fixture(autouse=True)
+def _device_drained(request):
+    """After every GPU test: the whole device synchronized and its status
+    checked -- every stream, the library's own and its resident servers
+    included -- so a device fault is charged to the test whose work
+    faulted, not to a later test's first HIP call."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import torch
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _pageable_mode():
+    """TCSUM_TEST_PAGEABLE=1: tcsum_host_batch_peso copies a pageable arena
+    with the runtime's own pageable hipMemcpyAsync (debug knob page_stage =
+    0), as it did in round 4 (devcopy.py)."""
+    from devcopy import PAGEABLE
+    if not PAGEABLE:
+        yield
+        return
+    import tcp_amd
+    tcp_amd.debug_set("page_stage", 0)
+    yield
+    tcp_amd.debug_set("page_stage", -1)

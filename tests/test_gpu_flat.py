@@ -14,6 +14,7 @@ one window than it has lanes, and break the stream precondition (descriptors
 out of arena order, overlaps, a span the byte hint does not cover) so that
 the per-packet fallback inside the same launch runs.  Bit-exact throughout.
 """
+from devcopy import down, up
 import numpy as np
 import pytest
 
@@ -92,7 +93,7 @@ def tc(prod, torch):
 def to_dev(torch, a: np.ndarray, pad: int = 256):
     t = torch.zeros(a.nbytes + pad, dtype=torch.uint8)
     t[: a.nbytes] = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1))
-    return t.pin_memory().cuda()
+    return up(t)
 
 
 def _all_modes(tc, torch, oracle, host, pk, hint=None, tx=True):
@@ -104,19 +105,19 @@ def _all_modes(tc, torch, oracle, host, pk, hint=None, tx=True):
     d = tc.descs_to_device(pk)
     out, fl = tc.batch_ipv4(arena, d, n, hint)
     exp, efl = oracle.batch_ipv4(host, pk, nthreads=8)
-    np.testing.assert_array_equal(out.cpu().numpy(), exp)
-    np.testing.assert_array_equal(fl.cpu().numpy(), efl)
+    np.testing.assert_array_equal(down(out), exp)
+    np.testing.assert_array_equal(down(fl), efl)
     rout = torch.empty(n, dtype=torch.uint32, device="cuda")
     verdict, vfl = tc.batch_ipv4_rx_verify(arena, d, n, hint, out=rout)
     ev, evfl = oracle.batch_ipv4_rx_verify(host, pk, nthreads=8)
-    np.testing.assert_array_equal(verdict.cpu().numpy(), ev)
-    np.testing.assert_array_equal(vfl.cpu().numpy(), evfl)
-    np.testing.assert_array_equal(rout.cpu().numpy(), exp)  # rx reports the same sums
+    np.testing.assert_array_equal(down(verdict), ev)
+    np.testing.assert_array_equal(down(vfl), evfl)
+    np.testing.assert_array_equal(down(rout), exp)  # rx reports the same sums
     if not tx:
         return
     tout, tfl = tc.batch_ipv4_tx_offload(arena, d, n, hint)
     filled = host.copy()
-    tc.tx_apply_batch(filled, pk, tout.cpu().numpy(), tfl.cpu().numpy())
+    tc.tx_apply_batch(filled, pk, down(tout), down(tfl))
     want = host.copy()
     oracle.batch_ipv4_tx_fill(want, pk, nthreads=8)
     np.testing.assert_array_equal(filled, want)
@@ -125,8 +126,8 @@ def _all_modes(tc, torch, oracle, host, pk, hint=None, tx=True):
         a2 = to_dev(torch, host)
         fout = torch.empty(n, dtype=torch.uint32, device="cuda")
         tc.batch_ipv4_tx_fill(a2, d, n, hint, out=fout, want_flags=False)
-        np.testing.assert_array_equal(a2.cpu().numpy()[: host.size], filled)
-        np.testing.assert_array_equal(fout.cpu().numpy(), tout.cpu().numpy())
+        np.testing.assert_array_equal(down(a2)[: host.size], filled)
+        np.testing.assert_array_equal(down(fout), down(tout))
     tc.debug_set("tx_split", -1)
 
 
@@ -275,17 +276,17 @@ def test_flat_reference_fixtures(tc, torch, fixture):
         pk = np.zeros(cases.size, tc.PKT_DTYPE)
         pk["offset"], pk["len"] = cases["pool_off"], cases["frame_len"]
         out, flags = tc.batch_ipv4(to_dev(torch, pool), tc.descs_to_device(pk), pk.size, int(pk["len"].sum()))
-        out = out.cpu().numpy()
+        out = down(out)
         np.testing.assert_array_equal(out & 0xFFFF, cases["ip"])
         np.testing.assert_array_equal(out >> 16, cases["l4"])
-        np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+        np.testing.assert_array_equal(down(flags), cases["flags"])
     elif fixture == "rx":
         cases, pool = G.ipv4_rx_cases()
         pk = G.pkt_descs(cases, tc.PKT_DTYPE)
         verdict, flags = tc.batch_ipv4_rx_verify(to_dev(torch, pool), tc.descs_to_device(pk), cases.size,
                                                  int(pk["len"].sum()))
-        np.testing.assert_array_equal(verdict.cpu().numpy(), cases["verdict"])
-        np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+        np.testing.assert_array_equal(down(verdict), cases["verdict"])
+        np.testing.assert_array_equal(down(flags), cases["flags"])
     else:
         cases, pin, pout = G.ipv4_tx_cases() if fixture == "tx" else G.stack_tx_cases()
         pk = G.pkt_descs(cases, tc.PKT_DTYPE)
@@ -293,8 +294,8 @@ def test_flat_reference_fixtures(tc, torch, fixture):
             tc.debug_set("tx_split", split)
             arena = to_dev(torch, pin)
             flags = tc.batch_ipv4_tx_fill(arena, tc.descs_to_device(pk), cases.size, int(pk["len"].sum()))
-            np.testing.assert_array_equal(arena.cpu().numpy()[: pout.size], pout)
-            np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+            np.testing.assert_array_equal(down(arena)[: pout.size], pout)
+            np.testing.assert_array_equal(down(flags), cases["flags"])
 
 
 @pytest.mark.parametrize("config", ["mixed", "mixed_aligned"])
@@ -306,23 +307,23 @@ def test_flat_full_mixed_config(tc, torch, oracle, config):
     b = workload.make_batch(config)
     arena, descs = workload.materialize(b)
     out, fl = tc.batch_ipv4(arena, descs, b.n, b.total_bytes)
-    host = arena.cpu().numpy()
+    host = down(arena)
     exp, efl = oracle.batch_ipv4(host, b.descs, nthreads=16)
-    np.testing.assert_array_equal(out.cpu().numpy(), exp)
-    np.testing.assert_array_equal(fl.cpu().numpy(), efl)
+    np.testing.assert_array_equal(down(out), exp)
+    np.testing.assert_array_equal(down(fl), efl)
     del host
     tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes)
     verdict, _ = tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes)
-    assert (verdict.cpu().numpy() == 0).all()
+    assert (down(verdict) == 0).all()
     rng = np.random.default_rng(55)
     bad = rng.choice(b.n, 2000, replace=False)
     pos = (b.descs["offset"][bad] + 20 + (rng.integers(0, 1 << 30, bad.size) % (b.descs["len"][bad] - 20)))
-    arena[torch.from_numpy(pos.astype(np.int64)).pin_memory().cuda()] ^= 0x04
+    arena[up(torch.from_numpy(pos.astype(np.int64)))] ^= 0x04
     verdict, flags = tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes)
-    v = verdict.cpu().numpy()
-    ev, ef = oracle.batch_ipv4_rx_verify(arena.cpu().numpy(), b.descs, nthreads=16)
+    v = down(verdict)
+    ev, ef = oracle.batch_ipv4_rx_verify(down(arena), b.descs, nthreads=16)
     np.testing.assert_array_equal(v, ev)
-    np.testing.assert_array_equal(flags.cpu().numpy(), ef)
+    np.testing.assert_array_equal(down(flags), ef)
     assert (v[bad] == -13).mean() > 0.99
 
 
@@ -350,15 +351,15 @@ def test_ipv4_layout_hints_give_the_same_results(prod, torch, oracle, layout):
         arena = to_dev(torch, host)
         fl = torch.empty(n, dtype=torch.uint8, device="cuda")
         out, _, _ = tc.batch(tc.OP_IPV4, arena, d, n, flags=fl, total_bytes=total, layout=lay)
-        np.testing.assert_array_equal(out.cpu().numpy(), exp)
-        np.testing.assert_array_equal(fl.cpu().numpy(), efl)
+        np.testing.assert_array_equal(down(out), exp)
+        np.testing.assert_array_equal(down(fl), efl)
         rout = torch.empty(n, dtype=torch.uint32, device="cuda")
         _, _, v = tc.batch(tc.OP_IPV4_RX_VERIFY, arena, d, n, out=rout, total_bytes=total, layout=lay)
-        np.testing.assert_array_equal(v.cpu().numpy(), ev)
-        np.testing.assert_array_equal(rout.cpu().numpy(), exp)
+        np.testing.assert_array_equal(down(v), ev)
+        np.testing.assert_array_equal(down(rout), exp)
         tout, tfl, _ = tc.batch(tc.OP_IPV4_TX_OFFLOAD, arena, d, n, total_bytes=total, layout=lay)
         filled = host.copy()
-        tc.tx_apply_batch(filled, pk, tout.cpu().numpy(), tfl.cpu().numpy())
+        tc.tx_apply_batch(filled, pk, down(tout), down(tfl))
         np.testing.assert_array_equal(filled, want)
         tc.batch(tc.OP_IPV4_TX_FILL, arena, d, n, total_bytes=total, layout=lay)
-        np.testing.assert_array_equal(arena.cpu().numpy()[: host.size], want)
+        np.testing.assert_array_equal(down(arena)[: host.size], want)

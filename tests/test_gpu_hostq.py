@@ -24,21 +24,19 @@ def tc():
     return tcp_amd
 
 
-# Every buffer a test has registered stays allocated for the rest of the
-# process after it is unregistered, so its pages are never handed to a later
-# array.  Three suites (rounds 4 and 5) stopped on hipErrorIllegalAddress from
-# the runtime's own pageable host-to-device copy -- twice in
-# tcsum_host_batch_peso's first copy right after a registered fuzz case, once
-# in a torch .cuda() of a fresh 2-MB array some tests after this file's
-# registered cases -- with no kernel in flight; a freed, once-registered range
-# handed to a new array is the one thing they share.
-_RETIRED = []
+# Registered test buffers are freed once unregistered and their pages handed
+# to later arrays, as any stack's would be.  Round 5 kept them instead, one
+# of its measures against the hipErrorIllegalAddress stops; the runtime does
+# not fault that way (scripts/register_reuse_probe.py: 10,000 register / GPU
+# read / unregister / free / pinned-alloc cycles between pageable copies,
+# clean), and the GPU suite with every round-4 pageable path back ran clean
+# (profiles/r06/).
+from devcopy import down  # noqa: E402
 
 
 class _Registered:
     """Pageable memory pinned in place with tcsum_host_register (the way the
-    stack would pin its static block pool, pktbuf.c:13); unpinned on release,
-    its pages then kept (_RETIRED)."""
+    stack would pin its static block pool, pktbuf.c:13); unpinned on release."""
 
     def __init__(self, tc, n):
         self.tc = tc
@@ -52,7 +50,6 @@ class _Registered:
             self.tc.host_unregister(self.region)
         except Exception:
             pass
-        _RETIRED.append(self.raw)
 
 
 def host_copy(tc, data: np.ndarray, where: str, shift: int = 0):
@@ -126,7 +123,7 @@ def test_host_queue_matches_device(tc, oracle, n, where):
     from tcp_amd import workload
     b = workload.make_batch("mixed_tx", n=n)
     arena, descs = workload.materialize(b)  # unfilled frames, generated on the GPU
-    raw = arena.cpu().numpy()
+    raw = down(arena)
     # pinned: read/written in place; pageable (> 16 MiB and > 64K packets at the
     # largest n): threaded staging copy, header windows copied back
     ha = tc.HostArena(raw.size) if where == "pinned" else None
@@ -136,7 +133,7 @@ def test_host_queue_matches_device(tc, oracle, n, where):
     tc.host_batch_ipv4_tx_fill(arg, b.descs)
     tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes)
     torch.cuda.synchronize()
-    np.testing.assert_array_equal(view, arena.cpu().numpy())
+    np.testing.assert_array_equal(view, down(arena))
     verdict, _, _ = tc.host_batch_ipv4_rx_verify(arg, b.descs)
     assert (verdict == 0).all()
     pos = (b.descs["offset"] + 20 + (np.arange(n) * 7919) % (b.descs["len"] - 20)).astype(np.int64)
@@ -227,7 +224,7 @@ def test_host_tx_fill_copy_engine_path(tc, oracle, dbg, where):
     from tcp_amd import workload
     b = workload.make_batch("mixed_tx", n=30000)  # ~140 MB: pieces of 64 and 128 MiB
     dev, _ = workload.materialize(b)
-    unfilled = dev.cpu().numpy()
+    unfilled = down(dev)
     want = unfilled.copy()
     wfl = oracle.batch_ipv4_tx_fill(want, b.descs, nthreads=8)
     ha = tc.HostArena(unfilled.size) if where == "pinned" else None
@@ -275,10 +272,10 @@ def test_host_pinned_copy_engine_path(tc, oracle, dbg, mode, where):
     ha = tc.HostArena(b.alloc_bytes) if where == "pinned" else None
     try:
         if ha is not None:
-            ha.array[:] = dev.cpu().numpy()
+            ha.array[:] = down(dev)
             arg, host = ha, ha.array
         else:
-            host = dev.cpu().numpy().copy()
+            host = down(dev).copy()
             arg = host
         if mode == "rx":
             v_dma, o_dma, f_dma = tc.host_batch_ipv4_rx_verify(arg, b.descs)

@@ -11,6 +11,7 @@ and then call every batch entry point: each must return OK with the oracle's
 results, and leave the caller's error where it was (the library neither
 consumes nor replaces it).  They also check the other direction: a call that
 polls its own stream while the kernel runs leaves a clear slot clear."""
+from devcopy import down
 import ctypes
 import os
 import subprocess
@@ -113,11 +114,11 @@ def mixed(tc, oracle):
     from tcp_amd import workload
     b = workload.make_batch("mixed", n=3000)
     arena, descs = workload.materialize(b)
-    host = arena.cpu().numpy()
+    host = down(arena)
     eo, ef = oracle.batch_ipv4(host, b.descs, nthreads=8)
     p = workload.make_batch("mtu", n=5000)
     parena, pdescs = workload.materialize(p)
-    phost = parena.cpu().numpy()
+    phost = down(parena)
     pe = oracle.batch_peso(phost, p.descs, nthreads=8)
     torch.cuda.synchronize()
     return dict(b=b, arena=arena, descs=descs, host=host, eo=eo, ef=ef,
@@ -143,12 +144,12 @@ def test_device_batches_with_a_dirty_slot(tc, hip, oracle, mixed, dirt):
     run("ipv4 offload", lambda: tc.batch_ipv4_tx_offload(m["arena"], m["descs"], b.n, b.total_bytes)[0])
     run("ipv4 rx", lambda: tc.batch_ipv4_rx_verify(m["arena"], m["descs"], b.n, b.total_bytes)[0])
     for name, got in checks:
-        got = got.cpu().numpy()
+        got = down(got)
         if name.startswith("peso"):
             np.testing.assert_array_equal(got, m["pe"], err_msg=name)
         elif name == "ipv4 sums":
             np.testing.assert_array_equal(got, m["eo"], err_msg=name)
-    rx = checks[-1][1].cpu().numpy()
+    rx = down(checks[-1][1])
     ev, _ = oracle.batch_ipv4_rx_verify(m["host"], b.descs, nthreads=8)
     np.testing.assert_array_equal(rx, ev)
     # the tx fill (both forms) on a copy: bytes equal the oracle's fill
@@ -161,14 +162,14 @@ def test_device_batches_with_a_dirty_slot(tc, hip, oracle, mixed, dirt):
             expect = _dirty(hip, dirt)
             tc.batch_ipv4_tx_fill(a, m["descs"], b.n, b.total_bytes, flags=fl)
             _after(hip, expect)
-        np.testing.assert_array_equal(a.cpu().numpy(), want, err_msg=f"tx fill split={split}")
+        np.testing.assert_array_equal(down(a), want, err_msg=f"tx fill split={split}")
     a = m["arena"].clone()
     scratch = torch.empty(8 * b.n, dtype=torch.uint8, device="cuda")
     fl = torch.empty(b.n, dtype=torch.uint8, device="cuda")
     expect = _dirty(hip, dirt)
     tc.batch_ipv4_tx_fill(a, m["descs"], b.n, b.total_bytes, scratch=scratch, flags=fl)
     _after(hip, expect)
-    np.testing.assert_array_equal(a.cpu().numpy(), want, err_msg="tx fill scratch")
+    np.testing.assert_array_equal(down(a), want, err_msg="tx fill scratch")
 
 
 @pytest.mark.parametrize("dirt", DIRT)

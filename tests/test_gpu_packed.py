@@ -8,6 +8,7 @@ ranges lies inside that region; any other workgroup goes range by range.
 Both paths and their mix inside one batch are checked bit for bit, with
 ranges starting at every byte parity and chunk phase.
 """
+from devcopy import down, up
 import numpy as np
 import pytest
 
@@ -68,8 +69,8 @@ def test_packed_mtu_vs_oracle(tc, torch, oracle, packed, n, start):
     lens = np.full(n, 1500, np.uint32)
     host = _arena(rng, start + 1500 * n + 4096)
     p = _peso(tc, _packed_offs(lens, start), lens, rng)
-    out = tc.batch_peso(torch.from_numpy(host).pin_memory().cuda(), tc.descs_to_device(p), n, int(lens.sum()))
-    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
+    out = tc.batch_peso(up(torch.from_numpy(host)), tc.descs_to_device(p), n, int(lens.sum()))
+    np.testing.assert_array_equal(down(out), oracle.batch_peso(host, p, nthreads=8))
 
 
 @pytest.mark.parametrize("seed", range(6))
@@ -84,8 +85,8 @@ def test_packed_ragged_lengths(tc, torch, oracle, packed, seed):
     host = _arena(rng, start + int(lens.sum()) + 4096)
     p = _peso(tc, _packed_offs(lens, start), lens, rng)
     hint = int(rng.choice([int(lens.sum()), 1500 * n, 700 * n]))  # K from the hint only
-    out = tc.batch_peso(torch.from_numpy(host).pin_memory().cuda(), tc.descs_to_device(p), n, hint)
-    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
+    out = tc.batch_peso(up(torch.from_numpy(host)), tc.descs_to_device(p), n, hint)
+    np.testing.assert_array_equal(down(out), oracle.batch_peso(host, p, nthreads=8))
 
 
 LAYOUTS = ["short", "tiny", "gap", "aligned", "overlap", "duplicate", "zero", "reversed", "far", "shuffled"]
@@ -129,8 +130,8 @@ def test_packed_irregular_layouts(tc, torch, oracle, packed, layout):
         offs, lens = offs[perm], lens[perm]
     host = _arena(rng, int((offs + lens).max()) + 4096)
     p = _peso(tc, offs.astype(np.uint64), lens.astype(np.uint32), rng)
-    out = tc.batch_peso(torch.from_numpy(host).pin_memory().cuda(), tc.descs_to_device(p), n, int(lens.sum()))
-    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
+    out = tc.batch_peso(up(torch.from_numpy(host)), tc.descs_to_device(p), n, int(lens.sum()))
+    np.testing.assert_array_equal(down(out), oracle.batch_peso(host, p, nthreads=8))
 
 
 @pytest.mark.parametrize("hint_mean", [300, 1500, 9000])
@@ -144,8 +145,8 @@ def test_packed_multi_pass_regions(tc, torch, oracle, packed, hint_mean):
     start = int(rng.integers(0, 16))
     host = _arena(rng, start + int(lens.sum()) + 4096)
     p = _peso(tc, _packed_offs(lens, start), lens, rng)
-    out = tc.batch_peso(torch.from_numpy(host).pin_memory().cuda(), tc.descs_to_device(p), n, hint_mean * n)
-    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
+    out = tc.batch_peso(up(torch.from_numpy(host)), tc.descs_to_device(p), n, hint_mean * n)
+    np.testing.assert_array_equal(down(out), oracle.batch_peso(host, p, nthreads=8))
 
 
 def test_packed_long_range_word_sum_past_2_32(tc, torch, oracle, packed):
@@ -161,8 +162,8 @@ def test_packed_long_range_word_sum_past_2_32(tc, torch, oracle, packed):
     for i in (37, 150):
         host[int(offs[i]): int(offs[i]) + int(lens[i])] = 0xFF
     p = _peso(tc, offs, lens, rng)
-    out = tc.batch_peso(torch.from_numpy(host).pin_memory().cuda(), tc.descs_to_device(p), n, 1500 * n)
-    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
+    out = tc.batch_peso(up(torch.from_numpy(host)), tc.descs_to_device(p), n, 1500 * n)
+    np.testing.assert_array_equal(down(out), oracle.batch_peso(host, p, nthreads=8))
 
 
 @pytest.mark.parametrize("comp", [0, 1])
@@ -176,8 +177,8 @@ def test_packed_segments_mode(tc, torch, oracle, packed, comp):
     s = np.zeros(n, tc.SEG_DTYPE)
     s["offset"], s["len"] = _packed_offs(lens, 3), lens
     s["pre_sum"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
-    out = tc.batch_segments(torch.from_numpy(host).pin_memory().cuda(), tc.descs_to_device(s), n, comp, int(lens.sum()))
-    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_segments(host, s, comp, nthreads=8))
+    out = tc.batch_segments(up(torch.from_numpy(host)), tc.descs_to_device(s), n, comp, int(lens.sum()))
+    np.testing.assert_array_equal(down(out), oracle.batch_segments(host, s, comp, nthreads=8))
 
 
 def test_packed_exact_region_edges(tc, torch, oracle, packed):
@@ -191,8 +192,8 @@ def test_packed_exact_region_edges(tc, torch, oracle, packed):
         lens = np.full(n, L, np.uint32)
         host = _arena(rng, start + L * n + 4096)
         p = _peso(tc, _packed_offs(lens, start), lens, rng)
-        out = tc.batch_peso(torch.from_numpy(host).pin_memory().cuda(), tc.descs_to_device(p), n, L * n)
-        np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
+        out = tc.batch_peso(up(torch.from_numpy(host)), tc.descs_to_device(p), n, L * n)
+        np.testing.assert_array_equal(down(out), oracle.batch_peso(host, p, nthreads=8))
 
 
 def test_packed_full_mtu_config(tc, torch, oracle, packed):
@@ -201,8 +202,8 @@ def test_packed_full_mtu_config(tc, torch, oracle, packed):
     from tcp_amd import workload
     b = workload.make_batch("mtu")
     arena, descs = workload.materialize(b)
-    out = tc.batch_peso(arena, descs, b.n, b.total_bytes).cpu().numpy()
-    np.testing.assert_array_equal(out, oracle.batch_peso(arena.cpu().numpy(), b.descs, nthreads=16))
+    out = down(tc.batch_peso(arena, descs, b.n, b.total_bytes))
+    np.testing.assert_array_equal(out, oracle.batch_peso(down(arena), b.descs, nthreads=16))
 
 
 @pytest.mark.parametrize("seed", range(16))
@@ -228,17 +229,17 @@ def test_packed_fuzz(tc, torch, oracle, seed):
         offs[a:b], lens[a:b] = offs[perm], lens[perm]
     size = int((offs + lens).max()) + 4096
     host = _arena(rng, size)
-    arena = torch.from_numpy(host).pin_memory().cuda()
+    arena = up(torch.from_numpy(host))
     hint = int(rng.choice([int(lens.sum()), 300 * n, 1500 * n, 4000 * n]))
     p = _peso(tc, offs.astype(np.uint64), lens.astype(np.uint32), rng)
     out = tc.batch_peso(arena, tc.descs_to_device(p), n, hint)
-    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_peso(host, p, nthreads=8))
+    np.testing.assert_array_equal(down(out), oracle.batch_peso(host, p, nthreads=8))
     s = np.zeros(n, tc.SEG_DTYPE)
     s["offset"], s["len"] = offs, lens
     s["pre_sum"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
     comp = int(rng.integers(0, 2))
     out = tc.batch_segments(arena, tc.descs_to_device(s), n, comp, hint)
-    np.testing.assert_array_equal(out.cpu().numpy(), oracle.batch_segments(host, s, comp, nthreads=8))
+    np.testing.assert_array_equal(down(out), oracle.batch_segments(host, s, comp, nthreads=8))
 
 
 HINT_LAYOUTS = ["mtu", "shuffled", "ragged_gaps", "shuffled576", "shuffled4000"]
@@ -264,7 +265,7 @@ def test_layout_hints_give_the_same_results(tc, torch, oracle, layout):
     if layout.startswith("shuffled"):
         p = p[rng.permutation(n)]
     want = oracle.batch_peso(host, p, nthreads=8)
-    arena = torch.from_numpy(host).pin_memory().cuda()
+    arena = up(torch.from_numpy(host))
     d = tc.descs_to_device(p)
     s = np.zeros(n, tc.SEG_DTYPE)
     s["offset"], s["len"] = p["offset"], p["len"]
@@ -273,6 +274,6 @@ def test_layout_hints_give_the_same_results(tc, torch, oracle, layout):
     want_s = oracle.batch_segments(host, s, 1, nthreads=8)
     for lay in (tc.LAYOUT_UNKNOWN, tc.LAYOUT_ORDERED, tc.LAYOUT_SHUFFLED):
         out, _, _ = tc.batch(tc.OP_PESO, arena, d, n, total_bytes=int(lens.sum()), layout=lay)
-        np.testing.assert_array_equal(out.cpu().numpy(), want)
+        np.testing.assert_array_equal(down(out), want)
         out, _, _ = tc.batch(tc.OP_SEGMENTS_COMP, arena, ds, n, total_bytes=int(lens.sum()), layout=lay)
-        np.testing.assert_array_equal(out.cpu().numpy(), want_s)
+        np.testing.assert_array_equal(down(out), want_s)

@@ -7,6 +7,7 @@ Every call goes through libtcsum.so's C ABI.  Expected values come from
   * the CPU oracle (oracle/, pinned to those fixtures) on seeded inputs.
 The bar is bit-exact: these are 16-bit integer results.
 """
+from devcopy import down, up
 import ctypes
 import os
 
@@ -65,7 +66,7 @@ def geometry(knobs):
 def to_dev(torch, a: np.ndarray, pad: int = 64):
     t = torch.zeros(a.nbytes + pad, dtype=torch.uint8)
     t[: a.nbytes] = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1))
-    return t.pin_memory().cuda()
+    return up(t)
 
 
 def test_native_library_is_loaded(tc):
@@ -236,7 +237,7 @@ def test_batch_peso_golden(tc, torch, geometry, g, u):
     arena = to_dev(torch, pool)
     d = peso_descs(tc, cases)
     out = tc.batch_peso(arena, tc.descs_to_device(d), d.size, int(d["len"].sum()))
-    np.testing.assert_array_equal(out.cpu().numpy(), cases["expected"].astype(np.uint16))
+    np.testing.assert_array_equal(down(out), cases["expected"].astype(np.uint16))
 
 
 
@@ -253,17 +254,17 @@ def test_xcd_block_order_golden(tc, torch, geometry, knobs, xg):
     out = torch.empty(d.size, dtype=torch.uint16, device="cuda")
     out.view(torch.int16).fill_(-0x5556)  # 0xAAAA: a result nobody wrote shows up
     tc.batch_peso(to_dev(torch, pool), tc.descs_to_device(d), d.size, out=out)
-    np.testing.assert_array_equal(out.cpu().numpy(), cases["expected"].astype(np.uint16))
+    np.testing.assert_array_equal(down(out), cases["expected"].astype(np.uint16))
     geometry(16, 4)
     cases, ipool = G.ipv4_rx_cases()
     pk = G.pkt_descs(cases, tc.PKT_DTYPE)
     verdict, flags = tc.batch_ipv4_rx_verify(to_dev(torch, ipool), tc.descs_to_device(pk), cases.size)
-    np.testing.assert_array_equal(verdict.cpu().numpy(), cases["verdict"])
-    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+    np.testing.assert_array_equal(down(verdict), cases["verdict"])
+    np.testing.assert_array_equal(down(flags), cases["flags"])
     cases, pin, pout = G.ipv4_tx_cases()
     arena = to_dev(torch, pin)
     tc.batch_ipv4_tx_fill(arena, tc.descs_to_device(G.pkt_descs(cases, tc.PKT_DTYPE)), cases.size)
-    np.testing.assert_array_equal(arena.cpu().numpy()[: pout.size], pout)
+    np.testing.assert_array_equal(down(arena)[: pout.size], pout)
 
 @pytest.mark.parametrize("g,u", [(32, 6), (16, 4), (1024, 4)])
 def test_batch_segments_golden(tc, torch, geometry, g, u):
@@ -288,7 +289,7 @@ def test_batch_segments_golden(tc, torch, geometry, g, u):
         s["pre_sum"][k.size:] = f["pre_sum"]
         exp = np.concatenate([k["expected"], f["expected"]]).astype(np.uint16)
         out = tc.batch_segments(arena, tc.descs_to_device(s), s.size, comp, int(s["len"].sum()))
-        np.testing.assert_array_equal(out.cpu().numpy(), exp)
+        np.testing.assert_array_equal(down(out), exp)
 
 
 @pytest.mark.parametrize("g,u", GEOMS_IP)
@@ -300,10 +301,10 @@ def test_batch_ipv4_golden(tc, torch, geometry, g, u):
     pk["offset"] = cases["pool_off"]
     pk["len"] = cases["frame_len"]
     out, flags = tc.batch_ipv4(arena, tc.descs_to_device(pk), pk.size, int(pk["len"].sum()))
-    out = out.cpu().numpy()
+    out = down(out)
     np.testing.assert_array_equal(out & 0xFFFF, cases["ip"])
     np.testing.assert_array_equal(out >> 16, cases["l4"])
-    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+    np.testing.assert_array_equal(down(flags), cases["flags"])
 
 
 @pytest.mark.parametrize("mean", [0, 64, 300, 1500, 9000, 70000])
@@ -315,10 +316,10 @@ def test_batch_ipv4_every_picked_geometry(tc, torch, mean):
     pk["offset"] = cases["pool_off"]
     pk["len"] = cases["frame_len"]
     out, flags = tc.batch_ipv4(arena, tc.descs_to_device(pk), pk.size, mean * pk.size)
-    out = out.cpu().numpy()
+    out = down(out)
     np.testing.assert_array_equal(out & 0xFFFF, cases["ip"])
     np.testing.assert_array_equal(out >> 16, cases["l4"])
-    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+    np.testing.assert_array_equal(down(flags), cases["flags"])
 
 
 @pytest.mark.parametrize("mean", [0, 20, 64, 300, 1500, 9000, 70000])
@@ -328,7 +329,7 @@ def test_batch_peso_every_picked_geometry(tc, torch, mean):
     arena = to_dev(torch, pool)
     d = peso_descs(tc, cases)
     out = tc.batch_peso(arena, tc.descs_to_device(d), d.size, mean * d.size)
-    np.testing.assert_array_equal(out.cpu().numpy(), cases["expected"].astype(np.uint16))
+    np.testing.assert_array_equal(down(out), cases["expected"].astype(np.uint16))
 
 
 def test_ipv4_odd_arena_base(tc, torch):
@@ -339,10 +340,10 @@ def test_ipv4_odd_arena_base(tc, torch):
     pk["offset"] = cases["pool_off"].astype(np.uint64) + 1
     pk["len"] = cases["frame_len"]
     out, flags = tc.batch_ipv4(arena, tc.descs_to_device(pk), pk.size)
-    out = out.cpu().numpy()
+    out = down(out)
     np.testing.assert_array_equal(out & 0xFFFF, cases["ip"])
     np.testing.assert_array_equal(out >> 16, cases["l4"])
-    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+    np.testing.assert_array_equal(down(flags), cases["flags"])
 
 
 TX_FORMS = ["fused", "deferred"]
@@ -365,10 +366,10 @@ def test_batch_ipv4_tx_fill_golden(tc, torch, geometry, knobs, g, u, form):
     arena = to_dev(torch, pin)
     d = tc.descs_to_device(G.pkt_descs(cases, tc.PKT_DTYPE))
     flags = tc.batch_ipv4_tx_fill(arena, d, cases.size, int(cases["frame_len"].sum()))
-    np.testing.assert_array_equal(arena.cpu().numpy()[: pout.size], pout)
-    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+    np.testing.assert_array_equal(down(arena)[: pout.size], pout)
+    np.testing.assert_array_equal(down(flags), cases["flags"])
     flags = tc.batch_ipv4_tx_fill(arena, d, cases.size)  # idempotent: fields read as zero
-    np.testing.assert_array_equal(arena.cpu().numpy()[: pout.size], pout)
+    np.testing.assert_array_equal(down(arena)[: pout.size], pout)
 
 
 @pytest.mark.parametrize("form", TX_FORMS)
@@ -386,12 +387,12 @@ def test_batch_ipv4_tx_fill_stack_golden(tc, torch, geometry, knobs, g, u, form)
     arena = to_dev(torch, pin)
     d = tc.descs_to_device(pk)
     flags = tc.batch_ipv4_tx_fill(arena, d, cases.size, int(cases["frame_len"].sum()))
-    np.testing.assert_array_equal(arena.cpu().numpy()[: pout.size], pout)
-    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+    np.testing.assert_array_equal(down(arena)[: pout.size], pout)
+    np.testing.assert_array_equal(down(flags), cases["flags"])
     arena = to_dev(torch, pin)
     out, flags = tc.batch_ipv4_tx_offload(arena, d, cases.size, int(cases["frame_len"].sum()))
     host = pin.copy()
-    tc.tx_apply_batch(host, pk, out.cpu().numpy(), flags.cpu().numpy())
+    tc.tx_apply_batch(host, pk, down(out), down(flags))
     np.testing.assert_array_equal(host[: pout.size], pout)
 
 
@@ -405,14 +406,14 @@ def test_batch_ipv4_tx_offload_golden(tc, torch, geometry, g, u):
     arena = to_dev(torch, pin)
     d = tc.descs_to_device(G.pkt_descs(cases, tc.PKT_DTYPE))
     out, flags = tc.batch_ipv4_tx_offload(arena, d, cases.size, int(cases["frame_len"].sum()))
-    np.testing.assert_array_equal(arena.cpu().numpy()[: pin.size], pin)
-    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+    np.testing.assert_array_equal(down(arena)[: pin.size], pin)
+    np.testing.assert_array_equal(down(flags), cases["flags"])
     host = pin.copy()
-    tc.tx_apply_batch(host, G.pkt_descs(cases, tc.PKT_DTYPE), out.cpu().numpy(), flags.cpu().numpy())
+    tc.tx_apply_batch(host, G.pkt_descs(cases, tc.PKT_DTYPE), down(out), down(flags))
     np.testing.assert_array_equal(host[: pout.size], pout)
     fill_out = torch.empty(cases.size, dtype=torch.uint32, device="cuda")
     tc.batch_ipv4_tx_fill(arena, d, cases.size, out=fill_out)
-    np.testing.assert_array_equal(out.cpu().numpy(), fill_out.cpu().numpy())
+    np.testing.assert_array_equal(down(out), down(fill_out))
 
 
 @pytest.mark.parametrize("form", TX_FORMS)
@@ -448,8 +449,8 @@ def test_tx_fill_neighbours(tc, torch, oracle, knobs, layout, top, form):
     wfl = oracle.batch_ipv4_tx_fill(want, pk)
     d_arena = to_dev(torch, arena)
     fl = tc.batch_ipv4_tx_fill(d_arena, tc.descs_to_device(pk), n, int(lens.sum()))
-    np.testing.assert_array_equal(fl.cpu().numpy(), wfl)
-    np.testing.assert_array_equal(d_arena.cpu().numpy()[: arena.size], want)
+    np.testing.assert_array_equal(down(fl), wfl)
+    np.testing.assert_array_equal(down(d_arena)[: arena.size], want)
 
 
 def test_tx_offload_full_mixed(tc, torch, knobs):
@@ -461,8 +462,8 @@ def test_tx_offload_full_mixed(tc, torch, knobs):
     arena, descs = workload.materialize(b)
     unfilled = arena.clone()
     out, flags = tc.batch_ipv4_tx_offload(arena, descs, b.n, b.total_bytes)
-    host = torch.from_numpy(arena.cpu().numpy())
-    tc.tx_apply_batch(host.numpy(), b.descs, out.cpu().numpy(), flags.cpu().numpy())
+    host = torch.from_numpy(down(arena))
+    tc.tx_apply_batch(host.numpy(), b.descs, down(out), down(flags))
     want = host.to(arena.device)
     del host
     fill_out = torch.empty_like(out)
@@ -485,10 +486,10 @@ def test_batch_ipv4_rx_verify_golden(tc, torch, oracle, geometry, g, u):
     pk = G.pkt_descs(cases, tc.PKT_DTYPE)
     out = torch.empty(cases.size, dtype=torch.uint32, device="cuda")
     verdict, flags = tc.batch_ipv4_rx_verify(arena, tc.descs_to_device(pk), cases.size, out=out)
-    np.testing.assert_array_equal(verdict.cpu().numpy(), cases["verdict"])
-    np.testing.assert_array_equal(flags.cpu().numpy(), cases["flags"])
+    np.testing.assert_array_equal(down(verdict), cases["verdict"])
+    np.testing.assert_array_equal(down(flags), cases["flags"])
     exp, _ = oracle.batch_ipv4(pool, pk)
-    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+    np.testing.assert_array_equal(down(out), exp)
 
 
 def test_tx_then_rx_full_mixed(tc, torch, oracle):
@@ -499,19 +500,19 @@ def test_tx_then_rx_full_mixed(tc, torch, oracle):
     arena, descs = workload.materialize(b)
     tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes)
     verdict, _ = tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes)
-    assert (verdict.cpu().numpy() == 0).all()
+    assert (down(verdict) == 0).all()
     rng = np.random.default_rng(5)
     bad = rng.choice(b.n, 2000, replace=False)
     pos = (b.descs["offset"][bad] + 20 + (rng.integers(0, 1 << 30, bad.size) % (b.descs["len"][bad] - 20))).astype(np.int64)
-    idx = torch.from_numpy(pos).pin_memory().cuda()
+    idx = up(torch.from_numpy(pos))
     arena[idx] ^= 0x04
     verdict, flags = tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes)
-    v = verdict.cpu().numpy()
+    v = down(verdict)
     assert (v[bad] == -13).mean() > 0.99 and (np.delete(v, bad) == 0).all()
-    host = arena.cpu().numpy()
+    host = down(arena)
     ev, ef = oracle.batch_ipv4_rx_verify(host, b.descs, nthreads=16)
     np.testing.assert_array_equal(v, ev)
-    np.testing.assert_array_equal(flags.cpu().numpy(), ef)
+    np.testing.assert_array_equal(down(flags), ef)
 
 
 # ------------------------------------------------- seeded batches vs oracle
@@ -531,16 +532,16 @@ def run_config(tc, torch, config, n):
 @pytest.mark.parametrize("config,n", [("mtu", 50000), ("tso", 600), ("mixed", 20000), ("mixed_aligned", 20000)])
 def test_config_vs_oracle(tc, torch, oracle, config, n):
     b, arena, out = run_config(tc, torch, config, n)
-    host = arena.cpu().numpy()
+    host = down(arena)
     # the device generator is the oracle's stream
     np.testing.assert_array_equal(host[:4096], oracle.synth_fill(b.byte_base, 4096, b.seed)[:4096]
                                   if b.kind == "peso" else host[:4096])
     if b.kind == "peso":
         exp = oracle.batch_peso(host, b.descs, nthreads=8)
-        np.testing.assert_array_equal(out.cpu().numpy(), exp)
+        np.testing.assert_array_equal(down(out), exp)
     else:
         exp, fl = oracle.batch_ipv4(host, b.descs, nthreads=8)
-        np.testing.assert_array_equal(out.cpu().numpy(), exp)
+        np.testing.assert_array_equal(down(out), exp)
         assert (fl == 0).all()  # synthetic headers are well formed
 
 
@@ -548,8 +549,8 @@ def test_config_vs_oracle(tc, torch, oracle, config, n):
 def test_geometries_vs_oracle(tc, torch, oracle, geometry, g, u):
     geometry(g, u)
     b, arena, out = run_config(tc, torch, "mtu", 4096)
-    exp = oracle.batch_peso(arena.cpu().numpy(), b.descs, nthreads=8)
-    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+    exp = oracle.batch_peso(down(arena), b.descs, nthreads=8)
+    np.testing.assert_array_equal(down(out), exp)
 
 
 def test_edge_segments(tc, torch, oracle):
@@ -571,9 +572,9 @@ def test_edge_segments(tc, torch, oracle):
     s["len"] = [n for _, n in segs]
     s["pre_sum"] = rng.integers(0, 1 << 32, len(segs), dtype=np.uint64).astype(np.uint32)
     s["pre_sum"][:12] = 0
-    arena = torch.from_numpy(host).pin_memory().cuda()  # no padding: the last chunk ends the allocation
+    arena = up(torch.from_numpy(host))  # no padding: the last chunk ends the allocation
     for comp in (0, 1):
-        out = tc.batch_segments(arena, tc.descs_to_device(s), s.size, comp).cpu().numpy()
+        out = down(tc.batch_segments(arena, tc.descs_to_device(s), s.size, comp))
         exp = oracle.batch_segments(host, s, comp, nthreads=8)
         np.testing.assert_array_equal(out, exp)
     assert exp[10] == 0  # the 0xFFFF-folding range, complemented
@@ -583,7 +584,7 @@ def test_edge_segments(tc, torch, oracle):
     p["src"] = rng.integers(0, 256, (len(segs), 4))
     p["dst"] = rng.integers(0, 256, (len(segs), 4))
     p["protocol"] = rng.choice([6, 17], len(segs))
-    out = tc.batch_peso(arena, tc.descs_to_device(p), p.size).cpu().numpy()
+    out = down(tc.batch_peso(arena, tc.descs_to_device(p), p.size))
     np.testing.assert_array_equal(out, oracle.batch_peso(host, p, nthreads=8))
 
 
@@ -599,9 +600,9 @@ def test_unsorted_overlapping_duplicate_descriptors(tc, torch, oracle):
     p["src"] = rng.integers(0, 256, (n, 4))
     p["dst"] = rng.integers(0, 256, (n, 4))
     p["protocol"] = rng.choice([6, 17, 1, 99], n)
-    arena = torch.from_numpy(host).pin_memory().cuda()
+    arena = up(torch.from_numpy(host))
     for mean in (0, 64, 1500, 70000):
-        out = tc.batch_peso(arena, tc.descs_to_device(p), n, mean * n).cpu().numpy()
+        out = down(tc.batch_peso(arena, tc.descs_to_device(p), n, mean * n))
         np.testing.assert_array_equal(out, oracle.batch_peso(host, p, nthreads=8))
 
 
@@ -619,13 +620,13 @@ def test_hip_graph_capture_and_replay(tc, torch, oracle):
     out.zero_()
     g.replay()
     torch.cuda.synchronize()
-    exp = oracle.batch_peso(arena.cpu().numpy(), b.descs, nthreads=8)
-    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+    exp = oracle.batch_peso(down(arena), b.descs, nthreads=8)
+    np.testing.assert_array_equal(down(out), exp)
     arena[: b.n * 1500].view(b.n, 1500)[:, 40] ^= 1  # new bytes, same graph
     g.replay()
     torch.cuda.synchronize()
-    exp2 = oracle.batch_peso(arena.cpu().numpy(), b.descs, nthreads=8)
-    np.testing.assert_array_equal(out.cpu().numpy(), exp2)
+    exp2 = oracle.batch_peso(down(arena), b.descs, nthreads=8)
+    np.testing.assert_array_equal(down(out), exp2)
     assert (exp2 != exp).mean() > 0.99
 
 
@@ -637,7 +638,7 @@ def test_hip_graph_capture_tx_fill(tc, torch, oracle):
     b = workload.make_batch("mixed_tx", n=140000)
     arena, descs = workload.materialize(b)
     unfilled = arena.clone()
-    want = arena.cpu().numpy()
+    want = down(arena)
     oracle.batch_ipv4_tx_fill(want, b.descs, nthreads=8)
     s = torch.cuda.Stream()
     torch.cuda.synchronize()
@@ -648,7 +649,7 @@ def test_hip_graph_capture_tx_fill(tc, torch, oracle):
         arena.copy_(unfilled)
         g.replay()
         torch.cuda.synchronize()
-        np.testing.assert_array_equal(arena.cpu().numpy(), want)
+        np.testing.assert_array_equal(down(arena), want)
 
 
 def test_hip_graph_capture_tx_fill_scratch(tc, torch, oracle):
@@ -660,18 +661,18 @@ def test_hip_graph_capture_tx_fill_scratch(tc, torch, oracle):
     b = workload.make_batch("mixed_tx", n=140000)
     arena, descs = workload.materialize(b)
     unfilled = arena.clone()
-    want = arena.cpu().numpy()
+    want = down(arena)
     oracle.batch_ipv4_tx_fill(want, b.descs, nthreads=8)
     scratch = torch.empty(8 * b.n, dtype=torch.uint8, device="cuda")
     out = torch.empty(b.n, dtype=torch.uint32, device="cuda")
     ref_out = torch.empty_like(out)
     tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, out=ref_out, want_flags=False)
     torch.cuda.synchronize()
-    assert np.array_equal(arena.cpu().numpy(), want)
+    assert np.array_equal(down(arena), want)
     arena.copy_(unfilled)
     tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False, scratch=scratch)  # no graph
     torch.cuda.synchronize()
-    assert np.array_equal(arena.cpu().numpy(), want)
+    assert np.array_equal(down(arena), want)
     s = torch.cuda.Stream()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
@@ -682,7 +683,7 @@ def test_hip_graph_capture_tx_fill_scratch(tc, torch, oracle):
         out.zero_()
         g.replay()
         torch.cuda.synchronize()
-        np.testing.assert_array_equal(arena.cpu().numpy(), want)
+        np.testing.assert_array_equal(down(arena), want)
         assert torch.equal(out, ref_out)
 
 
@@ -704,9 +705,9 @@ def test_concurrent_streams(tc, torch, oracle):
                 tc.batch_ipv4(arena, descs, b.n, b.total_bytes, out=o, want_flags=False, stream=st)
     torch.cuda.synchronize()
     for b, (arena, _), o in zip(bs, mats, outs):
-        host = arena.cpu().numpy()
+        host = down(arena)
         exp = oracle.batch_peso(host, b.descs) if b.kind == "peso" else oracle.batch_ipv4(host, b.descs)[0]
-        np.testing.assert_array_equal(o.cpu().numpy(), exp)
+        np.testing.assert_array_equal(down(o), exp)
 
 
 def test_huge_batch_index_math(tc, torch, oracle, geometry):
@@ -721,11 +722,11 @@ def test_huge_batch_index_math(tc, torch, oracle, geometry):
     s["offset"] = rng.integers(0, (1 << 16) - 40, n)
     s["len"] = rng.integers(0, 33, n)
     s["pre_sum"] = rng.integers(0, 1 << 16, n)
-    arena = torch.from_numpy(host).pin_memory().cuda()
+    arena = up(torch.from_numpy(host))
     d = tc.descs_to_device(s)
     out = tc.batch_segments(arena, d, n, 1)
     exp = oracle.batch_segments(host, s, 1, nthreads=16)
-    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+    np.testing.assert_array_equal(down(out), exp)
 
 
 def test_huge_ipv4_batch_index_math(tc, torch, oracle, geometry):
@@ -750,27 +751,27 @@ def test_huge_ipv4_batch_index_math(tc, torch, oracle, geometry):
     spk = np.zeros(idx.size, tc.PKT_DTYPE)
     spk["offset"] = np.arange(idx.size, dtype=np.uint64) * np.uint64(L)
     spk["len"] = L
-    arena = torch.from_numpy(host.reshape(-1)).pin_memory().cuda()
+    arena = up(torch.from_numpy(host.reshape(-1)))
     del host
     d = tc.descs_to_device(pk)
-    tidx = torch.from_numpy(idx).pin_memory().cuda()
+    tidx = up(torch.from_numpy(idx))
 
     out, flags = tc.batch_ipv4(arena, d, n, n * L)
     eo, ef = oracle.batch_ipv4(sample, spk)
-    np.testing.assert_array_equal(out.view(torch.int32)[tidx].cpu().numpy().view(np.uint32), eo)
-    np.testing.assert_array_equal(flags[tidx].cpu().numpy(), ef)
+    np.testing.assert_array_equal(down(out.view(torch.int32)[tidx]).view(np.uint32), eo)
+    np.testing.assert_array_equal(down(flags[tidx]), ef)
     del out, flags
 
     tflags = tc.batch_ipv4_tx_fill(arena, d, n, n * L)  # >= 131,072 packets: deferred stores
     efl = oracle.batch_ipv4_tx_fill(sample, spk)  # sample is filled in place
-    np.testing.assert_array_equal(tflags[tidx].cpu().numpy(), efl)
-    got = arena.view(n, L)[tidx].cpu().numpy().reshape(-1)
+    np.testing.assert_array_equal(down(tflags[tidx]), efl)
+    got = down(arena.view(n, L)[tidx]).reshape(-1)
     np.testing.assert_array_equal(got, sample)
 
     verdict, vflags = tc.batch_ipv4_rx_verify(arena, d, n, n * L)
     ev, evf = oracle.batch_ipv4_rx_verify(sample, spk)
-    np.testing.assert_array_equal(verdict[tidx].cpu().numpy(), ev)
-    np.testing.assert_array_equal(vflags[tidx].cpu().numpy(), evf)
+    np.testing.assert_array_equal(down(verdict[tidx]), ev)
+    np.testing.assert_array_equal(down(vflags[tidx]), evf)
 
 
 @pytest.mark.parametrize("order,chunk_mb", [("permuted", None), ("offset", None), ("offset", "1")])
@@ -927,15 +928,15 @@ def test_host_batch_multi_device_many_blocks(tc, oracle, devices):
 def test_full_mtu_batch_exact(tc, torch, oracle):
     """configs[1] at full size (1M x 1500 B): every result checked."""
     b, arena, out = run_config(tc, torch, "mtu", None)
-    exp = oracle.batch_peso(arena.cpu().numpy(), b.descs, nthreads=16)
-    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+    exp = oracle.batch_peso(down(arena), b.descs, nthreads=16)
+    np.testing.assert_array_equal(down(out), exp)
 
 
 def test_full_mixed_batch_exact(tc, torch, oracle):
     """configs[3] at full size (1M packets, ~4.4 GiB): every result checked."""
     b, arena, out = run_config(tc, torch, "mixed", None)
-    exp, fl = oracle.batch_ipv4(arena.cpu().numpy(), b.descs, nthreads=16)
-    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+    exp, fl = oracle.batch_ipv4(down(arena), b.descs, nthreads=16)
+    np.testing.assert_array_equal(down(out), exp)
 
 
 def test_full_tso_batch_properties(tc, torch, oracle):
@@ -949,14 +950,14 @@ def test_full_tso_batch_properties(tc, torch, oracle):
     out1 = tc.batch_peso(arena, descs, b.n, b.total_bytes)
     out2 = tc.batch_peso(arena, descs, b.n, b.total_bytes)
     torch.cuda.synchronize()
-    hc = out1.cpu().numpy()
-    np.testing.assert_array_equal(hc, out2.cpu().numpy())
+    hc = down(out1)
+    np.testing.assert_array_equal(hc, down(out2))
     with tc.debug(lanes=256, loads=16):  # k_segments_wg instead of k_segments_wgx
         out3 = tc.batch_peso(arena, descs, b.n, b.total_bytes)
-    np.testing.assert_array_equal(hc, out3.cpu().numpy())
+    np.testing.assert_array_equal(hc, down(out3))
     # every segment exact: the 16 GiB arena copied to the host once, the
     # oracle over all 262,144 segments on 16 threads
-    host = arena.cpu().numpy()
+    host = down(arena)
     np.testing.assert_array_equal(hc, oracle.batch_peso(host, b.descs, nthreads=16))
     del host
     # sampled exact parity through the single-segment oracle entry point
@@ -964,15 +965,15 @@ def test_full_tso_batch_properties(tc, torch, oracle):
     idx = np.sort(rng.choice(b.n, 512, replace=False))
     for i in idx:
         o, L = int(b.descs["offset"][i]), int(b.descs["len"][i])
-        seg = arena[o: o + L].cpu().numpy()
+        seg = down(arena[o: o + L])
         assert hc[i] == oracle.checksum_peso(seg, b.descs["dst"][i], b.descs["src"][i], 6)
     # incremental update: rewrite the word at offset 100 of every segment
     words = arena[: b.n * 65536].view(b.n, 65536)
-    old = words[:, 100:102].cpu().numpy().copy().view("<u2").reshape(-1).astype(np.uint32)
-    new_bytes = torch.from_numpy(rng.integers(0, 256, (b.n, 2), dtype=np.uint8)).pin_memory().cuda()
+    old = down(words[:, 100:102]).copy().view("<u2").reshape(-1).astype(np.uint32)
+    new_bytes = up(torch.from_numpy(rng.integers(0, 256, (b.n, 2), dtype=np.uint8)))
     words[:, 100:102] = new_bytes
-    new = new_bytes.cpu().numpy().copy().view("<u2").reshape(-1).astype(np.uint32)
-    out4 = tc.batch_peso(arena, descs, b.n, b.total_bytes).cpu().numpy().astype(np.uint32)
+    new = down(new_bytes).copy().view("<u2").reshape(-1).astype(np.uint32)
+    out4 = down(tc.batch_peso(arena, descs, b.n, b.total_bytes)).astype(np.uint32)
     s = (~hc.astype(np.uint32) & 0xFFFF) + (~old & 0xFFFF) + new
     s = (s & 0xFFFF) + (s >> 16)
     s = (s & 0xFFFF) + (s >> 16)
@@ -1004,7 +1005,7 @@ def test_fuzz_vs_oracle(tc, torch, oracle, geometry, seed):
     rng = np.random.default_rng(9000 + seed)
     size = 8 << 20
     host = _fuzz_arena(rng, size)
-    arena = torch.from_numpy(host).pin_memory().cuda()
+    arena = up(torch.from_numpy(host))
     geometry(*GEOMS_SEG[int(rng.integers(0, len(GEOMS_SEG)))])
     n = 4000
     lens = _fuzz_lens(rng, n, 70000)
@@ -1013,14 +1014,14 @@ def test_fuzz_vs_oracle(tc, torch, oracle, geometry, seed):
     s["offset"] = rng.integers(0, size - lens)
     s["pre_sum"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
     comp = int(rng.integers(0, 2))
-    out = tc.batch_segments(arena, tc.descs_to_device(s), n, comp).cpu().numpy()
+    out = down(tc.batch_segments(arena, tc.descs_to_device(s), n, comp))
     np.testing.assert_array_equal(out, oracle.batch_segments(host, s, comp, nthreads=8))
     p = np.zeros(n, tc.PESO_DTYPE)
     p["offset"], p["len"] = s["offset"], s["len"]
     p["src"] = rng.integers(0, 256, (n, 4))
     p["dst"] = rng.integers(0, 256, (n, 4))
     p["protocol"] = rng.choice([6, 17], n)
-    out = tc.batch_peso(arena, tc.descs_to_device(p), n).cpu().numpy()
+    out = down(tc.batch_peso(arena, tc.descs_to_device(p), n))
     np.testing.assert_array_equal(out, oracle.batch_peso(host, p, nthreads=8))
 
     # IPv4 packets packed with random gaps; headers mostly plausible
@@ -1048,23 +1049,23 @@ def test_fuzz_vs_oracle(tc, torch, oracle, geometry, seed):
         if ln >= 40 and rng.random() < 0.2:
             ip[o + 20 + 16: o + 20 + 18] = 0  # TCP checksum field zero (rx skip rule)
             ip[o + 20 + 6: o + 20 + 8] = 0    # UDP checksum field zero
-    d_ip = torch.from_numpy(ip).pin_memory().cuda()
+    d_ip = up(torch.from_numpy(ip))
     d_pk = tc.descs_to_device(pk)
     out, fl = tc.batch_ipv4(d_ip, d_pk, m)
     exp, efl = oracle.batch_ipv4(ip, pk, nthreads=8)
-    np.testing.assert_array_equal(out.cpu().numpy(), exp)
-    np.testing.assert_array_equal(fl.cpu().numpy(), efl)
+    np.testing.assert_array_equal(down(out), exp)
+    np.testing.assert_array_equal(down(fl), efl)
     verdict, vfl = tc.batch_ipv4_rx_verify(d_ip, d_pk, m)
     ev, evfl = oracle.batch_ipv4_rx_verify(ip, pk, nthreads=8)
-    np.testing.assert_array_equal(verdict.cpu().numpy(), ev)
+    np.testing.assert_array_equal(down(verdict), ev)
     tfl = tc.batch_ipv4_tx_fill(d_ip, d_pk, m)
     efl2 = oracle.batch_ipv4_tx_fill(ip, pk, nthreads=8)  # ip is filled in place
-    np.testing.assert_array_equal(tfl.cpu().numpy(), efl2)
-    np.testing.assert_array_equal(d_ip.cpu().numpy(), ip)
+    np.testing.assert_array_equal(down(tfl), efl2)
+    np.testing.assert_array_equal(down(d_ip), ip)
     # and verify what was filled: well-formed packets now pass
     verdict, _ = tc.batch_ipv4_rx_verify(d_ip, d_pk, m)
     ev, _ = oracle.batch_ipv4_rx_verify(ip, pk, nthreads=8)
-    np.testing.assert_array_equal(verdict.cpu().numpy(), ev)
+    np.testing.assert_array_equal(down(verdict), ev)
     assert (ev == 0).sum() > m // 4
 
 
@@ -1100,7 +1101,7 @@ def test_ragged_batch_sizes_write_only_their_results(tc, torch, oracle, geometry
     result equals the oracle's and nothing past out[n) is written."""
     rng = np.random.default_rng(77)
     host = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
-    arena = torch.from_numpy(host).pin_memory().cuda()
+    arena = up(torch.from_numpy(host))
     geometry(g, u)
     for n in (1, 2, 3, 15, 17, 63, 65, 1001):
         p = np.zeros(n, tc.PESO_DTYPE)
@@ -1111,7 +1112,7 @@ def test_ragged_batch_sizes_write_only_their_results(tc, torch, oracle, geometry
         p["protocol"] = rng.choice([6, 17], n)
         out = torch.full((n + 300,), 0xABCD, dtype=torch.int32, device="cuda").view(torch.uint16)
         tc.batch_peso(arena, tc.descs_to_device(p), n, int(p["len"].sum()), out=out)
-        got = out.cpu().numpy()
+        got = down(out)
         np.testing.assert_array_equal(got[:n], oracle.batch_peso(host, p, nthreads=8))
         sentinel = np.full(n + 300, 0xABCD, np.int32).view(np.uint16)  # int32 fill seen as u16 pairs
         np.testing.assert_array_equal(got[n:], sentinel[n:])

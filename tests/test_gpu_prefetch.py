@@ -7,6 +7,7 @@ packed, shuffled, TSO-sized and K = 8 batches, distances from 1 to far past
 the grid, descriptor arrays at the end of their allocation; and the IPv4
 kernels, which must be unaffected by the knob.  Also the same path's scalar
 descriptor reads (debug knob "pk_early") for every group width."""
+from devcopy import down, up
 import numpy as np
 import pytest
 
@@ -61,19 +62,19 @@ def test_peso_batches_with_prefetch(tc, torch, oracle, pf, layout):
     if layout == "shuffled":
         p = p[rng.permutation(n)]
     want = oracle.batch_peso(host, p, nthreads=8)
-    arena = torch.from_numpy(host).pin_memory().cuda()
+    arena = up(torch.from_numpy(host))
     d = _descs_at_end(torch, tc, p)
     with tc.debug(pf_dist=pf):
-        got = tc.batch_peso(arena, d, n, int(lens.sum())).cpu().numpy()
+        got = down(tc.batch_peso(arena, d, n, int(lens.sum())))
         segs = np.zeros(n, tc.SEG_DTYPE)  # the same ranges as pktbuf_checksum16 (16-B descriptors)
         segs["offset"], segs["len"], segs["pre_sum"] = p["offset"], p["len"], rng.integers(0, 1 << 17, n)
-        gs = tc.batch_segments(arena, _descs_at_end(torch, tc, segs), n, 1, int(lens.sum())).cpu().numpy()
+        gs = down(tc.batch_segments(arena, _descs_at_end(torch, tc, segs), n, 1, int(lens.sum())))
     np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(gs, oracle.batch_segments(host, segs, 1, nthreads=8))
     # the per-range kernels (the SHUFFLED route for short ranges) with their own prefetch knob
     with tc.debug(pf_range=pf, packed=0):
         gr, _, _ = tc.batch(tc.OP_PESO, arena, d, n, total_bytes=int(lens.sum()), layout=tc.LAYOUT_SHUFFLED)
-    np.testing.assert_array_equal(gr.cpu().numpy(), want)
+    np.testing.assert_array_equal(down(gr), want)
 
 
 @pytest.mark.parametrize("pf", DISTANCES)
@@ -81,7 +82,7 @@ def test_ipv4_batches_with_prefetch(tc, torch, oracle, pf):
     from tcp_amd import workload
     b = workload.make_batch("mixed", n=9001)
     arena, descs = workload.materialize(b)
-    host = arena.cpu().numpy()
+    host = down(arena)
     d = _descs_at_end(torch, tc, b.descs)
     eo, ef = oracle.batch_ipv4(host, b.descs, nthreads=8)
     ev, _ = oracle.batch_ipv4_rx_verify(host, b.descs, nthreads=8)
@@ -94,10 +95,10 @@ def test_ipv4_batches_with_prefetch(tc, torch, oracle, pf):
             a2 = arena.clone()
             with tc.debug(tx_split=split):
                 tc.batch_ipv4_tx_fill(a2, d, b.n, b.total_bytes)
-            np.testing.assert_array_equal(a2.cpu().numpy(), want)
-    np.testing.assert_array_equal(out.cpu().numpy(), eo)
-    np.testing.assert_array_equal(fl.cpu().numpy(), ef)
-    np.testing.assert_array_equal(v.cpu().numpy(), ev)
+            np.testing.assert_array_equal(down(a2), want)
+    np.testing.assert_array_equal(down(out), eo)
+    np.testing.assert_array_equal(down(fl), ef)
+    np.testing.assert_array_equal(down(v), ev)
 
 
 EARLY_LAYOUTS = ["packed", "shuffled", "mtu", "wide", "tail", "mid", "small", "tiny", "k17", "s400",
@@ -156,12 +157,12 @@ def test_pk_early_descriptors(tc, torch, oracle, layout, early):
             i, j = K * k + K // 2, K * (k + 100) + K // 3
             p[[i, j]] = p[[j, i]]
     want = oracle.batch_peso(host, p, nthreads=8)
-    arena = torch.from_numpy(host).pin_memory().cuda()
+    arena = up(torch.from_numpy(host))
     segs = np.zeros(n, tc.SEG_DTYPE)
     segs["offset"], segs["len"], segs["pre_sum"] = p["offset"], p["len"], rng.integers(0, 1 << 17, n)
     with tc.debug(pk_early=early, packed=1):
-        got = tc.batch_peso(arena, _descs_at_end(torch, tc, p), n, int(lens.sum())).cpu().numpy()
-        gs = tc.batch_segments(arena, _descs_at_end(torch, tc, segs), n, 1, int(lens.sum())).cpu().numpy()
+        got = down(tc.batch_peso(arena, _descs_at_end(torch, tc, p), n, int(lens.sum())))
+        gs = down(tc.batch_segments(arena, _descs_at_end(torch, tc, segs), n, 1, int(lens.sum())))
     np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(gs, oracle.batch_segments(host, segs, 1, nthreads=8))
 
@@ -189,9 +190,9 @@ def test_per_range_scalar_descriptors(tc, torch, oracle, shape, sdesc):
     p = p[rng.permutation(n)]
     segs = np.zeros(n, tc.SEG_DTYPE)
     segs["offset"], segs["len"], segs["pre_sum"] = p["offset"], p["len"], rng.integers(0, 1 << 17, n)
-    arena = torch.from_numpy(host).pin_memory().cuda()
+    arena = up(torch.from_numpy(host))
     with tc.debug(seg_sdesc=sdesc, packed=0, lanes=g, loads=u):
-        got = tc.batch_peso(arena, _descs_at_end(torch, tc, p), n, int(lens.sum())).cpu().numpy()
-        gs = tc.batch_segments(arena, _descs_at_end(torch, tc, segs), n, 1, int(lens.sum())).cpu().numpy()
+        got = down(tc.batch_peso(arena, _descs_at_end(torch, tc, p), n, int(lens.sum())))
+        gs = down(tc.batch_segments(arena, _descs_at_end(torch, tc, segs), n, 1, int(lens.sum())))
     np.testing.assert_array_equal(got, oracle.batch_peso(host, p, nthreads=8))
     np.testing.assert_array_equal(gs, oracle.batch_segments(host, segs, 1, nthreads=8))

@@ -4,6 +4,7 @@ the launch-per-batch path -- the reference's tx bytes, rx verdicts and both
 checksums (tests/golden/ipv4_*.bin) -- over many back-to-back jobs, across the
 grid leaving when idle and being relaunched, and with few workgroups (several
 rounds per job)."""
+from devcopy import down
 import time
 
 import numpy as np
@@ -89,7 +90,7 @@ def test_server_many_small_queues(tc, oracle, server):
     b = workload.make_batch("mixed_rx", n=4096)
     arena, _ = workload.materialize(b)
     ha = tc.HostArena(arena.numel())
-    ha.array[:] = arena.cpu().numpy()
+    ha.array[:] = down(arena)
     want_out, want_flags = oracle.batch_ipv4(ha.array, b.descs)
     want_v, _ = oracle.batch_ipv4_rx_verify(ha.array, b.descs)
     rng = np.random.default_rng(11)

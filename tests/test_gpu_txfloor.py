@@ -6,6 +6,7 @@ else, or the floor it prices is not the fill's.  The field addresses come
 from its prepare pass; the expected ones from the product's tx offload (the
 fields tcsum_tx_apply writes).  Measurement code, so the check is on
 addresses, not values (the probe writes junk)."""
+from devcopy import down, up
 import numpy as np
 import pytest
 
@@ -43,10 +44,10 @@ def _batch(tc, seed):
 def _written(tc, torch, host, pk):
     """Byte positions the fill writes: apply all-zero and all-one values
     through the product's offload flags and see which bytes differ."""
-    arena = torch.from_numpy(host.copy()).pin_memory().cuda()
+    arena = up(torch.from_numpy(host.copy()))
     d = tc.descs_to_device(pk)
     _, fl = tc.batch_ipv4_tx_offload(arena, d, pk.size, int(pk["len"].sum()))
-    fl = fl.cpu().numpy()
+    fl = down(fl)
     a, b = host.copy(), host.copy()
     tc.tx_apply_batch(a, pk, np.zeros(pk.size, np.uint32), fl)
     tc.tx_apply_batch(b, pk, np.full(pk.size, 0xFFFFFFFF, np.uint32), fl)
@@ -60,23 +61,23 @@ def test_txfloor_writes_the_fills_fields(tc, torch, seed):
     assert expect, "the batch has fields to fill"
     for deferred in (False, True):
         arena = torch.zeros(host.size + 256, dtype=torch.uint8, device="cuda")
-        arena[: host.size] = torch.from_numpy(host).pin_memory().cuda()
+        arena[: host.size] = up(torch.from_numpy(host))
         d = tc.descs_to_device(pk)
         h = tc.txfloor_prepare(arena, host.size, d, pk.size, int(pk["len"].sum()))
-        fpos = h["fpos"].cpu().numpy()
+        fpos = down(h["fpos"])
         field = set()
         for f in fpos[fpos >= 0].tolist():
             field |= {f, f + 1}
         assert field == expect
         # each window's first packet: packets starting in it, in arena order
-        ff = h["ffirst"].cpu().numpy()
+        ff = down(h["ffirst"])
         w = pk["offset"] // 16384
         for k in range(ff.size - 1):
             assert ff[k] == np.searchsorted(w, k, side="left")
         for _ in range(3):  # any number of launches touches only the fields
             tc.probe_txfloor(h, deferred=deferred)
         torch.cuda.synchronize()
-        after = arena.cpu().numpy()
+        after = down(arena)
         changed = set(np.nonzero(after[: host.size] != host)[0].tolist())
         assert changed <= expect
         assert not after[host.size:].any()

@@ -1,8 +1,9 @@
 """tcp_amd.to_host / to_host_tensor: device tensors read back through pinned
-memory only, and the tests' `.cpu()` routed through it
-(tests/conftest.py)."""
+memory only, and the tests' read-back helper over it
+(tests/devcopy.py)."""
 import numpy as np
 import pytest
+from devcopy import down
 
 
 def test_host_tensor_passes_through():
@@ -12,13 +13,6 @@ def test_host_tensor_passes_through():
     t = torch.arange(10, dtype=torch.int16)
     assert tc.to_host_tensor(t) is t
     np.testing.assert_array_equal(tc.to_host(t), np.arange(10, dtype=np.int16))
-
-
-def test_cpu_is_routed():
-    import torch
-    assert getattr(torch.Tensor.cpu, "_pinned", False)
-    t = torch.arange(5)
-    assert t.cpu() is t  # a host tensor: unchanged semantics
 
 
 @pytest.mark.gpu
@@ -40,7 +34,7 @@ def test_to_host_values(n, dtype):
     h = tc.to_host_tensor(d)
     assert h.device.type == "cpu" and h.dtype == dt and tuple(h.shape) == (n,)
     np.testing.assert_array_equal(h.numpy(), want)
-    np.testing.assert_array_equal(d.cpu().numpy(), want)  # the routed .cpu()
+    np.testing.assert_array_equal(down(d), want)  # the tests' read-back helper
 
 
 @pytest.mark.gpu

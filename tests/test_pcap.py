@@ -8,6 +8,7 @@ GPU: the reference's own rx fixtures (tests/golden/ipv4_rx_*.bin, verdicts
 from the compiled reference stack) wrapped into captures and verified in
 place through tcsum_host_batch_ipv4_rx_verify.
 """
+from devcopy import down
 import numpy as np
 import pytest
 
@@ -170,7 +171,7 @@ def test_capture_rx_verify_mixed_vs_oracle(pcap, oracle):
     from tcp_amd import workload
     b = workload.make_batch("mixed_rx", n=20000)
     dev, _ = workload.materialize(b)  # IPv4 packets generated in HBM, tx-filled like a sender
-    arena = dev.cpu().numpy()
+    arena = down(dev)
     rng = np.random.default_rng(11)
     frames = [arena[o: o + n].tobytes() for o, n in zip(b.descs["offset"], b.descs["len"])]
     for i in rng.choice(len(frames), 300, replace=False):

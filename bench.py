@@ -41,6 +41,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 GIB = float(1 << 30)
+_T0 = time.perf_counter()  # process start, for the line's wall-time figure
+DRIVER_LIMIT_S = 600  # the driver's per-run limit an N-GPU run must fit
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 METRIC = "Internet-checksum GiB/s (device-resident), 1500B & 64KB packet batches"
 
@@ -538,6 +540,87 @@ def cpu_model():
         return None
 
 
+def _cpuset_count(text):
+    """Logical CPUs in a cpuset list such as "0-15,32-47"."""
+    n = 0
+    for part in text.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            n += int(b or a) - int(a) + 1
+    return n
+
+
+def cpu_allowance():
+    """The CPUs this process may actually use, which on a shared GPU box is not
+    os.cpu_count() (the whole host): the affinity mask, and the cgroup's
+    cpuset and CPU quota (v2 cpu.max, or v1 cfs_quota_us / cfs_period_us).
+    `effective` = the smallest of them (a quota of 16.0 CPUs means at most
+    16 threads' worth of CPU time however many threads run)."""
+    import math
+    out = {"host_logical": os.cpu_count()}
+    try:
+        out["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    v2, v1 = "", {}
+    try:
+        with open("/proc/self/cgroup") as f:
+            for ln in f:
+                h, ctl, path = ln.strip().split(":", 2)
+                if h == "0" and not ctl:
+                    v2 = path
+                for c in ctl.split(","):
+                    if c:
+                        v1[c] = path
+    except (OSError, ValueError):
+        pass
+    base = "/sys/fs/cgroup"
+    quotas, cpusets = [], []
+
+    def walk(root, rel):  # the process's own cgroup and each ancestor: the tightest limit binds
+        d = os.path.normpath(root + rel) if rel and rel != "/" else root
+        while d.startswith(root):
+            yield d
+            if d == root:
+                break
+            d = os.path.dirname(d)
+
+    def read(path):
+        try:
+            with open(path) as f:
+                return f.read().strip()
+        except OSError:
+            return ""
+
+    for d in walk(base, v2):  # cgroup v2
+        t = read(os.path.join(d, "cpu.max")).split()
+        if len(t) == 2 and t[0] != "max":
+            quotas.append(int(t[0]) / int(t[1]))
+        t = read(os.path.join(d, "cpuset.cpus.effective"))
+        if t:
+            cpusets.append(_cpuset_count(t))
+    if "cpu" in v1:  # cgroup v1
+        for root in (f"{base}/cpu", f"{base}/cpu,cpuacct"):
+            for d in walk(root, v1["cpu"]):
+                q, per = read(os.path.join(d, "cpu.cfs_quota_us")), read(os.path.join(d, "cpu.cfs_period_us"))
+                if q and per and int(q) > 0:
+                    quotas.append(int(q) / int(per))
+    if "cpuset" in v1:
+        for d in walk(f"{base}/cpuset", v1["cpuset"]):
+            t = read(os.path.join(d, "cpuset.effective_cpus")) or read(os.path.join(d, "cpuset.cpus"))
+            if t:
+                cpusets.append(_cpuset_count(t))
+    if quotas:
+        out["cpu_quota"] = round(min(quotas), 2)
+    if cpusets:
+        out["cpuset"] = min(cpusets)
+    lim = [v for v in (out.get("affinity"), out.get("cpuset")) if v]
+    if quotas:
+        lim.append(max(1, math.floor(min(quotas))))
+    out["effective"] = min(lim) if lim else (os.cpu_count() or 1)
+    return out
+
+
 def cpu_baseline(torch, r, seconds, kind="reference", cache_sample=True):
     """The reference's checksum_peso (oracle/_ref/libtcpref.so, compiled from
     /root/reference; kind "port" = the oracle's restatement) on the same
@@ -546,7 +629,10 @@ def cpu_baseline(torch, r, seconds, kind="reference", cache_sample=True):
       value      1 thread -- the reference checksums on its single work_thread
                  (exmsg.c:123) -- over a DRAM-resident sample (>= 1 GiB of the
                  batch, larger than any L3; re-summed for >= `seconds`);
-      value_all  every logical CPU of the host (os.cpu_count()), same sample;
+      value_all  as many threads as this process's CPU allowance holds
+                 (cpu_allowance: affinity, cgroup cpuset and quota -- on a
+                 shared box far fewer than the host's os.cpu_count()), same
+                 sample, with each thread's own rate (min / median / max);
       cache_resident  both, over a ~100 MB sample that fits the host's L3.
 
     cache_sample=False (the secondary configs): the DRAM sample only.
@@ -581,8 +667,10 @@ def cpu_baseline(torch, r, seconds, kind="reference", cache_sample=True):
             want = int((r["out"][:n].to(torch.int64) >> 16).sum().item())
         return host, segs, want, n
 
-    threads_all = min(256, os.cpu_count() or 1)  # orc_time_peso runs at most 256 threads
-    res = {"unit": "GiB/s", "kind": kind, "cores": 1, "cores_all": threads_all, "host_cpu": cpu_model(),
+    allow = cpu_allowance()
+    threads_all = min(256, allow["effective"])  # orc_time_peso runs at most 256 threads
+    res = {"unit": "GiB/s", "kind": kind, "cores": 1, "cores_all": os.cpu_count(), "cores_effective": threads_all,
+           "cpu_allowance": allow, "host_cpu": cpu_model(),
            "placement": "each timing thread pinned to its own logical CPU, its slice of the sample copied "
                         "(first-touched) by that thread before the timed region: NUMA-local"}
     what = "segments" if b.kind == "peso" else "packets' L4 ranges"
@@ -591,8 +679,13 @@ def cpu_baseline(torch, r, seconds, kind="reference", cache_sample=True):
     for label, nbytes, secs in legs:
         host, segs, want, n = sample(nbytes)
         rate1, got_kind, cs1 = pyoracle.time_peso(host, segs, 1, secs, kind=kind)
-        rate_all, _, cs_all = pyoracle.time_peso(host, segs, threads_all, max(2.0, secs / 2), kind=kind)
+        rate_all, _, cs_all, per = pyoracle.time_peso(host, segs, threads_all, max(2.0, secs / 2), kind=kind,
+                                                     thread_rates=True)
+        per = sorted(per)
         part = {"value": round(rate1 / GIB, 3), "value_all": round(rate_all / GIB, 3),
+                "threads_all": threads_all, "scaling_all": round(rate_all / rate1, 2) if rate1 else None,
+                "per_thread_all": {"min": round(per[0] / GIB, 3), "median": round(per[len(per) // 2] / GIB, 3),
+                                   "max": round(per[-1] / GIB, 3)},
                 "sample_bytes": int(segs["len"].sum()),
                 "sample": f"first {n} {what} of the {b.config} batch ({int(segs['len'].sum()) / 1e6:.0f} MB), "
                           f"re-summed for >= {secs:.0f} s (1 thread) / {max(2.0, secs / 2):.0f} s "
@@ -920,6 +1013,7 @@ def rehearsal(args, rank, world) -> None:
                                     "payload_bytes": int(b.total_bytes), "stand_in_sum": s, "device": dev,
                                     "ms_per_step": dt * 1e3 / max(args.steps, 1),
                                     "self_check": {"segments": 1, "mismatches": bad}})
+    wall = D.max_over_ranks(dist, time.perf_counter() - _T0)  # every rank: a collective
     if rank == 0:
         print(json.dumps({"rehearsal": "cpu-gloo (numpy stand-in for the kernel; not a measurement)",
                           "n_gpus": world, "steps": args.steps, "scaling": "weak",
@@ -930,7 +1024,9 @@ def rehearsal(args, rank, world) -> None:
                                                  "max": round(max(r["ms_per_step"] for r in ranks), 4)},
                           "self_check": {"segments_per_rank": 1,
                                          "mismatches": sum(r["self_check"]["mismatches"] for r in ranks)},
-                          "e2e": {"multi_device": multi}}),
+                          "e2e": {"multi_device": multi},
+                          "process_wall_s": round(wall, 2),
+                          "driver_limit_s": DRIVER_LIMIT_S}),
               flush=True)
     D.barrier(dist)
     dist.destroy_process_group()
@@ -1160,6 +1256,14 @@ def main():
         del head
         torch.cuda.empty_cache()
 
+    # this rank's wall time from process start to the line: at N > 1 the
+    # whole run (arena generation, timed steps, self-check; no secondary
+    # configs, CPU or host-memory legs), which per-GPU work fixes whatever N
+    wall = D.max_over_ranks(dist, time.perf_counter() - _T0, device="cuda" if backend == "nccl" else "cpu")
+    line["process_wall_s"] = round(wall, 1)
+    if world > 1:
+        line["driver_limit_s"] = DRIVER_LIMIT_S
+        line["wall_fraction_of_limit"] = round(wall / DRIVER_LIMIT_S, 3)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -498,6 +498,13 @@ double orc_time_peso(orc_peso_fn fn, const uint8_t *arena, const orc_peso_t *seg
                      uint32_t n, int nthreads, double min_seconds,
                      uint64_t *checksum_of_checksums)
 {
+    return orc_time_peso_rates(fn, arena, segs, n, nthreads, min_seconds, checksum_of_checksums, NULL);
+}
+
+double orc_time_peso_rates(orc_peso_fn fn, const uint8_t *arena, const orc_peso_t *segs,
+                           uint32_t n, int nthreads, double min_seconds,
+                           uint64_t *checksum_of_checksums, double *thread_rates)
+{
     if (nthreads < 1)
         nthreads = 1;
     if (nthreads > 256)
@@ -528,6 +535,8 @@ double orc_time_peso(orc_peso_fn fn, const uint8_t *arena, const orc_peso_t *seg
         pthread_join(th[t], NULL);
         total += jobs[t].bytes;
         csum += jobs[t].csum;
+        if (thread_rates) /* each thread's own bytes / its own seconds */
+            thread_rates[t] = jobs[t].secs > 0 ? (double)jobs[t].bytes / jobs[t].secs : 0.0;
         if (jobs[t].secs > max_secs)
             max_secs = jobs[t].secs;
     }

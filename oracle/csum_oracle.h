@@ -139,6 +139,11 @@ typedef uint16_t (*orc_peso_fn)(const uint8_t *seg, uint32_t len,
 double orc_time_peso(orc_peso_fn fn, const uint8_t *arena, const orc_peso_t *segs,
                      uint32_t n, int nthreads, double min_seconds,
                      uint64_t *checksum_of_checksums);
+/* orc_time_peso, and each thread's own rate (bytes / its seconds) into
+ * thread_rates[0..nthreads) when not NULL. */
+double orc_time_peso_rates(orc_peso_fn fn, const uint8_t *arena, const orc_peso_t *segs,
+                           uint32_t n, int nthreads, double min_seconds,
+                           uint64_t *checksum_of_checksums, double *thread_rates);
 
 #ifdef __cplusplus
 }

@@ -81,6 +81,10 @@ def lib() -> ctypes.CDLL:
         L.orc_time_peso.argtypes = [ctypes.c_void_p, u8p, u8p, ctypes.c_uint32, ctypes.c_int,
                                     ctypes.c_double, ctypes.POINTER(ctypes.c_uint64)]
         L.orc_time_peso.restype = ctypes.c_double
+        L.orc_time_peso_rates.argtypes = [ctypes.c_void_p, u8p, u8p, ctypes.c_uint32, ctypes.c_int,
+                                          ctypes.c_double, ctypes.POINTER(ctypes.c_uint64),
+                                          ctypes.POINTER(ctypes.c_double)]
+        L.orc_time_peso_rates.restype = ctypes.c_double
         _lib = L
     return _lib
 
@@ -190,14 +194,15 @@ def synth_fill(byte_offset: int, nbytes: int, seed: int) -> np.ndarray:
 
 
 def time_peso(arena: np.ndarray, segs: np.ndarray, nthreads: int, min_seconds: float,
-              kind: str = "reference"):
+              kind: str = "reference", thread_rates: bool = False):
     """Bytes/s of a checksum_peso-shaped CPU routine over the batch.
 
     kind "reference" times the reference's own checksum_peso
     (oracle/_ref/libtcpref.so, built from /root/reference at the reference's
     -O2; "reference_o3": the same sources at -O3 -march=x86-64-v3) and raises
     FileNotFoundError when it was not built; kind "port" times this
-    restatement.  Returns (bytes_per_second, kind, checksum_of_checksums).
+    restatement.  Returns (bytes_per_second, kind, checksum_of_checksums),
+    and with thread_rates=True a fourth item: each thread's own bytes/s.
     """
     L = lib()
     if kind in ("reference", "reference_o3"):
@@ -212,6 +217,9 @@ def time_peso(arena: np.ndarray, segs: np.ndarray, nthreads: int, min_seconds: f
     else:
         raise ValueError(kind)
     cs = ctypes.c_uint64()
-    rate = L.orc_time_peso(fn, _ptr(arena), _ptr(segs), segs.size, nthreads, min_seconds,
-                           ctypes.byref(cs))
+    per = (ctypes.c_double * max(1, min(256, nthreads)))()
+    rate = L.orc_time_peso_rates(fn, _ptr(arena), _ptr(segs), segs.size, nthreads, min_seconds,
+                                 ctypes.byref(cs), per)
+    if thread_rates:
+        return rate, kind, cs.value, list(per)[: max(1, min(256, nthreads))]
     return rate, kind, cs.value

@@ -24,6 +24,7 @@ DYN_ONLY = "--dyn" in sys.argv  # packets handed out inside the workgroup (k_ipv
 ROLL_ONLY = "--roll" in sys.argv  # rolling load slots: a multi-pass packet keeps its loads in flight
 HDRX_ONLY = "--hdrx" in sys.argv  # header chunks shuffled from the first data pass instead of loaded
 SDESC_ONLY = "--sdesc" in sys.argv  # the descriptors by scalar loads
+LDS_ONLY = "--lds" in sys.argv  # later passes by LDS-DMA into a per-wave ring (PIPE 5); the 3rd header chunk as a dword
 for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mixed_aligned", "mixed_rx"]):
     b = workload.make_batch(cfg)
     arena, descs = workload.materialize(b)
@@ -59,7 +60,15 @@ for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mi
                 f(o, v)
         return g
 
-    if SDESC_ONLY:
+    if LDS_ONLY:
+        if rx:
+            kinds.update({"LDS ring 16x6": shape(256, 800), "LDS ring 16x4": shape(256, 804),
+                          "LDS ring 32x6": shape(256, 832)})
+        else:
+            kinds.update({"3rd header chunk as a dword (H1)": shape(256, 900), "LDS ring 32x6": shape(256, 800),
+                          "LDS ring 32x6 + H1": shape(256, 905), "LDS ring 32x4": shape(256, 804),
+                          "LDS ring 32x8": shape(256, 808), "LDS ring 16x6": shape(256, 816)})
+    elif SDESC_ONLY:
         kinds.update({"descriptors by scalar loads": shape(256, 700)})
     elif HDRX_ONLY:
         kinds.update({"header from the data pass": shape(256, 600)})

@@ -501,7 +501,7 @@ static hipError_t launch_probe_desc(const void *arena, const void *descs, uint32
             return hipErrorInvalidValue;
         note_launch(launch(k_segments_pk<MODE_PESO, kPkWaves, kPkLoads, true>, dim3((n + K - 1) / K),
                            dim3(kPkWaves * 64), 0, stream, a, descs, n, reinterpret_cast<uint16_t *>(sink), 0u, xg,
-                           K));
+                           K, static_cast<uint32_t *>(nullptr)));
         return take_launch_rc();
     }
     if (g.lanes == 1024 && g.loads == 4) { // k_segments_wgx<16, 32, 4>'s loads
@@ -853,6 +853,14 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 600 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 0, 3>)) } // header from the data pass
         if (occ == 700 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 0, 4>)) } // scalar descriptors
         if (occ == 100 + 64 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 64>)) }
+        // the next pass by LDS-DMA into a per-wave LDS ring (PIPE 5)
+        if (occ == 800 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 0, 5>)) }
+        if (occ == 804 && wg == 256) { TCSUM_SH((k_ipv4<32, 4, IP_SUMS, 256, 0, 5>)) }
+        if (occ == 808 && wg == 256) { TCSUM_SH((k_ipv4<32, 8, IP_SUMS, 256, 0, 5>)) }
+        if (occ == 816 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_SUMS, 256, 0, 5>)) }
+        // the third header chunk as one dword (H1), alone and with PIPE 5
+        if (occ == 900 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 0, 0, true>)) }
+        if (occ == 905 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 0, 5, true>)) }
         // packets handed out inside the workgroup, M = occ - 300 per lane group
         if (occ == 302 && wg == 256) { TCSUM_SH((k_ipv4_dyn<32, 6, IP_SUMS, 2>)) }
         if (occ == 304 && wg == 256) { TCSUM_SH((k_ipv4_dyn<32, 6, IP_SUMS, 4>)) }
@@ -879,6 +887,9 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 506 && wg == 256) { TCSUM_SH((k_ipv4_occ<16, 6, IP_RX, 6, 2>)) } // rolling, <= 80 VGPRs
         if (occ == 600 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256, 0, 3>)) } // header from the data pass
         if (occ == 700 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256, 0, 4>)) } // scalar descriptors
+        if (occ == 800 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256, 0, 5>)) } // LDS-DMA ring
+        if (occ == 804 && wg == 256) { TCSUM_SH((k_ipv4<16, 4, IP_RX, 256, 0, 5>)) }
+        if (occ == 832 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_RX, 256, 0, 5>)) }
     }
 #undef TCSUM_SH
     return hipErrorInvalidValue;

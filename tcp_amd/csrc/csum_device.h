@@ -826,6 +826,9 @@ __device__ __forceinline__ void pk_ranges(const uint8_t *__restrict__ arena, con
 
 constexpr uint32_t kPkMaxPasses = 64; // longer regions go range by range
 constexpr uint32_t kPkEarly = 1u << 7; // aux: the range-by-range path's descriptors by scalar loads (pk_wave_descs)
+// K above which a workgroup whose ranges are not one region hands them to a
+// follow-up launch (k_segments_list) instead of summing them itself
+constexpr uint32_t kPkListMin = 16;
 
 // Lanes per range on k_segments_pk's range-by-range path for kw ranges.
 __device__ __forceinline__ uint32_t pk_group(uint32_t T, uint32_t kw)
@@ -870,10 +873,14 @@ __device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, c
 }
 
 
+// list (K > kPkListMin, or nullptr): list[0] counts the workgroups whose
+// ranges are not one region, list[1 + i] names them; such a workgroup only
+// appends itself and leaves, and k_segments_list -- launched next on the
+// same stream -- sums their ranges with the per-range kernel's lane groups.
 template <int MODE, int W = kPkWaves, int U = kPkLoads, bool PROBE = false>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) void k_segments_pk(
     const uint8_t *__restrict__ arena, const void *__restrict__ descs, uint32_t n, uint16_t *__restrict__ out,
-    uint32_t aux, uint32_t xg, uint32_t K)
+    uint32_t aux, uint32_t xg, uint32_t K, uint32_t *__restrict__ list)
 {
     static_assert(MODE != MODE_EXACT, "the exact u32 sum stays on k_segments");
     static_assert(W <= 16, "the sub-range totals are scanned by 32 lanes");
@@ -904,6 +911,14 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     // safe to load before the ranges are known to lie inside it
     const bool span_ok = len0 != 0 && lenl != 0 && rend > r0 &&
                          rend - r0 <= (uint64_t)kPkMaxPasses * CH * 16u - s0;
+    if (!PROBE && !span_ok && list != nullptr) {
+        // a shuffled batch's small ranges (K > 16): K ranges in one 256-thread
+        // workgroup leave its lane groups half idle in a last round; the
+        // follow-up launch's groups take them 256 / G at a time instead
+        if (t == 0)
+            list[1u + __hip_atomic_fetch_add(list, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)] = blk;
+        return;
+    }
     if (!PROBE && !span_ok) {
         // workgroup-uniform, known from the two scalar descriptors: range by
         // range at once (a shuffled batch's usual case), before any stream
@@ -1064,6 +1079,41 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
         out[first + rr] = finalize<MODE>(pe - ps, reinterpret_cast<uintptr_t>(arena + d.off), d, aux, q16);
 }
 
+// The follow-up of k_segments_pk with a list: the ranges of the listed
+// workgroups (list[0] of them, K ranges each -- fewer for the batch's last),
+// G lanes x U loads per range as the per-range kernel k_segments would take
+// them, 256 / G ranges per block and round.  A grid of at most a few
+// thousand blocks walks them (a batch with nothing listed costs one launch
+// whose blocks read list[0] and leave).
+template <int G, int U, int MODE>
+__global__ __launch_bounds__(256) void k_segments_list(const uint8_t *__restrict__ arena,
+                                                       const void *__restrict__ descs, uint32_t n,
+                                                       uint16_t *__restrict__ out, uint32_t aux, uint32_t K,
+                                                       const uint32_t *__restrict__ list)
+{
+    static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G");
+    constexpr uint32_t PER = 256u / G;
+    const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane((int)list[0]);
+    const uint32_t total = cnt * K; // <= n + K - 1: k_segments_pk's grid is ceil(n / K)
+    const uint32_t gl = threadIdx.x & (G - 1u);
+    for (uint32_t v0 = blockIdx.x * PER; v0 < total; v0 += gridDim.x * PER) { // block-uniform
+        const uint32_t v = v0 + threadIdx.x / G;
+        const bool in = v < total;
+        const uint32_t wi = in ? v / K : 0u;
+        const uint32_t seg = list[1u + wi] * K + (v - wi * K);
+        const bool live = in && seg < n;
+        const SegDesc d = load_desc<MODE>(descs, seg, live);
+        uint32_t q16 = 0;
+        uint32_t acc = sum_range<G, U, false>(arena, d.off, d.len, gl, [&] {
+            if constexpr (MODE == MODE_PESO)
+                q16 = pinned(peso_pseudo16(d));
+        });
+        acc = group_sum<G>(acc);
+        if (live && gl == 0)
+            out[seg] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + d.off), d, aux, q16);
+    }
+}
+
 // ---------------------------------------------------------------- IPv4
 //
 // Both checksums of a captured IPv4 packet in one pass over its bytes, in one
@@ -1092,6 +1142,23 @@ constexpr uint32_t IP_OPT_DEFER = 2u;
 constexpr int IP_TX_OFFLOAD = 3;
 // launch_ipv4 mode 4: the tx fill as k_ipv4<IP_TX> with IP_OPT_DEFER + k_tx_scatter
 constexpr int IP_TX_SPLIT = 4;
+
+// One 16-byte LDS-DMA per lane (global_load_lds_dwordx4, nontemporal):
+// lane l's chunk lands at slot[l] -- the wave-uniform slot base plus 16 * l.
+__device__ __forceinline__ void lds_dma16(const u32x4 *src, u32x4 *slot)
+{
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src),
+                                     (__attribute__((address_space(3))) void *)(slot), 16, 0, 2);
+}
+
+// k_ipv4 PIPE 5's LDS: per wave of a 256-thread workgroup, U slots of 64
+// chunks (U KiB), this wave's returned.
+template <int U>
+__device__ __forceinline__ u32x4 *ipv4_lds_ring()
+{
+    __shared__ u32x4 ring[4][U * 64];
+    return ring[threadIdx.x >> 6];
+}
 
 // The 20 fixed header bytes at byte s0 (0..15) of the three aligned chunks
 // h0, h1, h2, as five dwords: hd[k] = bytes [s0 + 4k, s0 + 4k + 4).  Two
@@ -1334,8 +1401,16 @@ __device__ __forceinline__ void ip_finish(const IpHdr &ih, uint32_t fl, bool big
 // soon as its chunk is taken, so a multi-pass packet keeps U loads in flight
 // per lane with no more registers than one pass; 3 = no header loads, the
 // header chunks taken from the lanes whose first data-pass load holds them;
-// 4 = the descriptors by scalar loads, a wave's 2 or 4 at once.
-template <int G, int U, int IPM, int SKEW = 0, int PIPE = 0>
+// 4 = the descriptors by scalar loads, a wave's 2 or 4 at once;
+// 5 = a multi-pass packet's next pass streamed into LDS by LDS-DMA
+// (global_load_lds_dwordx4, one 1-KiB wave-instruction per load slot) while
+// the current pass is summed from registers: two passes in flight with no
+// second register set (ipv4_lds_ring; 256-thread workgroups).
+// H1: the third header chunk (whose first dword alone the sums / tx modes
+// use) loaded as that one dword, so no dead part of a 16-byte header load
+// is a register the compiler reuses -- with a vmcnt wait for the header
+// loads -- before the data pass's loads are issued.
+template <int G, int U, int IPM, int SKEW = 0, int PIPE = 0, bool H1 = false>
 __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                             uint32_t pk, uint32_t n, uint32_t *__restrict__ out,
                                             uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
@@ -1392,6 +1467,12 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
         c2 = hload(nch > 2 ? base + 2 : &g_zero_chunk);
         c3 = hload(nch > 3 && s0 >= 12 ? base + 3 : &g_zero_chunk);
         h2 = s0 > 12 ? c2 : u32x4(0u);
+    } else if constexpr (H1) {
+        h0 = hload(hb);
+        h1 = hload(hb + h1i);
+        const uint32_t h2x = *reinterpret_cast<const uint32_t *>(hb + (big_enough ? (s0 > 12 ? 2u : 1u) : 0u));
+        h2 = u32x4(0u);
+        h2.x = s0 > 12 ? h2x : 0u;
     } else {
         h0 = hload(hb);
         h1 = hload(hb + h1i);
@@ -1420,6 +1501,19 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
     for (int u = 0; u < U; ++u) {
         const uint32_t idx = u * G + gl;
         v[u] = load16<true>(dbase + (idx < dch ? idx : dlast));
+    }
+    // PIPE 5: the wave's LDS slots -- load slot u of lane l at ring[u][l] --
+    // and pass 1's chunks into them, in flight with pass 0's
+    [[maybe_unused]] u32x4 *ring = nullptr;
+    if constexpr (PIPE == 5) {
+        ring = ipv4_lds_ring<U>();
+        if (dch > (uint32_t)(G * U)) { // group-uniform: this packet has a second pass
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t idx = (uint32_t)(G * U + u * G) + gl;
+                lds_dma16(dbase + (idx < dch ? idx : dlast), ring + u * 64);
+            }
+        }
     }
     issue_fence();
     if constexpr (PIPE == 3) {
@@ -1545,6 +1639,26 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
             acc_h += ph;
             acc_l = fold_step(acc_l + pl);
         }
+    } else if constexpr (PIPE == 5) {
+        if (dch)
+            pass(v, 0u);
+        const uint32_t ln = threadIdx.x & 63u;
+        for (uint32_t b0 = G * U; b0 < dch; b0 += G * U) { // group-divergent: a done group's lanes idle
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this pass's DMA has landed
+            u32x4 w[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                w[u] = ring[u * 64 + ln];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // read out before the slots are refilled
+            if (b0 + G * U < dch) { // the next pass streams in while this one is summed
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t idx = b0 + (uint32_t)(G * U + u * G) + gl;
+                    lds_dma16(dbase + (idx < dch ? idx : dlast), ring + u * 64);
+                }
+            }
+            pass(w, b0);
+        }
     } else if constexpr (PIPE == 1) {
         u32x4 nx[U];
 #pragma unroll
@@ -1587,15 +1701,15 @@ __device__ __forceinline__ void ipv4_packet(uint8_t *__restrict__ arena, const t
                        verdict_out, opts);
 }
 
-template <int G, int U, int IPM, int T = 256, int SKEW = 0, int PIPE = 0>
+template <int G, int U, int IPM, int T = 256, int SKEW = 0, int PIPE = 0, bool H1 = false>
 __global__ __launch_bounds__(T) void k_ipv4(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                             uint32_t n, uint32_t *__restrict__ out,
                                             uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
                                             uint32_t opts, uint32_t xg)
 {
     const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
-    ipv4_packet<G, U, IPM, SKEW, PIPE>(arena, pkts, blk * (uint32_t)(T / G) + threadIdx.x / G, n, out, flags_out,
-                                       verdict_out, opts); // no 32-bit wrap for any n
+    ipv4_packet<G, U, IPM, SKEW, PIPE, H1>(arena, pkts, blk * (uint32_t)(T / G) + threadIdx.x / G, n, out,
+                                           flags_out, verdict_out, opts); // no 32-bit wrap for any n
 }
 
 // k_ipv4 with two data passes in flight per lane group (measurement)

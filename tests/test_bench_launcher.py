@@ -192,4 +192,7 @@ def test_launcher_rehearsal_many_ranks(world):
     assert line["self_check"]["mismatches"] == 0
     assert len(line["ranks_ms_per_step"]) == world and line["ms_per_step_spread"]["max"] >= \
         line["ms_per_step_spread"]["min"] > 0
+    # the slowest rank's wall time from process start is in the line, and the
+    # whole N-rank run fits the driver's limit with margin
+    assert 0 < line["process_wall_s"] < 0.5 * line["driver_limit_s"]
     check_multi_device(line, world)

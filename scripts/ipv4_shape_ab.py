@@ -5,7 +5,8 @@ take sums 66 VGPRs = 7 waves, rx 74 = 6).  One process, interleaved rounds,
 median us per launch; every form's results must equal the product's.
 tcsum_probe_ipv4_shape (libtcsum_bench.so).
 
-  python scripts/ipv4_shape_ab.py [config ...]   (mixed, mixed_aligned: sums; mixed_rx: rx verify)
+  python scripts/ipv4_shape_ab.py [config ...]   (mixed, mixed_aligned: sums; mixed_rx: rx verify;
+                                                 uNNNN / uNNNN_rx: every packet NNNN B)
 """
 import os
 import sys
@@ -25,8 +26,21 @@ ROLL_ONLY = "--roll" in sys.argv  # rolling load slots: a multi-pass packet keep
 HDRX_ONLY = "--hdrx" in sys.argv  # header chunks shuffled from the first data pass instead of loaded
 SDESC_ONLY = "--sdesc" in sys.argv  # the descriptors by scalar loads
 LDS_ONLY = "--lds" in sys.argv  # later passes by LDS-DMA into a per-wave ring (PIPE 5); the 3rd header chunk as a dword
+
+def equal_length(L, op):
+    """Packets of L bytes each, as many as configs[3]'s bytes hold (uNNNN, uNNNN_rx)."""
+    from tcp_amd.csum import PKT_DTYPE
+    total = workload.make_batch("mixed").total_bytes
+    n = total // L
+    d = np.zeros(n, PKT_DTYPE)
+    d["offset"] = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    d["len"] = L
+    return workload.Batch("mixed", "ipv4", n, d, n * L, n * L, 0, op="rx" if op else "sums")
+
+
 for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mixed_aligned", "mixed_rx"]):
-    b = workload.make_batch(cfg)
+    b = equal_length(int(cfg[1:].split("_")[0]), cfg.endswith("_rx")) if cfg.startswith("u") else \
+        workload.make_batch(cfg)
     arena, descs = workload.materialize(b)
     n = b.n
     rx = b.op == "rx"

@@ -501,7 +501,7 @@ static hipError_t launch_probe_desc(const void *arena, const void *descs, uint32
             return hipErrorInvalidValue;
         note_launch(launch(k_segments_pk<MODE_PESO, kPkWaves, kPkLoads, true>, dim3((n + K - 1) / K),
                            dim3(kPkWaves * 64), 0, stream, a, descs, n, reinterpret_cast<uint16_t *>(sink), 0u, xg,
-                           K, static_cast<uint32_t *>(nullptr)));
+                           K));
         return take_launch_rc();
     }
     if (g.lanes == 1024 && g.loads == 4) { // k_segments_wgx<16, 32, 4>'s loads
@@ -827,7 +827,7 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
     if (n == 0)
         return hipSuccess;
     const uint32_t xg = (uint32_t)route(1500).xcd;
-    const uint32_t G = occ == 516 ? 16u : occ == 532 ? 32u : mode == IP_RX ? 16u : 32u;
+    const uint32_t G = occ == 516 || occ == 816 ? 16u : occ == 532 || occ == 832 ? 32u : mode == IP_RX ? 16u : 32u;
     if (wg != 256 && wg != 512 && wg != 1024)
         return hipErrorInvalidValue;
     const uint32_t dyn_m = occ > 300 && occ < 500 ? (uint32_t)((occ - 300) & 15 ? (occ - 300) & 15 : 16) : 1u; // k_ipv4_dyn's M

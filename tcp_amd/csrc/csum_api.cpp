@@ -9,6 +9,7 @@
 #include <condition_variable>
 #include <deque>
 #include <functional>
+#include <future>
 #include <chrono>
 #include <mutex>
 #include <stddef.h>
@@ -485,7 +486,7 @@ static const struct {
     {"hostq_dma_kb", tcsum::KNOB_HOSTQ_DMA_KB}, {"hostq_dma_keep_mb", tcsum::KNOB_HOSTQ_DMA_KEEP_MB},
     {"copy_threads", tcsum::KNOB_COPY_THREADS}, {"pf_dist", tcsum::KNOB_PF_DIST}, {"pf_range", tcsum::KNOB_PF_RANGE},
     {"pk_early", tcsum::KNOB_PK_EARLY}, {"page_stage", tcsum::KNOB_PAGE_STAGE},
-    {"seg_sdesc", tcsum::KNOB_SEG_SDESC}, {"pk_list", tcsum::KNOB_PK_LIST},
+    {"seg_sdesc", tcsum::KNOB_SEG_SDESC}, {"pk_one_round", tcsum::KNOB_PK_ONE_ROUND},
 };
 
 static int knob_of(const char *key)
@@ -1047,8 +1048,24 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
     if (const hipError_t e = stage_out ? c.q_res.reserve(sizeof(uint16_t) * n + 64) : hipSuccess; e != hipSuccess)
         return fail(note_mem(16, e));
     uint16_t *hout = stage_out ? reinterpret_cast<uint16_t *>(c.q_res.h) : out;
-    if (const hipError_t e = pl.early ? hipSuccess : copy_span(ch[0].buf, ch[0].sp); e != hipSuccess)
-        return fail_sys(3, e); // its bytes cross while the host stages
+    // The first chunk's bytes cross while the host stages the descriptors.
+    // From pinned memory its copy is queued and returns at once; a pageable
+    // arena's goes slot by slot through host copies that wait on the copy
+    // engine, so a large one (a shuffled batch collapses to ONE chunk, the
+    // whole span) runs on a thread of its own beside the descriptor pass.
+    std::future<hipError_t> first_copy;
+    if (!pl.early) {
+        uint64_t lo, hi;
+        span_copy(ch[0].sp, arena_bytes, lo, hi);
+        if (pageable && hi > lo && hi - lo >= kPageSlot) {
+            first_copy = std::async(std::launch::async, [&, device] {
+                const hipError_t e = hipSetDevice(device); // HIP's current device is per thread
+                return e != hipSuccess ? e : copy_span(ch[0].buf, ch[0].sp);
+            });
+        } else if (const hipError_t e = copy_span(ch[0].buf, ch[0].sp); e != hipSuccess) {
+            return fail_sys(3, e);
+        }
+    }
     tcsum_seg_t *hseg = reinterpret_cast<tcsum_seg_t *>(c.q_desc.h);
     parallel_for(n, size_t(1) << 16, [&](size_t b, size_t e) {
         for (size_t i = b; i < e; ++i) {
@@ -1066,6 +1083,9 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
             hseg[i].pre_sum = (uint32_t)q;
         }
     });
+    if (first_copy.valid())
+        if (const hipError_t e = first_copy.get(); e != hipSuccess)
+            return fail_sys(3, e);
     if (const hipError_t e = hipMemcpyAsync(c.d_descs, hseg, sizeof(tcsum_seg_t) * n, hipMemcpyHostToDevice, cs);
         e != hipSuccess)
         return fail_sys(4, e);

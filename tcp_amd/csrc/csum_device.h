@@ -826,15 +826,16 @@ __device__ __forceinline__ void pk_ranges(const uint8_t *__restrict__ arena, con
 
 constexpr uint32_t kPkMaxPasses = 64; // longer regions go range by range
 constexpr uint32_t kPkEarly = 1u << 7; // aux: the range-by-range path's descriptors by scalar loads (pk_wave_descs)
-// K above which a workgroup whose ranges are not one region hands them to a
-// follow-up launch (k_segments_list) instead of summing them itself
-constexpr uint32_t kPkListMin = 16;
+// aux: the range-by-range path gives every range a group in ONE round where
+// round 5's shapes took two (kw 17..22: 8 lanes x 6 loads instead of 16 x 3;
+// kw 33..64: 4 x 6 instead of 8 x 4) -- debug knob "pk_one_round"
+constexpr uint32_t kPkOneRound = 1u << 6;
 
 // Lanes per range on k_segments_pk's range-by-range path for kw ranges.
-__device__ __forceinline__ uint32_t pk_group(uint32_t T, uint32_t kw)
+__device__ __forceinline__ uint32_t pk_group(uint32_t T, uint32_t kw, bool one_round = false)
 {
     const uint32_t lanes_per = T / kw;
-    return lanes_per >= 64 ? 64u : lanes_per >= 32 ? 32u : lanes_per >= 16 || kw <= 22u ? 16u : 8u;
+    return lanes_per >= 64 ? 64u : lanes_per >= 32 ? 32u : lanes_per >= 16 || (kw <= 22u && !one_round) ? 16u : 8u;
 }
 
 // A workgroup of k_segments_pk whose kw ranges are not one region: G lanes
@@ -852,6 +853,13 @@ __device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, c
     // second round for the ranges past 16 -- and 8 x 4 = 512 B for 23..64,
     // 4 x 2 = 128 B for more; profiles/r05/pk_early/pk_mid*.txt, pk_tiny*.txt)
     const uint32_t lanes_per = T / kw;
+    if ((aux & kPkOneRound) != 0u && lanes_per < 16u && kw <= 64u) {
+        if (kw <= 32u) // ~380..720 B: 8 lanes x 6 loads (768 B), one round
+            pk_ranges<MODE, 8, 6, true>(arena, descs, out, aux, first, kw, T, e0, have0);
+        else // ~190..370 B: 4 lanes x 6 loads (384 B), one round
+            pk_ranges<MODE, 4, 6>(arena, descs, out, aux, first, kw, T, e0, have0);
+        return;
+    }
     if (lanes_per >= 64)
         pk_ranges<MODE, 64, 4, true>(arena, descs, out, aux, first, kw, T, e0, have0);
     else if (lanes_per >= 32)
@@ -873,14 +881,10 @@ __device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, c
 }
 
 
-// list (K > kPkListMin, or nullptr): list[0] counts the workgroups whose
-// ranges are not one region, list[1 + i] names them; such a workgroup only
-// appends itself and leaves, and k_segments_list -- launched next on the
-// same stream -- sums their ranges with the per-range kernel's lane groups.
 template <int MODE, int W = kPkWaves, int U = kPkLoads, bool PROBE = false>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) void k_segments_pk(
     const uint8_t *__restrict__ arena, const void *__restrict__ descs, uint32_t n, uint16_t *__restrict__ out,
-    uint32_t aux, uint32_t xg, uint32_t K, uint32_t *__restrict__ list)
+    uint32_t aux, uint32_t xg, uint32_t K)
 {
     static_assert(MODE != MODE_EXACT, "the exact u32 sum stays on k_segments");
     static_assert(W <= 16, "the sub-range totals are scanned by 32 lanes");
@@ -911,14 +915,6 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     // safe to load before the ranges are known to lie inside it
     const bool span_ok = len0 != 0 && lenl != 0 && rend > r0 &&
                          rend - r0 <= (uint64_t)kPkMaxPasses * CH * 16u - s0;
-    if (!PROBE && !span_ok && list != nullptr) {
-        // a shuffled batch's small ranges (K > 16): K ranges in one 256-thread
-        // workgroup leave its lane groups half idle in a last round; the
-        // follow-up launch's groups take them 256 / G at a time instead
-        if (t == 0)
-            list[1u + __hip_atomic_fetch_add(list, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)] = blk;
-        return;
-    }
     if (!PROBE && !span_ok) {
         // workgroup-uniform, known from the two scalar descriptors: range by
         // range at once (a shuffled batch's usual case), before any stream
@@ -937,7 +933,7 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
         // with scalar loads -- lines the span's loads just brought into the
         // scalar cache -- instead of every lane's vector load going to the L2
         // for them, and each group picks its own
-        const uint32_t G = pk_group(T, kw);
+        const uint32_t G = pk_group(T, kw, (aux & kPkOneRound) != 0u);
         const bool early = (aux & kPkEarly) != 0u && kw <= 32u; // workgroup-uniform
         SegDesc e0{0, 0, 0, 0, 0, 0};
         if (early) {
@@ -1077,41 +1073,6 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
     if (mine)
         out[first + rr] = finalize<MODE>(pe - ps, reinterpret_cast<uintptr_t>(arena + d.off), d, aux, q16);
-}
-
-// The follow-up of k_segments_pk with a list: the ranges of the listed
-// workgroups (list[0] of them, K ranges each -- fewer for the batch's last),
-// G lanes x U loads per range as the per-range kernel k_segments would take
-// them, 256 / G ranges per block and round.  A grid of at most a few
-// thousand blocks walks them (a batch with nothing listed costs one launch
-// whose blocks read list[0] and leave).
-template <int G, int U, int MODE>
-__global__ __launch_bounds__(256) void k_segments_list(const uint8_t *__restrict__ arena,
-                                                       const void *__restrict__ descs, uint32_t n,
-                                                       uint16_t *__restrict__ out, uint32_t aux, uint32_t K,
-                                                       const uint32_t *__restrict__ list)
-{
-    static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G");
-    constexpr uint32_t PER = 256u / G;
-    const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane((int)list[0]);
-    const uint32_t total = cnt * K; // <= n + K - 1: k_segments_pk's grid is ceil(n / K)
-    const uint32_t gl = threadIdx.x & (G - 1u);
-    for (uint32_t v0 = blockIdx.x * PER; v0 < total; v0 += gridDim.x * PER) { // block-uniform
-        const uint32_t v = v0 + threadIdx.x / G;
-        const bool in = v < total;
-        const uint32_t wi = in ? v / K : 0u;
-        const uint32_t seg = list[1u + wi] * K + (v - wi * K);
-        const bool live = in && seg < n;
-        const SegDesc d = load_desc<MODE>(descs, seg, live);
-        uint32_t q16 = 0;
-        uint32_t acc = sum_range<G, U, false>(arena, d.off, d.len, gl, [&] {
-            if constexpr (MODE == MODE_PESO)
-                q16 = pinned(peso_pseudo16(d));
-        });
-        acc = group_sum<G>(acc);
-        if (live && gl == 0)
-            out[seg] = finalize<MODE>(acc, reinterpret_cast<uintptr_t>(arena + d.off), d, aux, q16);
-    }
 }
 
 // ---------------------------------------------------------------- IPv4

@@ -411,46 +411,6 @@ static hipError_t seg_u(int G, int U, uint32_t xg, uint32_t n, const void *arena
     return refused();
 }
 
-static hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t stream);
-
-// The per-range shapes pick_geometry gives ranges short enough for K > 16
-// (mean < ~720 B): the follow-up launch's lane groups.
-static constexpr struct {
-    int g, u;
-} kListShapes[] = {{16, 3}, {16, 4}, {8, 4}, {4, 2}, {4, 1}};
-
-static bool list_shape(Mode mode, int G, int U)
-{
-    if (mode == MODE_EXACT)
-        return false;
-    for (const auto &x : kListShapes)
-        if (x.g == G && x.u == U)
-            return true;
-    return false;
-}
-
-// The follow-up of a listed k_segments_pk launch: enough blocks for every
-// listed range, at most kListBlocks (8 per CU: the per-range kernel's
-// occupancy), each walking the list 256 / G ranges at a time.
-static constexpr uint32_t kListBlocks = 2048;
-
-static hipError_t launch_list(Mode mode, int G, int U, const uint8_t *a, const void *descs, uint32_t n, uint16_t *out,
-                              uint32_t aux, uint32_t K, const uint32_t *list, uint32_t pk_blocks, hipStream_t s)
-{
-    const uint64_t ranges = (uint64_t)pk_blocks * K;
-    const uint32_t per = 256u / (uint32_t)G;
-    const uint64_t want = (ranges + per - 1) / per;
-    const dim3 grid((uint32_t)(want < kListBlocks ? want : kListBlocks)), block(256);
-#define TCSUM_LIST(GG, UU)                                                                                       \
-    if (G == GG && U == UU)                                                                                    \
-        return mode == MODE_SEG                                                                                \
-                   ? launch(k_segments_list<GG, UU, MODE_SEG>, grid, block, 0, s, a, descs, n, out, aux, K, list) \
-                   : launch(k_segments_list<GG, UU, MODE_PESO>, grid, block, 0, s, a, descs, n, out, aux, K, list);
-    TCSUM_LIST(16, 3) TCSUM_LIST(16, 4) TCSUM_LIST(8, 4) TCSUM_LIST(4, 2) TCSUM_LIST(4, 1)
-#undef TCSUM_LIST
-    return refused();
-}
-
 // The AQL dispatch packet counts work-items in 32 bits: one launch may carry
 // at most 2^24 - 1 workgroups of 256 threads.  Larger batches are split into
 // several launches over consecutive descriptor ranges.
@@ -486,30 +446,11 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
                                                                           : kPkMaxRanges * kPkWaves;
         const uint8_t *a = static_cast<const uint8_t *>(arena);
         const dim3 gr((n + K - 1) / K), bl(kPkWaves * 64);
-        const uint32_t ax = aux | (pf_dist() << 8) | (pk_early() ? kPkEarly : 0u);
-        // K > 16: a workgroup whose ranges are not one region hands them to a
-        // follow-up launch in the per-range kernel's lane groups
-        const bool listed = K > kPkListMin && knob(KNOB_PK_LIST) != 0 && list_shape(mode, g.lanes, g.loads);
-        uint32_t *list = nullptr;
-        if (listed) {
-            hipError_t e = scratch_alloc(reinterpret_cast<void **>(&list), 4ull * (1ull + gr.x), stream);
-            if (e == hipSuccess && (e = hipMemsetAsync(list, 0, 4, stream)) != hipSuccess)
-                (void)hipFreeAsync(list, stream);
-            if (e != hipSuccess)
-                return e;
-        }
-        hipError_t e = mode == MODE_SEG
-                           ? launch(k_segments_pk<MODE_SEG>, gr, bl, 0, stream, a, descs, n, out, ax, (uint32_t)g.xcd,
-                                    K, list)
-                           : launch(k_segments_pk<MODE_PESO>, gr, bl, 0, stream, a, descs, n, out, ax,
-                                    (uint32_t)g.xcd, K, list);
-        if (listed) {
-            if (e == hipSuccess)
-                e = launch_list(mode, g.lanes, g.loads, a, descs, n, out, aux, K, list, gr.x, stream);
-            const hipError_t f = hipFreeAsync(list, stream);
-            e = e != hipSuccess ? e : f;
-        }
-        return e;
+        const uint32_t ax = aux | (pf_dist() << 8) | (pk_early() ? kPkEarly : 0u) |
+                            (knob(KNOB_PK_ONE_ROUND) > 0 ? kPkOneRound : 0u);
+        if (mode == MODE_SEG)
+            return launch(k_segments_pk<MODE_SEG>, gr, bl, 0, stream, a, descs, n, out, ax, (uint32_t)g.xcd, K);
+        return launch(k_segments_pk<MODE_PESO>, gr, bl, 0, stream, a, descs, n, out, ax, (uint32_t)g.xcd, K);
     }
     if (mode == MODE_EXACT) {
         return launch(k_segments<64, 8, MODE_EXACT>, dim3((n + 3) / 4), dim3(256), 0, stream,

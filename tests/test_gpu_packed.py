@@ -279,24 +279,23 @@ def test_layout_hints_give_the_same_results(tc, torch, oracle, layout):
         np.testing.assert_array_equal(down(out), want_s)
 
 
-LIST_CASES = [(64, "shuffled"), (200, "shuffled"), (576, "shuffled"), (700, "shuffled"), (200, "half"),
-              (576, "half"), (64, "packed"), (576, "packed"), (300, "zeros")]
+SMALL_CASES = [(64, "shuffled"), (200, "shuffled"), (576, "shuffled"), (700, "shuffled"), (400, "shuffled"),
+               (200, "half"), (576, "half"), (64, "packed"), (576, "packed"), (300, "zeros")]
 
 
-@pytest.mark.parametrize("mean,layout", LIST_CASES)
+@pytest.mark.parametrize("mean,layout", SMALL_CASES)
 @pytest.mark.parametrize("mode", ["peso", "segments"])
-def test_listed_follow_up(tc, torch, oracle, mean, layout, mode):
-    """K > 16 with no layout hint (the router's own choice): the packed
-    kernel's workgroups whose ranges are not one region append themselves to
-    a device list and k_segments_list sums their ranges in the per-range
-    kernel's lane groups.  Fully shuffled, half the workgroups shuffled
-    (both paths in one launch), fully packed (an empty list), and ranges of
-    length 0; n never a multiple of K.  Results equal the oracle's and the
-    knob-off run (pk_list = 0: the in-workgroup fallback)."""
+def test_small_ranges_unknown_layout(tc, torch, oracle, mean, layout, mode):
+    """Ranges under ~750 B (K > 16 ranges per packed workgroup) with no
+    layout hint, the router's own choice: fully shuffled (every workgroup
+    range by range), half the workgroups shuffled (both paths in one launch),
+    fully packed, and ranges of length 0; n never a multiple of K.  The
+    range-by-range path in its default shapes and in one round of lane
+    groups (debug knob pk_one_round) equals the oracle."""
     r = tc.route(mean)
-    assert r["packed"] > 16, r  # the shapes under test take the list path
+    assert r["packed"] > 16, r
     K = r["packed"]
-    rng = np.random.default_rng(mean * 7 + LIST_CASES.index((mean, layout)) * 131 + (mode == "peso"))
+    rng = np.random.default_rng(mean * 7 + SMALL_CASES.index((mean, layout)) * 131 + (mode == "peso"))
     n = K * 97 + int(rng.integers(1, K))
     lens = rng.integers(max(1, mean // 2), mean * 3 // 2 + 1, n).astype(np.uint32)
     if layout == "zeros":
@@ -305,11 +304,10 @@ def test_listed_follow_up(tc, torch, oracle, mean, layout, mode):
     offs = _packed_offs(lens, start)
     if layout == "shuffled":
         perm = rng.permutation(n)
-    elif layout == "half":  # every other workgroup's K ranges shuffled among themselves and a far one
+    elif layout == "half":  # every other workgroup's K ranges permuted among themselves
         perm = np.arange(n)
         for w in range(0, n // K, 2):
-            blk = perm[w * K:(w + 1) * K].copy()
-            perm[w * K:(w + 1) * K] = rng.permutation(blk)
+            perm[w * K:(w + 1) * K] = rng.permutation(perm[w * K:(w + 1) * K])
     else:
         perm = np.arange(n)
     host = _arena(rng, start + int(lens.sum()) + 4096)
@@ -326,5 +324,5 @@ def test_listed_follow_up(tc, torch, oracle, mean, layout, mode):
         run = lambda: tc.batch_segments(up(torch.from_numpy(host)), tc.descs_to_device(d), n, 1, total)  # noqa: E731
         want = oracle.batch_segments(host, d, 1, nthreads=8)
     np.testing.assert_array_equal(down(run()), want)
-    with tc.debug(pk_list=0):
+    with tc.debug(pk_one_round=1):
         np.testing.assert_array_equal(down(run()), want)

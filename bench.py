@@ -49,7 +49,7 @@ METRIC = "Internet-checksum GiB/s (device-resident), 1500B & 64KB packet batches
 
 def _host(t):
     """A device tensor's values as numpy, copied through pinned memory only
-    (tcp_amd.to_host; DESIGN.md §5)."""
+    (tcp_amd.to_host; DESIGN.md §4)."""
     from tcp_amd import to_host
     return to_host(t)
 
@@ -126,7 +126,7 @@ def algorithmic_bytes(batch) -> int:
 
 # Counter bytes per byte of each access class the step kernels make, measured
 # by scripts/pmc_calib.py on MI355X (known byte counts, each class alone after
-# an L2 flush; profiles/r03/pmc_calib.json).  Keys: the class
+# an L2 flush; profiles/r03/pmc_calib.json, profiles/history/DESIGN_rounds1-5.md §6).  Keys: the class
 # kernels of scripts/pmc_calib.hip; None would fall back to the guide's
 # blanket x2 for FETCH_SIZE.
 PMC_CALIB = {

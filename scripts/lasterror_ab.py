@@ -1,4 +1,4 @@
-"""Round 4's intermittent TCSUM_ERR_SYS, before and after:
+"""Round 4's intermittent TCSUM_ERR_SYS, before and after (profiles/history/DESIGN_rounds1-5.md §5):
 one process, two builds of libtcsum.so -- round 4's (launches judged by the
 thread's last-error slot) and this tree's (each launch's own status) -- each
 called right after the calling thread's slot was left dirty, by a NotReady

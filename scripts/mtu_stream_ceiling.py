@@ -14,7 +14,7 @@ One process.  Interleaved rounds (the leg timed first rotated each round) of:
   read_eq   tcsum_probe_read over 1.6001 GB
 Median us per launch; GB/s priced on the bytes each leg moves.  Round 4's
 verdict read the gap between mtu and as64k in microseconds; in bytes per
-second it is the descriptor array.
+second it is the descriptor array (profiles/r05/README.md).
 
   python scripts/mtu_stream_ceiling.py [ROUNDS]
 """

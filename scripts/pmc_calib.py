@@ -1,4 +1,4 @@
-"""Calibrate FETCH_SIZE / WRITE_SIZE per access class.
+"""Calibrate FETCH_SIZE / WRITE_SIZE per access class (profiles/history/DESIGN_rounds1-5.md §6).
 
 Runs scripts/build/pmc_calib (scripts/pmc_calib.hip) under rocprofv3 twice,
 one counter per pass (FETCH_SIZE, then WRITE_SIZE: they cannot share a pass),

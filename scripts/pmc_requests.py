@@ -1,4 +1,4 @@
-"""What FETCH_SIZE is made of, per kernel: the L2's
+"""What FETCH_SIZE is made of, per kernel (profiles/r05/README.md): the L2's
 memory-side read requests (TCC_EA0_RDREQ, of which TCC_EA0_RDREQ_32B are
 32-byte and TCC_BUBBLE 128-byte ones; FETCH_SIZE = 128 x BUBBLE + 64 x (the
 rest) + 32 x 32B), the scalar cache's read requests to the L2

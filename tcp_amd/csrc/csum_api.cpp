@@ -591,7 +591,7 @@ int tcsum_batch(int op, void *arena, const void *descs, uint32_t n, void *out, u
         // all the field stores in one short second launch (mode 4) -- 4-6 %
         // faster on configs[3] than storing each packet's fields as its sums
         // finish, which trickles a million isolated writes through the read
-        // stream (tx fill).  Small batches keep one launch.
+        // stream (profiles/history/DESIGN_rounds1-5.md §6, tx fill).  Small batches keep one launch.
         // Debug knob "tx_split" forces.  Under hipGraph capture the
         // single-launch form is taken: it allocates nothing (tcsum.h).
         const int64_t ks = tcsum::knob(tcsum::KNOB_TX_SPLIT);
@@ -940,13 +940,13 @@ int tcsum_host_batch_peso(int device, const void *host_arena, uint64_t arena_byt
         return hipSuccess;
     };
     // Pageable caller memory passes through the context's pinned slots (host
-    // threads fill one while the copy engine drains the others), so no copy
-    // ever reads the caller's pages through the runtime's own pageable path.
-    // Two suites stopped on that path: round 4 (TCSUM_ERR_SYS, fuzz seed 26)
-    // and round 5 (hipErrorIllegalAddress from this call's first copy, fuzz
-    // seed 27), each in the batch right after a hipHostRegister'ed arena was
-    // unregistered and freed.  Debug knob "page_stage" = 0: the
-    // runtime's path (measurement).
+    // threads fill one while the copy engine drains the others): every DMA
+    // reads memory the library owns.  Round 5 moved off the runtime's own
+    // pageable path after two suites stopped at this call's first copy; round
+    // 6 found the runtime's path clean on its own and the fault's cause
+    // elsewhere unrecorded.  Debug knob "page_stage" = 0: the
+    // runtime's path (measurement: 50.5 against 49.6 GiB/s,
+    // profiles/r06/ab/e2e_pageable.txt).
     const bool pageable = tcsum::knob(tcsum::KNOB_PAGE_STAGE) != 0 && mapped_host(host_arena) == nullptr;
     if (pageable && !c.pev_ok) {
         for (auto &e : c.pev) // a failure part-way keeps those made: the next call makes only the rest

@@ -44,7 +44,7 @@ namespace tcsum {
 // on that thread may have left set -- a caller's own failed call, or a
 // hipStreamQuery that answered hipErrorNotReady -- and a launch that
 // succeeded was then reported as failed (round 4's intermittent
-// TCSUM_ERR_SYS from tcsum_host_batch_peso).  The arguments
+// TCSUM_ERR_SYS from tcsum_host_batch_peso, profiles/history/DESIGN_rounds1-5.md §5).  The arguments
 // are converted to the kernel's parameter types first, as a <<<>>> call
 // would convert them.
 template <typename... P, typename... A>
@@ -1097,7 +1097,7 @@ constexpr uint32_t IP_OPT_NO_STORE = 1u; // IP_TX: compute the fill's values, le
 // IP_TX, deferred stores (launch_ipv4 mode 4): the values go to `out` and each
 // packet's store positions to a side array (through the verdict pointer, which
 // tx never uses); k_tx_scatter then writes them into the packets in a second,
-// short launch (DESIGN.md Â§6, tx fill)
+// short launch (profiles/history/DESIGN_rounds1-5.md §6, tx fill)
 constexpr uint32_t IP_OPT_DEFER = 2u;
 // launch_ipv4 mode 3: IP_TX kernels with IP_OPT_NO_STORE
 constexpr int IP_TX_OFFLOAD = 3;

@@ -63,7 +63,7 @@ def _torch():
 def descs_to_device(descs: np.ndarray, device="cuda"):
     """Copy a structured descriptor array to the device as raw bytes, through
     pinned host memory: the runtime's own pageable host-to-device path is the
-    one three GPU suites stopped on (DESIGN.md §5)."""
+    one three GPU suites stopped on (DESIGN.md §4)."""
     torch = _torch()
     raw = np.ascontiguousarray(descs).view(np.uint8)
     return torch.from_numpy(raw.copy()).pin_memory().to(device)
@@ -75,7 +75,7 @@ _HOST_CHUNK = 64 << 20
 def to_host_tensor(t):
     """A device tensor's values in host memory, copied by the GPU only into
     pinned memory: the runtime's pageable device-to-host path is, with the
-    host-to-device one, where the round-5 GPU suites stopped (DESIGN.md §5).
+    host-to-device one, where the round-5 GPU suites stopped (DESIGN.md §4).
     Up to 64 MiB: one pinned tensor; larger: chunk by chunk through a 64-MiB
     pinned bounce buffer into a pageable tensor (a power-of-two pinned block
     per multi-GB result would pin twice its size).  Synchronous, like

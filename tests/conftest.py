@@ -42,7 +42,7 @@ def _device_drained(request):
     """After every GPU test: the whole device synchronized and its status
     checked -- every stream, the library's own and its resident servers
     included -- so a device fault is charged to the test whose work
-    faulted, not to a later test's first HIP call (DESIGN.md §5)."""
+    faulted, not to a later test's first HIP call (DESIGN.md §4)."""
     yield
     if request.node.get_closest_marker("gpu") is None:
         return

@@ -2,7 +2,7 @@
 
 Default: through pinned host memory -- up(): pin_memory() then .cuda();
 down(): tcp_amd.to_host (a pinned tensor, or a 64-MiB pinned bounce buffer).
-TCSUM_TEST_PAGEABLE=1 (the diagnostic suite of DESIGN.md §5): the runtime's
+TCSUM_TEST_PAGEABLE=1 (the diagnostic suite of DESIGN.md §4): the runtime's
 pageable copies in both directions and the library's pageable staging off
 (debug knob page_stage = 0, conftest.py) -- round 4's configuration, the one
 the five hipErrorIllegalAddress stops came in.

@@ -94,7 +94,7 @@ def test_product_code_object_holds_only_product_kernels(libpath):
     stray = [k for k in prod if not any(f in k for f in families) or "true>" in k]
     assert not stray, stray
     assert not any("k_probe" in k or "k_synth" in k or "k_segments_p<" in k or "k_segments_pp<" in k for k in prod)
-    # the byte-window stream lost to k_ipv4 and is not
+    # the byte-window stream lost to k_ipv4 (profiles/r04/README.md) and is not
     # routed: measurement code, in libtcsum_bench.so only
     assert not any("k_flat_" in k for k in prod)
     bench = code_object_kernels(_lib.BENCH_LIB_PATH)

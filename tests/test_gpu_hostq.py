@@ -30,7 +30,7 @@ def tc():
 # not fault that way (scripts/register_reuse_probe.py: 10,000 register / GPU
 # read / unregister / free / pinned-alloc cycles between pageable copies,
 # clean), and the GPU suite with every round-4 pageable path back ran clean
-# (profiles/r06/, DESIGN.md §5).
+# (profiles/r06/, DESIGN.md §4).
 from devcopy import down  # noqa: E402
 
 

@@ -1,4 +1,4 @@
-"""Round 4's intermittent TCSUM_ERR_SYS, made deterministic.
+"""Round 4's intermittent TCSUM_ERR_SYS (profiles/history/DESIGN_rounds1-5.md §5), made deterministic.
 
 Every launch of libtcsum.so used to judge itself by hipGetLastError(), the
 calling thread's last-error slot -- which holds the first failed runtime

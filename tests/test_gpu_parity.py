@@ -795,7 +795,7 @@ def test_host_batch_pageable_staging(tc, oracle, order):
     """A pageable arena crosses through the context's three 32-MiB pinned
     slots -- 150 MB, so every slot is refilled after its copy-done event.
     (The runtime's own pageable copy, debug knob page_stage = 0, is not run
-    here: DESIGN.md §5.)"""
+    here: DESIGN.md §4.)"""
     from tcp_amd import workload
     b = workload.make_batch("mtu", n=100000)
     host = oracle.synth_fill(b.byte_base, b.alloc_bytes, b.seed)

@@ -1,5 +1,5 @@
 """tcp_amd.to_host / to_host_tensor: device tensors read back through pinned
-memory only (DESIGN.md §5), and the tests' read-back helper over it
+memory only (DESIGN.md §4), and the tests' read-back helper over it
 (tests/devcopy.py)."""
 import numpy as np
 import pytest

@@ -34,9 +34,6 @@ extern "C" {
  *                     -- lines its span check just cached -- instead of
  *                     vector loads through the L2; with 0, SHUFFLED batches
  *                     always take the per-range kernel
- *   "pk_one_round"    0 / 1 (default 0): that path gives 17..64 ranges one
- *                     round of lane groups (8 x 6 or 4 x 6 loads) instead of
- *                     two (measurement)
  *   "lanes", "loads"  per-range kernel shape (lanes per range x 16-B loads per
  *                     lane): one of the shapes the router picks -- 4x1, 4x2,
  *                     8x4, 16x3, 16x4, 16x6, 16x8, 32x6, 256x16, 1024x4 (IPv4

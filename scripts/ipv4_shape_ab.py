@@ -76,8 +76,11 @@ for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mi
 
     if LDS_ONLY:
         if rx:
+            def lanes32(o, v):
+                with tc.debug(lanes=32, loads=6):
+                    product(o, v)
             kinds.update({"LDS ring 16x6": shape(256, 800), "LDS ring 16x4": shape(256, 804),
-                          "LDS ring 32x6": shape(256, 832)})
+                          "LDS ring 32x6": shape(256, 832), "product at 32 x 6 (no ring)": lanes32})
         else:
             kinds.update({"3rd header chunk as a dword (H1)": shape(256, 900), "LDS ring 32x6": shape(256, 800),
                           "LDS ring 32x6 + H1": shape(256, 905), "LDS ring 32x4": shape(256, 804),

@@ -826,16 +826,12 @@ __device__ __forceinline__ void pk_ranges(const uint8_t *__restrict__ arena, con
 
 constexpr uint32_t kPkMaxPasses = 64; // longer regions go range by range
 constexpr uint32_t kPkEarly = 1u << 7; // aux: the range-by-range path's descriptors by scalar loads (pk_wave_descs)
-// aux: the range-by-range path gives every range a group in ONE round where
-// round 5's shapes took two (kw 17..22: 8 lanes x 6 loads instead of 16 x 3;
-// kw 33..64: 4 x 6 instead of 8 x 4) -- debug knob "pk_one_round"
-constexpr uint32_t kPkOneRound = 1u << 6;
 
 // Lanes per range on k_segments_pk's range-by-range path for kw ranges.
-__device__ __forceinline__ uint32_t pk_group(uint32_t T, uint32_t kw, bool one_round = false)
+__device__ __forceinline__ uint32_t pk_group(uint32_t T, uint32_t kw)
 {
     const uint32_t lanes_per = T / kw;
-    return lanes_per >= 64 ? 64u : lanes_per >= 32 ? 32u : lanes_per >= 16 || (kw <= 22u && !one_round) ? 16u : 8u;
+    return lanes_per >= 64 ? 64u : lanes_per >= 32 ? 32u : lanes_per >= 16 || kw <= 22u ? 16u : 8u;
 }
 
 // A workgroup of k_segments_pk whose kw ranges are not one region: G lanes
@@ -852,14 +848,10 @@ __device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, c
     // K = 9..11, 16 x 4 = 1 KiB for 12..16, 16 x 3 = 768 B for 17..22 -- a
     // second round for the ranges past 16 -- and 8 x 4 = 512 B for 23..64,
     // 4 x 2 = 128 B for more; profiles/r05/pk_early/pk_mid*.txt, pk_tiny*.txt)
+    // (One round of narrower groups instead -- 8 x 6 for 17..32 ranges, 4 x 6
+    // for 33..64 -- measured 1.08-1.15x slower on shuffled 200-576-B ranges,
+    // profiles/r06/ab2/pk_one_round_ab.txt.)
     const uint32_t lanes_per = T / kw;
-    if ((aux & kPkOneRound) != 0u && lanes_per < 16u && kw <= 64u) {
-        if (kw <= 32u) // ~380..720 B: 8 lanes x 6 loads (768 B), one round
-            pk_ranges<MODE, 8, 6, true>(arena, descs, out, aux, first, kw, T, e0, have0);
-        else // ~190..370 B: 4 lanes x 6 loads (384 B), one round
-            pk_ranges<MODE, 4, 6>(arena, descs, out, aux, first, kw, T, e0, have0);
-        return;
-    }
     if (lanes_per >= 64)
         pk_ranges<MODE, 64, 4, true>(arena, descs, out, aux, first, kw, T, e0, have0);
     else if (lanes_per >= 32)
@@ -933,7 +925,7 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(8))) voi
         // with scalar loads -- lines the span's loads just brought into the
         // scalar cache -- instead of every lane's vector load going to the L2
         // for them, and each group picks its own
-        const uint32_t G = pk_group(T, kw, (aux & kPkOneRound) != 0u);
+        const uint32_t G = pk_group(T, kw);
         const bool early = (aux & kPkEarly) != 0u && kw <= 32u; // workgroup-uniform
         SegDesc e0{0, 0, 0, 0, 0, 0};
         if (early) {

@@ -446,8 +446,7 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
                                                                           : kPkMaxRanges * kPkWaves;
         const uint8_t *a = static_cast<const uint8_t *>(arena);
         const dim3 gr((n + K - 1) / K), bl(kPkWaves * 64);
-        const uint32_t ax = aux | (pf_dist() << 8) | (pk_early() ? kPkEarly : 0u) |
-                            (knob(KNOB_PK_ONE_ROUND) > 0 ? kPkOneRound : 0u);
+        const uint32_t ax = aux | (pf_dist() << 8) | (pk_early() ? kPkEarly : 0u);
         if (mode == MODE_SEG)
             return launch(k_segments_pk<MODE_SEG>, gr, bl, 0, stream, a, descs, n, out, ax, (uint32_t)g.xcd, K);
         return launch(k_segments_pk<MODE_PESO>, gr, bl, 0, stream, a, descs, n, out, ax, (uint32_t)g.xcd, K);

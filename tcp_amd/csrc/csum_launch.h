@@ -68,7 +68,6 @@ enum Knob : int {
     KNOB_PK_EARLY,     // 0 / 1: k_segments_pk's range-by-range path reads its descriptors with scalar loads (1)
     KNOB_PAGE_STAGE,   // 0 / 1: tcsum_host_batch_peso copies a pageable arena through its own pinned slots (1)
     KNOB_SEG_SDESC,    // 0 / 1: the per-range kernel (8-16 lanes per range) reads its descriptors with scalar loads (1)
-    KNOB_PK_ONE_ROUND, // 0 / 1: k_segments_pk's range-by-range path in one round for kw 17..64 (measurement, 0)
     KNOB_COUNT
 };
 int64_t knob(Knob k);

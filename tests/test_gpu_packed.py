@@ -289,9 +289,9 @@ def test_small_ranges_unknown_layout(tc, torch, oracle, mean, layout, mode):
     """Ranges under ~750 B (K > 16 ranges per packed workgroup) with no
     layout hint, the router's own choice: fully shuffled (every workgroup
     range by range), half the workgroups shuffled (both paths in one launch),
-    fully packed, and ranges of length 0; n never a multiple of K.  The
-    range-by-range path in its default shapes and in one round of lane
-    groups (debug knob pk_one_round) equals the oracle."""
+    fully packed, and ranges of length 0; n never a multiple of K.  Every
+    path equals the oracle; so does the per-range kernel the SHUFFLED hint
+    takes for these lengths."""
     r = tc.route(mean)
     assert r["packed"] > 16, r
     K = r["packed"]
@@ -324,5 +324,5 @@ def test_small_ranges_unknown_layout(tc, torch, oracle, mean, layout, mode):
         run = lambda: tc.batch_segments(up(torch.from_numpy(host)), tc.descs_to_device(d), n, 1, total)  # noqa: E731
         want = oracle.batch_segments(host, d, 1, nthreads=8)
     np.testing.assert_array_equal(down(run()), want)
-    with tc.debug(pk_one_round=1):
+    with tc.debug(packed=0):
         np.testing.assert_array_equal(down(run()), want)

@@ -550,7 +550,7 @@ def _cpuset_count(text):
     return n
 
 
-def cpu_allowance():
+def cpu_allowance(base="/sys/fs/cgroup", proc_cgroup="/proc/self/cgroup"):
     """The CPUs this process may actually use, which on a shared GPU box is not
     os.cpu_count() (the whole host): the affinity mask, and the cgroup's
     cpuset and CPU quota (v2 cpu.max, or v1 cfs_quota_us / cfs_period_us).
@@ -564,7 +564,7 @@ def cpu_allowance():
         pass
     v2, v1 = "", {}
     try:
-        with open("/proc/self/cgroup") as f:
+        with open(proc_cgroup) as f:
             for ln in f:
                 h, ctl, path = ln.strip().split(":", 2)
                 if h == "0" and not ctl:
@@ -574,7 +574,6 @@ def cpu_allowance():
                         v1[c] = path
     except (OSError, ValueError):
         pass
-    base = "/sys/fs/cgroup"
     quotas, cpusets = [], []
 
     def walk(root, rel):  # the process's own cgroup and each ancestor: the tightest limit binds

@@ -196,3 +196,36 @@ def test_launcher_rehearsal_many_ranks(world):
     # whole N-rank run fits the driver's limit with margin
     assert 0 < line["process_wall_s"] < 0.5 * line["driver_limit_s"]
     check_multi_device(line, world)
+
+
+def test_cpu_allowance_reads_cgroup_limits(tmp_path):
+    """The all-core CPU baseline runs as many threads as the process may use:
+    the affinity mask, and the tightest cgroup cpuset and CPU quota on the
+    way to the root (v2 cpu.max / cpuset.cpus.effective; v1 cfs quota and
+    cpuset), not the host's os.cpu_count()."""
+    import os
+
+    import bench
+    assert bench._cpuset_count("0-15,32-47\n") == 32 and bench._cpuset_count("3") == 1
+    aff = len(os.sched_getaffinity(0))
+    # v2: a 16-CPU quota on the lease's cgroup, 32 CPUs in its parent's cpuset
+    root = tmp_path / "v2"
+    (root / "lease" / "job").mkdir(parents=True)
+    (root / "lease" / "cpu.max").write_text("1600000 100000\n")
+    (root / "cpuset.cpus.effective").write_text("0-15,32-47\n")
+    (root / "lease" / "job" / "cpu.max").write_text("max 100000\n")
+    (tmp_path / "cg2").write_text("0::/lease/job\n")
+    a = bench.cpu_allowance(str(root), str(tmp_path / "cg2"))
+    assert a["cpu_quota"] == 16.0 and a["cpuset"] == 32 and a["effective"] == min(aff, 16)
+    # v1: cfs quota of 2.5 CPUs under the cpu controller's path
+    root = tmp_path / "v1"
+    (root / "cpu" / "grp").mkdir(parents=True)
+    (root / "cpu" / "grp" / "cpu.cfs_quota_us").write_text("250000\n")
+    (root / "cpu" / "grp" / "cpu.cfs_period_us").write_text("100000\n")
+    (tmp_path / "cg1").write_text("4:cpu,cpuacct:/grp\n3:cpuset:/\n")
+    a = bench.cpu_allowance(str(root), str(tmp_path / "cg1"))
+    assert a["cpu_quota"] == 2.5 and a["effective"] == min(aff, 2)
+    # nothing limits: the affinity mask
+    (tmp_path / "cg0").write_text("0::/\n")
+    a = bench.cpu_allowance(str(tmp_path / "empty"), str(tmp_path / "cg0"))
+    assert "cpu_quota" not in a and a["effective"] == aff

@@ -827,7 +827,8 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
     if (n == 0)
         return hipSuccess;
     const uint32_t xg = (uint32_t)route(1500).xcd;
-    const uint32_t G = occ == 516 || occ == 816 ? 16u : occ == 532 || occ == 832 ? 32u : mode == IP_RX ? 16u : 32u;
+    const uint32_t G = occ == 516 || occ == 816 ? 16u : occ == 964 ? 64u : occ == 532 || occ == 832 ? 32u
+                       : mode == IP_RX ? 16u : 32u;
     if (wg != 256 && wg != 512 && wg != 1024)
         return hipErrorInvalidValue;
     const uint32_t dyn_m = occ > 300 && occ < 500 ? (uint32_t)((occ - 300) & 15 ? (occ - 300) & 15 : 16) : 1u; // k_ipv4_dyn's M
@@ -858,6 +859,9 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 804 && wg == 256) { TCSUM_SH((k_ipv4<32, 4, IP_SUMS, 256, 0, 5>)) }
         if (occ == 808 && wg == 256) { TCSUM_SH((k_ipv4<32, 8, IP_SUMS, 256, 0, 5>)) }
         if (occ == 816 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_SUMS, 256, 0, 5>)) }
+        // one 6-KiB pass per packet: a wave per packet (64 x 6) or 32 lanes x 12 loads
+        if (occ == 964 && wg == 256) { TCSUM_SH((k_ipv4<64, 6, IP_SUMS, 256>)) }
+        if (occ == 932 && wg == 256) { TCSUM_SH((k_ipv4<32, 12, IP_SUMS, 256>)) }
         // the third header chunk as one dword (H1), alone and with PIPE 5
         if (occ == 900 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 0, 0, true>)) }
         if (occ == 905 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 0, 5, true>)) }

@@ -26,6 +26,7 @@ ROLL_ONLY = "--roll" in sys.argv  # rolling load slots: a multi-pass packet keep
 HDRX_ONLY = "--hdrx" in sys.argv  # header chunks shuffled from the first data pass instead of loaded
 SDESC_ONLY = "--sdesc" in sys.argv  # the descriptors by scalar loads
 LDS_ONLY = "--lds" in sys.argv  # later passes by LDS-DMA into a per-wave ring (PIPE 5); the 3rd header chunk as a dword
+PAIR_ONLY = "--pair" in sys.argv  # two packets a wave streamed as one run of chunks (k_ipv4_pair)
 PASS_ONLY = "--pass" in sys.argv  # 6-KiB passes: a wave per packet (64 x 6), or 32 lanes x 12 loads
 
 def equal_length(L, op):
@@ -75,7 +76,11 @@ for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mi
                 f(o, v)
         return g
 
-    if PASS_ONLY:
+    if PAIR_ONLY:
+        kinds.update({"pair stream, 64 x 6": shape(256, 1006), "pair stream, 64 x 4": shape(256, 1004)})
+        if not rx:
+            kinds["pair stream, 64 x 3"] = shape(256, 1003)
+    elif PASS_ONLY:
         kinds.update({"64 lanes x 6 (a wave per packet)": shape(256, 964), "32 lanes x 12": shape(256, 932)})
     elif LDS_ONLY:
         if rx:

@@ -827,7 +827,8 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
     if (n == 0)
         return hipSuccess;
     const uint32_t xg = (uint32_t)route(1500).xcd;
-    const uint32_t G = occ == 516 || occ == 816 ? 16u : occ == 964 ? 64u : occ == 532 || occ == 832 ? 32u
+    const uint32_t G = occ == 516 || occ == 816 ? 16u : occ == 964 ? 64u
+                       : occ == 532 || occ == 832 || (occ >= 1000 && occ < 1100) ? 32u
                        : mode == IP_RX ? 16u : 32u;
     if (wg != 256 && wg != 512 && wg != 1024)
         return hipErrorInvalidValue;
@@ -859,6 +860,10 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 804 && wg == 256) { TCSUM_SH((k_ipv4<32, 4, IP_SUMS, 256, 0, 5>)) }
         if (occ == 808 && wg == 256) { TCSUM_SH((k_ipv4<32, 8, IP_SUMS, 256, 0, 5>)) }
         if (occ == 816 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_SUMS, 256, 0, 5>)) }
+        // two packets a wave streamed as one run of chunks (ipv4_pair)
+        if (occ == 1006 && wg == 256) { TCSUM_SH((k_ipv4_pair<6, IP_SUMS>)) }
+        if (occ == 1004 && wg == 256) { TCSUM_SH((k_ipv4_pair<4, IP_SUMS>)) }
+        if (occ == 1003 && wg == 256) { TCSUM_SH((k_ipv4_pair<3, IP_SUMS>)) }
         // one 6-KiB pass per packet: a wave per packet (64 x 6) or 32 lanes x 12 loads
         if (occ == 964 && wg == 256) { TCSUM_SH((k_ipv4<64, 6, IP_SUMS, 256>)) }
         if (occ == 932 && wg == 256) { TCSUM_SH((k_ipv4<32, 12, IP_SUMS, 256>)) }
@@ -892,6 +897,8 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 600 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256, 0, 3>)) } // header from the data pass
         if (occ == 700 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256, 0, 4>)) } // scalar descriptors
         if (occ == 800 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256, 0, 5>)) } // LDS-DMA ring
+        if (occ == 1006 && wg == 256) { TCSUM_SH((k_ipv4_pair<6, IP_RX>)) } // two packets a wave, one stream
+        if (occ == 1004 && wg == 256) { TCSUM_SH((k_ipv4_pair<4, IP_RX>)) }
         if (occ == 804 && wg == 256) { TCSUM_SH((k_ipv4<16, 4, IP_RX, 256, 0, 5>)) }
         if (occ == 832 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_RX, 256, 0, 5>)) }
     }

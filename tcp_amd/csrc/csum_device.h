@@ -1718,6 +1718,170 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
                                     opts);
 }
 
+// Two packets per wave streamed as ONE run of chunks (measurement, round 6):
+// the wave's 64 lanes walk packet A's chunks (from its 128-B line) and then
+// packet B's in passes of 64 x U, so the pair takes ceil((chunks A + chunks
+// B) / 64U) passes where k_ipv4's two 32-lane groups take the longer
+// packet's ceil(chunks / 32U) -- on configs[3] 2.00 passes a wave against
+// 2.44.  Lanes 0..31 load and parse A's header, 32..63 B's (as k_ipv4<32>'s
+// groups do); the stream's per-packet bounds are read out to scalars; each
+// lane keeps a header and an L4 sum per packet; lane 0 finishes A, lane 32 B.
+template <int U, int IPM>
+__device__ __forceinline__ void ipv4_pair(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
+                                          uint32_t pa, uint32_t n, uint32_t *__restrict__ out,
+                                          uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
+                                          uint32_t opts)
+{
+    const uint32_t ln = threadIdx.x & 63u;
+    const uint32_t pk = pa + (ln >> 5); // this lane's home packet: A (lanes 0..31) or B
+    const bool live = pk < n;
+    const u32x4 dv = *reinterpret_cast<const u32x4 *>(pkts + (live ? pk : 0u));
+    const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+    const uint32_t frame = live ? dv.z : 0u;
+    const bool big_enough = frame >= 20;
+    uint8_t *pp = arena + off;
+    const uintptr_t start = reinterpret_cast<uintptr_t>(pp);
+    const uint32_t s0 = (uint32_t)(start & 15u);
+    const u32x4 *base = reinterpret_cast<const u32x4 *>(pp - s0);
+    const uint32_t frame_ld = frame < 65600u ? frame : 65600u;
+    const uint32_t nch = big_enough ? (frame_ld + s0 + 15) >> 4 : 0u;
+    const uint32_t sl = (uint32_t)(start & 127u);
+    const uint32_t dch = big_enough ? (frame_ld + sl + 15) >> 4 : 0u;
+    // the pair's stream: A's chunks [0, dA), then B's [dA, dA + dB)
+    const uint32_t dA = (uint32_t)__builtin_amdgcn_readlane((int)dch, 0);
+    const uint32_t dB = (uint32_t)__builtin_amdgcn_readlane((int)dch, 32);
+    const uint32_t total = dA + dB;
+    const uint64_t lineA = readlane64((uint64_t)(start - sl), 0), lineB = readlane64((uint64_t)(start - sl), 32);
+    const u32x4 *la = reinterpret_cast<const u32x4 *>(lineA);
+    const u32x4 *lb = reinterpret_cast<const u32x4 *>(lineB);
+    auto chunk_at = [&](uint32_t c) -> const u32x4 * { // unconditional: past the end, the last chunk again
+        if (total == 0u)
+            return &g_zero_chunk;
+        const uint32_t cc = c < total ? c : total - 1u;
+        return cc < dA ? la + cc : lb + (cc - dA);
+    };
+
+    // fixed header of the home packet: bytes [s0, s0 + 20) of base[0..2]
+    const u32x4 *hb = big_enough ? base : &g_zero_chunk;
+    const uint32_t h1i = big_enough ? 1u : 0u;
+    auto hload = [](const u32x4 *q) { return load16<false>(q); };
+    u32x4 h0, h1, h2 = u32x4(0u), c2 = u32x4(0u), c3 = u32x4(0u);
+    if constexpr (IPM == IP_RX) {
+        h0 = hload(hb);
+        h1 = hload(hb + h1i);
+        c2 = hload(nch > 2 ? base + 2 : &g_zero_chunk);
+        c3 = hload(nch > 3 && s0 >= 12 ? base + 3 : &g_zero_chunk);
+        h2 = s0 > 12 ? c2 : u32x4(0u);
+    } else {
+        h0 = hload(hb);
+        h1 = hload(hb + h1i);
+        const u32x4 h2v = hload(hb + (big_enough ? (s0 > 12 ? 2u : 1u) : 0u));
+        h2 = s0 > 12 ? h2v : u32x4(0u);
+    }
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        v[u] = load16<true>(chunk_at((uint32_t)(u * 64) + ln));
+    issue_fence();
+
+    const Hdr5 hd = header_dwords(h0, h1, h2, s0);
+    const IpHdr ih = ip_parse<IPM>(hd, frame, big_enough, [=](uint32_t ihl4) {
+        const uint32_t o = s0 + ihl4, cw = o >> 4;
+        u32x4 wa, wb;
+        if (ihl4 == 20) {
+            wa = cw == 1 ? h1 : c2;
+            wb = cw == 1 ? c2 : c3;
+        } else {
+            wa = load16<false>(base + cw);
+            wb = load16<false>(cw + 1 < nch ? base + cw + 1 : &g_zero_chunk);
+        }
+        return header_dwords(wa, wb, u32x4(0u), o & 15u);
+    });
+    // the home packet's byte ranges from its line base, then both packets' in scalars
+    const int h_end = (int)(ih.hl < 65600u ? ih.hl : 65600u) + (int)sl;
+    const int l_end = (int)(ih.end < 65600u ? ih.end : 65600u) + (int)sl;
+    const int f0 = ih.field_on ? (int)(ih.hl + ih.fld) + (int)sl : -64;
+    const int hA = __builtin_amdgcn_readlane(h_end, 0), hB = __builtin_amdgcn_readlane(h_end, 32);
+    const int lA = __builtin_amdgcn_readlane(l_end, 0), lB = __builtin_amdgcn_readlane(l_end, 32);
+    const int fA = __builtin_amdgcn_readlane(f0, 0), fB = __builtin_amdgcn_readlane(f0, 32);
+    const int sA = __builtin_amdgcn_readlane((int)sl, 0), sB = __builtin_amdgcn_readlane((int)sl, 32);
+    const bool onA = __builtin_amdgcn_readlane((int)ih.field_on, 0) != 0;
+    const bool onB = __builtin_amdgcn_readlane((int)ih.field_on, 32) != 0;
+
+    uint32_t ahA = 0, alA = 0, afA = 0, ahB = 0, alB = 0, afB = 0;
+    auto pass = [&](const u32x4 (&vv)[U], uint32_t b0) {
+        uint32_t phA = 0, plA = 0, phB = 0, plB = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t ci = b0 + (uint32_t)(u * 64) + ln;
+            const bool valid = ci < total;
+            const bool isA = ci < dA;
+            const int c = (int)(16u * (isA ? ci : ci - dA));
+            const int hs = isA ? sA : sB, he = isA ? hA : hB, le = isA ? lA : lB, fo = isA ? fA : fB;
+            const bool on = isA ? onA : onB;
+            const bool inner = valid && c >= he && c + 16 <= le && (fo + 2 <= c || fo >= c + 16);
+            if (valid && !inner) { // header chunks, the field chunk(s), the last chunk: rare
+                uint32_t th = region_sum(vv[u], c, hs, he);
+                uint32_t tl4 = region_sum(vv[u], c, he, le);
+                if (on) {
+                    const uint32_t tf = region_sum(vv[u], c, fo, fo + 2);
+                    if (IPM == IP_TX)
+                        tl4 -= tf;
+                    else if (isA)
+                        afA += tf;
+                    else
+                        afB += tf;
+                }
+                if (IPM == IP_TX)
+                    th -= region_sum(vv[u], c, hs + 10, hs + 12);
+                phA += isA ? th : 0u;
+                plA += isA ? tl4 : 0u;
+                phB += isA ? 0u : th;
+                plB += isA ? 0u : tl4;
+            }
+            const uint32_t w = chunk_sum_w(0u, vv[u], inner ? 0x00010001u : 0u); // < 2^19
+            plA += isA ? w : 0u;
+            plB += isA ? 0u : w;
+        }
+        ahA += phA;
+        ahB += phB;
+        alA = fold_step(alA + plA);
+        alB = fold_step(alB + plB);
+    };
+    if (total)
+        pass(v, 0u);
+    for (uint32_t b0 = 64u * U; b0 < total; b0 += 64u * U) { // wave-uniform
+        u32x4 w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            w[u] = load16<true>(chunk_at(b0 + (uint32_t)(u * 64) + ln));
+        pass(w, b0);
+    }
+    ahA = group_sum<64>(ahA);
+    alA = group_sum<64>(alA);
+    ahB = group_sum<64>(ahB);
+    alB = group_sum<64>(alB);
+    if (IPM == IP_RX) {
+        afA = group_sum<64>(afA);
+        afB = group_sum<64>(afB);
+    }
+    const bool home_b = ln >= 32u;
+    if (live && (ln & 31u) == 0u)
+        ip_finish<IPM>(ih, ih.fl, big_enough, (uint32_t)(start & 1u), home_b ? ahB : ahA, home_b ? alB : alA,
+                       home_b ? afB : afA, pp, pk, out, flags_out, verdict_out, opts);
+}
+
+// ipv4_pair over the batch: 8 packets per 256-thread workgroup, as k_ipv4<32>
+template <int U, int IPM>
+__global__ __launch_bounds__(256) void k_ipv4_pair(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
+                                                   uint32_t n, uint32_t *__restrict__ out,
+                                                   uint8_t *__restrict__ flags_out, int8_t *__restrict__ verdict_out,
+                                                   uint32_t opts, uint32_t xg)
+{
+    const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, xg);
+    ipv4_pair<U, IPM>(arena, pkts, (blk * 4u + (threadIdx.x >> 6)) * 2u, n, out, flags_out, verdict_out, opts);
+}
+
 // The deferred tx stores (IP_OPT_DEFER): one lane per packet writes the values
 // k_ipv4 left in `csums` at the positions it left in `pos` (bit 16: the IPv4
 // header field; low 16 bits: the L4 field's offset, 0 for none).  All the

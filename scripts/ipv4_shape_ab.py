@@ -26,6 +26,7 @@ ROLL_ONLY = "--roll" in sys.argv  # rolling load slots: a multi-pass packet keep
 HDRX_ONLY = "--hdrx" in sys.argv  # header chunks shuffled from the first data pass instead of loaded
 SDESC_ONLY = "--sdesc" in sys.argv  # the descriptors by scalar loads
 LDS_ONLY = "--lds" in sys.argv  # later passes by LDS-DMA into a per-wave ring (PIPE 5); the 3rd header chunk as a dword
+SMALLWG_ONLY = "--smallwg" in sys.argv  # one- and two-wave workgroups
 PAIR_ONLY = "--pair" in sys.argv  # two packets a wave streamed as one run of chunks (k_ipv4_pair)
 PASS_ONLY = "--pass" in sys.argv  # 6-KiB passes: a wave per packet (64 x 6), or 32 lanes x 12 loads
 
@@ -76,7 +77,9 @@ for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mi
                 f(o, v)
         return g
 
-    if PAIR_ONLY:
+    if SMALLWG_ONLY:
+        kinds.update({"64 threads (one wave)": shape(64, 0), "128 threads": shape(128, 0)})
+    elif PAIR_ONLY:
         kinds.update({"pair stream, 64 x 6": shape(256, 1006), "pair stream, 64 x 4": shape(256, 1004)})
         if not rx:
             kinds["pair stream, 64 x 3"] = shape(256, 1003)

@@ -830,7 +830,7 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
     const uint32_t G = occ == 516 || occ == 816 ? 16u : occ == 964 ? 64u
                        : occ == 532 || occ == 832 || (occ >= 1000 && occ < 1100) ? 32u
                        : mode == IP_RX ? 16u : 32u;
-    if (wg != 256 && wg != 512 && wg != 1024)
+    if (wg != 64 && wg != 128 && wg != 256 && wg != 512 && wg != 1024)
         return hipErrorInvalidValue;
     const uint32_t dyn_m = occ > 300 && occ < 500 ? (uint32_t)((occ - 300) & 15 ? (occ - 300) & 15 : 16) : 1u; // k_ipv4_dyn's M
     const uint32_t per = (uint32_t)wg / G * dyn_m;
@@ -844,6 +844,8 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 0 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256>)) }
         if (occ == 0 && wg == 512) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 512>)) }
         if (occ == 0 && wg == 1024) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 1024>)) }
+        if (occ == 0 && wg == 64) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 64>)) }
+        if (occ == 0 && wg == 128) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 128>)) }
         if (occ == 8 && wg == 256) { TCSUM_SH((k_ipv4_occ<32, 6, IP_SUMS, 8>)) }
         if (occ == 100 + 16 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 16>)) } // data pass skewed 16 B
         if (occ == 200 && wg == 256) { TCSUM_SH((k_ipv4_db<32, 6, IP_SUMS>)) } // two passes in flight
@@ -886,6 +888,8 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 300 + 16 * 7 + 4 && wg == 256) { TCSUM_SH((k_ipv4_dyn<16, 6, IP_RX, 4, 7>)) }
         if (occ == 0 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256>)) }
         if (occ == 0 && wg == 1024) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 1024>)) }
+        if (occ == 0 && wg == 64) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 64>)) }
+        if (occ == 0 && wg == 128) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 128>)) }
         if (occ == 7 && wg == 256) { TCSUM_SH((k_ipv4_occ<16, 6, IP_RX, 7>)) }
         if (occ == 8 && wg == 256) { TCSUM_SH((k_ipv4_occ<16, 6, IP_RX, 8>)) }
         if (occ == 100 + 16 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256, 16>)) }

@@ -44,6 +44,8 @@ extern "C" {
  *                     packed-stream kernel (k_segments_pk) off / on; K > 1: on,
  *                     with K ranges per workgroup (measurement)
  *   "tx_split"        0 / 1: the tx fill's stores in the kernel / deferred
+ *   "tx_warm"         0 / 1: the deferred stores load each field's dword
+ *                     first (packets in device memory; default 1)
  *   "args_launch"     0: drop-in calls pass their descriptor in pinned memory
  *   "sync_block"      1: drop-in calls block in hipStreamSynchronize
  *   "e2e_trace"       1: tcsum_host_batch_peso prints phase times on stderr

@@ -382,6 +382,162 @@ __global__ __launch_bounds__(256) void k_floor_scatter(uint8_t *__restrict__ are
     floor_store(arena, nbytes, fpos[2ull * i + 1u], v >> 16);
 }
 
+// The deferred scatter at a store granularity GR (tx-fill write-cost study;
+// launched after the plain read, so the fields' lines are not in cache):
+// GR = 2 is k_floor_scatter's two byte stores per field; GR >= 16 writes the
+// whole GR-aligned block holding each field (once when both fields share a
+// block) as GR / 16 16-B stores of the value.  The bytes around the fields are
+// overwritten: the arena is junk afterwards.  Measurement only.
+template <int GR>
+__global__ __launch_bounds__(256) void k_floor_scatter_gr(uint8_t *__restrict__ arena, uint64_t nbytes,
+                                                          const uint64_t *__restrict__ fpos,
+                                                          const uint32_t *__restrict__ vals, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t v = vals[i];
+    const uint64_t a = fpos[2ull * i], b = fpos[2ull * i + 1u];
+    if constexpr (GR == 2) {
+        floor_store(arena, nbytes, a, v);
+        floor_store(arena, nbytes, b, v >> 16);
+    } else {
+        const u32x4 w = {v, v ^ 1u, v ^ 2u, v ^ 3u};
+        const uint64_t ba = a == kFloorNone ? kFloorNone : a & ~(uint64_t)(GR - 1);
+        const uint64_t bb = b == kFloorNone ? kFloorNone : b & ~(uint64_t)(GR - 1);
+        if (ba != kFloorNone && ba + GR <= nbytes) {
+            u32x4 *q = reinterpret_cast<u32x4 *>(arena + ba);
+#pragma unroll
+            for (int k = 0; k < GR / 16; ++k)
+                q[k] = w;
+        }
+        if (bb != kFloorNone && bb != ba && bb + GR <= nbytes) {
+            u32x4 *q = reinterpret_cast<u32x4 *>(arena + bb);
+#pragma unroll
+            for (int k = 0; k < GR / 16; ++k)
+                q[k] = w;
+        }
+    }
+}
+
+// Dword k of a 64-B line with the 2-B field at line byte o set to v (the
+// field may straddle into the next dword: each dword takes its own bytes).
+__device__ __forceinline__ uint32_t line_put16(uint32_t d, uint32_t k, uint32_t o, uint32_t v)
+{
+    const int sh = (int)o - 4 * (int)k + 1; // field start in a window that begins one byte early
+    if (sh < 0 || sh > 4)
+        return d;
+    const uint32_t mm = (uint32_t)((0xFFFFull << (8 * sh)) >> 8);
+    const uint32_t vv = (uint32_t)(((uint64_t)(v & 0xFFFFu) << (8 * sh)) >> 8);
+    return (d & ~mm) | vv;
+}
+
+// The deferred scatter as a read-modify-write of whole 64-B lines: each lane
+// loads the line(s) holding its packet's fields, sets the fields, stores the
+// whole line(s) (one line when both fields share it).  Junk values, as
+// k_floor_scatter_gr.  Measurement only.
+__global__ __launch_bounds__(256) void k_floor_scatter_rmw(uint8_t *__restrict__ arena, uint64_t nbytes,
+                                                           const uint64_t *__restrict__ fpos,
+                                                           const uint32_t *__restrict__ vals, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t v = vals[i];
+    const uint64_t a = fpos[2ull * i], b = fpos[2ull * i + 1u];
+    const bool ha = a != kFloorNone && (a | 63u) < nbytes, hb = b != kFloorNone && (b | 63u) < nbytes;
+    const uint64_t la = a & ~63ull, lb = b & ~63ull;
+    const bool shared = ha && hb && la == lb;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+        if (f == 0 ? !ha : (!hb || shared))
+            continue;
+        const uint64_t l = f == 0 ? la : lb;
+        u32x4 *q = reinterpret_cast<u32x4 *>(arena + l);
+        u32x4 c[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            c[k] = q[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t w[4] = {c[k].x, c[k].y, c[k].z, c[k].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (f == 0)
+                    w[j] = line_put16(w[j], 4 * k + j, (uint32_t)(a - l), v);
+                if (f == 1 || shared)
+                    w[j] = line_put16(w[j], 4 * k + j, (uint32_t)(b - l), v >> 16);
+            }
+            q[k] = u32x4{w[0], w[1], w[2], w[3]};
+        }
+    }
+}
+
+// Two more forms of the same scatter (measurement only): MODE 0 sets each
+// field with device-scope atomics on the dword(s) holding it (and-not, then
+// or: the other bytes untouched, no ordering assumption); MODE 1 loads the
+// field's 64-B line first (into L2) and then stores only the 2 bytes; MODE 2
+// loads only the dword at each field first.
+__device__ __forceinline__ void atomic_put16(uint8_t *arena, uint64_t a, uint32_t v)
+{
+    const uint64_t d = a & ~3ull;
+    const uint32_t sh = (uint32_t)(a & 3u) * 8u;
+    const uint64_t m = 0xFFFFull << sh, x = (uint64_t)(v & 0xFFFFu) << sh;
+    uint32_t *w = reinterpret_cast<uint32_t *>(arena + d);
+    atomicAnd(w, ~(uint32_t)m);
+    atomicOr(w, (uint32_t)x);
+    if (m >> 32) {
+        atomicAnd(w + 1, ~(uint32_t)(m >> 32));
+        atomicOr(w + 1, (uint32_t)(x >> 32));
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_floor_scatter_x(uint8_t *__restrict__ arena, uint64_t nbytes,
+                                                         const uint64_t *__restrict__ fpos,
+                                                         const uint32_t *__restrict__ vals, uint32_t n,
+                                                         uint32_t *__restrict__ sink)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t v = vals[i];
+    const uint64_t a = fpos[2ull * i], b = fpos[2ull * i + 1u];
+    const bool ha = a != kFloorNone && (a | 63u) < nbytes, hb = b != kFloorNone && (b | 63u) < nbytes;
+    if constexpr (MODE == 0) {
+        if (ha)
+            atomic_put16(arena, a, v);
+        if (hb)
+            atomic_put16(arena, b, v >> 16);
+    } else if constexpr (MODE == 2) { // one dword at each field, then the 2-B stores
+        uint32_t x = 0;
+        if (ha)
+            x ^= *reinterpret_cast<const uint32_t *>(arena + (a & ~3ull));
+        if (hb)
+            x ^= *reinterpret_cast<const uint32_t *>(arena + (b & ~3ull));
+        if (x == 0x9E3779B9u)
+            sink[0] = x;
+        floor_store(arena, nbytes, a, v);
+        floor_store(arena, nbytes, b, v >> 16);
+    } else {
+        uint32_t x = 0;
+        if (ha) {
+            const u32x4 *q = reinterpret_cast<const u32x4 *>(arena + (a & ~63ull));
+            for (int k = 0; k < 4; ++k)
+                x ^= q[k].x;
+        }
+        if (hb) {
+            const u32x4 *q = reinterpret_cast<const u32x4 *>(arena + (b & ~63ull));
+            for (int k = 0; k < 4; ++k)
+                x ^= q[k].y;
+        }
+        if (x == 0x9E3779B9u)
+            sink[0] = x;
+        floor_store(arena, nbytes, a, v);
+        floor_store(arena, nbytes, b, v >> 16);
+    }
+}
+
 static Geometry route(uint64_t mean_len);
 
 // ---------------------------------------------------------------- window read
@@ -612,7 +768,7 @@ static hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, 
 #undef TCSUM_PI
     if (mode == PM_TX && !ext_side) {
         if (e == hipSuccess) { // the product's scatter, on the probe's values and positions
-            note_launch(launch(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, const_cast<uint8_t *>(a),
+            note_launch(launch(k_tx_scatter<true>, dim3((n + 255) / 256), dim3(256), 0, stream, const_cast<uint8_t *>(a),
                                pkts, n, vals, posv));
             e = take_launch_rc();
         }
@@ -649,6 +805,44 @@ static hipError_t launch_floor(void *arena, uint64_t nbytes, const uint64_t *fpo
     if (variant == 0) {
         note_launch(launch(k_floor_stream, dim3(floor_windows(nbytes)), dim3(256), 0, stream, q, nchunks, a, nbytes,
                            fpos, ffirst, n, sink));
+        return take_launch_rc();
+    }
+    if (variant >= 2 && variant <= 7) { // the read, then the scatter at granularity 2 / 16 / 32 / 64 / 128 / 256 B
+        const hipError_t r = launch_probe_read(arena, nbytes, sink, stream);
+        if (r != hipSuccess)
+            return r;
+        const dim3 grid((n + 255u) / 256u);
+        switch (variant) {
+        case 2: note_launch(launch(k_floor_scatter_gr<2>, grid, dim3(256), 0, stream, a, nbytes, fpos, vals, n)); break;
+        case 3: note_launch(launch(k_floor_scatter_gr<16>, grid, dim3(256), 0, stream, a, nbytes, fpos, vals, n)); break;
+        case 4: note_launch(launch(k_floor_scatter_gr<32>, grid, dim3(256), 0, stream, a, nbytes, fpos, vals, n)); break;
+        case 5: note_launch(launch(k_floor_scatter_gr<64>, grid, dim3(256), 0, stream, a, nbytes, fpos, vals, n)); break;
+        case 6: note_launch(launch(k_floor_scatter_gr<128>, grid, dim3(256), 0, stream, a, nbytes, fpos, vals, n)); break;
+        default: note_launch(launch(k_floor_scatter_gr<256>, grid, dim3(256), 0, stream, a, nbytes, fpos, vals, n)); break;
+        }
+        return take_launch_rc();
+    }
+    if (variant == 8) { // the read, then the 64-B line read-modify-write scatter
+        const hipError_t r = launch_probe_read(arena, nbytes, sink, stream);
+        if (r != hipSuccess)
+            return r;
+        note_launch(launch(k_floor_scatter_rmw, dim3((n + 255u) / 256u), dim3(256), 0, stream, a, nbytes, fpos, vals,
+                           n));
+        return take_launch_rc();
+    }
+    if (variant == 9 || variant == 10 || variant == 11) { // the read, then the atomic / load-then-2-B scatter
+        const hipError_t r = launch_probe_read(arena, nbytes, sink, stream);
+        if (r != hipSuccess)
+            return r;
+        if (variant == 9)
+            note_launch(launch(k_floor_scatter_x<0>, dim3((n + 255u) / 256u), dim3(256), 0, stream, a, nbytes, fpos,
+                               vals, n, sink));
+        else if (variant == 10)
+            note_launch(launch(k_floor_scatter_x<1>, dim3((n + 255u) / 256u), dim3(256), 0, stream, a, nbytes, fpos,
+                               vals, n, sink));
+        else
+            note_launch(launch(k_floor_scatter_x<2>, dim3((n + 255u) / 256u), dim3(256), 0, stream, a, nbytes, fpos,
+                               vals, n, sink));
         return take_launch_rc();
     }
     if (variant != 1)
@@ -799,7 +993,7 @@ static hipError_t launch_ipv4_flat(int ip_mode, uint32_t xg, uint8_t *arena, con
             e = flat_u<IP_TX>(w, xg, arena, pkts, n, vals, flags, reinterpret_cast<int8_t *>(side), IP_OPT_DEFER,
                               plan, wfirst, slot, gen, stream);
             if (e == hipSuccess) {
-                e = launch(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, arena, pkts, n, vals, side);
+                e = launch(k_tx_scatter<true>, dim3((n + 255) / 256), dim3(256), 0, stream, arena, pkts, n, vals, side);
             }
             break;
         }

@@ -486,7 +486,7 @@ static const struct {
     {"hostq_dma_kb", tcsum::KNOB_HOSTQ_DMA_KB}, {"hostq_dma_keep_mb", tcsum::KNOB_HOSTQ_DMA_KEEP_MB},
     {"copy_threads", tcsum::KNOB_COPY_THREADS}, {"pf_dist", tcsum::KNOB_PF_DIST}, {"pf_range", tcsum::KNOB_PF_RANGE},
     {"pk_early", tcsum::KNOB_PK_EARLY}, {"page_stage", tcsum::KNOB_PAGE_STAGE},
-    {"seg_sdesc", tcsum::KNOB_SEG_SDESC},
+    {"seg_sdesc", tcsum::KNOB_SEG_SDESC}, {"tx_warm", tcsum::KNOB_TX_WARM},
 };
 
 static int knob_of(const char *key)

@@ -1888,9 +1888,16 @@ __global__ __launch_bounds__(256) void k_ipv4_pair(uint8_t *__restrict__ arena, 
 // packets' field writes then reach memory in one short burst instead of one at
 // a time through the read stream (u16 or nontemporal stores: no different;
 // system-scope write-through stores: slower; profiles/r02/ab_tx_split*.txt).
+// WARM (the packets in HBM): each lane first loads the dword under each of its
+// fields and only then stores the 2 bytes.  A 2-B store into a line L2 does
+// not hold cost ~140 us per 2M fields after the fill's read; into a line the
+// load brought in, ~100 us including the load (profiles/r06/ab7/).  The loads
+// stay inside the packet's own dwords; the stored bytes are the same.  Not for
+// host memory (`store` across PCIe): a read there is a round trip.
+template <bool WARM>
 __global__ __launch_bounds__(256) void k_tx_scatter(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                                     uint32_t n, const uint32_t *__restrict__ csums,
-                                                    const uint32_t *__restrict__ pos)
+                                                    uint32_t *__restrict__ pos)
 {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n)
@@ -1900,13 +1907,26 @@ __global__ __launch_bounds__(256) void k_tx_scatter(uint8_t *__restrict__ arena,
         return;
     const uint32_t v = csums[i];
     uint8_t *pp = arena + pkts[i].offset;
+    const uint32_t f = q & 0xFFFFu;
+    // WARM: the dwords holding bytes 10-11 and f..f+1 (f >= 22: both inside
+    // the packet's first bytes), loaded before the stores; folded into a
+    // store after them that practically never fires (it would clear the
+    // lane's own position word, which nothing reads after this kernel), so
+    // the loads are kept and the field stores do not wait for them
+    uint32_t w0 = 0, w1 = 0;
+    if constexpr (WARM) {
+        const uint32_t m = (uint32_t)(reinterpret_cast<uintptr_t>(pp) & 3u);
+        w0 = *reinterpret_cast<const uint32_t *>(pp + 8 - m);
+        w1 = *reinterpret_cast<const uint32_t *>(pp + (((f ? f : 8u) + m) & ~3u) - m); // no L4 field: w0's again
+    }
     pp[10] = (uint8_t)v; // ipv4.c:643,656, host order like the struct field
     pp[11] = (uint8_t)(v >> 8);
-    const uint32_t f = q & 0xFFFFu;
     if (f) { // tcp_out.c:19-20 / udp.c:320-321 / icmpv4.c:45-58
         pp[f] = (uint8_t)(v >> 16);
         pp[f + 1] = (uint8_t)(v >> 24);
     }
+    if (WARM && (w0 ^ w1) == 0x9E3779B9u && v == 0x7F4A7C15u)
+        pos[i] = 0u;
 }
 
 

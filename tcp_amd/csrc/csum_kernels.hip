@@ -549,7 +549,13 @@ static hipError_t tx_split_in(Geometry g, dim3 grid, uint32_t xg, uint8_t *arena
     hipError_t e = ipv4_u<IP_TX>(g.lanes, g.loads, grid, arena, pkts, n, vals, flags,
                                  reinterpret_cast<int8_t *>(side), IP_OPT_DEFER, xg, stream);
     if (e == hipSuccess) {
-        e = launch(k_tx_scatter, dim3((n + 255) / 256), dim3(256), 0, stream, store, pkts, n, vals, side);
+        // the warming loads only where the packets sit in device memory
+        hipPointerAttribute_t at{};
+        const bool hbm = quiet(hipPointerGetAttributes(&at, store)) == hipSuccess && at.type == hipMemoryTypeDevice;
+        if (hbm && knob(KNOB_TX_WARM) != 0)
+            e = launch(k_tx_scatter<true>, dim3((n + 255) / 256), dim3(256), 0, stream, store, pkts, n, vals, side);
+        else
+            e = launch(k_tx_scatter<false>, dim3((n + 255) / 256), dim3(256), 0, stream, store, pkts, n, vals, side);
     }
     return e;
 }

@@ -68,6 +68,7 @@ enum Knob : int {
     KNOB_PK_EARLY,     // 0 / 1: k_segments_pk's range-by-range path reads its descriptors with scalar loads (1)
     KNOB_PAGE_STAGE,   // 0 / 1: tcsum_host_batch_peso copies a pageable arena through its own pinned slots (1)
     KNOB_SEG_SDESC,    // 0 / 1: the per-range kernel (8-16 lanes per range) reads its descriptors with scalar loads (1)
+    KNOB_TX_WARM,      // 0 / 1: the deferred tx scatter loads each field's dword before storing it (1, HBM only)
     KNOB_COUNT
 };
 int64_t knob(Knob k);

@@ -442,12 +442,18 @@ def txfloor_prepare(arena, nbytes: int, pkts, n: int, total_bytes: int, stream=N
     return h
 
 
-def probe_txfloor(h: dict, deferred: bool = False, stream=None):
+def probe_txfloor(h: dict, deferred: bool = False, stream=None, variant: int | None = None):
     """tcsum_probe_txfloor: one read of the batch's bytes plus the fill's
-    field writes, in-stream (deferred=False) or as one dense scatter."""
+    field writes, in-stream (deferred=False) or as one dense scatter.
+    variant 2-7: the read, then a scatter writing each field's aligned block
+    of 2 / 16 / 32 / 64 / 128 / 256 bytes (junk around the fields); 8: the
+    read, then a read-modify-write of each field's whole 64-B line; 9: the
+    fields by device atomics; 10: each field's line loaded, then 2-B stores;
+    11: the dword at each field loaded, then 2-B stores."""
+    v = variant if variant is not None else 1 if deferred else 0
     _lib.check(_lib.bench_lib().tcsum_probe_txfloor(
         h["arena"].data_ptr(), h["nbytes"], h["fpos"].data_ptr(), h["side"].data_ptr(), h["n"],
-        h["ffirst"].data_ptr(), 1 if deferred else 0, h["sink"].data_ptr(), _stream_ptr(stream)),
+        h["ffirst"].data_ptr(), v, h["sink"].data_ptr(), _stream_ptr(stream)),
         "tcsum_probe_txfloor")
 
 

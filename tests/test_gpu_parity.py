@@ -346,13 +346,15 @@ def test_ipv4_odd_arena_base(tc, torch):
     np.testing.assert_array_equal(down(flags), cases["flags"])
 
 
-TX_FORMS = ["fused", "deferred"]
+TX_FORMS = ["fused", "deferred", "deferred_cold"]
 
 
 def set_tx_form(knobs, form):
-    """The two forms of the in-place tx fill: stores in the kernel
-    (k_ipv4<IP_TX>) or deferred to k_tx_scatter."""
-    knobs(tx_split=1 if form == "deferred" else 0)
+    """The forms of the in-place tx fill: stores in the kernel
+    (k_ipv4<IP_TX>) or deferred to k_tx_scatter, which by default first
+    loads the dword under each field (debug "tx_warm"; "deferred_cold"
+    stores without it)."""
+    knobs(tx_split=0 if form == "fused" else 1, tx_warm=0 if form == "deferred_cold" else -1)
 
 
 @pytest.mark.parametrize("form", TX_FORMS)

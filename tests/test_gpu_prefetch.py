@@ -91,9 +91,9 @@ def test_ipv4_batches_with_prefetch(tc, torch, oracle, pf):
     with tc.debug(pf_dist=pf):
         out, fl = tc.batch_ipv4(arena, d, b.n, b.total_bytes)
         v, _ = tc.batch_ipv4_rx_verify(arena, d, b.n, b.total_bytes)
-        for split in (0, 1):
+        for split, warm in ((0, None), (1, None), (1, 0)):
             a2 = arena.clone()
-            with tc.debug(tx_split=split):
+            with tc.debug(tx_split=split, tx_warm=warm):
                 tc.batch_ipv4_tx_fill(a2, d, b.n, b.total_bytes)
             np.testing.assert_array_equal(down(a2), want)
     np.testing.assert_array_equal(down(out), eo)

@@ -1,5 +1,6 @@
-"""The tx fill's design-independent floor probe (libtcsum_bench.so,
-tcsum_probe_txfloor): it must write exactly the bytes the fill writes --
+"""The tx fill's floor probe (libtcsum_bench.so, tcsum_probe_txfloor; in
+stream, deferred, and deferred after loading each field's dword): it must
+write exactly the bytes the fill writes --
 each packet's IPv4 header checksum field (ipv4.c:643,656) and its TCP / UDP /
 ICMP field (tcp_out.c:19-20, udp.c:320-321, icmpv4.c:45-58) -- and nothing
 else, or the floor it prices is not the fill's.  The field addresses come
@@ -59,7 +60,7 @@ def test_txfloor_writes_the_fills_fields(tc, torch, seed):
     host, pk = _batch(tc, seed)
     expect = _written(tc, torch, host, pk)
     assert expect, "the batch has fields to fill"
-    for deferred in (False, True):
+    for variant in (0, 1, 11):
         arena = torch.zeros(host.size + 256, dtype=torch.uint8, device="cuda")
         arena[: host.size] = up(torch.from_numpy(host))
         d = tc.descs_to_device(pk)
@@ -75,7 +76,7 @@ def test_txfloor_writes_the_fills_fields(tc, torch, seed):
         for k in range(ff.size - 1):
             assert ff[k] == np.searchsorted(w, k, side="left")
         for _ in range(3):  # any number of launches touches only the fields
-            tc.probe_txfloor(h, deferred=deferred)
+            tc.probe_txfloor(h, variant=variant)
         torch.cuda.synchronize()
         after = down(arena)
         changed = set(np.nonzero(after[: host.size] != host)[0].tolist())

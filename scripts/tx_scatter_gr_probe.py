@@ -46,8 +46,8 @@ def run(legs):
     return {k: sorted(v)[len(v) // 2] for k, v in ts.items()}
 
 
-def fill_split(v):
-    with tc.debug(tx_split=v):
+def fill_split(v, warm=None):
+    with tc.debug(tx_split=v, tx_warm=warm):
         tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
 
 

@@ -1897,7 +1897,7 @@ __global__ __launch_bounds__(256) void k_ipv4_pair(uint8_t *__restrict__ arena, 
 template <bool WARM>
 __global__ __launch_bounds__(256) void k_tx_scatter(uint8_t *__restrict__ arena, const tcsum_pkt_t *__restrict__ pkts,
                                                     uint32_t n, const uint32_t *__restrict__ csums,
-                                                    uint32_t *__restrict__ pos)
+                                                    const uint32_t *__restrict__ pos)
 {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n)
@@ -1909,10 +1909,9 @@ __global__ __launch_bounds__(256) void k_tx_scatter(uint8_t *__restrict__ arena,
     uint8_t *pp = arena + pkts[i].offset;
     const uint32_t f = q & 0xFFFFu;
     // WARM: the dwords holding bytes 10-11 and f..f+1 (f >= 22: both inside
-    // the packet's first bytes), loaded before the stores; folded into a
-    // store after them that practically never fires (it would clear the
-    // lane's own position word, which nothing reads after this kernel), so
-    // the loads are kept and the field stores do not wait for them
+    // the packet's first bytes), loaded before the stores; an empty asm after
+    // the stores takes their value, so the loads are kept and the stores do
+    // not wait for them (no side effect of the loaded bytes)
     uint32_t w0 = 0, w1 = 0;
     if constexpr (WARM) {
         const uint32_t m = (uint32_t)(reinterpret_cast<uintptr_t>(pp) & 3u);
@@ -1925,8 +1924,8 @@ __global__ __launch_bounds__(256) void k_tx_scatter(uint8_t *__restrict__ arena,
         pp[f] = (uint8_t)(v >> 16);
         pp[f + 1] = (uint8_t)(v >> 24);
     }
-    if (WARM && (w0 ^ w1) == 0x9E3779B9u && v == 0x7F4A7C15u)
-        pos[i] = 0u;
+    if constexpr (WARM)
+        asm volatile("" ::"v"(w0), "v"(w1));
 }
 
 

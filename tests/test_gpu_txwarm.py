@@ -6,8 +6,9 @@ leave the packet's own dwords: fuzzed packets of 0..9000 B (many of them
 every arena phase, the last frame ending at the end of its allocation,
 warm and cold, against the oracle's tx fill (net/src/ipv4.c:643,656,
 tcp_out.c:19-20, udp.c:320-321, icmpv4.c:45-58).  The same fill on a
-pinned host arena (the kernel reads and writes host memory in place) takes
-the cold stores and gives the same bytes."""
+pinned host arena (the kernel reads and writes host memory in place; the
+library picks the plain stores there, as hipPointerGetAttributes calls it
+host memory) gives the same bytes."""
 from devcopy import down
 import numpy as np
 import pytest
@@ -74,7 +75,7 @@ def test_warm_scatter_matches_oracle(tc, torch, oracle, seed, phase):
         np.testing.assert_array_equal(down(arena), want)
 
 
-def test_pinned_host_arena_takes_the_cold_stores(tc, torch, oracle):
+def test_pinned_host_arena_same_bytes(tc, torch, oracle):
     host, pk = _batch(tc, 7, 3)
     want = host.copy()
     oracle.batch_ipv4_tx_fill(want, pk, nthreads=8)

@@ -39,7 +39,7 @@ for cfg in configs:
     arena, descs = workload.materialize(b)
     peso = b.kind == "peso"
     outs = [torch.empty(b.n, dtype=torch.uint16 if peso else torch.uint32, device="cuda") for _ in libs]
-    verdict = torch.empty(b.n, dtype=torch.int8, device="cuda")
+    verdicts = [torch.zeros(b.n, dtype=torch.int8, device="cuda") for _ in libs]
     if cfg == "mixed_tx":  # fill once: every timed launch rewrites the same values
         tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, want_flags=False)
 
@@ -50,7 +50,7 @@ for cfg in configs:
         elif cfg == "mixed_tx":
             tc.batch_ipv4_tx_fill(arena, descs, b.n, b.total_bytes, out=outs[i], want_flags=False)
         elif cfg == "mixed_rx":
-            tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes, verdict=verdict, out=outs[i],
+            tc.batch_ipv4_rx_verify(arena, descs, b.n, b.total_bytes, verdict=verdicts[i], out=outs[i],
                                     want_flags=False)
         else:
             tc.batch_ipv4(arena, descs, b.n, b.total_bytes, out=outs[i], want_flags=False)
@@ -67,7 +67,7 @@ for cfg in configs:
             e1.record()
             torch.cuda.synchronize()
             times[i].append(e0.elapsed_time(e1) / reps)
-    same = all(torch.equal(outs[0], o) for o in outs[1:])
+    same = all(torch.equal(outs[0], o) for o in outs[1:]) and all(torch.equal(verdicts[0], v) for v in verdicts[1:])
     print(f"== {cfg} n={b.n} bytes={b.total_bytes} identical={same}", flush=True)
     for i, p in enumerate(paths):
         med = float(np.median(times[i]))

@@ -64,6 +64,7 @@ res = run({
     "tx fill, cold scatter (tx_warm 0)": lambda: fill_warm(0),
     "read only": lambda: tc.probe_read(arena, nbytes),
     "floor: read + 2-B scatter": lambda: tc.probe_txfloor(fh, deferred=True),
+    "floor: in-stream 2-B stores": lambda: tc.probe_txfloor(fh, deferred=False),
 })
 # phase 2 (junks the arena): the read, then the scatter by block size
 legs = {f"read + {gr}-B block scatter": (lambda v=v: tc.probe_txfloor(fh, variant=v))
@@ -72,6 +73,8 @@ legs["read + 64-B line RMW scatter"] = lambda: tc.probe_txfloor(fh, variant=8)
 legs["read + atomic and/or scatter"] = lambda: tc.probe_txfloor(fh, variant=9)
 legs["read + line load, then 2-B stores"] = lambda: tc.probe_txfloor(fh, variant=10)
 legs["read + field dword load, then 2-B"] = lambda: tc.probe_txfloor(fh, variant=11)
+legs["in-stream 64-B line writes"] = lambda: tc.probe_txfloor(fh, variant=12)
+legs["in-stream, dword loaded, then 2-B"] = lambda: tc.probe_txfloor(fh, variant=13)
 res.update(run(legs))
 torch.cuda.synchronize()
 pos = fh["fpos"].view(-1, 2)

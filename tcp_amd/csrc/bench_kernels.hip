@@ -336,6 +336,10 @@ __device__ __forceinline__ void floor_store(uint8_t *arena, uint64_t nbytes, uin
 // (i) in-stream: workgroup w reads window w as k_probe_read<4> does, then its
 // threads write the fields of the packets that start in it, with values from
 // their own loads (the stores wait for the window, as a fill's would).
+// ST (tx-fill write-cost study): 0 the two byte stores per field; 64 the
+// whole 64-B line holding each field written (junk around the fields, once
+// when both fields share it); 1 the dword under each field loaded first.
+template <int ST = 0>
 __global__ __launch_bounds__(256) void k_floor_stream(const u32x4 *__restrict__ p, uint64_t nchunks,
                                                       uint8_t *__restrict__ arena, uint64_t nbytes,
                                                       const uint64_t *__restrict__ fpos,
@@ -363,8 +367,35 @@ __global__ __launch_bounds__(256) void k_floor_stream(const u32x4 *__restrict__ 
         sink[0] = acc;
     const uint32_t hi = f1 < n ? f1 : n;
     for (uint32_t i = f0 + threadIdx.x; i < hi; i += 256u) {
-        floor_store(arena, nbytes, fpos[2ull * i], acc);
-        floor_store(arena, nbytes, fpos[2ull * i + 1u], acc >> 16);
+        const uint64_t a = fpos[2ull * i], b = fpos[2ull * i + 1u];
+        if constexpr (ST == 64) {
+            const u32x4 wv = {acc, acc ^ 1u, acc ^ 2u, acc ^ 3u};
+            const uint64_t la = a == kFloorNone ? kFloorNone : a & ~63ull;
+            const uint64_t lb = b == kFloorNone ? kFloorNone : b & ~63ull;
+            if (la != kFloorNone && la + 64u <= nbytes) {
+                u32x4 *q = reinterpret_cast<u32x4 *>(arena + la);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    q[k] = wv;
+            }
+            if (lb != kFloorNone && lb != la && lb + 64u <= nbytes) {
+                u32x4 *q = reinterpret_cast<u32x4 *>(arena + lb);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    q[k] = wv;
+            }
+        } else {
+            uint32_t x0 = 0, x1 = 0;
+            if constexpr (ST == 1) {
+                if (a != kFloorNone && (a | 3u) < nbytes)
+                    x0 = *reinterpret_cast<const uint32_t *>(arena + (a & ~3ull));
+                if (b != kFloorNone && (b | 3u) < nbytes)
+                    x1 = *reinterpret_cast<const uint32_t *>(arena + (b & ~3ull));
+            }
+            floor_store(arena, nbytes, a, acc);
+            floor_store(arena, nbytes, b, acc >> 16);
+            asm volatile("" ::"v"(x0), "v"(x1));
+        }
     }
 }
 
@@ -803,7 +834,7 @@ static hipError_t launch_floor(void *arena, uint64_t nbytes, const uint64_t *fpo
     uint8_t *a = static_cast<uint8_t *>(arena);
     const u32x4 *q = static_cast<const u32x4 *>(arena);
     if (variant == 0) {
-        note_launch(launch(k_floor_stream, dim3(floor_windows(nbytes)), dim3(256), 0, stream, q, nchunks, a, nbytes,
+        note_launch(launch(k_floor_stream<0>, dim3(floor_windows(nbytes)), dim3(256), 0, stream, q, nchunks, a, nbytes,
                            fpos, ffirst, n, sink));
         return take_launch_rc();
     }
@@ -828,6 +859,15 @@ static hipError_t launch_floor(void *arena, uint64_t nbytes, const uint64_t *fpo
             return r;
         note_launch(launch(k_floor_scatter_rmw, dim3((n + 255u) / 256u), dim3(256), 0, stream, a, nbytes, fpos, vals,
                            n));
+        return take_launch_rc();
+    }
+    if (variant == 12 || variant == 13) { // in-stream: whole 64-B lines (junk) / the dword loaded first
+        if (variant == 12)
+            note_launch(launch(k_floor_stream<64>, dim3(floor_windows(nbytes)), dim3(256), 0, stream, q, nchunks, a,
+                               nbytes, fpos, ffirst, n, sink));
+        else
+            note_launch(launch(k_floor_stream<1>, dim3(floor_windows(nbytes)), dim3(256), 0, stream, q, nchunks, a,
+                               nbytes, fpos, ffirst, n, sink));
         return take_launch_rc();
     }
     if (variant == 9 || variant == 10 || variant == 11) { // the read, then the atomic / load-then-2-B scatter

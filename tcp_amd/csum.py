@@ -449,7 +449,8 @@ def probe_txfloor(h: dict, deferred: bool = False, stream=None, variant: int | N
     of 2 / 16 / 32 / 64 / 128 / 256 bytes (junk around the fields); 8: the
     read, then a read-modify-write of each field's whole 64-B line; 9: the
     fields by device atomics; 10: each field's line loaded, then 2-B stores;
-    11: the dword at each field loaded, then 2-B stores."""
+    11: the dword at each field loaded, then 2-B stores; 12 / 13: in-stream,
+    each field's 64-B line written whole (junk) / its dword loaded first."""
     v = variant if variant is not None else 1 if deferred else 0
     _lib.check(_lib.bench_lib().tcsum_probe_txfloor(
         h["arena"].data_ptr(), h["nbytes"], h["fpos"].data_ptr(), h["side"].data_ptr(), h["n"],

@@ -361,11 +361,18 @@ Geometry pick_geometry(uint64_t mean_len)
 // Descriptor prefetch distance of k_segments_pk's range-by-range path, in
 // workgroups (in aux >> 8): 2048 -- 1024 / 2048 / 4096 measured alike on a
 // shuffled configs[1] batch (profiles/r05/pk_layouts_pf.txt); debug knob
-// "pf_dist" overrides, 0 = off.
-static uint32_t pf_dist()
+// "pf_dist" overrides, 0 = off.  Off by default above K = 32 ranges per
+// workgroup: there the descriptors
+// are a large share of the bytes (24 of every 88 for 64-B ranges), and the
+// prefetch's own touches cost more than they save (shuffled 64-B ranges
+// 909 -> 888 us, 200-B 635 -> 628 us without it; 576-B, K = 21, 325 -> 349
+// us: profiles/r06/ab15/pk_pf_ab.txt).
+static uint32_t pf_dist(uint32_t K)
 {
     const int64_t v = knob(KNOB_PF_DIST);
-    return v < 0 ? 2048u : (uint32_t)(v < (1 << 23) ? v : (1 << 23) - 1);
+    if (v < 0)
+        return K <= 32u ? 2048u : 0u;
+    return (uint32_t)(v < (1 << 23) ? v : (1 << 23) - 1);
 }
 
 // k_segments_pk's range-by-range path reads its descriptors with scalar
@@ -446,7 +453,7 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
                                                                           : kPkMaxRanges * kPkWaves;
         const uint8_t *a = static_cast<const uint8_t *>(arena);
         const dim3 gr((n + K - 1) / K), bl(kPkWaves * 64);
-        const uint32_t ax = aux | (pf_dist() << 8) | (pk_early() ? kPkEarly : 0u);
+        const uint32_t ax = aux | (pf_dist(K) << 8) | (pk_early() ? kPkEarly : 0u);
         if (mode == MODE_SEG)
             return launch(k_segments_pk<MODE_SEG>, gr, bl, 0, stream, a, descs, n, out, ax, (uint32_t)g.xcd, K);
         return launch(k_segments_pk<MODE_PESO>, gr, bl, 0, stream, a, descs, n, out, ax, (uint32_t)g.xcd, K);

@@ -846,7 +846,8 @@ __device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, c
     // per-range kernel would size it (32 x 3 = 1.5 KiB at K = 8; 16 x 6 for
     // K = 9..11, 16 x 4 = 1 KiB for 12..16, 16 x 3 = 768 B for 17..22 -- a
     // second round for the ranges past 16 -- and 8 x 4 = 512 B for 23..64,
-    // 4 x 2 = 128 B for more; profiles/r05/pk_early/pk_mid*.txt, pk_tiny*.txt)
+    // 4 x 2 = 128 B for 65..127, 4 x 1 for more; profiles/r05/pk_early/pk_mid*.txt,
+    // pk_tiny*.txt, profiles/r06/ab16/)
     // (One round of narrower groups instead -- 8 x 6 for 17..32 ranges, 4 x 6
     // for 33..64 -- measured 1.08-1.15x slower on shuffled 200-576-B ranges,
     // profiles/r06/ab2/pk_one_round_ab.txt.)
@@ -867,8 +868,12 @@ __device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, c
         pk_ranges<MODE, 8, 6, true>(arena, descs, out, aux, first, kw, T, e0, have0);
     else if (kw <= 64u) // ~190..370 B: 8 lanes x 4 loads, two rounds
         pk_ranges<MODE, 8>(arena, descs, out, aux, first, kw, T, e0, have0);
-    else // shorter: 4 lanes x 2 loads (128 B), 64 ranges a round
+    else if (kw < 128u) // ~96..190 B: 4 lanes x 2 loads (128 B), 64 ranges a round
         pk_ranges<MODE, 4, 2>(arena, descs, out, aux, first, kw, T, e0, have0);
+    else // shorter: 4 lanes x 1 load, as the per-range kernel takes them (pick_geometry:
+         // at most 4 interior chunks); the spare second load slot was the gap to it
+         // (shuffled 64-B ranges 887 -> 769 us, 40-B 1,536 -> 1,325: profiles/r06/ab16/)
+        pk_ranges<MODE, 4, 1>(arena, descs, out, aux, first, kw, T, e0, have0);
 }
 
 

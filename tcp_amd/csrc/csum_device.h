@@ -845,10 +845,10 @@ __device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, c
     // about 12 KiB / K, and each group's pass is sized to hold one, as the
     // per-range kernel would size it (32 x 3 = 1.5 KiB at K = 8; 16 x 6 for
     // K = 9..11, 16 x 4 = 1 KiB for 12..16, 16 x 3 = 768 B for 17..22 -- a
-    // second round for the ranges past 16 -- 8 x 4 = 512 B for 23..42, 4 x 4
-    // / 4 x 3 in one round for 43..64, 4 x 2 = 128 B for 65..127, 4 x 1 for
-    // more; profiles/r05/pk_early/pk_mid*.txt, pk_tiny*.txt,
-    // profiles/r06/ab16/, ab17/)
+    // second round for the ranges past 16 -- 8 x 4 = 512 B for 23..29, 8 x 3
+    // for 30..54, 4 x 3 in one round for 55..64, 4 x 2 = 128 B for 65..127,
+    // 4 x 1 for more; profiles/r05/pk_early/pk_mid*.txt, pk_tiny*.txt,
+    // profiles/r06/ab16/, ab17/, ab19/)
     // (One round of narrower groups instead -- 8 x 6 for 17..32 ranges, 4 x 6
     // for 33..64 -- measured 1.08-1.15x slower on shuffled 200-576-B ranges,
     // profiles/r06/ab2/pk_one_round_ab.txt.)
@@ -863,21 +863,19 @@ __device__ __forceinline__ void pk_fallback(const uint8_t *__restrict__ arena, c
         pk_ranges<MODE, 16, 6, true>(arena, descs, out, aux, first, kw, T, e0, have0);
     else if (kw <= 22u) // 17..22 ranges of ~560..720 B: 16 lanes x 3 loads, a second round for the last few
         pk_ranges<MODE, 16, 3, true>(arena, descs, out, aux, first, kw, T, e0, have0);
-    // ~190..287 B: one round of 4-lane groups with just enough loads for the
-    // range's interior chunks (3 up to ~223 B, 4 up to ~287 B) -- shuffled
-    // 200-B ranges 628 -> 544 us, 250-B 547 -> 517, below the per-range
-    // kernel's 605 / 518; with 5 or 6 loads (~290..415 B) or 8-lane groups
-    // for 17..22 ranges one round lost 2-8 % (profiles/r06/ab17/)
+    // ~190..223 B: one round of 4-lane groups, 3 loads each -- just enough
+    // for the interior chunks (shuffled 200-B ranges 628 -> 544 us,
+    // profiles/r06/ab17/); ~224..415 B: 8 x 3, one or two rounds (250-B
+    // 547 -> 504 us, 320-B 451 -> 424, 400-B 386 -> 371, profiles/r06/ab19/;
+    // past ~415 B 3 loads leave a second pass: 480-B ranges lost 20 %).
+    // With 5 or 6 loads, or 8-lane groups for 17..22 ranges, one round lost
+    // 2-8 % (ab17/).
     else if (kw >= 55u && kw <= 64u)
         pk_ranges<MODE, 4, 3>(arena, descs, out, aux, first, kw, T, e0, false);
-    else if (kw >= 43u && kw <= 64u)
-        pk_ranges<MODE, 4, 4>(arena, descs, out, aux, first, kw, T, e0, false);
-    else if (kw >= 23u && kw <= 32u) // ~530 B and less: 512-B passes
+    else if (kw >= 30u && kw <= 64u) // (8-lane groups: the early descriptors' layout for 30..32)
+        pk_ranges<MODE, 8, 3, true>(arena, descs, out, aux, first, kw, T, e0, have0);
+    else if (kw <= 32u) // 23..29 ranges, ~420..530 B: 512-B passes
         pk_ranges<MODE, 8, 4, true>(arena, descs, out, aux, first, kw, T, e0, have0);
-    else if (kw <= 32u)
-        pk_ranges<MODE, 8, 6, true>(arena, descs, out, aux, first, kw, T, e0, have0);
-    else if (kw <= 64u) // ~290..370 B: 8 lanes x 4 loads, two rounds
-        pk_ranges<MODE, 8>(arena, descs, out, aux, first, kw, T, e0, have0);
     else if (kw < 128u) // ~96..190 B: 4 lanes x 2 loads (128 B), 64 ranges a round
         pk_ranges<MODE, 4, 2>(arena, descs, out, aux, first, kw, T, e0, have0);
     else // shorter: 4 lanes x 1 load, as the per-range kernel takes them (pick_geometry:

@@ -302,9 +302,10 @@ Geometry pick_geometry(uint64_t mean_len)
 {
     // xcd: 64 workgroups per XCD run (scripts/xcd_tune.py, profiles/r01/xcd_tune.txt:
     // 2-4 % on every config, flat from 32 to 512)
-    Geometry g{32, 4, 64, 0};
+    Geometry g{32, 4, 64, 0, 0};
     const uint64_t chunks = mean_len / 16 + 1;
     const uint64_t interior = chunks > 2 ? chunks - 2 : 0;
+    g.interior = (int)(interior < 65536 ? interior : 65536);
     if (chunks >= 3072) {
         // >= 48 KiB (TSO): one range per 16-wave workgroup, 32-lane groups on
         // 2-KiB sub-ranges, 4 loads per lane: a 64-KiB range is one pass of
@@ -406,8 +407,8 @@ static hipError_t seg_u(int G, int U, uint32_t xg, uint32_t n, const void *arena
                       descs, n, out, aux | (pf_range() << 8) | (knob(KNOB_SEG_SDESC) != 0 ? kSegScalarDesc : 0u), \
                       xg);                                                                                    \
     }
-    TCSUM_SEG(4, 1) TCSUM_SEG(4, 2) TCSUM_SEG(8, 4) TCSUM_SEG(16, 3) TCSUM_SEG(16, 4) TCSUM_SEG(16, 6)
-    TCSUM_SEG(16, 8) TCSUM_SEG(32, 6)
+    TCSUM_SEG(4, 1) TCSUM_SEG(4, 2) TCSUM_SEG(4, 3) TCSUM_SEG(8, 3) TCSUM_SEG(8, 4) TCSUM_SEG(16, 3) TCSUM_SEG(16, 4)
+    TCSUM_SEG(16, 6) TCSUM_SEG(16, 8) TCSUM_SEG(32, 6)
 #undef TCSUM_SEG
     if (G == 1024 && U == 4) { // one range per 16-wave workgroup, 2 KiB sub-ranges (TSO)
         return launch(k_segments_wgx<16, 32, 4, MODE>, dim3(n), dim3(1024), 0, s, a, descs, n, out, aux, xg);
@@ -457,6 +458,23 @@ hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void 
         if (mode == MODE_SEG)
             return launch(k_segments_pk<MODE_SEG>, gr, bl, 0, stream, a, descs, n, out, ax, (uint32_t)g.xcd, K);
         return launch(k_segments_pk<MODE_PESO>, gr, bl, 0, stream, a, descs, n, out, ax, (uint32_t)g.xcd, K);
+    }
+    if (mode != MODE_EXACT && g.lanes == 8 && g.loads == 4 && g.interior >= 9 && g.interior <= 24 &&
+        knob(KNOB_LANES) < 0 && knob(KNOB_LOADS) < 0) {
+        // the per-range kernel for ranges of ~144-415 B (SHUFFLED hint, or a
+        // packed batch's K < 3: never at these lengths): fewer load slots than
+        // the 8 x 4 the IPv4 kernels keep from pick_geometry -- shuffled 160-B
+        // ranges 702 -> 559 us at 4 x 2, 200-B 607 -> 533 at 4 x 3, 250-400-B
+        // 7-8 % faster at 8 x 3 (profiles/r06/ab18/seg_shapes.txt)
+        if (g.interior <= 10) {
+            g.lanes = 4;
+            g.loads = 2;
+        } else if (g.interior <= 12) {
+            g.lanes = 4;
+            g.loads = 3;
+        } else {
+            g.loads = 3;
+        }
     }
     if (mode == MODE_EXACT) {
         return launch(k_segments<64, 8, MODE_EXACT>, dim3((n + 3) / 4), dim3(256), 0, stream,

@@ -42,6 +42,7 @@ struct Geometry {
     int xcd;    // consecutive workgroups kept on one XCD (1: dispatch order)
     int packed; // K > 0: checksum_peso / pktbuf_checksum16 batches as a packed
                 // stream, K consecutive ranges per 4-wave workgroup (k_segments_pk)
+    int interior; // a mean-length range's interior 16-B chunks (0: unknown), for the per-range shape
 };
 
 // Test and measurement overrides (include/tcsum_debug.h): -1 = the router's

@@ -280,7 +280,8 @@ def test_layout_hints_give_the_same_results(tc, torch, oracle, layout):
 
 
 SMALL_CASES = [(64, "shuffled"), (200, "shuffled"), (576, "shuffled"), (700, "shuffled"), (400, "shuffled"),
-               (200, "half"), (576, "half"), (64, "packed"), (576, "packed"), (300, "zeros")]
+               (200, "half"), (576, "half"), (64, "packed"), (576, "packed"), (300, "zeros"), (160, "shuffled"),
+               (250, "half"), (80, "shuffled")]
 
 
 @pytest.mark.parametrize("mean,layout", SMALL_CASES)
@@ -291,7 +292,7 @@ def test_small_ranges_unknown_layout(tc, torch, oracle, mean, layout, mode):
     range by range), half the workgroups shuffled (both paths in one launch),
     fully packed, and ranges of length 0; n never a multiple of K.  Every
     path equals the oracle; so does the per-range kernel the SHUFFLED hint
-    takes for these lengths."""
+    takes for these lengths (4 x 1 .. 8 x 3 by the mean, launch_segments)."""
     r = tc.route(mean)
     assert r["packed"] > 16, r
     K = r["packed"]

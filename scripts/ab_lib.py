@@ -5,7 +5,8 @@ whichever it was), median ms per launch, and the outputs of every build must
 be identical (AB_ALLOW_DIFF=1 for measurement builds that store nothing).
 
   python scripts/ab_lib.py LIB_A LIB_B [LIB_C ...] [configs]
-  (configs: mtu,tso,mixed,mixed_tx,mixed_rx)
+  (configs: mtu,tso,mixed,mixed_tx,mixed_rx; uNNNN / uNNNN_rx / uNNNN_tx:
+  IPv4 packets of NNNN bytes each, as many as configs[3]'s bytes hold)
 """
 import ctypes
 import os
@@ -33,9 +34,24 @@ rest = [a for a in sys.argv[1:] if not a.endswith(".so")]
 libs = [load(p) for p in paths]
 configs = rest[0].split(",") if rest else ["mtu", "tso", "mixed", "mixed_tx", "mixed_rx"]
 rounds, reps = 8, 10
+def equal_length(L):
+    from tcp_amd.csum import PKT_DTYPE
+    total = workload.make_batch("mixed").total_bytes
+    n = total // L
+    d = np.zeros(n, PKT_DTYPE)
+    d["offset"] = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    d["len"] = L
+    return workload.Batch("mixed", "ipv4", n, d, n * L, n * L, 0, op="sums")
+
+
 for cfg in configs:
-    base = cfg.split("_")[0] if cfg in ("mixed_tx", "mixed_rx") else cfg
-    b = workload.make_batch(base)
+    label = cfg
+    if cfg.startswith("u"):
+        b = equal_length(int(cfg[1:].split("_")[0]))
+        cfg = "mixed" + cfg[len(cfg.split("_")[0]):]
+    else:
+        base = cfg.split("_")[0] if cfg in ("mixed_tx", "mixed_rx") else cfg
+        b = workload.make_batch(base)
     arena, descs = workload.materialize(b)
     peso = b.kind == "peso"
     outs = [torch.empty(b.n, dtype=torch.uint16 if peso else torch.uint32, device="cuda") for _ in libs]
@@ -68,7 +84,7 @@ for cfg in configs:
             torch.cuda.synchronize()
             times[i].append(e0.elapsed_time(e1) / reps)
     same = all(torch.equal(outs[0], o) for o in outs[1:]) and all(torch.equal(verdicts[0], v) for v in verdicts[1:])
-    print(f"== {cfg} n={b.n} bytes={b.total_bytes} identical={same}", flush=True)
+    print(f"== {label} n={b.n} bytes={b.total_bytes} identical={same}", flush=True)
     for i, p in enumerate(paths):
         med = float(np.median(times[i]))
         print(f"  {os.path.basename(p):24s} {med * 1e3:8.1f} us  {b.total_bytes / med / 1e6:8.1f} GB/s payload"

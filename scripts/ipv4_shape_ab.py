@@ -27,6 +27,7 @@ HDRX_ONLY = "--hdrx" in sys.argv  # header chunks shuffled from the first data p
 SDESC_ONLY = "--sdesc" in sys.argv  # the descriptors by scalar loads
 LDS_ONLY = "--lds" in sys.argv  # later passes by LDS-DMA into a per-wave ring (PIPE 5); the 3rd header chunk as a dword
 SMALLWG_ONLY = "--smallwg" in sys.argv  # one- and two-wave workgroups
+NARROW_ONLY = "--narrow" in sys.argv  # 4- / 8- / 16-lane groups for short packets
 PAIR_ONLY = "--pair" in sys.argv  # two packets a wave streamed as one run of chunks (k_ipv4_pair)
 PASS_ONLY = "--pass" in sys.argv  # 6-KiB passes: a wave per packet (64 x 6), or 32 lanes x 12 loads
 
@@ -77,7 +78,15 @@ for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mi
                 f(o, v)
         return g
 
-    if SMALLWG_ONLY:
+    if NARROW_ONLY:
+        kinds = {"product (256 threads)": product}
+        shapes = ((4, 3), (4, 4), (8, 3), (8, 4), (8, 6), (16, 4)) if rx else \
+            ((4, 3), (4, 4), (4, 6), (8, 2), (8, 3), (8, 4), (8, 6), (8, 8), (16, 2), (16, 3), (16, 4), (16, 6))
+        kinds.update({f"{g} lanes x {u}": shape(256, 1200 + 10 * g + u) if g < 16 else shape(256, 1360 + u)
+                      for g, u in shapes})
+        if not rx:
+            kinds["32 lanes x 6"] = shape(256, 0)
+    elif SMALLWG_ONLY:
         kinds.update({"64 threads (one wave)": shape(64, 0), "128 threads": shape(128, 0)})
     elif PAIR_ONLY:
         kinds.update({"pair stream, 64 x 6": shape(256, 1006), "pair stream, 64 x 4": shape(256, 1004)})

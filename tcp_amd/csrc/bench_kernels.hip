@@ -39,7 +39,9 @@ static hipError_t take_launch_rc()
 // field positions k_ipv4<IP_TX> derives from the header (same rules) -- and
 // then k_tx_scatter, the product's own scatter, writing the fields.  The
 // values are the XOR fold, so the packets' checksum fields end up junk.
-enum ProbeMode : int { PM_SUMS = 0, PM_RX = 1, PM_TX = 2 };
+enum ProbeMode : int { PM_SUMS = 0, PM_RX = 1, PM_TX = 2, PM_MASKED = 3 };
+// PM_MASKED: PM_SUMS with the data pass's loads past the packet's last chunk
+// masked off instead of clamped to it (the cost of the spare load slots).
 template <int G, int U, int PM>
 __global__ __launch_bounds__(256) void k_probe_ipv4(const uint8_t *__restrict__ arena,
                                                     const tcsum_pkt_t *__restrict__ pkts, uint32_t n,
@@ -80,7 +82,12 @@ __global__ __launch_bounds__(256) void k_probe_ipv4(const uint8_t *__restrict__ 
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t idx = b0 + u * G + gl;
-            x ^= load16<true>(dbase + (idx < dch ? idx : dlast));
+            if constexpr (PM == PM_MASKED) {
+                if (idx < dch)
+                    x ^= load16<true>(dbase + idx);
+            } else {
+                x ^= load16<true>(dbase + (idx < dch ? idx : dlast));
+            }
         }
     }
     const uint32_t acc = x.x ^ x.y ^ x.z ^ x.w;
@@ -757,15 +764,19 @@ static hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, 
 {
     if (n == 0)
         return hipSuccess;
-    if (mode < PM_SUMS || mode > PM_TX)
+    if (mode < PM_SUMS || mode > PM_MASKED)
         return hipErrorInvalidValue;
     Geometry g = route(mean_len); // launch_ipv4's geometry rules
-    if (g.lanes < 16)
-        g.lanes = 16;
-    if (g.lanes > 64)
-        g.lanes = 64;
-    if (mode == PM_RX && g.lanes == 32 && tcsum_debug_get("lanes") < 0)
-        g.lanes = 16;
+    const uint64_t chunks = mean_len / 16 + 1;
+    const bool forced = tcsum_debug_get("lanes") >= 0 || tcsum_debug_get("loads") >= 0;
+    if (forced || !ipv4_short_shape(g, mode == PM_RX ? 2 : 0, chunks > 2 ? chunks - 2 : 0)) {
+        if (g.lanes < (forced ? 4 : 16))
+            g.lanes = forced ? 4 : 16;
+        if (g.lanes > 64)
+            g.lanes = 64;
+        if (mode == PM_RX && g.lanes == 32 && tcsum_debug_get("lanes") < 0)
+            g.lanes = 16;
+    }
     const uint32_t per_block = 256u / (uint32_t)g.lanes;
     const uint64_t blocks = ((uint64_t)n + per_block - 1) / per_block;
     if (blocks >= (1u << 24))
@@ -789,11 +800,15 @@ static hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, 
         else if (mode == PM_TX)                                                                              \
             note_launch(launch(k_probe_ipv4<GG, UU, PM_TX>, dim3((uint32_t)blocks), dim3(256), 0, stream, a,   \
                                pkts, n, sink, xg, vals, posv));                                              \
+        else if (mode == PM_MASKED)                                                                          \
+            note_launch(launch(k_probe_ipv4<GG, UU, PM_MASKED>, dim3((uint32_t)blocks), dim3(256), 0, stream,  \
+                               a, pkts, n, sink, xg, vals, posv));                                           \
         else                                                                                                 \
             note_launch(launch(k_probe_ipv4<GG, UU, PM_SUMS>, dim3((uint32_t)blocks), dim3(256), 0, stream, a, \
                                pkts, n, sink, xg, vals, posv));                                              \
         e = take_launch_rc();                                                                               \
     }
+    TCSUM_PI(4, 4) TCSUM_PI(8, 3) TCSUM_PI(8, 4) TCSUM_PI(8, 6)
     TCSUM_PI(16, 1) TCSUM_PI(16, 2) TCSUM_PI(16, 3) TCSUM_PI(16, 4) TCSUM_PI(16, 6) TCSUM_PI(16, 8)
     TCSUM_PI(32, 6) TCSUM_PI(64, 4) TCSUM_PI(64, 16)
 #undef TCSUM_PI
@@ -1061,7 +1076,9 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
     if (n == 0)
         return hipSuccess;
     const uint32_t xg = (uint32_t)route(1500).xcd;
-    const uint32_t G = occ == 516 || occ == 816 ? 16u : occ == 964 ? 64u
+    const uint32_t G = occ >= 1240 && occ < 1250 ? 4u : occ >= 1280 && occ < 1290 ? 8u
+                       : occ >= 1360 && occ < 1370 ? 16u
+                       : occ == 516 || occ == 816 ? 16u : occ == 964 ? 64u
                        : occ == 532 || occ == 832 || (occ >= 1000 && occ < 1100) ? 32u
                        : mode == IP_RX ? 16u : 32u;
     if (wg != 64 && wg != 128 && wg != 256 && wg != 512 && wg != 1024)
@@ -1106,6 +1123,19 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         // the third header chunk as one dword (H1), alone and with PIPE 5
         if (occ == 900 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 0, 0, true>)) }
         if (occ == 905 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 0, 5, true>)) }
+        // narrower lane groups for short packets (occ = 1200 + 10 * G + U)
+        if (occ == 1243 && wg == 256) { TCSUM_SH((k_ipv4<4, 3, IP_SUMS, 256>)) }
+        if (occ == 1244 && wg == 256) { TCSUM_SH((k_ipv4<4, 4, IP_SUMS, 256>)) }
+        if (occ == 1246 && wg == 256) { TCSUM_SH((k_ipv4<4, 6, IP_SUMS, 256>)) }
+        if (occ == 1283 && wg == 256) { TCSUM_SH((k_ipv4<8, 3, IP_SUMS, 256>)) }
+        if (occ == 1284 && wg == 256) { TCSUM_SH((k_ipv4<8, 4, IP_SUMS, 256>)) }
+        if (occ == 1286 && wg == 256) { TCSUM_SH((k_ipv4<8, 6, IP_SUMS, 256>)) }
+        if (occ == 1288 && wg == 256) { TCSUM_SH((k_ipv4<8, 8, IP_SUMS, 256>)) }
+        if (occ == 1282 && wg == 256) { TCSUM_SH((k_ipv4<8, 2, IP_SUMS, 256>)) }
+        if (occ == 1362 && wg == 256) { TCSUM_SH((k_ipv4<16, 2, IP_SUMS, 256>)) }
+        if (occ == 1363 && wg == 256) { TCSUM_SH((k_ipv4<16, 3, IP_SUMS, 256>)) }
+        if (occ == 1364 && wg == 256) { TCSUM_SH((k_ipv4<16, 4, IP_SUMS, 256>)) }
+        if (occ == 1366 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_SUMS, 256>)) }
         // packets handed out inside the workgroup, M = occ - 300 per lane group
         if (occ == 302 && wg == 256) { TCSUM_SH((k_ipv4_dyn<32, 6, IP_SUMS, 2>)) }
         if (occ == 304 && wg == 256) { TCSUM_SH((k_ipv4_dyn<32, 6, IP_SUMS, 4>)) }
@@ -1139,6 +1169,13 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 1004 && wg == 256) { TCSUM_SH((k_ipv4_pair<4, IP_RX>)) }
         if (occ == 804 && wg == 256) { TCSUM_SH((k_ipv4<16, 4, IP_RX, 256, 0, 5>)) }
         if (occ == 832 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_RX, 256, 0, 5>)) }
+        // narrower lane groups for short packets (occ = 1200 + 10 * G + U)
+        if (occ == 1243 && wg == 256) { TCSUM_SH((k_ipv4<4, 3, IP_RX, 256>)) }
+        if (occ == 1244 && wg == 256) { TCSUM_SH((k_ipv4<4, 4, IP_RX, 256>)) }
+        if (occ == 1283 && wg == 256) { TCSUM_SH((k_ipv4<8, 3, IP_RX, 256>)) }
+        if (occ == 1284 && wg == 256) { TCSUM_SH((k_ipv4<8, 4, IP_RX, 256>)) }
+        if (occ == 1286 && wg == 256) { TCSUM_SH((k_ipv4<8, 6, IP_RX, 256>)) }
+        if (occ == 1364 && wg == 256) { TCSUM_SH((k_ipv4<16, 4, IP_RX, 256>)) }
     }
 #undef TCSUM_SH
     return hipErrorInvalidValue;
@@ -1206,7 +1243,7 @@ int tcsum_probe_segments(const void *arena, const tcsum_peso_t *segs, uint32_t n
 int tcsum_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, uint32_t n, uint64_t total_bytes_hint, int mode,
                      uint32_t *sink, void *stream)
 {
-    if (!arena || !pkts || !sink || mode < 0 || mode > 2)
+    if (!arena || !pkts || !sink || mode < 0 || mode > 3)
         return TCSUM_ERR_PARAM;
     return rc_of(tcsum::launch_probe_ipv4(arena, pkts, n, mean_of(total_bytes_hint, n), mode, sink,
                                           static_cast<hipStream_t>(stream)));

@@ -497,6 +497,7 @@ static hipError_t ipv4_u(int G, int U, dim3 grid, uint8_t *arena, const tcsum_pk
         return launch(k_ipv4<GG, UU, IPM>, grid, dim3(256), 0, s, arena, pkts, n, out, flags, verdict, opts, \
                       xg);                                                                           \
     }
+    TCSUM_IP(4, 4) TCSUM_IP(8, 3) TCSUM_IP(8, 4) TCSUM_IP(8, 6)
     TCSUM_IP(16, 1) TCSUM_IP(16, 2) TCSUM_IP(16, 3) TCSUM_IP(16, 4) TCSUM_IP(16, 6) TCSUM_IP(16, 8)
     TCSUM_IP(32, 6) TCSUM_IP(64, 4) TCSUM_IP(64, 16)
 #undef TCSUM_IP
@@ -597,12 +598,14 @@ static hipError_t tx_split(Geometry g, dim3 grid, uint32_t xg, uint8_t *arena, u
     return e != hipSuccess ? e : f;
 }
 
+static void ipv4_geometry(Geometry &g, int ip_mode);
+
 hipError_t launch_ipv4_tx_scratch(Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
                                   uint8_t *flags, uint32_t *scratch, hipStream_t stream)
 {
     if (n == 0)
         return hipSuccess;
-    g.lanes = g.lanes < 16 ? 16 : g.lanes > 64 ? 64 : g.lanes; // launch_ipv4's rules
+    ipv4_geometry(g, IP_TX); // launch_ipv4's rules
     const uint64_t per_launch = kMaxBlocks * (256u / (uint32_t)g.lanes);
     if (n > per_launch) { // each part uses the scratch of its own packets
         for (uint64_t i0 = 0; i0 < n; i0 += per_launch) {
@@ -624,7 +627,7 @@ hipError_t launch_ipv4_tx_to(Geometry g, uint8_t *arena, uint8_t *store, const t
 {
     if (n == 0)
         return hipSuccess;
-    g.lanes = g.lanes < 16 ? 16 : g.lanes > 64 ? 64 : g.lanes; // launch_ipv4's rules
+    ipv4_geometry(g, IP_TX); // launch_ipv4's rules
     const uint64_t per_launch = kMaxBlocks * (256u / (uint32_t)g.lanes);
     if (n > per_launch) {
         for (uint64_t i0 = 0; i0 < n; i0 += per_launch) {
@@ -641,13 +644,16 @@ hipError_t launch_ipv4_tx_to(Geometry g, uint8_t *arena, uint8_t *store, const t
                     out, flags, stream);
 }
 
-hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
-                       uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream)
+// k_ipv4's shape for geometry g: short packets by ipv4_short_shape (unless
+// a debug knob forces lanes or loads; a forced shape k_ipv4 is not built in
+// is refused), the rest with lanes clamped to 16..64.
+static void ipv4_geometry(Geometry &g, int ip_mode)
 {
-    if (n == 0)
-        return hipSuccess;
-    if (g.lanes < 16)
-        g.lanes = 16;
+    const bool forced = knob(KNOB_LANES) >= 0 || knob(KNOB_LOADS) >= 0;
+    if (!forced && ipv4_short_shape(g, ip_mode == IP_RX ? 2 : 0, (uint64_t)g.interior))
+        return;
+    if (g.lanes < (forced ? 4 : 16))
+        g.lanes = forced ? 4 : 16;
     if (g.lanes > 64) // k_ipv4 keeps a packet inside one wave (no workgroup-per-packet form)
         g.lanes = 64;
     // rx keeps more registers live through the data pass (the gate codes, the
@@ -655,6 +661,14 @@ hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_
     // faster on configs[3] (profiles/r02/geom_rx.txt); the other modes keep 32
     if (ip_mode == IP_RX && g.lanes == 32 && knob(KNOB_LANES) < 0)
         g.lanes = 16;
+}
+
+hipError_t launch_ipv4(int ip_mode, Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n,
+                       uint32_t *out, uint8_t *flags, int8_t *verdict, hipStream_t stream)
+{
+    if (n == 0)
+        return hipSuccess;
+    ipv4_geometry(g, ip_mode);
     const uint64_t per_launch = kMaxBlocks * (256u / (uint32_t)g.lanes);
     if (n > per_launch) { // see kMaxBlocks
         for (uint64_t i0 = 0; i0 < n; i0 += per_launch) {

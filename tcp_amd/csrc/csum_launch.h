@@ -90,6 +90,45 @@ inline void shuffled_route(Geometry &g, int64_t packed_knob)
         g.packed = 0;
 }
 
+// k_ipv4's lane groups for packets of mean length ~16 * (interior + 1) B when
+// no debug knob forces one (launch_ipv4 and the bench lib's probe).  Short
+// packets take narrow groups: the header parse, the gates and the result
+// are per-lane work every lane of a group repeats, and a 16-lane group on a
+// 100-B packet repeats it 16 times for 7 chunks.  Equal-length batches,
+// one process (profiles/r06/ab21/ipv4_narrow*.txt), route against 16 x 2..8:
+// sums 100 B 2.44x faster at 4 x 4, 200 B 1.9x, 300 B 1.66x at 8 x 4, 600 B
+// 1.37x at 8 x 6, 1,000 B 1.23x at 8 x 3, 1,500-3,000 B 3-7 % at 16 x 4 /
+// 16 x 3 / 16 x 6; rx 100-300 B 1.8-2.3x at 4 x 4, 600 B 1.35x at 8 x 6,
+// 1,000 B 1.35x at 8 x 3.  Longer packets keep pick_geometry's lanes (>= 16;
+// rx at 16 where the others take 32).  Returns false when nothing changed.
+inline bool ipv4_short_shape(Geometry &g, int ip_mode, uint64_t interior)
+{
+    const bool rx = ip_mode == 2;
+    int G = 0, U = 0;
+    if (interior == 0 || interior > 246) // unknown, or ~4 KiB and longer
+        return false;
+    if (interior <= 14) { // < ~250 B
+        G = 4, U = 4;
+    } else if (interior <= 27) { // ~250-450 B
+        G = rx ? 4 : 8, U = 4;
+    } else if (interior <= 48) { // ~450-800 B
+        G = 8, U = 6;
+    } else if (interior <= 80) { // ~800-1300 B
+        G = 8, U = 3;
+    } else if (rx) {
+        return false;
+    } else if (interior <= 111) { // ~1300-1800 B
+        G = 16, U = 4;
+    } else if (interior <= 155) { // ~1800-2500 B
+        G = 16, U = 3;
+    } else { // ~2500-4000 B
+        G = 16, U = 6;
+    }
+    g.lanes = G;
+    g.loads = U;
+    return true;
+}
+
 // aux: MODE_SEG -> complement; MODE_EXACT -> complement | (offset parity << 1).
 hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void *descs,
                            uint32_t n, uint16_t *out, uint32_t aux, hipStream_t stream);

@@ -412,14 +412,16 @@ def probe_segments(arena, segs, n: int, total_bytes: int, sink=None, stream=None
     return sink
 
 
-def probe_ipv4(arena, pkts, n: int, total_bytes: int, rx: bool = False, sink=None, stream=None, tx: bool = False):
+def probe_ipv4(arena, pkts, n: int, total_bytes: int, rx: bool = False, sink=None, stream=None, tx: bool = False,
+               masked: bool = False):
     """tcsum_probe_ipv4: the IPv4 batch calls' loads with free arithmetic;
     tx=True adds the deferred tx fill's scratch writes and field scatter (the
-    fields are left junk)."""
+    fields are left junk); masked=True: the sums loads with the slots past a
+    packet's last chunk masked off instead of clamped."""
     torch = _torch()
     if sink is None:
         sink = torch.zeros(1, dtype=torch.uint32, device=arena.device)
-    mode = 2 if tx else 1 if rx else 0
+    mode = 3 if masked else 2 if tx else 1 if rx else 0
     _lib.check(_lib.bench_lib().tcsum_probe_ipv4(arena.data_ptr(), pkts.data_ptr(), n, total_bytes, mode,
                                            sink.data_ptr(), _stream_ptr(stream)), "tcsum_probe_ipv4")
     return sink

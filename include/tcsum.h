@@ -159,8 +159,10 @@ int tcsum_batch_ipv4(const void *arena /*[dev]*/, const tcsum_pkt_t *pkts /*[dev
  *   ICMP checksum (L4 + 2)                  icmpv4.c:45-58
  * L4 fields are left alone for fragments and short L4s; nothing is written
  * for SHORT / BAD_* packets.  out (ip | l4 << 16) and flags may be NULL.
- * From 131,072 packets on the stores are deferred (tests and measurement
- * force either form with tcsum_debug_set("tx_split", 0 / 1), tcsum_debug.h): one launch computes every packet's values and field
+ * From 131,072 packets of a mean length of 2,800 B or more (total_bytes_hint
+ * / n; 1,500 B when the hint is 0) the stores are deferred (tests and
+ * measurement force either form with tcsum_debug_set("tx_split", 0 / 1),
+ * tcsum_debug.h): one launch computes every packet's values and field
  * positions into stream-ordered scratch (4-8 B per packet, from a memory
  * pool the library keeps per device, up to 1 GiB retained between calls;
  * freed on the stream), a second short launch writes all the fields.  Same

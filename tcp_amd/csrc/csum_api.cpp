@@ -544,8 +544,14 @@ static int rc_of(hipError_t e)
 
 static uint64_t mean_of(uint64_t total, uint32_t n) { return total && n ? total / n : 1500; }
 
-// device tx fills of at least this many packets defer their stores (mode 4)
+// device tx fills of at least this many packets, of at least this mean
+// length, defer their stores (mode 4).  Shorter packets keep the stores in
+// the kernel: equal 100-B packets 3,451 against 5,852 us deferred, 300-B
+// 1,794 / 2,801, 1,000-B 1,077 / 1,200, 2,500-B 895 / 919; 3,000-B 891 /
+// 838 (profiles/r06/ab24/tx_short*.txt) -- millions of scattered field
+// writes in a second launch cost more than the in-kernel stores save there.
 static constexpr uint32_t kTxSplitMin = 131072;
+static constexpr uint64_t kTxSplitMinLen = 2800;
 
 // The route for a batch and what its caller knows of the layout
 // (tcsum_hint_t): SHUFFLED skips the stream kernel where its workgroups,
@@ -595,7 +601,7 @@ int tcsum_batch(int op, void *arena, const void *descs, uint32_t n, void *out, u
         // Debug knob "tx_split" forces.  Under hipGraph capture the
         // single-launch form is taken: it allocates nothing (tcsum.h).
         const int64_t ks = tcsum::knob(tcsum::KNOB_TX_SPLIT);
-        bool split = ks >= 0 ? ks != 0 : n >= kTxSplitMin;
+        bool split = ks >= 0 ? ks != 0 : n >= kTxSplitMin && mean_of(total, n) >= kTxSplitMinLen;
         hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
         if (split && tcsum::quiet(hipStreamIsCapturing(st, &cap)) == hipSuccess && cap != hipStreamCaptureStatusNone)
             split = false;

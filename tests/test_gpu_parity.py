@@ -764,11 +764,15 @@ def test_huge_ipv4_batch_index_math(tc, torch, oracle, geometry):
     np.testing.assert_array_equal(down(flags[tidx]), ef)
     del out, flags
 
-    tflags = tc.batch_ipv4_tx_fill(arena, d, n, n * L)  # >= 131,072 packets: deferred stores
+    tflags = tc.batch_ipv4_tx_fill(arena, d, n, n * L)  # 28-B packets: the stores in the kernel
     efl = oracle.batch_ipv4_tx_fill(sample, spk)  # sample is filled in place
     np.testing.assert_array_equal(down(tflags[tidx]), efl)
     got = down(arena.view(n, L)[tidx]).reshape(-1)
     np.testing.assert_array_equal(got, sample)
+    with tc.debug(tx_split=1):  # and deferred to k_tx_scatter (idempotent: the fields read as zero)
+        tflags = tc.batch_ipv4_tx_fill(arena, d, n, n * L)
+    np.testing.assert_array_equal(down(tflags[tidx]), efl)
+    np.testing.assert_array_equal(down(arena.view(n, L)[tidx]).reshape(-1), sample)
 
     verdict, vflags = tc.batch_ipv4_rx_verify(arena, d, n, n * L)
     ev, evf = oracle.batch_ipv4_rx_verify(sample, spk)

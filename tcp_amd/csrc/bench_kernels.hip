@@ -1175,7 +1175,9 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 1283 && wg == 256) { TCSUM_SH((k_ipv4<8, 3, IP_RX, 256>)) }
         if (occ == 1284 && wg == 256) { TCSUM_SH((k_ipv4<8, 4, IP_RX, 256>)) }
         if (occ == 1286 && wg == 256) { TCSUM_SH((k_ipv4<8, 6, IP_RX, 256>)) }
+        if (occ == 1363 && wg == 256) { TCSUM_SH((k_ipv4<16, 3, IP_RX, 256>)) }
         if (occ == 1364 && wg == 256) { TCSUM_SH((k_ipv4<16, 4, IP_RX, 256>)) }
+        if (occ == 1366 && wg == 256) { TCSUM_SH((k_ipv4<16, 6, IP_RX, 256>)) }
     }
 #undef TCSUM_SH
     return hipErrorInvalidValue;

@@ -99,8 +99,9 @@ inline void shuffled_route(Geometry &g, int64_t packed_knob)
 // sums 100 B 2.44x faster at 4 x 4, 200 B 1.9x, 300 B 1.66x at 8 x 4, 600 B
 // 1.37x at 8 x 6, 1,000 B 1.23x at 8 x 3, 1,500-3,000 B 3-7 % at 16 x 4 /
 // 16 x 3 / 16 x 6; rx 100-300 B 1.8-2.3x at 4 x 4, 600 B 1.35x at 8 x 6,
-// 1,000 B 1.35x at 8 x 3.  Longer packets keep pick_geometry's lanes (>= 16;
-// rx at 16 where the others take 32).  Returns false when nothing changed.
+// 1,000 B 1.35x at 8 x 3, 1,500 B 1.22x, 2,000 B 1.14x (ab25/).  Longer
+// packets keep pick_geometry's lanes (>= 16; rx at 16 where the others take
+// 32).  Returns false when nothing changed.
 inline bool ipv4_short_shape(Geometry &g, int ip_mode, uint64_t interior)
 {
     const bool rx = ip_mode == 2;
@@ -115,8 +116,10 @@ inline bool ipv4_short_shape(Geometry &g, int ip_mode, uint64_t interior)
         G = 8, U = 6;
     } else if (interior <= 80) { // ~800-1300 B
         G = 8, U = 3;
-    } else if (rx) {
-        return false;
+    } else if (rx) { // ~1300-2500 B: 8 x 3, then 16 x 3 (1,500-B 1.22x, 2,000-B 1.14x); longer: the old rule
+        if (interior > 155)
+            return false;
+        G = interior <= 111 ? 8 : 16, U = 3;
     } else if (interior <= 111) { // ~1300-1800 B
         G = 16, U = 4;
     } else if (interior <= 155) { // ~1800-2500 B

@@ -118,6 +118,11 @@ int tcsum_debug_shards(tcsum_shard_stat_t *out, int max);
  * the per-range kernel).  libtcsum_bench.so's probes follow it. */
 void tcsum_debug_route(uint64_t mean_len, int32_t out[5]);
 
+/* The k_ipv4 lane group an IPv4 batch of that mean packet length takes, with
+ * the knobs applied: out[0] lanes per packet, out[1] loads per lane.
+ * ip_mode: 0 sums, 1 tx fill, 2 rx verify, 3 tx offload. */
+void tcsum_debug_ipv4_route(uint64_t mean_len, int ip_mode, int32_t out[2]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,7 +11,7 @@ from .csum import (LAYOUT_ORDERED, LAYOUT_SHUFFLED, LAYOUT_UNKNOWN, OP_IPV4, OP_
                    batch_ipv4_tx_offload, tx_apply_batch, batch_peso, batch_segments,
                    checksum16, checksum_peso, descs_to_device, device_count, host_batch_peso, host_batch_peso_multi,
                    HostArena, host_register, host_unregister, host_batch_ipv4, host_batch_ipv4_rx_verify, host_batch_ipv4_tx_fill,
-                   pick_geometry, route, debug, last_shards, flat_ipv4, debug_get, debug_set, pktbuf_checksum16, plat_init, probe_ipv4, probe_read, probe_segments, probe_tile, probe_txfloor, txfloor_prepare, queue_server, release, call_server, synth_fill,
+                   pick_geometry, route, ipv4_route, debug, last_shards, flat_ipv4, debug_get, debug_set, pktbuf_checksum16, plat_init, probe_ipv4, probe_read, probe_segments, probe_tile, probe_txfloor, txfloor_prepare, queue_server, release, call_server, synth_fill,
                    synth_ipv4, to_host, to_host_tensor)
 from .pktbuf import IpAddr, PktBuf
 from . import pcap, workload
@@ -20,7 +20,7 @@ __all__ = [
     "checksum16", "checksum_peso", "pktbuf_checksum16", "batch", "batch_segments", "batch_peso", "batch_ipv4",
     "batch_ipv4_tx_fill", "batch_ipv4_tx_offload", "tx_apply_batch", "batch_ipv4_rx_verify",
     "host_batch_peso", "host_batch_peso_multi", "HostArena", "host_register", "host_unregister", "host_batch_ipv4", "host_batch_ipv4_tx_fill", "host_batch_ipv4_rx_verify",
-    "synth_fill", "synth_ipv4", "descs_to_device", "device_count", "pick_geometry", "route", "debug", "last_shards", "flat_ipv4",
+    "synth_fill", "synth_ipv4", "descs_to_device", "device_count", "pick_geometry", "route", "ipv4_route", "debug", "last_shards", "flat_ipv4",
     "debug_get", "debug_set", "to_host", "to_host_tensor",
     "plat_init", "probe_ipv4", "probe_read", "probe_segments", "probe_tile", "probe_txfloor", "txfloor_prepare", "queue_server", "release", "call_server", "PktBuf", "IpAddr", "SEG_DTYPE", "PESO_DTYPE", "PKT_DTYPE", "pcap", "workload",
 ]

@@ -65,6 +65,7 @@ SIGNATURES = {
     "tcsum_debug_set": (_I, [ctypes.c_char_p, ctypes.c_int64]),
     "tcsum_debug_get": (ctypes.c_int64, [ctypes.c_char_p]),
     "tcsum_debug_route": (None, [_U64, ctypes.POINTER(ctypes.c_int32)]),
+    "tcsum_debug_ipv4_route": (None, [_U64, _I, ctypes.POINTER(ctypes.c_int32)]),
     "tcsum_debug_plan_host_peso": (ctypes.c_int64, [_V, _U32, _U64, _V, _U32, _V]),
     "tcsum_debug_shards": (_I, [_V, _I]),
 }

@@ -519,6 +519,16 @@ int64_t tcsum_debug_get(const char *key)
     return k < 0 ? -2 : tcsum::knob((tcsum::Knob)k);
 }
 
+void tcsum_debug_ipv4_route(uint64_t mean_len, int ip_mode, int32_t out[2])
+{
+    Geometry g = tcsum::pick_geometry(mean_len);
+    tcsum::ipv4_geometry(g, ip_mode);
+    if (out) {
+        out[0] = g.lanes;
+        out[1] = g.loads;
+    }
+}
+
 void tcsum_debug_route(uint64_t mean_len, int32_t out[5])
 {
     const Geometry g = tcsum::pick_geometry(mean_len);

@@ -598,8 +598,6 @@ static hipError_t tx_split(Geometry g, dim3 grid, uint32_t xg, uint8_t *arena, u
     return e != hipSuccess ? e : f;
 }
 
-static void ipv4_geometry(Geometry &g, int ip_mode);
-
 hipError_t launch_ipv4_tx_scratch(Geometry g, uint8_t *arena, const tcsum_pkt_t *pkts, uint32_t n, uint32_t *out,
                                   uint8_t *flags, uint32_t *scratch, hipStream_t stream)
 {
@@ -647,7 +645,7 @@ hipError_t launch_ipv4_tx_to(Geometry g, uint8_t *arena, uint8_t *store, const t
 // k_ipv4's shape for geometry g: short packets by ipv4_short_shape (unless
 // a debug knob forces lanes or loads; a forced shape k_ipv4 is not built in
 // is refused), the rest with lanes clamped to 16..64.
-static void ipv4_geometry(Geometry &g, int ip_mode)
+void ipv4_geometry(Geometry &g, int ip_mode)
 {
     const bool forced = knob(KNOB_LANES) >= 0 || knob(KNOB_LOADS) >= 0;
     if (!forced && ipv4_short_shape(g, ip_mode == IP_RX ? 2 : 0, (uint64_t)g.interior))

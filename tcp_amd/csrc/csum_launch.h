@@ -132,6 +132,11 @@ inline bool ipv4_short_shape(Geometry &g, int ip_mode, uint64_t interior)
     return true;
 }
 
+// The k_ipv4 shape launch_ipv4 takes for geometry g and ip_mode (below):
+// ipv4_short_shape unless a debug knob forces lanes / loads, else lanes
+// clamped to 16..64 (forced: 4..64), rx at 16 where the others take 32.
+void ipv4_geometry(Geometry &g, int ip_mode);
+
 // aux: MODE_SEG -> complement; MODE_EXACT -> complement | (offset parity << 1).
 hipError_t launch_segments(Mode mode, Geometry g, const void *arena, const void *descs,
                            uint32_t n, uint16_t *out, uint32_t aux, hipStream_t stream);

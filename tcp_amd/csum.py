@@ -475,6 +475,15 @@ def route(mean_len: int) -> dict:
     return dict(zip(("lanes", "loads", "xcd", "packed", "shuffled_packed"), list(r)))
 
 
+def ipv4_route(mean_len: int, ip_mode: int = 0):
+    """(lanes, loads) of the k_ipv4 launch an IPv4 batch of this mean packet
+    length takes (tcsum_debug_ipv4_route; ip_mode 0 sums, 1 tx fill, 2 rx
+    verify, 3 tx offload; debug knobs applied)."""
+    r = (ctypes.c_int32 * 2)()
+    _lib.lib().tcsum_debug_ipv4_route(mean_len, ip_mode, r)
+    return r[0], r[1]
+
+
 def flat_ipv4(mode: int, arena, pkts, n: int, total_bytes: int, out=None, flags=None, verdict=None, stream=None):
     """The byte-window stream (libtcsum_bench.so's tcsum_flat_ipv4, measurement
     and tests only): mode 0 sums, 1 tx fill, 2 rx verify, 3 tx offload, 4 tx

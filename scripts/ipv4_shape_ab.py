@@ -80,8 +80,11 @@ for cfg in ([a for a in sys.argv[1:] if not a.startswith("--")] or ["mixed", "mi
 
     if NARROW_ONLY:
         kinds = {"product (256 threads)": product}
-        shapes = ((4, 3), (4, 4), (8, 3), (8, 4), (8, 6), (16, 3), (16, 4), (16, 6)) if rx else \
-            ((4, 3), (4, 4), (4, 6), (8, 2), (8, 3), (8, 4), (8, 6), (8, 8), (16, 2), (16, 3), (16, 4), (16, 6))
+        shapes = ((2, 4), (4, 2), (4, 3), (4, 4), (8, 3), (8, 4), (8, 6), (16, 3), (16, 4), (16, 6)) if rx else \
+            ((2, 4), (2, 6), (4, 2), (4, 3), (4, 4), (4, 6), (8, 2), (8, 3), (8, 4), (8, 6), (8, 8), (16, 2), (16, 3),
+             (16, 4), (16, 6))
+        if "--tiny" in sys.argv:
+            shapes = ((2, 4), (2, 6), (4, 2), (4, 3), (4, 4)) if not rx else ((2, 4), (4, 2), (4, 3), (4, 4))
         kinds.update({f"{g} lanes x {u}": shape(256, 1200 + 10 * g + u) if g < 16 else shape(256, 1360 + u)
                       for g, u in shapes})
         if not rx:

@@ -808,7 +808,7 @@ static hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, 
                                pkts, n, sink, xg, vals, posv));                                              \
         e = take_launch_rc();                                                                               \
     }
-    TCSUM_PI(4, 4) TCSUM_PI(8, 3) TCSUM_PI(8, 4) TCSUM_PI(8, 6)
+    TCSUM_PI(2, 4) TCSUM_PI(4, 4) TCSUM_PI(8, 3) TCSUM_PI(8, 4) TCSUM_PI(8, 6)
     TCSUM_PI(16, 1) TCSUM_PI(16, 2) TCSUM_PI(16, 3) TCSUM_PI(16, 4) TCSUM_PI(16, 6) TCSUM_PI(16, 8)
     TCSUM_PI(32, 6) TCSUM_PI(64, 4) TCSUM_PI(64, 16)
 #undef TCSUM_PI
@@ -1076,7 +1076,8 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
     if (n == 0)
         return hipSuccess;
     const uint32_t xg = (uint32_t)route(1500).xcd;
-    const uint32_t G = occ >= 1240 && occ < 1250 ? 4u : occ >= 1280 && occ < 1290 ? 8u
+    const uint32_t G = occ >= 1220 && occ < 1230 ? 2u : occ >= 1240 && occ < 1250 ? 4u
+                       : occ >= 1280 && occ < 1290 ? 8u
                        : occ >= 1360 && occ < 1370 ? 16u
                        : occ == 516 || occ == 816 ? 16u : occ == 964 ? 64u
                        : occ == 532 || occ == 832 || (occ >= 1000 && occ < 1100) ? 32u
@@ -1124,6 +1125,9 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 900 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 0, 0, true>)) }
         if (occ == 905 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_SUMS, 256, 0, 5, true>)) }
         // narrower lane groups for short packets (occ = 1200 + 10 * G + U)
+        if (occ == 1224 && wg == 256) { TCSUM_SH((k_ipv4<2, 4, IP_SUMS, 256>)) }
+        if (occ == 1226 && wg == 256) { TCSUM_SH((k_ipv4<2, 6, IP_SUMS, 256>)) }
+        if (occ == 1242 && wg == 256) { TCSUM_SH((k_ipv4<4, 2, IP_SUMS, 256>)) }
         if (occ == 1243 && wg == 256) { TCSUM_SH((k_ipv4<4, 3, IP_SUMS, 256>)) }
         if (occ == 1244 && wg == 256) { TCSUM_SH((k_ipv4<4, 4, IP_SUMS, 256>)) }
         if (occ == 1246 && wg == 256) { TCSUM_SH((k_ipv4<4, 6, IP_SUMS, 256>)) }
@@ -1170,6 +1174,8 @@ static hipError_t launch_ipv4_shape(uint8_t *arena, const tcsum_pkt_t *pkts, uin
         if (occ == 804 && wg == 256) { TCSUM_SH((k_ipv4<16, 4, IP_RX, 256, 0, 5>)) }
         if (occ == 832 && wg == 256) { TCSUM_SH((k_ipv4<32, 6, IP_RX, 256, 0, 5>)) }
         // narrower lane groups for short packets (occ = 1200 + 10 * G + U)
+        if (occ == 1224 && wg == 256) { TCSUM_SH((k_ipv4<2, 4, IP_RX, 256>)) }
+        if (occ == 1242 && wg == 256) { TCSUM_SH((k_ipv4<4, 2, IP_RX, 256>)) }
         if (occ == 1243 && wg == 256) { TCSUM_SH((k_ipv4<4, 3, IP_RX, 256>)) }
         if (occ == 1244 && wg == 256) { TCSUM_SH((k_ipv4<4, 4, IP_RX, 256>)) }
         if (occ == 1283 && wg == 256) { TCSUM_SH((k_ipv4<8, 3, IP_RX, 256>)) }

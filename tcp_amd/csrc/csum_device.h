@@ -194,7 +194,8 @@ template <int G>
 __device__ __forceinline__ uint32_t group_sum(uint32_t x)
 {
     x = dpp_add<0xB1>(x); // quad_perm [1,0,3,2]: lane ^ 1
-    x = dpp_add<0x4E>(x); // quad_perm [2,3,0,1]: lane ^ 2
+    if constexpr (G >= 4)
+        x = dpp_add<0x4E>(x); // quad_perm [2,3,0,1]: lane ^ 2
     if constexpr (G == 8)
         x += __shfl_xor(x, 4, 64);
     if constexpr (G >= 16) {

@@ -497,7 +497,7 @@ static hipError_t ipv4_u(int G, int U, dim3 grid, uint8_t *arena, const tcsum_pk
         return launch(k_ipv4<GG, UU, IPM>, grid, dim3(256), 0, s, arena, pkts, n, out, flags, verdict, opts, \
                       xg);                                                                           \
     }
-    TCSUM_IP(4, 4) TCSUM_IP(8, 3) TCSUM_IP(8, 4) TCSUM_IP(8, 6)
+    TCSUM_IP(2, 4) TCSUM_IP(4, 4) TCSUM_IP(8, 3) TCSUM_IP(8, 4) TCSUM_IP(8, 6)
     TCSUM_IP(16, 1) TCSUM_IP(16, 2) TCSUM_IP(16, 3) TCSUM_IP(16, 4) TCSUM_IP(16, 6) TCSUM_IP(16, 8)
     TCSUM_IP(32, 6) TCSUM_IP(64, 4) TCSUM_IP(64, 16)
 #undef TCSUM_IP

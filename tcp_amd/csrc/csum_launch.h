@@ -96,7 +96,8 @@ inline void shuffled_route(Geometry &g, int64_t packed_knob)
 // are per-lane work every lane of a group repeats, and a 16-lane group on a
 // 100-B packet repeats it 16 times for 7 chunks.  Equal-length batches,
 // one process (profiles/r06/ab21/ipv4_narrow*.txt), route against 16 x 2..8:
-// sums 100 B 2.44x faster at 4 x 4, 200 B 1.9x, 300 B 1.66x at 8 x 4, 600 B
+// sums 40-64 B 1.3-1.5x faster again at 2 x 4 than at 4 x 4 (ab26/; rx 40-100 B
+// 1.2-1.3x), 100 B 2.44x at 4 x 4, 200 B 1.9x, 300 B 1.66x at 8 x 4, 600 B
 // 1.37x at 8 x 6, 1,000 B 1.23x at 8 x 3, 1,500-3,000 B 3-7 % at 16 x 4 /
 // 16 x 3 / 16 x 6; rx 100-300 B 1.8-2.3x at 4 x 4, 600 B 1.35x at 8 x 6,
 // 1,000 B 1.35x at 8 x 3, 1,500 B 1.22x, 2,000 B 1.14x (ab25/).  Longer
@@ -108,7 +109,9 @@ inline bool ipv4_short_shape(Geometry &g, int ip_mode, uint64_t interior)
     int G = 0, U = 0;
     if (interior == 0 || interior > 246) // unknown, or ~4 KiB and longer
         return false;
-    if (interior <= 14) { // < ~250 B
+    if (interior <= (rx ? 6u : 4u)) { // < ~96 B (rx: < ~128 B): two lanes a packet
+        G = 2, U = 4;
+    } else if (interior <= 14) { // < ~250 B
         G = 4, U = 4;
     } else if (interior <= 27) { // ~250-450 B
         G = rx ? 4 : 8, U = 4;

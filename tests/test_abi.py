@@ -219,16 +219,16 @@ def test_ipv4_route_table(libpath):
     ipv4_short_shape; profiles/r06/ab21-ab25): narrow groups for short
     packets, configs[3]'s 32 x 6 (rx 16 x 6) untouched.  No device needed."""
     from tcp_amd import ipv4_route
-    sums = {100: (4, 4), 200: (4, 4), 300: (8, 4), 600: (8, 6), 1000: (8, 3), 1500: (16, 4), 2000: (16, 3),
+    sums = {40: (2, 4), 64: (2, 4), 100: (4, 4), 200: (4, 4), 300: (8, 4), 600: (8, 6), 1000: (8, 3), 1500: (16, 4), 2000: (16, 3),
             3000: (16, 6), 4535: (32, 6), 9000: (32, 6)}
-    rx = {100: (4, 4), 300: (4, 4), 600: (8, 6), 1000: (8, 3), 1500: (8, 3), 2000: (16, 3), 3000: (16, 6),
+    rx = {40: (2, 4), 100: (2, 4), 200: (4, 4), 300: (4, 4), 600: (8, 6), 1000: (8, 3), 1500: (8, 3), 2000: (16, 3), 3000: (16, 6),
           4535: (16, 6), 9000: (16, 6)}
     for mean, want in sums.items():
         for mode in (0, 1, 3):  # sums, tx fill, tx offload
             assert ipv4_route(mean, mode) == want, (mean, mode)
     for mean, want in rx.items():
         assert ipv4_route(mean, 2) == want, mean
-    shapes = {(4, 4), (8, 3), (8, 4), (8, 6), (16, 1), (16, 2), (16, 3), (16, 4), (16, 6), (16, 8), (32, 6),
+    shapes = {(2, 4), (4, 4), (8, 3), (8, 4), (8, 6), (16, 1), (16, 2), (16, 3), (16, 4), (16, 6), (16, 8), (32, 6),
               (64, 4), (64, 16)}
     for mean in range(0, 70000, 37):  # every routed shape is an instantiated k_ipv4
         for mode in range(4):

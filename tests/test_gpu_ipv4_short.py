@@ -1,5 +1,5 @@
 """Short IPv4 packets on the narrow lane groups the router gives them
-(csum_launch.h ipv4_short_shape: 4 x 4 under ~250 B, 8 x 4 / 8 x 6 / 8 x 3
+(csum_launch.h ipv4_short_shape: 2 x 4 under ~96 B (rx ~128 B), 4 x 4 under ~250 B, 8 x 4 / 8 x 6 / 8 x 3
 to ~1.3 KiB, 16 x 4 / 16 x 3 / 16 x 6 to ~4 KiB; rx keeps 16+ lanes past
 ~1.3 KiB).  Fuzzed packets around each mean (headers mostly plausible, some
 short frames, random arena phase) through sums, rx verify, tx offload and
@@ -30,7 +30,7 @@ def tc(torch):
     return tcp_amd
 
 
-MEANS = [40, 100, 200, 300, 600, 1000, 1500, 2000, 3000]
+MEANS = [40, 64, 100, 200, 300, 600, 1000, 1500, 2000, 3000]
 
 
 @pytest.mark.parametrize("mean", MEANS)
@@ -73,7 +73,7 @@ def _dev(torch, a):
     return up(torch.from_numpy(np.concatenate([a, np.zeros(64, np.uint8)])))
 
 
-@pytest.mark.parametrize("g,u", [(4, 4), (8, 3), (8, 4), (8, 6)])
+@pytest.mark.parametrize("g,u", [(2, 4), (4, 4), (8, 3), (8, 4), (8, 6)])
 def test_forced_narrow_shapes_on_golden_packets(tc, torch, g, u):
     cases, ipool = G.ipv4_cases()
     pk = G.pkt_descs(cases, tc.PKT_DTYPE)

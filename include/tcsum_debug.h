@@ -36,9 +36,10 @@ extern "C" {
  *                     always take the per-range kernel
  *   "lanes", "loads"  per-range kernel shape (lanes per range x 16-B loads per
  *                     lane): one of the shapes the router picks -- 4x1, 4x2,
- *                     8x4, 16x3, 16x4, 16x6, 16x8, 32x6, 256x16, 1024x4 (IPv4
- *                     calls: lanes clamped to 16..64); another shape makes the
- *                     batch call return TCSUM_ERR_PARAM
+ *                     4x3, 8x3, 8x4, 16x3, 16x4, 16x6, 16x8, 32x6, 256x16,
+ *                     1024x4; IPv4 calls: 2x4, 4x4, 8x3, 8x4, 8x6, 16x1..16x8,
+ *                     32x6, 64x4, 64x16 (lanes clamped to 2..64); another
+ *                     shape makes the batch call return TCSUM_ERR_PARAM
  *   "xcd"             workgroups per XCD run (1 = dispatch order)
  *   "packed"          0 / 1: checksum_peso / pktbuf_checksum16 batches on the
  *                     packed-stream kernel (k_segments_pk) off / on; K > 1: on,

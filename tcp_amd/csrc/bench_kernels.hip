@@ -770,8 +770,8 @@ static hipError_t launch_probe_ipv4(const void *arena, const tcsum_pkt_t *pkts, 
     const uint64_t chunks = mean_len / 16 + 1;
     const bool forced = tcsum_debug_get("lanes") >= 0 || tcsum_debug_get("loads") >= 0;
     if (forced || !ipv4_short_shape(g, mode == PM_RX ? 2 : 0, chunks > 2 ? chunks - 2 : 0)) {
-        if (g.lanes < (forced ? 4 : 16))
-            g.lanes = forced ? 4 : 16;
+        if (g.lanes < (forced ? 2 : 16))
+            g.lanes = forced ? 2 : 16;
         if (g.lanes > 64)
             g.lanes = 64;
         if (mode == PM_RX && g.lanes == 32 && tcsum_debug_get("lanes") < 0)

@@ -650,8 +650,8 @@ void ipv4_geometry(Geometry &g, int ip_mode)
     const bool forced = knob(KNOB_LANES) >= 0 || knob(KNOB_LOADS) >= 0;
     if (!forced && ipv4_short_shape(g, ip_mode == IP_RX ? 2 : 0, (uint64_t)g.interior))
         return;
-    if (g.lanes < (forced ? 4 : 16))
-        g.lanes = forced ? 4 : 16;
+    if (g.lanes < (forced ? 2 : 16))
+        g.lanes = forced ? 2 : 16;
     if (g.lanes > 64) // k_ipv4 keeps a packet inside one wave (no workgroup-per-packet form)
         g.lanes = 64;
     // rx keeps more registers live through the data pass (the gate codes, the

@@ -137,7 +137,7 @@ inline bool ipv4_short_shape(Geometry &g, int ip_mode, uint64_t interior)
 
 // The k_ipv4 shape launch_ipv4 takes for geometry g and ip_mode (below):
 // ipv4_short_shape unless a debug knob forces lanes / loads, else lanes
-// clamped to 16..64 (forced: 4..64), rx at 16 where the others take 32.
+// clamped to 16..64 (forced: 2..64), rx at 16 where the others take 32.
 void ipv4_geometry(Geometry &g, int ip_mode);
 
 // aux: MODE_SEG -> complement; MODE_EXACT -> complement | (offset parity << 1).

@@ -11,7 +11,7 @@ Layouts (all ~1.5 GB, device-resident):
   gaps       1500-B ranges with 0..63-B gaps between them
   ragged     packed, lengths uniform in 64..2936 B (mean 1500)
   small / big / tiny / s200 / j9000 / k16 / m1000 / m400   packed, 576 / 4000 / 64 / 200 / 9000 /
-             16384 / 1000 / 400 B each; s40 / s72 / s80 / s100 / s128 / s160 / s250 / s320 / s480 / s640 likewise
+             16384 / 1000 / 400 B each; s40 / s72 / s80 / s100 / s128 / s160 / s250 / s320 / s440 / s480 / s530 / s640 likewise
   mixedlen   packed, lengths uniform in 64..9000 B
   shufNAME   any of the above with the descriptor order permuted (shufsmall, shufragged, ...)
 """
@@ -33,7 +33,7 @@ rng = np.random.default_rng(7)
 
 FIXED = {"mtu": 1500, "shuffled": 1500, "gaps": 1500, "small": 576, "big": 4000, "tiny": 64, "s200": 200,
          "j9000": 9000, "k16": 16384, "m1000": 1000, "m400": 400, "s40": 40, "s72": 72, "s80": 80, "s100": 100,
-         "s128": 128, "s160": 160, "s250": 250, "s320": 320, "s640": 640, "s480": 480}
+         "s128": 128, "s160": 160, "s250": 250, "s320": 320, "s640": 640, "s480": 480, "s440": 440, "s530": 530}
 RAGGED = {"ragged": (64, 2937), "mixedlen": (64, 9001)}
 NAMES = sys.argv[1].split(",") if len(sys.argv) > 1 and "=" not in sys.argv[1] else \
     ["mtu", "shuffled", "gaps", "ragged", "small", "big", "tiny", "s200", "j9000", "k16", "mixedlen"]
